@@ -1,0 +1,84 @@
+"""ctypes binding of libbnn.so (C ABI declared in include/bnn.h).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly when the .so is
+missing, and every op raises when handed a non-ROCm tensor.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so libbnn binds to the same one
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbnn.so")
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int32
+F32 = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/bnn.h
+SIGNATURES = {
+    "bnn_version": (I32, []),
+    "bnn_last_error": (ctypes.c_char_p, []),
+    "bnn_sign_pack_i8": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
+    "bnn_sign_f32": (I32, [P, P, I64, P]),
+    "bnn_sign_pack_bits": (I32, [P, I64, I64, I64, P, P, I64, P]),
+    "bnn_quant_rows": (I32, [P, I64, I64, I64, P, I64, I64, P, P]),
+    "bnn_quant_cols_workspace": (I64, [I64, I64]),
+    "bnn_quant_cols_t": (I32, [P, I64, I64, I64, P, I64, I64, P, P, P, P]),
+    "bnn_gemm_i8": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_xnor": (I32, [P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
+    "bnn_conv2d_fwd": (I32, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
+    "bnn_conv2d_bwd_data": (I32, [P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
+    "bnn_conv2d_bwd_filter_workspace": (I64, [I64, I64, I64, I64, I64, I32]),
+    "bnn_conv2d_bwd_filter": (I32, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32,
+                                    I32, P]),
+    "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
+    "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
+}
+
+_lib = None
+
+
+def library_path():
+    return os.environ.get("BNN_LIB", DEFAULT_PATH)
+
+
+def lib():
+    """Load libbnn.so once.  Raises RuntimeError (no fallback) if it is missing."""
+    global _lib
+    if _lib is None:
+        path = library_path()
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"libbnn.so not found at {path}: build it with "
+                "`make -C distributed-mnist-bnns_amd/csrc` (or __graft_entry__.build()). "
+                "The BNN hot path has no CPU fallback.")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class BnnError(RuntimeError):
+    pass
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().bnn_last_error().decode(errors="replace")
+        raise BnnError(f"{name} failed (code {rc}): {msg}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (or NULL for None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

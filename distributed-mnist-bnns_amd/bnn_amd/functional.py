@@ -1,0 +1,283 @@
+"""Tensor-level wrappers of libbnn and the autograd Functions of the binarized layers.
+
+Semantics restated from the reference operator module (models/binarized_modules.py):
+
+* ``Binarize(t, 'det') = t.sign()`` (:11-13) -- ternary, sign(0) = 0.
+* ``BinarizeLinear.forward`` (:73-85): input binarised unless ``input.size(1) == 784`` (:75),
+  ``F.linear(input, sign(w))`` (:80), then ``out += bias`` in fp32 (:81-83).
+* ``BinarizeConv2d.forward`` (:93-107): input binarised unless ``input.size(1) == 3`` (:94).
+* autograd: binarisation goes through ``.data`` so the straight-through estimator is the
+  identity: dX = dY.W_b, dW = dY^T.X_b, dB = sum dY.
+
+Every op here runs on ROCm tensors through libbnn.so; there is no CPU fallback.
+"""
+import torch
+
+from . import _lib as L
+
+__all__ = [
+    "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
+    "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_",
+    "BinaryLinearFunction", "BinaryConv2dFunction",
+]
+
+ALIGN = 64
+
+
+def round_up(x, m=ALIGN):
+    return (x + m - 1) // m * m
+
+
+def _check(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("bnn_amd: libbnn runs on ROCm (cuda) tensors only; "
+                               f"got a {t.device} tensor (there is no CPU fallback)")
+        if t.dtype != torch.float32:
+            raise TypeError(f"bnn_amd: expected float32, got {t.dtype}")
+
+
+def _c2d(x):
+    """Contiguous fp32 2-D view."""
+    return x if x.is_contiguous() else x.contiguous()
+
+
+# ----------------------------------------------------------------------------- (1) sign / pack
+def sign(x, out=None):
+    """``Binarize(x, 'det')`` as a new fp32 tensor (models/binarized_modules.py:13)."""
+    _check(x)
+    x = _c2d(x)
+    y = torch.empty_like(x) if out is None else out
+    L.call("bnn_sign_f32", L.ptr(x), L.ptr(y), x.numel(), L.stream())
+    return y
+
+
+def sign_pack(x, want_q=True, want_qt=False):
+    """fp32 [M,K] -> (q int8 [M, ldq] ternary, qt int8 [K, ldqt] transposed); padding zeroed."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    q = qt = None
+    if want_q:
+        q = torch.empty((M, round_up(K)), dtype=torch.int8, device=x.device)
+    if want_qt:
+        qt = torch.empty((K, round_up(M)), dtype=torch.int8, device=x.device)
+    L.call("bnn_sign_pack_i8", L.ptr(x), M, K, K, L.ptr(q), q.shape[1] if q is not None else 0,
+           L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    return q, qt
+
+
+def sign_pack_bits(x, words=None):
+    """fp32 [M,K] -> (sign bits, nonzero bits) int32 [M, words], words >= ceil(K/32)."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    kw = words if words is not None else round_up((K + 31) // 32, 32)
+    sb = torch.empty((M, kw), dtype=torch.int32, device=x.device)
+    nz = torch.empty((M, kw), dtype=torch.int32, device=x.device)
+    L.call("bnn_sign_pack_bits", L.ptr(x), M, K, K, L.ptr(sb), L.ptr(nz), kw, L.stream())
+    return sb, nz
+
+
+def quant_rows(x):
+    """fp32 [M,K] -> (digits int8 [3, M, ldq], scale fp32 [M]) with x ~= scale*(d2*2^16+d1*2^8+d0)."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    ldq = round_up(K)
+    dg = torch.empty((3, M, ldq), dtype=torch.int8, device=x.device)
+    sc = torch.empty((M,), dtype=torch.float32, device=x.device)
+    L.call("bnn_quant_rows", L.ptr(x), M, K, K, L.ptr(dg), ldq, M * ldq, L.ptr(sc), L.stream())
+    return dg, sc
+
+
+def quant_cols_t(x, want_colsum=False):
+    """fp32 [M,N] -> (digits_t int8 [3, N, ldqt], scale [N], colsum [N] or None)."""
+    _check(x)
+    x = _c2d(x)
+    M, N = x.shape
+    ldqt = round_up(M)
+    dg = torch.empty((3, N, ldqt), dtype=torch.int8, device=x.device)
+    sc = torch.empty((N,), dtype=torch.float32, device=x.device)
+    cs = torch.empty((N,), dtype=torch.float32, device=x.device) if want_colsum else None
+    ws = torch.empty((L.lib().bnn_quant_cols_workspace(M, N),), dtype=torch.uint8, device=x.device)
+    L.call("bnn_quant_cols_t", L.ptr(x), M, N, N, L.ptr(dg), ldqt, N * ldqt, L.ptr(sc), L.ptr(cs),
+           L.ptr(ws), L.stream())
+    return dg, sc, cs
+
+
+# ----------------------------------------------------------------------------- (2) GEMMs
+def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=None, out=None):
+    """C[M,N] = combine(sum_k A[.,m,k] B[.,n,k]) * a_scale[m] * b_scale[n] + bias[n].
+
+    A: int8 [M, K] (a_digits=1) or [3, M, K]; B: int8 [N, K] or [3, N, K]; K = padded length
+    (multiple of 64, zero padding)."""
+    K = A.shape[-1]
+    assert B.shape[-1] == K and K % ALIGN == 0
+    lda, ldb = A.shape[-1], B.shape[-1]
+    a_plane = A.shape[-2] * lda if a_digits > 1 else 0
+    b_plane = B.shape[-2] * ldb if b_digits > 1 else 0
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device) if out is None else out
+    if M == 0 or N == 0:
+        return C
+    if K == 0:
+        C.zero_()
+        if bias is not None:
+            C += bias
+        return C
+    L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
+           L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
+    return C
+
+
+def gemm_xnor(a_bits, b_bits, M, N, bias=None):
+    """XNOR-popcount GEMM on (sign, nonzero) bit-plane pairs; same result as the (1,1) int8 form."""
+    (As, An), (Bs, Bn) = a_bits, b_bits
+    kw = As.shape[1]
+    C = torch.empty((M, N), dtype=torch.float32, device=As.device)
+    if M == 0 or N == 0:
+        return C
+    L.call("bnn_gemm_xnor", L.ptr(As), L.ptr(An), kw, L.ptr(Bs), L.ptr(Bn), Bs.shape[1], L.ptr(bias),
+           L.ptr(C), N, M, N, kw, L.stream())
+    return C
+
+
+# ----------------------------------------------------------------------------- linear
+class BinaryLinearFunction(torch.autograd.Function):
+    """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, binarize_input, backend="mfma"):
+        _check(x, weight, bias)
+        M, K = x.shape
+        N = weight.shape[0]
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dx)
+        b = bias.detach() if bias is not None else None
+        if binarize_input:
+            if backend == "xnor":
+                y = gemm_xnor(sign_pack_bits(x), sign_pack_bits(weight), M, N, bias=b)
+                xqt = sign_pack(x, want_q=False, want_qt=True)[1] if need_dw else None
+            else:
+                xq, xqt = sign_pack(x, want_q=True, want_qt=need_dw)
+                y = gemm_i8(xq, 1, wq, 1, M, N, bias=b)
+            ctx.save_for_backward(xqt, wqt)
+        else:
+            xd, sx = quant_rows(x)
+            y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b)
+            ctx.save_for_backward(x if need_dw else None, wqt)
+        ctx.binarize_input = binarize_input
+        ctx.dims = (M, K, N)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, wqt = ctx.saved_tensors
+        M, K, N = ctx.dims
+        dy = _c2d(dy)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            d, s = quant_rows(dy)                                   # [3, M, ldN]
+            dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s)             # dY . W_b
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or need_db:
+            dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)      # [3, N, ldM]
+            if ctx.needs_input_grad[1]:
+                if ctx.binarize_input:
+                    dw = gemm_i8(dt, 3, xs, 1, N, K, a_scale=sc)    # dY^T . X_b
+                else:
+                    xt, sxc, _ = quant_cols_t(xs)
+                    dw = gemm_i8(dt, 3, xt, 3, N, K, a_scale=sc, b_scale=sxc)
+            db = cs
+        return dx, dw, db, None, None
+
+
+def binary_linear(x, weight, bias=None, binarize_input=True, backend="mfma"):
+    """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened)."""
+    lead = x.shape[:-1]
+    y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend)
+    return y.reshape(*lead, weight.shape[0])
+
+
+# ----------------------------------------------------------------------------- conv2d
+def _pair_same(v, what):
+    if isinstance(v, (tuple, list)):
+        if len(set(v)) != 1:
+            raise NotImplementedError(f"bnn_amd: asymmetric {what} {v} is not supported")
+        return int(v[0])
+    return int(v)
+
+
+class BinaryConv2dFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, binarize_input, stride, padding, dilation, groups):
+        _check(x, weight, bias)
+        x = _c2d(x)
+        w = _c2d(weight.detach())
+        N, C, H, W = x.shape
+        Co, _, KH, KW = w.shape
+        OH = (H + 2 * padding - dilation * (KH - 1) - 1) // stride + 1
+        OW = (W + 2 * padding - dilation * (KW - 1) - 1) // stride + 1
+        y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
+        b = bias.detach() if bias is not None else None
+        L.call("bnn_conv2d_fwd", L.ptr(x), int(binarize_input), L.ptr(w), L.ptr(b), L.ptr(y),
+               N, C, H, W, Co, KH, KW, stride, padding, dilation, groups, L.stream())
+        ctx.save_for_backward(x, w)
+        ctx.conf = (binarize_input, stride, padding, dilation, groups)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        binarize_input, stride, padding, dilation, groups = ctx.conf
+        dy = _c2d(dy)
+        N, C, H, W = x.shape
+        Co, _, KH, KW = w.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            L.call("bnn_conv2d_bwd_data", L.ptr(dy), L.ptr(w), L.ptr(dx), N, C, H, W, Co, KH, KW,
+                   stride, padding, dilation, groups, L.stream())
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or need_db:
+            dw = torch.empty_like(w)
+            db = torch.empty((Co,), dtype=torch.float32, device=x.device) if need_db else None
+            ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
+                             dtype=torch.uint8, device=x.device)
+            L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
+                   L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
+                   L.stream())
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db, None, None, None, None, None
+
+
+def binary_conv2d(x, weight, bias=None, binarize_input=True, stride=1, padding=0, dilation=1, groups=1):
+    return BinaryConv2dFunction.apply(x, weight, bias, binarize_input, _pair_same(stride, "stride"),
+                                      _pair_same(padding, "padding"), _pair_same(dilation, "dilation"),
+                                      int(groups))
+
+
+# ----------------------------------------------------------------------------- (3) STE helpers
+def hardtanh_backward(x, g):
+    _check(x, g)
+    x, g = _c2d(x), _c2d(g)
+    out = torch.empty_like(g)
+    L.call("bnn_hardtanh_bwd", L.ptr(x), L.ptr(g), L.ptr(out), g.numel(), L.stream())
+    return out
+
+
+def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
+                grad_scale=1.0, clamp=True):
+    """In-place fused Adam (torch formula) + clamp to [-1, 1] on a latent weight."""
+    _check(p, grad, exp_avg, exp_avg_sq)
+    for t in (p, grad, exp_avg, exp_avg_sq):
+        if not t.is_contiguous():
+            raise ValueError("adam_clamp_: tensors must be contiguous")
+    L.call("bnn_adam_clamp", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), p.numel(),
+           float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale),
+           int(bool(clamp)), L.stream())

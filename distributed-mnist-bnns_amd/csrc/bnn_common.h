@@ -1,0 +1,81 @@
+// Shared helpers for libbnn (gfx950 / MI355X only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define BNN_API extern "C" __attribute__((visibility("default")))
+
+namespace bnn {
+
+// Error codes returned by every entry point (include/bnn.h):
+//   0 = ok, BNN_EINVAL (-1) = bad arguments, >0 = hipError_t of the failed launch.
+constexpr int kErrInval = -1;
+
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int check_launch(const char* what);
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// Ternary sign as used by the reference (models/binarized_modules.py:13, Tensor.sign()):
+// +1 for x>0, -1 for x<0, 0 for x==0 (NaN maps to 0 here; the reference would propagate NaN).
+__device__ __forceinline__ int tsign(float x) { return (x > 0.f) - (x < 0.f); }
+
+// Block-uniform wave index (provably uniform for the compiler -> SGPR).
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Digit quantisation shared by quant_rows / quant_cols_t (see DESIGN.md "fp32 operands"):
+// a vector with max|x| = f*2^E (f in [0.5,1)) is scaled by 2^(22-E) to integers |v| <= 2^22 and
+// split into balanced base-256 digits v = d2*2^16 + d1*2^8 + d0, d0,d1 in [-128,127],
+// d2 in [-65,65].  Scale s = 2^(E-22) is a power of two, so x ~= s*v with |err| <= s/2.
+struct Digits { int8_t d0, d1, d2; };
+
+__device__ __forceinline__ Digits to_digits(float x, int shift) {
+  const int v = __float2int_rn(ldexpf(x, shift));
+  const int d0 = ((v + 128) & 255) - 128;
+  const int v1 = (v - d0) >> 8;
+  const int d1 = ((v1 + 128) & 255) - 128;
+  const int d2 = (v1 - d1) >> 8;
+  return Digits{(int8_t)d0, (int8_t)d1, (int8_t)d2};
+}
+
+// From the absolute maximum of a vector: the shift 22-E and the scale 2^(E-22).
+// amax == 0 -> scale 0 (all digits 0); non-finite -> scale NaN (outputs become NaN).
+__device__ __forceinline__ void digit_scale(float amax, int* shift, float* scale) {
+  if (!(amax == amax) || amax == __builtin_inff()) {
+    *shift = 0;
+    *scale = __builtin_nanf("");
+    return;
+  }
+  if (amax == 0.f) {
+    *shift = 0;
+    *scale = 0.f;
+    return;
+  }
+  int e;
+  frexpf(amax, &e);
+  *shift = 22 - e;
+  *scale = ldexpf(1.f, e - 22);
+}
+
+}  // namespace bnn

@@ -1,0 +1,261 @@
+// Subsystem (2)+(3): the int8 MFMA GEMM behind BinarizeLinear (models/binarized_modules.py:80)
+// and both GEMMs of its autograd (dX = dY.W_b, dW = dY^T.X_b).
+//
+//   C[m][n] = cvt( sum_{i,j} 2^(8(i+j)) sum_k A_i[m][k] B_j[n][k] ) * a_scale[m] * b_scale[n] + bias[n]
+//
+// Both operands are K-contiguous int8 ("NT" layout) -- exactly what v_mfma_i32_32x32x32_i8 wants
+// for its A and B fragments.  Ternary x ternary sums are exact int32, so the (1,1) form followed by
+// one fp32 bias add is bit-identical to the reference's F.linear(x_b, W_b) + bias.  fp32 operands
+// arrive as 3 balanced base-256 digit planes with a power-of-two scale per row (bnn_pack.hip);
+// their partial sums are exact int32 and are combined in fp64 in the epilogue (one fp32 rounding).
+//
+// Structure (CDNA4): 256-thread workgroups = 4 waves in 2x2; each wave owns WM x WN 32x32 output
+// tiles; BK = 64 bytes of K per stage; operands staged global->LDS with global_load_lds_dwordx4
+// (16 B per lane, LDS image lane-linear, chunk XOR-swizzle applied on the SOURCE address so the
+// ds_read_b128 fragment reads are bank-conflict free); two LDS buffers; XCD-aware bijective
+// block remap + grouped raster so blocks sharing an A panel run on one XCD's L2.
+#include <algorithm>
+
+#include "bnn_common.h"
+
+namespace bnn {
+namespace {
+
+constexpr int BK = 64;
+
+struct GemmParams {
+  const int8_t* A;
+  const int8_t* B;
+  int64_t lda, ldb, a_plane, b_plane;
+  const float* a_scale;
+  const float* b_scale;
+  const float* bias;
+  float* C;
+  int64_t ldc;
+  int M, N, K;
+  int gm, gn;
+};
+
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// Bijective XCD remap (blocks b and b+8 share an XCD under round-robin dispatch: speed only)
+// followed by a grouped raster (8 tile-rows per group) so an XCD works on neighbouring tiles.
+__device__ __forceinline__ void tile_of(int bid, int gm, int gn, int& tm, int& tn) {
+  const int nwg = gm * gn;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  constexpr int G = 8;
+  const int per_group = G * gn;
+  const int g = L / per_group, first = g * G;
+  const int gs = min(gm - first, G);
+  const int in = L - g * per_group;
+  tm = first + in % gs;
+  tn = in / gs;
+}
+
+template <int DA, int DB>
+struct Cfg {
+  static constexpr int NC = (DA == 1 && DB == 1) ? 1 : 3;  // accumulator classes
+  static constexpr bool FLUSH = (DB == 3);                 // int32 -> f32 flush (digit x digit)
+  static constexpr int FLUSH_KT = 512;                      // k-tiles per flush: 32768 k
+};
+
+template <int DA, int DB, int WM, int WN>
+__global__ __launch_bounds__(256) void gemm_i8_k(GemmParams p) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int A_ST = DA * BM * BK, B_ST = DB * BN * BK, ST = A_ST + B_ST;
+  constexpr int NC = Cfg<DA, DB>::NC;
+  constexpr bool FLUSH = Cfg<DA, DB>::FLUSH;
+  __shared__ __attribute__((aligned(16))) char smem[2 * ST];
+
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  tile_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- global -> LDS staging: one glds = 1 KiB = 16 rows x 64 B; lane i -> row i/4, slot i%4,
+  // source chunk slot ^ ((row>>2)&3) (the swizzle lives on the source address: rule 21).
+  const int srow = lane >> 2, sslot = lane & 3;
+  const int schunk = sslot ^ ((srow >> 2) & 3);
+  auto stage = [&](int kt, int buf) {
+    char* sA = smem + buf * ST;
+    char* sB = sA + A_ST;
+    const int k0 = kt * BK + 16 * schunk;
+#pragma unroll
+    for (int j = wave; j < DA * BM / 16; j += 4) {
+      const int d = j / (BM / 16), jr = j % (BM / 16);
+      const int row = min(m0 + jr * 16 + srow, p.M - 1);
+      glds16(p.A + d * p.a_plane + (int64_t)row * p.lda + k0, sA + d * BM * BK + jr * 1024);
+    }
+#pragma unroll
+    for (int j = wave; j < DB * BN / 16; j += 4) {
+      const int e = j / (BN / 16), jr = j % (BN / 16);
+      const int row = min(n0 + jr * 16 + srow, p.N - 1);
+      glds16(p.B + e * p.b_plane + (int64_t)row * p.ldb + k0, sB + e * BN * BK + jr * 1024);
+    }
+  };
+
+  v16i acc[NC][WM][WN];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < WM; ++t)
+#pragma unroll
+      for (int u = 0; u < WN; ++u) acc[c][t][u] = v16i{0};
+  float facc[FLUSH ? WM : 1][FLUSH ? WN : 1][16];
+  if constexpr (FLUSH) {
+#pragma unroll
+    for (int t = 0; t < WM; ++t)
+#pragma unroll
+      for (int u = 0; u < WN; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) facc[t][u][i] = 0.f;
+  }
+
+  const int r = lane & 31, h = lane >> 5, sw = (r >> 2) & 3;
+  const int nk = p.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const char* sA = smem + buf * ST;
+    const char* sB = sA + A_ST;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int off = 16 * ((2 * ks + h) ^ sw);
+      v4i a[DA][WM], b[DB][WN];
+#pragma unroll
+      for (int d = 0; d < DA; ++d)
+#pragma unroll
+        for (int t = 0; t < WM; ++t)
+          a[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BK + (wm * WM * 32 + t * 32 + r) * BK + off);
+#pragma unroll
+      for (int e = 0; e < DB; ++e)
+#pragma unroll
+        for (int u = 0; u < WN; ++u)
+          b[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BK + (wn * WN * 32 + u * 32 + r) * BK + off);
+#pragma unroll
+      for (int t = 0; t < WM; ++t)
+#pragma unroll
+        for (int u = 0; u < WN; ++u) {
+          if constexpr (DA == 1 && DB == 1) {
+            acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0][t], b[0][u], acc[0][t][u], 0, 0, 0);
+          } else if constexpr (DB == 1) {
+#pragma unroll
+            for (int d = 0; d < DA; ++d)
+              acc[d][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[d][t], b[0][u], acc[d][t][u], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int i = 0; i < DA; ++i)
+#pragma unroll
+              for (int j = 0; j < DB; ++j)
+                if (i + j >= 2)
+                  acc[i + j - 2][t][u] =
+                      __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i][t], b[j][u], acc[i + j - 2][t][u], 0, 0, 0);
+          }
+        }
+    }
+    if constexpr (FLUSH) {
+      if ((kt + 1) % Cfg<DA, DB>::FLUSH_KT == 0 || kt + 1 == nk) {
+#pragma unroll
+        for (int t = 0; t < WM; ++t)
+#pragma unroll
+          for (int u = 0; u < WN; ++u) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              facc[t][u][i] += (float)((double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 +
+                                       (double)acc[0][t][u][i]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c][t][u] = v16i{0};
+          }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: C/D map of the 32x32 MFMA: reg i -> row (i&3)+8(i>>2)+4h, col = lane&31.
+#pragma unroll
+  for (int t = 0; t < WM; ++t)
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int col = n0 + wn * WN * 32 + u * 32 + r;
+      if (col >= p.N) continue;
+      const float bs = p.b_scale ? p.b_scale[col] : 1.f;
+      const float bb = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WM * 32 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        double v;
+        if constexpr (DA == 1 && DB == 1) {
+          v = (double)acc[0][t][u][i];
+        } else if constexpr (DB == 1) {
+          v = (double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 + (double)acc[0][t][u][i];
+        } else {
+          v = (double)facc[t][u][i] * 65536.0;
+        }
+        if (p.a_scale) v *= (double)p.a_scale[row];
+        v *= (double)bs;
+        float f = (float)v;
+        if (p.bias) f += bb;
+        p.C[(int64_t)row * p.ldc + col] = f;
+      }
+    }
+}
+
+template <int DA, int DB, int WM, int WN>
+int launch(GemmParams p, hipStream_t s) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  p.gm = (p.M + BM - 1) / BM;
+  p.gn = (p.N + BN - 1) / BN;
+  const int64_t nblk = (int64_t)p.gm * p.gn;
+  if (nblk > 0x7fffffff) {
+    set_error("bnn_gemm_i8: too many tiles");
+    return kErrInval;
+  }
+  hipLaunchKernelGGL((gemm_i8_k<DA, DB, WM, WN>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+  return check_launch("bnn_gemm_i8");
+}
+
+}  // namespace
+}  // namespace bnn
+
+using namespace bnn;
+
+BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
+                        const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
+                        const float* a_scale, const float* b_scale, const float* bias, float* C,
+                        int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+  const bool cfg_ok = (a_digits == 1 && b_digits == 1) || (a_digits == 3 && b_digits == 1) ||
+                      (a_digits == 3 && b_digits == 3);
+  if (!A || !B || !C || !cfg_ok || M < 0 || N < 0 || K < 0 || K % BK != 0 || lda < K || ldb < K ||
+      lda % 16 != 0 || ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) ||
+      M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff ||
+      (a_digits > 1 && (a_plane < M * lda || a_plane % 16 != 0)) ||
+      (b_digits > 1 && (b_plane < N * ldb || b_plane % 16 != 0))) {
+    set_error("bnn_gemm_i8: bad arguments (M=%lld N=%lld K=%lld lda=%lld ldb=%lld digits=%d,%d)",
+              (long long)M, (long long)N, (long long)K, (long long)lda, (long long)ldb, a_digits,
+              b_digits);
+    return kErrInval;
+  }
+  if (M == 0 || N == 0) return 0;
+  GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
+               (int)M, (int)N, (int)K, 0, 0};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (K == 0) {
+    // Empty reduction: C = bias (or 0).  Reuse the kernel with one zero k-tile is not possible
+    // without operand memory, so handle it here.
+    set_error("bnn_gemm_i8: K == 0 is not supported (pad K to 64 with zeros)");
+    return kErrInval;
+  }
+  if (a_digits == 1) return launch<1, 1, 2, 2>(p, s);
+  if (b_digits == 1) return launch<3, 1, 2, 2>(p, s);
+  return launch<3, 3, 2, 1>(p, s);
+}

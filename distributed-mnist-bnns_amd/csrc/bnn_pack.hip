@@ -1,0 +1,394 @@
+// Subsystem (1): sign-and-pack, plus the fp32 -> digit quantisers that feed fp32 operands
+// (fc1 input, backward dY) to the same int8 MFMA GEMM.  All kernels are HBM-bound streams:
+// coalesced 16-B loads, LDS-tiled transposes, no atomics, deterministic.
+//
+// Reference behaviour restated: Binarize(t,'det') = t.sign() (models/binarized_modules.py:11-13)
+// applied to inputs (:76, :95) and to the latent weight (:79, :98); sign(0) = 0 -> ternary.
+#include <algorithm>
+
+#include "bnn_common.h"
+
+namespace bnn {
+namespace {
+
+constexpr int TILE = 64;
+
+// max|v| accumulation that turns NaN into +inf (fmaxf alone would drop NaN) so a non-finite
+// row/column gets a NaN scale and propagates NaN like the reference's fp32 GEMM would.
+__device__ __forceinline__ float absmax_acc(float amax, float v) {
+  const float a = fabsf(v);
+  return (a == a) ? fmaxf(amax, a) : __builtin_inff();
+}
+
+__device__ __forceinline__ void load16(const float* __restrict__ row, int64_t k, int64_t K, bool vec,
+                                       float (&v)[16]) {
+  if (vec && k + 16 <= K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 f = *reinterpret_cast<const float4*>(row + k + 4 * i);
+      v[4 * i + 0] = f.x;
+      v[4 * i + 1] = f.y;
+      v[4 * i + 2] = f.z;
+      v[4 * i + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = (k + j < K) ? row[k + j] : 0.f;
+  }
+}
+
+__device__ __forceinline__ int pack4(int a, int b, int c, int d) {
+  return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16) | ((d & 255) << 24);
+}
+
+// One 64x64 tile of x -> ternary int8 rows (q) and/or the transposed tile (qt).
+__global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
+                                                        int64_t K, int64_t ldx, int8_t* __restrict__ q,
+                                                        int64_t ldq, int8_t* __restrict__ qt,
+                                                        int64_t ldqt, int vec) {
+  __shared__ int tile[TILE][TILE + 1];
+  const int64_t m0 = (int64_t)blockIdx.y * TILE, k0 = (int64_t)blockIdx.x * TILE;
+  const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
+  const int64_t m = m0 + r;
+  float v[16];
+  if (m < M) {
+    load16(x + m * ldx, k0 + c, K, vec, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+  }
+  int s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = tsign(v[j]);
+  if (q != nullptr && m < M && k0 + c < ldq) {
+    v4i w;
+    w.x = pack4(s[0], s[1], s[2], s[3]);
+    w.y = pack4(s[4], s[5], s[6], s[7]);
+    w.z = pack4(s[8], s[9], s[10], s[11]);
+    w.w = pack4(s[12], s[13], s[14], s[15]);
+    *reinterpret_cast<v4i*>(q + m * ldq + k0 + c) = w;
+  }
+  if (qt != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) tile[r][c + j] = s[j];
+    __syncthreads();
+    const int kk = t >> 2, mc = (t & 3) * 16;
+    const int64_t k = k0 + kk;
+    if (k < K && m0 + mc < ldqt) {
+      int g[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][kk];
+      v4i w;
+      w.x = pack4(g[0], g[1], g[2], g[3]);
+      w.y = pack4(g[4], g[5], g[6], g[7]);
+      w.z = pack4(g[8], g[9], g[10], g[11]);
+      w.w = pack4(g[12], g[13], g[14], g[15]);
+      *reinterpret_cast<v4i*>(qt + k * ldqt + m0 + mc) = w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sign_f32_k(const float* __restrict__ x, float* __restrict__ y,
+                                                  int64_t n, int vec) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    for (int64_t j = i; j < n4; j += stride) {
+      float4 f = reinterpret_cast<const float4*>(x)[j];
+      f.x = (float)tsign(f.x);
+      f.y = (float)tsign(f.y);
+      f.z = (float)tsign(f.z);
+      f.w = (float)tsign(f.w);
+      reinterpret_cast<float4*>(y)[j] = f;
+    }
+    for (int64_t j = n4 * 4 + i; j < n; j += stride) y[j] = (float)tsign(x[j]);
+  } else {
+    for (int64_t j = i; j < n; j += stride) y[j] = (float)tsign(x[j]);
+  }
+}
+
+// One wave per (row, 64-wide k chunk): ballots give the sign and nonzero bit-planes.
+__global__ __launch_bounds__(256) void sign_pack_bits_k(const float* __restrict__ x, int64_t M,
+                                                        int64_t K, int64_t ldx,
+                                                        uint32_t* __restrict__ sb,
+                                                        uint32_t* __restrict__ nb, int64_t ldw) {
+  const int lane = threadIdx.x & 63;
+  const int64_t chunks = (ldw + 1) / 2;
+  const int64_t total = M * chunks;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv < total; wv += nwaves) {
+    const int64_t m = wv / chunks, ch = wv % chunks;
+    const int64_t k = ch * 64 + lane;
+    const float v = (k < K) ? x[m * ldx + k] : 0.f;
+    const unsigned long long s = __ballot(v < 0.f);
+    const unsigned long long z = __ballot(v != 0.f);
+    const int64_t w = ch * 2 + (lane & 1);
+    if (lane < 2 && w < ldw) {
+      sb[m * ldw + w] = (uint32_t)(lane ? (s >> 32) : s);
+      nb[m * ldw + w] = (uint32_t)(lane ? (z >> 32) : z);
+    }
+  }
+}
+
+// Row-scaled digits: one block per row (grid-stride over rows).
+__global__ __launch_bounds__(256) void quant_rows_k(const float* __restrict__ x, int64_t M, int64_t K,
+                                                    int64_t ldx, int8_t* __restrict__ dg,
+                                                    int64_t ldq, int64_t plane,
+                                                    float* __restrict__ scale, int vec) {
+  __shared__ float red[4];
+  const int t = threadIdx.x;
+  for (int64_t m = blockIdx.x; m < M; m += gridDim.x) {
+    const float* __restrict__ xr = x + m * ldx;
+    float amax = 0.f;
+    for (int64_t k = 4 * t; k < K; k += 1024) {
+      if (vec && k + 4 <= K) {
+        const float4 f = *reinterpret_cast<const float4*>(xr + k);
+        amax = absmax_acc(absmax_acc(absmax_acc(absmax_acc(amax, f.x), f.y), f.z), f.w);
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (k + j < K) amax = absmax_acc(amax, xr[k + j]);
+      }
+    }
+    amax = wave_max(amax);
+    if ((t & 63) == 0) red[t >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    int shift;
+    float s;
+    digit_scale(amax, &shift, &s);
+    if (t == 0) scale[m] = s;
+    for (int64_t k = 4 * t; k < ldq; k += 1024) {
+      float v[4];
+      if (vec && k + 4 <= K) {
+        const float4 f = *reinterpret_cast<const float4*>(xr + k);
+        v[0] = f.x;
+        v[1] = f.y;
+        v[2] = f.z;
+        v[3] = f.w;
+      } else {
+        for (int j = 0; j < 4; ++j) v[j] = (k + j < K) ? xr[k + j] : 0.f;
+      }
+      Digits d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = to_digits(v[j], shift);
+      int8_t* o = dg + m * ldq + k;
+      *reinterpret_cast<int*>(o) = pack4(d[0].d0, d[1].d0, d[2].d0, d[3].d0);
+      *reinterpret_cast<int*>(o + plane) = pack4(d[0].d1, d[1].d1, d[2].d1, d[3].d1);
+      *reinterpret_cast<int*>(o + 2 * plane) = pack4(d[0].d2, d[1].d2, d[2].d2, d[3].d2);
+    }
+  }
+}
+
+constexpr int COL_ROWS = 256;  // rows per column-statistics chunk
+
+// Pass 1: per (row chunk, column) absolute max and double sum.
+__global__ __launch_bounds__(256) void colstats_k(const float* __restrict__ x, int64_t M, int64_t N,
+                                                  int64_t ldx, float* __restrict__ pmax,
+                                                  double* __restrict__ psum) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * COL_ROWS;
+  if (n >= N) return;
+  const int64_t r1 = (M < r0 + COL_ROWS) ? M : r0 + COL_ROWS;
+  float amax = 0.f;
+  double sum = 0.0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float v = x[r * ldx + n];
+    amax = absmax_acc(amax, v);
+    sum += (double)v;
+  }
+  pmax[blockIdx.y * N + n] = amax;
+  psum[blockIdx.y * N + n] = sum;
+}
+
+// Pass 2: reduce the chunks in a fixed order -> scale[n], colsum[n].
+__global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax,
+                                                  const double* __restrict__ psum, int64_t N,
+                                                  int64_t R, float* __restrict__ scale,
+                                                  float* __restrict__ colsum) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float amax = 0.f;
+  double sum = 0.0;
+  for (int64_t r = 0; r < R; ++r) {
+    amax = fmaxf(amax, pmax[r * N + n]);
+    sum += psum[r * N + n];
+  }
+  int shift;
+  float s;
+  digit_scale(amax, &shift, &s);
+  scale[n] = s;
+  if (colsum != nullptr) colsum[n] = (float)sum;
+}
+
+// Pass 3: quantise with the column scale and write the transposed digit planes.
+__global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ x, int64_t M,
+                                                      int64_t N, int64_t ldx,
+                                                      const float* __restrict__ scale,
+                                                      int8_t* __restrict__ dt, int64_t ldqt,
+                                                      int64_t plane, int vec) {
+  __shared__ int tile[TILE][TILE + 1];
+  __shared__ int sh[TILE];
+  const int64_t n0 = (int64_t)blockIdx.x * TILE, m0 = (int64_t)blockIdx.y * TILE;
+  const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
+  if (t < TILE) {
+    const int64_t n = n0 + t;
+    const float s = (n < N) ? scale[n] : 0.f;
+    sh[t] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;  // INT32_MIN -> digits 0
+  }
+  __syncthreads();
+  const int64_t m = m0 + r;
+  float v[16];
+  if (m < M) {
+    load16(x + m * ldx, n0 + c, N, vec, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int sft = sh[c + j];
+    int packed = 0;
+    if (sft != INT32_MIN) {
+      const Digits d = to_digits(v[j], sft);
+      packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
+    }
+    tile[r][c + j] = packed;
+  }
+  __syncthreads();
+  const int nn = t >> 2, mc = (t & 3) * 16;
+  const int64_t n = n0 + nn;
+  if (n < N && m0 + mc < ldqt) {
+    int g[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][nn];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int sh8 = 8 * d;
+      v4i w;
+      w.x = pack4(g[0] >> sh8, g[1] >> sh8, g[2] >> sh8, g[3] >> sh8);
+      w.y = pack4(g[4] >> sh8, g[5] >> sh8, g[6] >> sh8, g[7] >> sh8);
+      w.z = pack4(g[8] >> sh8, g[9] >> sh8, g[10] >> sh8, g[11] >> sh8);
+      w.w = pack4(g[12] >> sh8, g[13] >> sh8, g[14] >> sh8, g[15] >> sh8);
+      *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc) = w;
+    }
+  }
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int grid_cap(int64_t want) { return (int)std::max<int64_t>(1, std::min<int64_t>(want, 8192)); }
+
+}  // namespace
+}  // namespace bnn
+
+using namespace bnn;
+
+BNN_API int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* q,
+                             int64_t ldq, int8_t* qt, int64_t ldqt, void* stream) {
+  if (!x || M < 0 || K < 0 || ldx < K || (!q && !qt)) {
+    set_error("bnn_sign_pack_i8: bad arguments (M=%lld K=%lld ldx=%lld)", (long long)M,
+              (long long)K, (long long)ldx);
+    return kErrInval;
+  }
+  if (q && (ldq % TILE != 0 || ldq < round_up(K, TILE) || !aligned16(q))) {
+    set_error("bnn_sign_pack_i8: ldq=%lld must be a multiple of 64 >= round_up(K,64), q 16-B aligned",
+              (long long)ldq);
+    return kErrInval;
+  }
+  if (qt && (ldqt % TILE != 0 || ldqt < round_up(M, TILE) || !aligned16(qt))) {
+    set_error("bnn_sign_pack_i8: ldqt=%lld must be a multiple of 64 >= round_up(M,64)", (long long)ldqt);
+    return kErrInval;
+  }
+  if (M == 0 && !qt) return 0;
+  const int vec = aligned16(x) && (ldx % 4 == 0);
+  const int64_t gx = q ? ldq / TILE : (K + TILE - 1) / TILE;
+  const int64_t gy = qt ? ldqt / TILE : (M + TILE - 1) / TILE;
+  if (gx == 0 || gy == 0) return 0;
+  if (gy > 65535) {
+    set_error("bnn_sign_pack_i8: M too large for one launch (%lld)", (long long)M);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL(sign_pack_tile_k, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x,
+                     M, K, ldx, q, ldq, qt, ldqt, vec);
+  return check_launch("bnn_sign_pack_i8");
+}
+
+BNN_API int bnn_sign_f32(const float* x, float* y, int64_t n, void* stream) {
+  if (!x || !y || n < 0) {
+    set_error("bnn_sign_f32: bad arguments");
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  const int vec = aligned16(x) && aligned16(y);
+  hipLaunchKernelGGL(sign_f32_k, dim3(grid_cap((n / 4 + 255) / 256)), dim3(256), 0, S(stream), x, y,
+                     n, vec);
+  return check_launch("bnn_sign_f32");
+}
+
+BNN_API int bnn_sign_pack_bits(const float* x, int64_t M, int64_t K, int64_t ldx, uint32_t* sbits,
+                               uint32_t* nzbits, int64_t ldw, void* stream) {
+  if (!x || !sbits || !nzbits || M < 0 || K < 0 || ldx < K || ldw < (K + 31) / 32) {
+    set_error("bnn_sign_pack_bits: bad arguments");
+    return kErrInval;
+  }
+  if (M == 0 || ldw == 0) return 0;
+  const int64_t waves = M * ((ldw + 1) / 2);
+  hipLaunchKernelGGL(sign_pack_bits_k, dim3(grid_cap((waves + 3) / 4)), dim3(256), 0, S(stream), x,
+                     M, K, ldx, sbits, nzbits, ldw);
+  return check_launch("bnn_sign_pack_bits");
+}
+
+BNN_API int bnn_quant_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* digits,
+                           int64_t ldq, int64_t plane, float* scale, void* stream) {
+  if (!x || !digits || !scale || M < 0 || K < 0 || ldx < K || ldq % TILE != 0 ||
+      ldq < round_up(K, TILE) || plane < M * ldq || (plane % 16) != 0 || !aligned16(digits)) {
+    set_error("bnn_quant_rows: bad arguments (M=%lld K=%lld ldq=%lld plane=%lld)", (long long)M,
+              (long long)K, (long long)ldq, (long long)plane);
+    return kErrInval;
+  }
+  if (M == 0) return 0;
+  const int vec = aligned16(x) && (ldx % 4 == 0);
+  hipLaunchKernelGGL(quant_rows_k, dim3((unsigned)std::min<int64_t>(M, 65536)), dim3(256), 0,
+                     S(stream), x, M, K, ldx, digits, ldq, plane, scale, vec);
+  return check_launch("bnn_quant_rows");
+}
+
+BNN_API int64_t bnn_quant_cols_workspace(int64_t M, int64_t N) {
+  const int64_t R = std::max<int64_t>(1, (M + COL_ROWS - 1) / COL_ROWS);
+  return round_up(R * N * (int64_t)sizeof(float), 256) + R * N * (int64_t)sizeof(double);
+}
+
+BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
+                             int64_t ldqt, int64_t plane, float* scale, float* colsum, void* work,
+                             void* stream) {
+  if (!x || !digits_t || !scale || !work || M < 0 || N < 0 || ldx < N || ldqt % TILE != 0 ||
+      ldqt < round_up(M, TILE) || plane < N * ldqt || (plane % 16) != 0 || !aligned16(digits_t)) {
+    set_error("bnn_quant_cols_t: bad arguments (M=%lld N=%lld ldqt=%lld plane=%lld)", (long long)M,
+              (long long)N, (long long)ldqt, (long long)plane);
+    return kErrInval;
+  }
+  if (N == 0) return 0;
+  const int64_t R = std::max<int64_t>(1, (M + COL_ROWS - 1) / COL_ROWS);
+  if (R > 65535 || ldqt / TILE > 65535) {
+    set_error("bnn_quant_cols_t: M too large for one launch (%lld)", (long long)M);
+    return kErrInval;
+  }
+  float* pmax = reinterpret_cast<float*>(work);
+  double* psum = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                           round_up(R * N * (int64_t)sizeof(float), 256));
+  const unsigned gn = (unsigned)((N + 255) / 256);
+  if (M > 0) {
+    hipLaunchKernelGGL(colstats_k, dim3(gn, (unsigned)R), dim3(256), 0, S(stream), x, M, N, ldx, pmax,
+                       psum);
+  } else {
+    (void)hipMemsetAsync(pmax, 0, R * N * sizeof(float), S(stream));
+    (void)hipMemsetAsync(psum, 0, R * N * sizeof(double), S(stream));
+  }
+  hipLaunchKernelGGL(colfinal_k, dim3(gn), dim3(256), 0, S(stream), pmax, psum, N, R, scale, colsum);
+  const int vec = aligned16(x) && (ldx % 4 == 0);
+  hipLaunchKernelGGL(quant_cols_t_k, dim3((unsigned)((N + TILE - 1) / TILE), (unsigned)(ldqt / TILE)),
+                     dim3(256), 0, S(stream), x, M, N, ldx, scale, digits_t, ldqt, plane, vec);
+  return check_launch("bnn_quant_cols_t");
+}

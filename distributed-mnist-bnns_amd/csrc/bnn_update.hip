@@ -1,0 +1,96 @@
+// Subsystem (3) helpers: Hardtanh STE mask and the fused latent-weight update.
+//
+// The reference's caller protocol (mnist-dist2.py:131-137) is
+//     p.data.copy_(p.org); optimizer.step(); p.org.copy_(p.data.clamp_(-1,1))
+// around torch.optim.Adam (mnist-dist2.py:91).  bnn_adam_clamp applies Adam to the latent
+// weight and clamps it in one HBM pass (7 fp32 streams: p, g, m, v read; p, m, v written).
+#include <algorithm>
+#include <cmath>
+
+#include "bnn_common.h"
+
+namespace bnn {
+namespace {
+
+__global__ __launch_bounds__(256) void hardtanh_bwd_k(const float* __restrict__ x,
+                                                      const float* __restrict__ g,
+                                                      float* __restrict__ out, int64_t n, int vec) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  auto f = [](float xv, float gv) { return (xv > -1.f && xv < 1.f) ? gv : 0.f; };
+  int64_t tail = 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = i0; i < n4; i += stride) {
+      const float4 xv = reinterpret_cast<const float4*>(x)[i];
+      const float4 gv = reinterpret_cast<const float4*>(g)[i];
+      reinterpret_cast<float4*>(out)[i] =
+          make_float4(f(xv.x, gv.x), f(xv.y, gv.y), f(xv.z, gv.z), f(xv.w, gv.w));
+    }
+    tail = n4 * 4;
+  }
+  for (int64_t i = tail + i0; i < n; i += stride) out[i] = f(x[i], g[i]);
+}
+
+// torch.optim.Adam single-tensor math in fp32 (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_,
+// denom = sqrt(v)/sqrt(bc2) + eps, p.addcdiv_(m, denom, -lr/bc1)), then clamp.
+__global__ __launch_bounds__(256) void adam_clamp_k(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    int64_t n, float b1, float b2, float eps,
+                                                    float step_size, float bc2_sqrt, float gscale,
+                                                    int clamp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * gscale;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i] * b2;
+    vi = fmaf((1.f - b2) * gi, gi, vi);
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    float pi = p[i] - step_size * (mi / denom);
+    if (clamp) pi = fminf(fmaxf(pi, -1.f), 1.f);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+inline int grid_for(int64_t n) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+}
+
+}  // namespace
+}  // namespace bnn
+
+using namespace bnn;
+
+BNN_API int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, void* stream) {
+  if (!x || !g || !out || n < 0) {
+    set_error("bnn_hardtanh_bwd: bad arguments");
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  const int vec = aligned16(x) && aligned16(g) && aligned16(out);
+  hipLaunchKernelGGL(hardtanh_bwd_k, dim3(grid_for(n / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, g, out, n, vec);
+  return check_launch("bnn_hardtanh_bwd");
+}
+
+BNN_API int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           float lr, float beta1, float beta2, float eps, int64_t step,
+                           float grad_scale, int32_t clamp, void* stream) {
+  if (!p || !grad || !exp_avg || !exp_avg_sq || n < 0 || step < 1) {
+    set_error("bnn_adam_clamp: bad arguments");
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  // torch computes the bias corrections as Python floats (double) from the step count.
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), p, grad, exp_avg, exp_avg_sq, n, beta1,
+                     beta2, eps, step_size, bc2_sqrt, grad_scale, clamp);
+  return check_launch("bnn_adam_clamp");
+}

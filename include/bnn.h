@@ -1,0 +1,134 @@
+/* libbnn -- MI355X (gfx950) binarized-network training hot path, C ABI.
+ *
+ * Drop-in boundary: the reference exposes no FFI; its operator API is the Python module
+ * models/binarized_modules.py (Binarize :11-15, BinarizeLinear :68-85, BinarizeConv2d :87-107)
+ * plus the DDP gradient exchange the trainers wrap around it (mnist-dist2.py:93, fires inside
+ * loss.backward() at :130).  Each entry point below replaces the torch/ATen work that interface
+ * triggers; the "replaces" line names the reference call site.  The Python mirror of the
+ * operator API (distributed-mnist-bnns_amd/models/binarized_modules.py) binds these through
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every pointer is a device pointer (hipMalloc / torch caching allocator) unless noted.
+ *  - All sizes are element counts (int64).  Row-major; "ld" = row stride in elements.
+ *  - `stream` is a hipStream_t (NULL = legacy default stream).  Calls are asynchronous,
+ *    allocate nothing, never synchronise, and are safe to capture into a hipGraph.
+ *  - Return value: 0 = ok; BNN_EINVAL (-1) = invalid argument (nothing launched);
+ *    >0 = hipError_t of a failed launch.  bnn_last_error() describes the last failure
+ *    (thread-local).
+ *  - Ternary operands: int8 {-1,0,+1} = Tensor.sign() of fp32 (sign(0) = 0).
+ *  - Digit operands (fp32 values entering a GEMM): D planes of int8 balanced base-256 digits
+ *    plus one power-of-two scale per row; see DESIGN.md "fp32 operands on the int8 MFMA".
+ */
+#ifndef BNN_H_
+#define BNN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BNN_EINVAL (-1)
+
+typedef void* bnn_stream_t; /* hipStream_t */
+
+/* ---------------------------------------------------------------- library */
+int bnn_version(void);
+const char* bnn_last_error(void);
+
+/* ---------------------------------------------------------------- (1) sign-and-pack
+ * replaces: Binarize(tensor) = tensor.sign()   models/binarized_modules.py:11-13,
+ *           as called on inputs (:76, :95) and latent weights (:79, :98).
+ *
+ * x fp32 [M][K] (row stride ldx) ->
+ *   q   int8 [M][ldq]    ternary, columns K..ldq-1 zero-filled          (nullable)
+ *   qt  int8 [K][ldqt]   ternary transpose, columns M..ldqt-1 zero-filled (nullable)
+ * ldq >= round_up(K,64) and ldqt >= round_up(M,64), both multiples of 64; q, qt 16-B aligned. */
+int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* q, int64_t ldq,
+                     int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+
+/* y[i] = sign(x[i]) as fp32 (the caller-visible `input.data = Binarize(input.data)` of :76/:95;
+ * y may alias x). */
+int bnn_sign_f32(const float* x, float* y, int64_t n, bnn_stream_t stream);
+
+/* Bit-planes for the XNOR-popcount path: word w of row m holds k = 32w..32w+31 (bit k%32);
+ * sbits = 1 where x<0, nzbits = 1 where x!=0.  ldw >= ceil(K/32) words, padding words zeroed. */
+int bnn_sign_pack_bits(const float* x, int64_t M, int64_t K, int64_t ldx, uint32_t* sbits,
+                       uint32_t* nzbits, int64_t ldw, bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- fp32 -> digit operands
+ * Row-scaled digits: for each row m of x [M][K], scale[m] = 2^(E-22) with max|x[m,:]| in
+ * [2^(E-1), 2^E), digits[d][m][k] (d = 0,1,2; plane stride `plane`) with
+ * x ~= scale*(d2*65536 + d1*256 + d0).  Columns K..ldq-1 zero-filled.
+ * replaces: the fp32 operand of F.linear / autograd (x of fc1 :80, dY of every backward). */
+int bnn_quant_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* digits, int64_t ldq,
+                   int64_t plane, float* scale, bnn_stream_t stream);
+
+/* Column-scaled, transposed digits: for each column n of x [M][N], scale[n] from max|x[:,n]|,
+ * digits_t[d][n][m] (plane stride `plane`, row stride ldqt >= round_up(M,64), padding zeroed).
+ * colsum (nullable) receives sum_m x[m,n] (double accumulation, fixed order): the bias
+ * gradient dB = sum_B dY of BinarizeLinear (:81-83).  `work` is scratch of
+ * bnn_quant_cols_workspace(M,N) bytes. */
+int64_t bnn_quant_cols_workspace(int64_t M, int64_t N);
+int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
+                     int64_t ldqt, int64_t plane, float* scale, float* colsum, void* work,
+                     bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- (2) forward GEMM, int8 MFMA
+ * C[m][n] = cvt( sum_{i,j} 2^(8(i+j)) * sum_k A_i[m][k]*B_j[n][k] ) * a_scale[m] * b_scale[n]
+ *           + bias[n]
+ * A: a_digits planes (1 or 3) of int8 [M][lda] (plane stride a_plane), B: b_digits planes
+ * (1 or 3) of int8 [N][ldb].  (a_digits,b_digits) in {(1,1),(3,1),(3,3)}.  K (the padded
+ * reduction length) must be a multiple of 64 and <= lda, ldb; lda, ldb multiples of 16;
+ * A, B 16-B aligned; a_scale/b_scale/bias nullable.  Integer sums are exact; the
+ * (1,1) form with bias is bit-exact against F.linear(x_b, W_b) + bias (:80-83).
+ * replaces: F.linear in BinarizeLinear.forward (:80) and the two GEMMs of its autograd
+ * (dX = dY.W_b, dW = dY^T.X_b). */
+int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
+                const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
+                const float* a_scale, const float* b_scale, const float* bias, float* C,
+                int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
+
+/* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
+ * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row
+ * (multiple of 32, <= lda/ldb in words). */
+int bnn_gemm_xnor(const uint32_t* As, const uint32_t* Anz, int64_t lda, const uint32_t* Bs,
+                  const uint32_t* Bnz, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                  int64_t M, int64_t N, int64_t kw, bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- binary conv2d (NCHW fp32)
+ * replaces: F.conv2d(input, W_b, None, stride, padding, dilation, groups) + bias (:100-105)
+ * and its autograd.  binarize_input != 0 -> sign(x) is used (the :94 rule is applied by the
+ * caller).  w_latent [Co][Ci/groups][KH][KW] is binarised on the fly (sign). */
+int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* w_latent,
+                   const float* bias, float* y, int64_t N, int64_t C, int64_t H, int64_t W,
+                   int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
+                   int32_t dil, int32_t groups, bnn_stream_t stream);
+int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* dx, int64_t N, int64_t C,
+                        int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride,
+                        int32_t pad, int32_t dil, int32_t groups, bnn_stream_t stream);
+/* dw = sum dy (x) x_used (x_used = sign(x) when binarize_input); db (nullable) = sum dy.
+ * `work` scratch of bnn_conv2d_bwd_filter_workspace(...) bytes. */
+int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co, int64_t KH, int64_t KW,
+                                        int32_t groups);
+int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_input, float* dw,
+                          float* db, void* work, int64_t N, int64_t C, int64_t H, int64_t W,
+                          int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
+                          int32_t dil, int32_t groups, bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- (3) STE backward helpers
+ * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */
+int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_stream_t stream);
+
+/* Fused latent update (replaces mnist-dist2.py:131-137 around torch.optim.Adam, :91):
+ * p <- Adam(p, grad*grad_scale) with torch's bias-corrected formula, then, if clamp != 0,
+ * p <- clamp(p, -1, 1).  step = 1-based Adam step count after this update. */
+int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,
+                   int32_t clamp, bnn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BNN_H_ */

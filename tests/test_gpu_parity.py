@@ -1,0 +1,223 @@
+"""GPU parity: libbnn (through its C ABI) against the oracle and the reference's golden outputs.
+
+Bars (written here, per BASELINE.json north_star):
+* binarised forward (ternary x ternary + bias): bit-exact (np.array_equal);
+* fp32-input forward (fc1 / RGB conv): norm-wise relative error <= 1e-6 vs float64;
+* gradients: norm-wise relative error <= 1e-5 vs the float64 oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import close, load_golden, rel_err
+from oracle import bnn_np as O
+
+pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 1e-5
+FP_FWD_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def F():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import functional
+    return functional
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def run_linear(F, x, w, b, dy, binarize, backend="mfma"):
+    xt = dev(x).requires_grad_(True)
+    wt = dev(w).requires_grad_(True)
+    bt = dev(b).requires_grad_(True) if b is not None else None
+    y = F.binary_linear(xt, wt, bt, binarize_input=binarize, backend=backend)
+    y.backward(dev(dy))
+    return (host(y), host(xt.grad), host(wt.grad), host(bt.grad) if bt is not None else None)
+
+
+@pytest.mark.parametrize("name", ["linear_first", "linear_hidden", "linear_nobias_zw"])
+def test_linear_matches_reference_golden(F, name):
+    g = load_golden(name)
+    binarize = not O.first_layer(g["x"])
+    b = g["bias"] if g["has_bias"] else None
+    y, dx, dw, db = run_linear(F, g["x"], g["w_latent"], b, g["dy"], binarize)
+    if binarize:
+        assert np.array_equal(y, g["y"])
+    else:
+        y64 = g["x"].astype(np.float64) @ np.sign(g["w_latent"]).astype(np.float64).T + (b if b is not None else 0)
+        assert rel_err(y, y64) < FP_FWD_TOL
+        assert rel_err(y, g["y"]) < FP_FWD_TOL
+    _, w64, _ = O.linear_backward(g["x_after"], g["w_latent"], g["dy"], need_dx=False)
+    dx64 = g["dy"].astype(np.float64) @ np.sign(g["w_latent"]).astype(np.float64)
+    dw64 = g["dy"].astype(np.float64).T @ g["x_after"].astype(np.float64)
+    assert rel_err(dx, dx64) < GRAD_TOL and rel_err(dx, g["dx"]) < GRAD_TOL
+    assert rel_err(dw, dw64) < GRAD_TOL and rel_err(dw, g["dw"]) < GRAD_TOL
+    if b is not None:
+        assert rel_err(db, g["db"]) < GRAD_TOL
+
+
+SHAPES = [(1, 64, 1), (3, 100, 37), (64, 256, 128), (100, 3072, 1536), (129, 1000, 257), (257, 784, 300),
+          (512, 1536, 768)]
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+@pytest.mark.parametrize("backend", ["mfma", "xnor"])
+def test_linear_random_shapes(F, M, K, N, backend):
+    rng = np.random.default_rng(M * 131 + K * 7 + N)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[rng.random((M, K)) < 0.05] = 0.0                     # sign(0) = 0 -> ternary
+    w = rng.uniform(-1, 1, (N, K)).astype(np.float32)
+    w[rng.random((N, K)) < 0.01] = 0.0
+    b = rng.standard_normal(N).astype(np.float32)
+    dy = rng.standard_normal((M, N)).astype(np.float32)
+    binarize = K != 784
+    y, dx, dw, db = run_linear(F, x, w, b, dy, binarize, backend)
+    y_ref, xu = O.linear_forward(x, w, b)
+    if binarize:
+        assert np.array_equal(y, y_ref)
+    else:
+        y64 = x.astype(np.float64) @ np.sign(w).astype(np.float64).T + b
+        assert rel_err(y, y64) < FP_FWD_TOL
+    dx64 = dy.astype(np.float64) @ np.sign(w).astype(np.float64)
+    dw64 = dy.astype(np.float64).T @ xu.astype(np.float64)
+    assert rel_err(dx, dx64) < GRAD_TOL
+    assert rel_err(dw, dw64) < GRAD_TOL
+    assert rel_err(db, dy.astype(np.float64).sum(0)) < GRAD_TOL
+
+
+def test_mfma_and_xnor_agree_bitwise(F):
+    rng = np.random.default_rng(5)
+    x = dev(np.where(rng.random((300, 2048)) < 0.1, 0, rng.standard_normal((300, 2048))).astype(np.float32))
+    w = dev(rng.uniform(-1, 1, (200, 2048)).astype(np.float32))
+    b = dev(rng.standard_normal(200).astype(np.float32))
+    y1 = F.binary_linear(x, w, b, True, "mfma")
+    y2 = F.binary_linear(x, w, b, True, "xnor")
+    assert torch.equal(y1, y2)
+
+
+def test_sign_pack_layouts(F):
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((70, 130)).astype(np.float32)
+    x[::3, ::5] = 0.0
+    q, qt = F.sign_pack(dev(x), True, True)
+    q, qt = host(q), host(qt)
+    s = np.sign(x).astype(np.int8)
+    assert q.shape == (70, 192) and qt.shape == (130, 128)
+    assert np.array_equal(q[:, :130], s) and not q[:, 130:].any()
+    assert np.array_equal(qt[:, :70], s.T) and not qt[:, 70:].any()
+    sb, nz = F.sign_pack_bits(dev(x))
+    sb, nz = host(sb).view(np.uint32), host(nz).view(np.uint32)
+    for k in (0, 31, 32, 129):
+        assert np.array_equal((sb[:, k // 32] >> (k % 32)) & 1, (x[:, k] < 0).astype(np.uint32))
+        assert np.array_equal((nz[:, k // 32] >> (k % 32)) & 1, (x[:, k] != 0).astype(np.uint32))
+    assert not sb[:, 5:].any() and not nz[:, 5:].any()
+
+
+def _recon(d, s):
+    d = d.astype(np.float64)
+    return (d[2] * 65536 + d[1] * 256 + d[0]) * s
+
+
+def test_digit_quantisation(F):
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal((50, 300)) * np.exp(rng.uniform(-20, 20, (50, 1)))).astype(np.float32)
+    x[3] = 0.0
+    d, s = F.quant_rows(dev(x))
+    d, s = host(d), host(s)
+    assert d[:, :, 300:].sum() == 0 and s[3] == 0 and np.all(np.abs(d[2]) <= 65)
+    r = _recon(d[:, :, :300], s[:, None])
+    amax = np.abs(x).max(1, keepdims=True)
+    assert np.all(np.abs(r - x) <= amax * 2.0 ** -22 + 1e-45)
+    dt, sc, cs = F.quant_cols_t(dev(x), want_colsum=True)
+    dt, sc, cs = host(dt), host(sc), host(cs)
+    r = _recon(dt[:, :, :50], sc[:, None]).T
+    amax = np.abs(x).max(0, keepdims=True)
+    assert np.all(np.abs(r - x) <= amax * 2.0 ** -22 + 1e-45)
+    assert rel_err(cs, x.astype(np.float64).sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["conv_c1", "conv_c16", "conv_c3", "conv_sdg"])
+def test_conv_matches_reference_golden(F, name):
+    g = load_golden(name)
+    s, p, d, gr = (int(v) for v in g["conv"])
+    binarize = O.conv_binarizes_input(g["x"])
+    xt = dev(g["x"]).requires_grad_(True)
+    wt = dev(g["w_latent"]).requires_grad_(True)
+    bt = dev(g["bias"]).requires_grad_(True) if g["has_bias"] else None
+    y = F.binary_conv2d(xt, wt, bt, binarize, s, p, d, gr)
+    y.backward(dev(g["dy"]))
+    if binarize:
+        assert np.array_equal(host(y), g["y"])
+    else:
+        assert rel_err(host(y), g["y"]) < FP_FWD_TOL
+    dx64, dw64, db64 = O.conv2d_backward(g["x_after"], g["w_latent"], g["dy"], s, p, d, gr)
+    assert rel_err(host(xt.grad), g["dx"]) < GRAD_TOL
+    assert rel_err(host(wt.grad), g["dw"]) < GRAD_TOL
+    if bt is not None:
+        assert rel_err(host(bt.grad), g["db"]) < GRAD_TOL
+
+
+def test_conv_cnn_shapes_vs_oracle(F):
+    rng = np.random.default_rng(3)
+    x = np.where(rng.random((6, 16, 14, 14)) < 0.3, 0, rng.standard_normal((6, 16, 14, 14))).astype(np.float32)
+    w = rng.uniform(-1, 1, (32, 16, 5, 5)).astype(np.float32)
+    b = rng.standard_normal(32).astype(np.float32)
+    dy = rng.standard_normal((6, 32, 14, 14)).astype(np.float32)
+    xt, wt, bt = dev(x).requires_grad_(True), dev(w).requires_grad_(True), dev(b).requires_grad_(True)
+    y = F.binary_conv2d(xt, wt, bt, True, 1, 2, 1, 1)
+    y.backward(dev(dy))
+    y_ref, xu = O.conv2d_forward(x, w, b, 1, 2, 1, 1)
+    assert np.array_equal(host(y), y_ref)
+    dx64, dw64, db64 = O.conv2d_backward(xu, w, dy, 1, 2, 1, 1)
+    assert rel_err(host(xt.grad), dx64) < GRAD_TOL
+    assert rel_err(host(wt.grad), dw64) < GRAD_TOL
+    assert rel_err(host(bt.grad), db64) < GRAD_TOL
+
+
+def test_hardtanh_backward(F):
+    x = torch.tensor([-2.0, -1.0, -0.5, 0.0, 0.5, 1.0, 3.0] * 11, device="cuda")
+    g = torch.randn_like(x)
+    out = F.hardtanh_backward(x, g)
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.hardtanh(xr).backward(g)
+    assert torch.equal(out, xr.grad)
+
+
+def test_adam_clamp_matches_torch(F):
+    torch.manual_seed(0)
+    p0 = torch.empty(10007, device="cuda").uniform_(-1.2, 1.2)
+    p_ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p_ref], lr=0.01)
+    p = p0.clone()
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step in range(1, 6):
+        g = torch.randn_like(p)
+        p_ref.grad = g.clone()
+        opt.step()
+        with torch.no_grad():
+            p_ref.clamp_(-1, 1)
+        F.adam_clamp_(p, g, m, v, step, lr=0.01)
+    assert close(host(p), host(p_ref), 1e-6, 0.0)
+
+
+def test_large_forward_exact_vs_rocblas(F):
+    """Size-independent property at wide-MLP scale: ternary products are integers < 2^24, so an
+    fp32 GEMM in any order is exact; libbnn must equal it bit-for-bit (plus the same bias add)."""
+    torch.manual_seed(1)
+    x = torch.randn(2048, 8192, device="cuda")
+    x[x.abs() < 0.01] = 0
+    w = torch.empty(8192, 8192, device="cuda").uniform_(-1, 1)
+    b = torch.randn(8192, device="cuda")
+    y = F.binary_linear(x, w, b, True)
+    ref = (torch.sign(x) @ torch.sign(w).t()) + b
+    assert torch.equal(y, ref)
