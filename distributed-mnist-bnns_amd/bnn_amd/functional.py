@@ -11,17 +11,77 @@ Semantics restated from the reference operator module (models/binarized_modules.
 
 Every op here runs on ROCm tensors through libbnn.so; there is no CPU fallback.
 """
+import contextlib
+
 import torch
 
 from . import _lib as L
 
 __all__ = [
-    "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
+    "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
     "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
 
 ALIGN = 64
+
+
+# ----------------------------------------------------------------------------- kernel timing
+class KernelTimer:
+    """HIP-event timing of libbnn launches on the stream they run on (bench.py's roofline).
+
+    Records (kernel, start, end, algorithmic ops, algorithmic bytes) per launch while installed
+    with ``timing(timer)``; ``summary()`` synchronises and aggregates per kernel."""
+
+    def __init__(self):
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e, ops, nbytes in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "ops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += s.elapsed_time(e)
+            d["ops"] += ops
+            d["bytes"] += nbytes
+        for d in out.values():
+            n = d["launches"]
+            d["avg_ms"] = d["ms"] / n
+            d["avg_ops"] = d["ops"] / n
+            d["avg_bytes"] = d["bytes"] / n
+        return out
+
+
+_TIMER = None
+
+
+@contextlib.contextmanager
+def timing(timer):
+    global _TIMER
+    prev, _TIMER = _TIMER, timer
+    try:
+        yield timer
+    finally:
+        _TIMER = prev
+
+
+@contextlib.contextmanager
+def _timed(name, ops=0.0, nbytes=0.0):
+    if _TIMER is None:
+        yield
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    yield
+    e.record()
+    _TIMER.records.append((name, s, e, float(ops), float(nbytes)))
+
+
+# kernel symbol per digit configuration (must match the dispatch in csrc/bnn_gemm.hip)
+GEMM_KERNEL = {(1, 1): "gemm_i8_k<1,1,2,2>", (3, 1): "gemm_i8_k<3,1,2,2>", (3, 3): "gemm_i8_k<3,3,2,1>"}
+GEMM_PAIRS = {(1, 1): 1, (3, 1): 3, (3, 3): 6}
 
 
 def round_up(x, m=ALIGN):
@@ -64,8 +124,10 @@ def sign_pack(x, want_q=True, want_qt=False):
         q = torch.empty((M, round_up(K)), dtype=torch.int8, device=x.device)
     if want_qt:
         qt = torch.empty((K, round_up(M)), dtype=torch.int8, device=x.device)
-    L.call("bnn_sign_pack_i8", L.ptr(x), M, K, K, L.ptr(q), q.shape[1] if q is not None else 0,
-           L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    nbytes = 4 * M * K + (q.numel() if q is not None else 0) + (qt.numel() if qt is not None else 0)
+    with _timed("sign_pack_tile_k", 0, nbytes):
+        L.call("bnn_sign_pack_i8", L.ptr(x), M, K, K, L.ptr(q), q.shape[1] if q is not None else 0,
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
     return q, qt
 
 
@@ -89,7 +151,8 @@ def quant_rows(x):
     ldq = round_up(K)
     dg = torch.empty((3, M, ldq), dtype=torch.int8, device=x.device)
     sc = torch.empty((M,), dtype=torch.float32, device=x.device)
-    L.call("bnn_quant_rows", L.ptr(x), M, K, K, L.ptr(dg), ldq, M * ldq, L.ptr(sc), L.stream())
+    with _timed("quant_rows_k", 0, 4 * M * K + dg.numel() + 4 * M):
+        L.call("bnn_quant_rows", L.ptr(x), M, K, K, L.ptr(dg), ldq, M * ldq, L.ptr(sc), L.stream())
     return dg, sc
 
 
@@ -103,13 +166,15 @@ def quant_cols_t(x, want_colsum=False):
     sc = torch.empty((N,), dtype=torch.float32, device=x.device)
     cs = torch.empty((N,), dtype=torch.float32, device=x.device) if want_colsum else None
     ws = torch.empty((L.lib().bnn_quant_cols_workspace(M, N),), dtype=torch.uint8, device=x.device)
-    L.call("bnn_quant_cols_t", L.ptr(x), M, N, N, L.ptr(dg), ldqt, N * ldqt, L.ptr(sc), L.ptr(cs),
-           L.ptr(ws), L.stream())
+    with _timed("quant_cols_t", 0, 4 * M * N + dg.numel() + 8 * N):
+        L.call("bnn_quant_cols_t", L.ptr(x), M, N, N, L.ptr(dg), ldqt, N * ldqt, L.ptr(sc), L.ptr(cs),
+               L.ptr(ws), L.stream())
     return dg, sc, cs
 
 
 # ----------------------------------------------------------------------------- (2) GEMMs
-def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=None, out=None):
+def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=None, out=None,
+            k_true=None):
     """C[M,N] = combine(sum_k A[.,m,k] B[.,n,k]) * a_scale[m] * b_scale[n] + bias[n].
 
     A: int8 [M, K] (a_digits=1) or [3, M, K]; B: int8 [N, K] or [3, N, K]; K = padded length
@@ -127,8 +192,12 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
         if bias is not None:
             C += bias
         return C
-    L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
-           L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
+    cfg = (a_digits, b_digits)
+    k_true = K if k_true is None else k_true
+    ops = 2.0 * M * N * k_true * GEMM_PAIRS[cfg]
+    with _timed(GEMM_KERNEL[cfg], ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
+        L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
+               L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
     return C
 
 
@@ -139,8 +208,9 @@ def gemm_xnor(a_bits, b_bits, M, N, bias=None):
     C = torch.empty((M, N), dtype=torch.float32, device=As.device)
     if M == 0 or N == 0:
         return C
-    L.call("bnn_gemm_xnor", L.ptr(As), L.ptr(An), kw, L.ptr(Bs), L.ptr(Bn), Bs.shape[1], L.ptr(bias),
-           L.ptr(C), N, M, N, kw, L.stream())
+    with _timed("gemm_xnor_k", 2.0 * M * N * kw * 32, 8 * (M + N) * kw + 4 * M * N):
+        L.call("bnn_gemm_xnor", L.ptr(As), L.ptr(An), kw, L.ptr(Bs), L.ptr(Bn), Bs.shape[1], L.ptr(bias),
+               L.ptr(C), N, M, N, kw, L.stream())
     return C
 
 
@@ -162,11 +232,11 @@ class BinaryLinearFunction(torch.autograd.Function):
                 xqt = sign_pack(x, want_q=False, want_qt=True)[1] if need_dw else None
             else:
                 xq, xqt = sign_pack(x, want_q=True, want_qt=need_dw)
-                y = gemm_i8(xq, 1, wq, 1, M, N, bias=b)
+                y = gemm_i8(xq, 1, wq, 1, M, N, bias=b, k_true=K)
             ctx.save_for_backward(xqt, wqt)
         else:
             xd, sx = quant_rows(x)
-            y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b)
+            y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b, k_true=K)
             ctx.save_for_backward(x if need_dw else None, wqt)
         ctx.binarize_input = binarize_input
         ctx.dims = (M, K, N)
@@ -181,16 +251,16 @@ class BinaryLinearFunction(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             d, s = quant_rows(dy)                                   # [3, M, ldN]
-            dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s)             # dY . W_b
+            dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or need_db:
             dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)      # [3, N, ldM]
             if ctx.needs_input_grad[1]:
                 if ctx.binarize_input:
-                    dw = gemm_i8(dt, 3, xs, 1, N, K, a_scale=sc)    # dY^T . X_b
+                    dw = gemm_i8(dt, 3, xs, 1, N, K, a_scale=sc, k_true=M)  # dY^T . X_b
                 else:
                     xt, sxc, _ = quant_cols_t(xs)
-                    dw = gemm_i8(dt, 3, xt, 3, N, K, a_scale=sc, b_scale=sxc)
+                    dw = gemm_i8(dt, 3, xt, 3, N, K, a_scale=sc, b_scale=sxc, k_true=M)
             db = cs
         return dx, dw, db, None, None
 

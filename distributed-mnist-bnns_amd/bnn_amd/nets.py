@@ -1,0 +1,102 @@
+"""Networks of the reference's training scripts, built on the libbnn layers.
+
+* ``Net`` -- mnist-dist2.py:46-76: 784-(1024r)-(512r)-(256r)-10, r = infl_ratio = 3,
+  fc -> BatchNorm1d -> Hardtanh per hidden layer, Dropout(0.3) between fc3 and bn3,
+  fc4 = nn.Linear, LogSoftmax.
+* ``SmallNet`` -- mnist-dist3.py:40-70 (64r = 192 wide; the source of the published CSVs).
+* ``WideNet`` -- BASELINE config 5: 784-8192x3-10, same topology.
+* ``BinCNN`` -- BASELINE config 4 (build-defined; the reference never instantiates
+  BinarizeConv2d): the ConvNet template of mnist-dist.py:31-51 with binarised convolutions and
+  Hardtanh in place of ReLU: conv5x5(1->16,p2)-BN-Hardtanh-MaxPool2, conv5x5(16->32,p2)-BN-
+  Hardtanh-MaxPool2, Linear(1568->10), LogSoftmax.
+"""
+import torch.nn as nn
+
+from .nn import BinarizeConv2d, BinarizeLinear
+
+
+def _configure(module, org_protocol, mutate_input, backend=None):
+    for m in module.modules():
+        if isinstance(m, (BinarizeLinear, BinarizeConv2d)):
+            m.org_protocol = org_protocol
+            m.mutate_input = mutate_input
+            if backend is not None and isinstance(m, BinarizeLinear):
+                m.backend = backend
+    return module
+
+
+class MLP(nn.Module):
+    """mnist-dist2.py:46-76 with explicit widths."""
+
+    def __init__(self, h1, h2, h3, p_drop=0.3, org_protocol=True, mutate_input=True, backend=None):
+        super().__init__()
+        self.fc1 = BinarizeLinear(784, h1)
+        self.htanh1 = nn.Hardtanh()
+        self.bn1 = nn.BatchNorm1d(h1)
+        self.fc2 = BinarizeLinear(h1, h2)
+        self.htanh2 = nn.Hardtanh()
+        self.bn2 = nn.BatchNorm1d(h2)
+        self.fc3 = BinarizeLinear(h2, h3)
+        self.htanh3 = nn.Hardtanh()
+        self.bn3 = nn.BatchNorm1d(h3)
+        self.fc4 = nn.Linear(h3, 10)
+        self.logsoftmax = nn.LogSoftmax(dim=1)
+        self.drop = nn.Dropout(p_drop)
+        _configure(self, org_protocol, mutate_input, backend)
+
+    def forward(self, x):
+        x = x.view(-1, 28 * 28)
+        x = self.htanh1(self.bn1(self.fc1(x)))
+        x = self.htanh2(self.bn2(self.fc2(x)))
+        x = self.fc3(x)
+        x = self.drop(x)
+        x = self.htanh3(self.bn3(x))
+        x = self.fc4(x)
+        return self.logsoftmax(x)
+
+
+def Net(infl_ratio=3, **kw):
+    """mnist-dist2.py Net: 784-3072-1536-768-10 at infl_ratio 3."""
+    return MLP(1024 * infl_ratio, 512 * infl_ratio, 256 * infl_ratio, **kw)
+
+
+def SmallNet(infl_ratio=3, **kw):
+    """mnist-dist3.py Net: 784-192-192-192-10."""
+    return MLP(64 * infl_ratio, 64 * infl_ratio, 64 * infl_ratio, **kw)
+
+
+def WideNet(width=8192, **kw):
+    """BASELINE config 5: 784-8192x3-10."""
+    return MLP(width, width, width, **kw)
+
+
+class BinCNN(nn.Module):
+    def __init__(self, num_classes=10, org_protocol=True, mutate_input=True):
+        super().__init__()
+        self.layer1 = nn.Sequential(BinarizeConv2d(1, 16, kernel_size=5, stride=1, padding=2),
+                                    nn.BatchNorm2d(16), nn.Hardtanh(), nn.MaxPool2d(kernel_size=2, stride=2))
+        self.layer2 = nn.Sequential(BinarizeConv2d(16, 32, kernel_size=5, stride=1, padding=2),
+                                    nn.BatchNorm2d(32), nn.Hardtanh(), nn.MaxPool2d(kernel_size=2, stride=2))
+        self.fc = nn.Linear(7 * 7 * 32, num_classes)
+        self.logsoftmax = nn.LogSoftmax(dim=1)
+        _configure(self, org_protocol, mutate_input)
+
+    def forward(self, x):
+        out = self.layer2(self.layer1(x))
+        out = out.reshape(out.size(0), -1)
+        return self.logsoftmax(self.fc(out))
+
+
+MODELS = {"mlp": Net, "small": SmallNet, "wide": WideNet, "cnn": BinCNN}
+
+
+def binary_params(model):
+    """Parameters the reference clamps: weights and biases of BinarizeLinear/BinarizeConv2d
+    (they carry ``.org``, mnist-dist2.py:131-137)."""
+    out = []
+    for m in model.modules():
+        if isinstance(m, (BinarizeLinear, BinarizeConv2d)):
+            out.append(m.weight)
+            if m.bias is not None:
+                out.append(m.bias)
+    return out

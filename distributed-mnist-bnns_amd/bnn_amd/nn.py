@@ -1,0 +1,123 @@
+"""The reference operator API (models/binarized_modules.py) on libbnn.
+
+Names, constructor signatures and side effects follow the reference:
+
+* ``Binarize(tensor, quant_mode='det')``                   -- :11-15
+* ``HingeLoss``                                            -- :20-32
+* ``SqrtHingeLossFunction`` (stub: the reference's is a pre-0.4 autograd Function with a
+  ``pdb.set_trace()`` in backward, :34-54)
+* ``Quantize(tensor, quant_mode='det', params=None, numBits=8)`` -- :56-63
+* ``BinarizeLinear(*kargs, **kwargs)`` (an ``nn.Linear``)   -- :68-85
+* ``BinarizeConv2d(*kargs, **kwargs)`` (an ``nn.Conv2d``)   -- :87-107
+
+Side effects kept (the caller loop of mnist-dist2.py:131-137 depends on them):
+  ``weight.org`` is created once on the first forward from ``weight.data`` (:77-78),
+  ``weight.data`` is replaced by ``sign(weight.org)`` every forward (:79),
+  ``bias.org`` is re-cloned every forward (:82, :104), and the caller's input tensor is
+  replaced by its sign unless the first-layer rule applies (:75-76, :94-95).
+
+Two class attributes switch behaviour for the build's own trainer:
+  ``org_protocol = False`` keeps the latent weight in the Parameter itself (no ``.org``,
+  binarised on the fly inside the kernel; pair it with ``bnn_amd.optim.LatentAdam``), and
+  ``mutate_input = False`` skips materialising ``sign(input)`` in fp32 (nothing reads it).
+"""
+import torch
+import torch.nn as nn
+
+from . import functional as BF
+
+__all__ = ["Binarize", "HingeLoss", "SqrtHingeLossFunction", "Quantize", "BinarizeLinear",
+           "BinarizeConv2d"]
+
+
+def Binarize(tensor, quant_mode="det"):
+    """Deterministic: ``tensor.sign()`` as a new tensor (libbnn).  Stochastic (reference :15, never
+    used by the reference modules): in place, ``round(clamp((x+1)/2 + U(-.5,.5), 0, 1))*2 - 1``."""
+    if quant_mode == "det":
+        return BF.sign(tensor)
+    noise = torch.rand(tensor.size(), device=tensor.device, dtype=tensor.dtype) - 0.5
+    prob = tensor.add_(1.0).div_(2.0).add_(noise).clamp_(0.0, 1.0)
+    return prob.round().mul_(2.0).sub_(1.0)
+
+
+class HingeLoss(nn.Module):
+    """mean(max(0, margin - input*target)), margin = 1 (reference :20-32)."""
+
+    def __init__(self):
+        super().__init__()
+        self.margin = 1.0
+
+    def hinge_loss(self, input, target):
+        return torch.clamp(self.margin - input * target, min=0.0).mean()
+
+    def forward(self, input, target):
+        return self.hinge_loss(input, target)
+
+
+class SqrtHingeLossFunction(torch.autograd.Function):
+    """Exported for import compatibility only.  The reference version (:34-54) is a legacy
+    non-static autograd.Function that drops into pdb in backward; no reference script uses it."""
+
+    @staticmethod
+    def forward(ctx, input, target):
+        raise NotImplementedError("SqrtHingeLossFunction is not part of the BNN hot path "
+                                  "(the reference implementation is non-functional)")
+
+
+def Quantize(tensor, quant_mode="det", params=None, numBits=8):
+    """Reference :56-63.  Deterministic mode clamps in place then rounds to numBits-1 fractional
+    bits; the stochastic mode calls an undefined ``quant_fixed`` in the reference (NameError)."""
+    lim = 2.0 ** (numBits - 1)
+    tensor.clamp_(-lim, lim)
+    if quant_mode == "det":
+        return tensor.mul(lim).round().div(lim)
+    raise NotImplementedError("Quantize(quant_mode!='det') calls an undefined quant_fixed in the reference")
+
+
+def _apply_org_protocol(p):
+    """binarized_modules.py:77-79: lazily keep the latent copy, expose its sign in .data."""
+    if not hasattr(p, "org"):
+        p.org = p.data.clone()
+    p.data = BF.sign(p.org)
+
+
+class BinarizeLinear(nn.Linear):
+    org_protocol = True
+    mutate_input = True
+    backend = "mfma"       # or "xnor" (VALU popcount path)
+
+    def __init__(self, *kargs, **kwargs):
+        super().__init__(*kargs, **kwargs)
+
+    def forward(self, input):
+        binarize = input.size(1) != 784                       # :75
+        if binarize and self.mutate_input:
+            input.data = BF.sign(input.data)                    # :76
+        if self.org_protocol:
+            _apply_org_protocol(self.weight)                    # :77-79
+            if self.bias is not None:
+                self.bias.org = self.bias.data.clone()          # :82
+        return BF.binary_linear(input, self.weight, self.bias, binarize, self.backend)
+
+
+class BinarizeConv2d(nn.Conv2d):
+    org_protocol = True
+    mutate_input = True
+
+    def __init__(self, *kargs, **kwargs):
+        super().__init__(*kargs, **kwargs)
+        if self.padding_mode != "zeros":
+            raise NotImplementedError("BinarizeConv2d: only zero padding (F.conv2d default, :100)")
+        if isinstance(self.padding, str):
+            raise NotImplementedError("BinarizeConv2d: string padding is not supported")
+
+    def forward(self, input):
+        binarize = input.size(1) != 3                         # :94
+        if binarize and self.mutate_input:
+            input.data = BF.sign(input.data)                    # :95
+        if self.org_protocol:
+            _apply_org_protocol(self.weight)                    # :96-98
+            if self.bias is not None:
+                self.bias.org = self.bias.data.clone()          # :104
+        return BF.binary_conv2d(input, self.weight, self.bias, binarize, self.stride, self.padding,
+                                self.dilation, self.groups)

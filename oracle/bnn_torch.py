@@ -1,0 +1,120 @@
+"""CPU restatement of the reference's training path in plain torch (fp32) -- TEST / BASELINE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may use
+this module.  It is what the reference runs on a CPU: torch's fp32 ``F.linear`` / ``F.conv2d`` on
+sign()ed operands, ``BatchNorm1d``, ``Hardtanh``, ``torch.optim.Adam`` and the ``.org``
+protocol.  bench.py times it on the GPU box's host cores as the ``"port"`` CPU baseline
+(the reference source itself never travels there).  Pinned to the reference's outputs by
+tests/test_oracle_golden.py::test_torch_restatement_* against tests/golden/*.npz.
+
+Restated from: models/binarized_modules.py:11-13 (Binarize), :68-85 (BinarizeLinear),
+:87-107 (BinarizeConv2d); mnist-dist2.py:46-76 (Net), :118-137 (train step).
+"""
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as tF
+
+
+def _latent_sign(p):
+    # binarized_modules.py:77-79 -- the latent copy is made once, its sign is exposed in .data
+    if not hasattr(p, "org"):
+        p.org = p.data.clone()
+    p.data = p.org.sign()
+
+
+class RefLinear(nn.Linear):
+    """BinarizeLinear semantics on CPU (binarized_modules.py:73-85)."""
+
+    def forward(self, inp):
+        if inp.size(1) != 784:
+            inp.data = inp.data.sign()
+        _latent_sign(self.weight)
+        y = tF.linear(inp, self.weight)
+        if self.bias is not None:
+            self.bias.org = self.bias.data.clone()
+            y += self.bias.view(1, -1).expand_as(y)
+        return y
+
+
+class RefConv2d(nn.Conv2d):
+    """BinarizeConv2d semantics on CPU (binarized_modules.py:93-107)."""
+
+    def forward(self, inp):
+        if inp.size(1) != 3:
+            inp.data = inp.data.sign()
+        _latent_sign(self.weight)
+        y = tF.conv2d(inp, self.weight, None, self.stride, self.padding, self.dilation, self.groups)
+        if self.bias is not None:
+            self.bias.org = self.bias.data.clone()
+            y += self.bias.view(1, -1, 1, 1).expand_as(y)
+        return y
+
+
+class RefMLP(nn.Module):
+    """mnist-dist2.py:46-76 topology with explicit widths."""
+
+    def __init__(self, h1, h2, h3, p_drop=0.3):
+        super().__init__()
+        self.fc1, self.bn1 = RefLinear(784, h1), nn.BatchNorm1d(h1)
+        self.fc2, self.bn2 = RefLinear(h1, h2), nn.BatchNorm1d(h2)
+        self.fc3, self.bn3 = RefLinear(h2, h3), nn.BatchNorm1d(h3)
+        self.fc4 = nn.Linear(h3, 10)
+        self.drop = nn.Dropout(p_drop)
+
+    def forward(self, x):
+        x = x.view(-1, 784)
+        x = tF.hardtanh(self.bn1(self.fc1(x)))
+        x = tF.hardtanh(self.bn2(self.fc2(x)))
+        x = tF.hardtanh(self.bn3(self.drop(self.fc3(x))))
+        return tF.log_softmax(self.fc4(x), dim=1)
+
+
+def train_step(model, opt, x, target, org_protocol=True):
+    """mnist-dist2.py:122-137 (org protocol) or mnist-dist3.py:113-119 (without)."""
+    opt.zero_grad()
+    loss = tF.cross_entropy(model(x), target)
+    loss.backward()
+    params = list(model.parameters())
+    if org_protocol:
+        for p in params:
+            if hasattr(p, "org"):
+                p.data.copy_(p.org)
+    opt.step()
+    if org_protocol:
+        for p in params:
+            if hasattr(p, "org"):
+                p.org.copy_(p.data.clamp_(-1, 1))
+    return loss.item()
+
+
+def synthetic_batch(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand((n, 1, 28, 28), generator=g)
+    v = torch.randint(1, 256, (n, 1, 28, 28), generator=g).float()
+    x = torch.where(u < 0.807, torch.zeros_like(v), v) / 255.0
+    return x, torch.randint(0, 10, (n,), generator=g)
+
+
+def time_training(widths, batch, threads, budget_s=10.0, max_steps=50, min_steps=2, warmup=1):
+    """Time the CPU reference training step (fp32, torch on `threads` host threads).
+
+    Returns (samples_per_s, steps, seconds)."""
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    model = RefMLP(*widths)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=0.01)
+    x, t = synthetic_batch(batch, 1234)
+    for _ in range(warmup):
+        train_step(model, opt, x.clone(), t)
+    steps, t0 = 0, time.perf_counter()
+    while steps < max_steps:
+        train_step(model, opt, x.clone(), t)
+        steps += 1
+        el = time.perf_counter() - t0
+        if steps >= min_steps and el >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return batch * steps / el, steps, el

@@ -1,0 +1,101 @@
+"""N>1 data-parallel path on CPU: world_size-2 gloo process group (the GPU box runs the same
+code over RCCL).  Checks GradExchange against torch's DistributedDataParallel -- the component
+the reference wraps around its model (mnist-dist2.py:93) -- and the sampler sharding rule."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT, load_golden
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    try:
+        for p in (ROOT, PKG):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from bnn_amd.parallel import GradExchange
+        from oracle.bnn_torch import RefMLP, synthetic_batch
+
+        def make():
+            torch.manual_seed(100 + rank)            # different init per rank on purpose
+            m = RefMLP(48, 32, 24, p_drop=0.0)
+            return m
+
+        ours, ref = make(), make()
+        # tiny buckets so the 14 parameters spread over several buckets
+        ex = GradExchange(ours, bucket_mb=0.004)
+        ddp = torch.nn.parallel.DistributedDataParallel(ref)
+        x, t = synthetic_batch(16, 1234 + rank)
+        results = {}
+        for step in range(2):
+            ex.zero_grad()
+            ref.zero_grad()
+            torch.nn.functional.cross_entropy(ours(x.clone()), t).backward()
+            ex.finish()
+            torch.nn.functional.cross_entropy(ddp(x.clone()), t).backward()
+            for (n, p), q_ in zip(ours.named_parameters(), ref.parameters()):
+                assert torch.allclose(p.grad, q_.grad, rtol=1e-5, atol=1e-7), (step, n)
+            with torch.no_grad():
+                for p, q_ in zip(ours.parameters(), ref.parameters()):
+                    p.add_(p.grad, alpha=-0.01)
+                    q_.add_(q_.grad, alpha=-0.01)
+        results["params"] = [p.detach().clone() for p in ours.parameters()]
+        # buffers follow DDP broadcast_buffers semantics: rank 0's stats before each forward,
+        # then this rank's own batch update
+        for a, b in zip(ours.buffers(), ref.buffers()):
+            assert torch.allclose(a.float(), b.float(), rtol=1e-5, atol=1e-6)
+        results["nbuckets"] = len(ex.buckets)
+        q.put((rank, {k: (v if not isinstance(v, list) else [t.numpy() for t in v])
+                      if not torch.is_tensor(v) else v.numpy() for k, v in results.items()}))
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures in the parent
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc()))
+
+
+def test_gradexchange_matches_torch_ddp_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert not isinstance(out[r], str), out[r]
+    assert out[0]["nbuckets"] > 1
+    # replicas stay identical: init broadcast + averaged gradients
+    for a, b in zip(out[0]["params"], out[1]["params"]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_shard_indices_match_distributed_sampler_golden():
+    from bnn_amd.data import shard_indices
+    g = load_golden("sampler")
+    for key, want in g.items():
+        n, ws, r = (int(s[1:] if s[0] == "n" else s[2:] if s.startswith("ws") else s[1:])
+                    for s in key.split("_"))
+        got = np.array(shard_indices(n, ws, r), np.int64)
+        if n >= 1000:
+            got = got[:64]
+        np.testing.assert_array_equal(got, want)
