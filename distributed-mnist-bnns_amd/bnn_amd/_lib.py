@@ -27,12 +27,18 @@ SIGNATURES = {
     "bnn_quant_cols_workspace": (I64, [I64, I64]),
     "bnn_quant_cols_t": (I32, [P, I64, I64, I64, P, I64, I64, P, P, P, P]),
     "bnn_gemm_i8": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_set_variant": (I32, [I32]),
+    "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64]),
     "bnn_gemm_xnor": (I32, [P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_conv2d_fwd": (I32, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_conv2d_bwd_data": (I32, [P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_conv2d_bwd_filter_workspace": (I64, [I64, I64, I64, I64, I64, I32]),
     "bnn_conv2d_bwd_filter": (I32, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32,
                                     I32, P]),
+    "bnn_bn_workspace": (I64, [I64, I64]),
+    "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, P, P]),
+    "bnn_bn_fwd_eval": (I32, [P, I64, I64, P, P, P, P, F32, P, I32, P, P]),
+    "bnn_bn_bwd": (I32, [P, P, I64, I64, P, P, P, P, I32, P, P, P, P, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
 }

@@ -19,7 +19,7 @@ from . import _lib as L
 
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
-    "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_",
+    "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "batch_norm_hardtanh",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
 
@@ -79,9 +79,12 @@ def _timed(name, ops=0.0, nbytes=0.0):
     _TIMER.records.append((name, s, e, float(ops), float(nbytes)))
 
 
-# kernel symbol per digit configuration (must match the dispatch in csrc/bnn_gemm.hip)
-GEMM_KERNEL = {(1, 1): "gemm_i8_k<1,1,2,2>", (3, 1): "gemm_i8_k<3,1,2,2>", (3, 3): "gemm_i8_k<3,3,2,1>"}
 GEMM_PAIRS = {(1, 1): 1, (3, 1): 3, (3, 3): 6}
+
+
+def gemm_kernel_name(a_digits, b_digits, M, N):
+    """The kernel instance libbnn launches for this GEMM (rocprofv3's name for it)."""
+    return L.lib().bnn_gemm_i8_kernel(a_digits, b_digits, M, N).decode()
 
 
 def round_up(x, m=ALIGN):
@@ -195,7 +198,8 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
     cfg = (a_digits, b_digits)
     k_true = K if k_true is None else k_true
     ops = 2.0 * M * N * k_true * GEMM_PAIRS[cfg]
-    with _timed(GEMM_KERNEL[cfg], ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
+    name = gemm_kernel_name(a_digits, b_digits, M, N) if _TIMER is not None else ""
+    with _timed(name, ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
         L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
                L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
     return C
@@ -351,3 +355,71 @@ def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, 
     L.call("bnn_adam_clamp", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), p.numel(),
            float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale),
            int(bool(clamp)), L.stream())
+
+
+# ----------------------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
+def _bn_ws(M, C, device):
+    return torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device=device)
+
+
+class BatchNormHardtanhFunction(torch.autograd.Function):
+    """nn.BatchNorm1d on [M, C] (train or eval) optionally followed by nn.Hardtanh, fused
+    (mnist-dist2.py:52-74).  Running stats are updated in place in training mode."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh):
+        _check(x, weight, bias, running_mean, running_var)
+        x = _c2d(x)
+        M, C = x.shape
+        y = torch.empty_like(x)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        ws = _bn_ws(M, C, x.device)
+        if training:
+            mean = torch.empty((C,), dtype=torch.float32, device=x.device)
+            invstd = torch.empty_like(mean)
+            with _timed("bn_fwd_train", 0, 12 * M * C):
+                L.call("bnn_bn_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                       L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
+                       L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
+        else:
+            mean = running_mean
+            invstd = (running_var + eps).rsqrt()
+            with _timed("bn_fwd_eval", 0, 8 * M * C):
+                L.call("bnn_bn_fwd_eval", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                       L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
+        ctx.save_for_backward(x, w, b, mean, invstd)
+        ctx.hardtanh = hardtanh
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, mean, invstd = ctx.saved_tensors
+        dy = _c2d(dy)
+        M, C = x.shape
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
+        db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
+        ws = _bn_ws(M, C, x.device)
+        with _timed("bn_bwd", 0, 16 * M * C):
+            L.call("bnn_bn_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+                   int(ctx.hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+        return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None)
+
+
+def batch_norm_hardtanh(x, bn, hardtanh=True):
+    """Apply an ``nn.BatchNorm1d`` module (its parameters, buffers, momentum / eps /
+    track_running_stats semantics as in torch's ``_BatchNorm.forward``) followed by Hardtanh,
+    through libbnn."""
+    factor = 0.0 if bn.momentum is None else bn.momentum
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+        if bn.momentum is None:               # cumulative moving average (host sync, rare)
+            factor = 1.0 / float(bn.num_batches_tracked)
+    bn_training = bn.training or (bn.running_mean is None and bn.running_var is None)
+    pass_stats = (not bn.training) or bn.track_running_stats
+    rm = bn.running_mean if pass_stats else None
+    rv = bn.running_var if pass_stats else None
+    return BatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
+                                           hardtanh)

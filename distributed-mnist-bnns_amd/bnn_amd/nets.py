@@ -12,6 +12,7 @@
 """
 import torch.nn as nn
 
+from . import functional as BF
 from .nn import BinarizeConv2d, BinarizeLinear
 
 
@@ -28,8 +29,12 @@ def _configure(module, org_protocol, mutate_input, backend=None):
 class MLP(nn.Module):
     """mnist-dist2.py:46-76 with explicit widths."""
 
-    def __init__(self, h1, h2, h3, p_drop=0.3, org_protocol=True, mutate_input=True, backend=None):
+    def __init__(self, h1, h2, h3, p_drop=0.3, org_protocol=True, mutate_input=True, backend=None,
+                 fused_bn=False):
         super().__init__()
+        # fused_bn: bn_i -> htanh_i run as one libbnn BatchNorm+Hardtanh pass (same parameters,
+        # buffers and math; replaces torch's BatchNorm1d kernels, DESIGN.md)
+        self.fused_bn = fused_bn
         self.fc1 = BinarizeLinear(784, h1)
         self.htanh1 = nn.Hardtanh()
         self.bn1 = nn.BatchNorm1d(h1)
@@ -44,13 +49,18 @@ class MLP(nn.Module):
         self.drop = nn.Dropout(p_drop)
         _configure(self, org_protocol, mutate_input, backend)
 
+    def _bnh(self, bn, ht, x):
+        if self.fused_bn and x.is_cuda and x.dim() == 2 and x.shape[1] % 4 == 0:
+            return BF.batch_norm_hardtanh(x, bn)
+        return ht(bn(x))
+
     def forward(self, x):
         x = x.view(-1, 28 * 28)
-        x = self.htanh1(self.bn1(self.fc1(x)))
-        x = self.htanh2(self.bn2(self.fc2(x)))
+        x = self._bnh(self.bn1, self.htanh1, self.fc1(x))
+        x = self._bnh(self.bn2, self.htanh2, self.fc2(x))
         x = self.fc3(x)
         x = self.drop(x)
-        x = self.htanh3(self.bn3(x))
+        x = self._bnh(self.bn3, self.htanh3, x)
         x = self.fc4(x)
         return self.logsoftmax(x)
 

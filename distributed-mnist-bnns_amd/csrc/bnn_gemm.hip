@@ -210,6 +210,212 @@ __global__ __launch_bounds__(256) void gemm_i8_k(GemmParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2: WAVES_M x WAVES_N waves, STAGES-deep LDS ring filled by global_load_lds, counted vmcnt
+// (the next STAGES-2 tiles stay in flight across the barrier), raw s_barrier (a __syncthreads()
+// would drain every in-flight LDS-DMA with vmcnt(0)).
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  // s_waitcnt simm16 (gfx9): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+#define BNN_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14))
+  switch (n) {
+    case 0: BNN_VMCNT(0); break;
+    case 2: BNN_VMCNT(2); break;
+    case 3: BNN_VMCNT(3); break;
+    case 4: BNN_VMCNT(4); break;
+    case 6: BNN_VMCNT(6); break;
+    case 7: BNN_VMCNT(7); break;
+    case 8: BNN_VMCNT(8); break;
+    case 12: BNN_VMCNT(12); break;
+    case 14: BNN_VMCNT(14); break;
+    case 16: BNN_VMCNT(16); break;
+    default: BNN_VMCNT(0); break;
+  }
+#undef BNN_VMCNT
+}
+
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
+  constexpr int A_ST = DA * BM * BK, B_ST = DB * BN * BK, ST = A_ST + B_ST;
+  constexpr int IA = DA * BM / 16, IB = DB * BN / 16;
+  static_assert(IA % NW == 0 && IB % NW == 0, "glds instructions must split evenly over waves");
+  constexpr int PER_WAVE = (IA + IB) / NW;
+  constexpr int NC = Cfg<DA, DB>::NC;
+  constexpr bool FLUSH = Cfg<DA, DB>::FLUSH;
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
+
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  int tm, tn;
+  tile_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int srow = lane >> 2, sslot = lane & 3;
+  const int schunk = sslot ^ ((srow >> 2) & 3);
+  auto stage = [&](int kt, int buf) {
+    char* sA = smem + buf * ST;
+    char* sB = sA + A_ST;
+    const int k0 = kt * BK + 16 * schunk;
+#pragma unroll
+    for (int j = wave; j < IA; j += NW) {
+      const int d = j / (BM / 16), jr = j % (BM / 16);
+      const int row = min(m0 + jr * 16 + srow, p.M - 1);
+      glds16(p.A + d * p.a_plane + (int64_t)row * p.lda + k0, sA + d * BM * BK + jr * 1024);
+    }
+#pragma unroll
+    for (int j = wave; j < IB; j += NW) {
+      const int e = j / (BN / 16), jr = j % (BN / 16);
+      const int row = min(n0 + jr * 16 + srow, p.N - 1);
+      glds16(p.B + e * p.b_plane + (int64_t)row * p.ldb + k0, sB + e * BN * BK + jr * 1024);
+    }
+  };
+
+  v16i acc[NC][WM][WN];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < WM; ++t)
+#pragma unroll
+      for (int u = 0; u < WN; ++u) acc[c][t][u] = v16i{0};
+  float facc[FLUSH ? WM : 1][FLUSH ? WN : 1][16];
+  if constexpr (FLUSH) {
+#pragma unroll
+    for (int t = 0; t < WM; ++t)
+#pragma unroll
+      for (int u = 0; u < WN; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) facc[t][u][i] = 0.f;
+  }
+
+  const int r = lane & 31, h = lane >> 5, sw = (r >> 2) & 3;
+  const int nk = p.K / BK;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(STAGES - 2, nk - 1 - kt);
+    wait_vmcnt(PER_WAVE * ahead);
+    block_barrier();
+    if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const int buf = kt % STAGES;
+    const char* sA = smem + buf * ST;
+    const char* sB = sA + A_ST;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int off = 16 * ((2 * ks + h) ^ sw);
+      v4i a[DA][WM], b[DB][WN];
+#pragma unroll
+      for (int d = 0; d < DA; ++d)
+#pragma unroll
+        for (int t = 0; t < WM; ++t)
+          a[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BK + (wm * WM * 32 + t * 32 + r) * BK + off);
+#pragma unroll
+      for (int e = 0; e < DB; ++e)
+#pragma unroll
+        for (int u = 0; u < WN; ++u)
+          b[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BK + (wn * WN * 32 + u * 32 + r) * BK + off);
+#pragma unroll
+      for (int t = 0; t < WM; ++t)
+#pragma unroll
+        for (int u = 0; u < WN; ++u) {
+          if constexpr (DA == 1 && DB == 1) {
+            acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0][t], b[0][u], acc[0][t][u], 0, 0, 0);
+          } else if constexpr (DB == 1) {
+#pragma unroll
+            for (int d = 0; d < DA; ++d)
+              acc[d][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[d][t], b[0][u], acc[d][t][u], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int i = 0; i < DA; ++i)
+#pragma unroll
+              for (int j = 0; j < DB; ++j)
+                if (i + j >= 2)
+                  acc[i + j - 2][t][u] =
+                      __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i][t], b[j][u], acc[i + j - 2][t][u], 0, 0, 0);
+          }
+        }
+    }
+    if constexpr (FLUSH) {
+      if ((kt + 1) % Cfg<DA, DB>::FLUSH_KT == 0 || kt + 1 == nk) {
+#pragma unroll
+        for (int t = 0; t < WM; ++t)
+#pragma unroll
+          for (int u = 0; u < WN; ++u) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              facc[t][u][i] += (float)((double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 +
+                                       (double)acc[0][t][u][i]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c][t][u] = v16i{0};
+          }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < WM; ++t)
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int col = n0 + wn * WN * 32 + u * 32 + r;
+      if (col >= p.N) continue;
+      const float bs = p.b_scale ? p.b_scale[col] : 1.f;
+      const float bb = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WM * 32 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        double v;
+        if constexpr (DA == 1 && DB == 1) {
+          v = (double)acc[0][t][u][i];
+        } else if constexpr (DB == 1) {
+          v = (double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 + (double)acc[0][t][u][i];
+        } else {
+          v = (double)facc[t][u][i] * 65536.0;
+        }
+        if (p.a_scale) v *= (double)p.a_scale[row];
+        v *= (double)bs;
+        float f = (float)v;
+        if (p.bias) f += bb;
+        p.C[(int64_t)row * p.ldc + col] = f;
+      }
+    }
+}
+
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+int launch_v2(GemmParams p, hipStream_t s) {
+  constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
+  p.gm = (p.M + BM - 1) / BM;
+  p.gn = (p.N + BN - 1) / BN;
+  const int64_t nblk = (int64_t)p.gm * p.gn;
+  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES>), dim3((unsigned)nblk),
+                     dim3(64 * WAVES_M * WAVES_N), 0, s, p);
+  return check_launch("bnn_gemm_i8");
+}
+
+int g_variant = -1;  // tuning hook (bnn_gemm_set_variant); -1 = default table
+
+// Kernel choice per digit configuration and shape (tools/gemm_sweep.py on MI355X, round 1):
+// 256x256 (8 waves) / 256x128 tiles once the grid has >= 512 of them, smaller tiles otherwise.
+int pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N) {
+  const int v = g_variant;
+  if (a_digits == 1) {
+    if (v >= 0) return std::min(v, 3);
+    return ((M + 255) / 256) * ((N + 255) / 256) >= 512 ? 2 : 1;
+  }
+  if (b_digits == 1) {
+    if (v >= 0) return 10 + std::min(v, 3);
+    return ((M + 255) / 256) * ((N + 127) / 128) >= 512 ? 12 : 13;
+  }
+  return v == 0 ? 20 : 21;
+}
+
 template <int DA, int DB, int WM, int WN>
 int launch(GemmParams p, hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -255,7 +461,38 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
     set_error("bnn_gemm_i8: K == 0 is not supported (pad K to 64 with zeros)");
     return kErrInval;
   }
-  if (a_digits == 1) return launch<1, 1, 2, 2>(p, s);
-  if (b_digits == 1) return launch<3, 1, 2, 2>(p, s);
-  return launch<3, 3, 2, 1>(p, s);
+  switch (pick_kernel(a_digits, b_digits, M, N)) {
+    case 0: return launch<1, 1, 2, 2>(p, s);
+    case 1: return launch_v2<1, 1, 2, 2, 2, 2, 3>(p, s);
+    case 2: return launch_v2<1, 1, 2, 4, 4, 2, 3>(p, s);
+    case 3: return launch_v2<1, 1, 2, 2, 4, 4, 2>(p, s);
+    case 10: return launch<3, 1, 2, 2>(p, s);
+    case 11: return launch_v2<3, 1, 2, 2, 2, 2, 3>(p, s);
+    case 12: return launch_v2<3, 1, 4, 2, 2, 2, 2>(p, s);
+    case 13: return launch_v2<3, 1, 2, 4, 2, 1, 3>(p, s);
+    case 20: return launch<3, 3, 2, 1>(p, s);
+    default: return launch_v2<3, 3, 2, 2, 2, 1, 2>(p, s);
+  }
+}
+
+BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N) {
+  switch (pick_kernel(a_digits, b_digits, M, N)) {
+    case 0: return "gemm_i8_k<1, 1, 2, 2>";
+    case 1: return "gemm_i8_v2_k<1, 1, 2, 2, 2, 2, 3>";
+    case 2: return "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 3>";
+    case 3: return "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2>";
+    case 10: return "gemm_i8_k<3, 1, 2, 2>";
+    case 11: return "gemm_i8_v2_k<3, 1, 2, 2, 2, 2, 3>";
+    case 12: return "gemm_i8_v2_k<3, 1, 4, 2, 2, 2, 2>";
+    case 13: return "gemm_i8_v2_k<3, 1, 2, 4, 2, 1, 3>";
+    case 20: return "gemm_i8_k<3, 3, 2, 1>";
+    default: return "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2>";
+  }
+}
+
+// Tuning hook: select a kernel variant for every later bnn_gemm_i8 call in this process
+// (-1 = built-in default).  Not part of the stable ABI contract; used by tools/gemm_sweep.py.
+BNN_API int bnn_gemm_set_variant(int32_t v) {
+  g_variant = v;
+  return 0;
 }

@@ -90,6 +90,13 @@ int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
                 const float* a_scale, const float* b_scale, const float* bias, float* C,
                 int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
 
+/* Tuning hook (not part of the stable contract): select the bnn_gemm_i8 kernel variant for all
+ * later calls in this process; -1 restores the built-in default table (tools/gemm_sweep.py). */
+int bnn_gemm_set_variant(int32_t variant);
+/* Name of the kernel instance bnn_gemm_i8 launches for this configuration (as rocprofv3 lists
+ * it), so host-side HIP-event timings can be matched with profiles. */
+const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N);
+
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row
  * (multiple of 32, <= lda/ldb in words). */
@@ -116,6 +123,26 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
                           float* db, void* work, int64_t N, int64_t C, int64_t H, int64_t W,
                           int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
                           int32_t dil, int32_t groups, bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
+ * The layers between the binarized GEMMs in the reference Net (mnist-dist2.py:52-74):
+ * nn.BatchNorm1d (train: batch stats, biased var; running stats with the unbiased var and
+ * `momentum`; eval: running stats) optionally followed by nn.Hardtanh (fused: y clamped to
+ * [-1,1] in forward, gradient masked by -1 < y < 1 in backward, y recomputed from x).
+ * x, y, dy, dx fp32 [M][C] row-major, C % 4 == 0, 16-B aligned; gamma/beta nullable (affine off);
+ * running_mean/var nullable in train mode (track_running_stats off; momentum < 0 skips the update).
+ * `work` scratch of bnn_bn_workspace(M, C) bytes.  Deterministic (fixed-order reductions). */
+int64_t bnn_bn_workspace(int64_t M, int64_t C);
+int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps,
+                     float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
+                     bnn_stream_t stream);
+int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+                    const float* running_mean, const float* running_var, float eps, float* y,
+                    int32_t hardtanh, void* work, bnn_stream_t stream);
+int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+               const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
+               float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */

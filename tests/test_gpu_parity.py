@@ -221,3 +221,68 @@ def test_large_forward_exact_vs_rocblas(F):
     y = F.binary_linear(x, w, b, True)
     ref = (torch.sign(x) @ torch.sign(w).t()) + b
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("M,C", [(7, 12), (300, 64), (1000, 1536)])
+@pytest.mark.parametrize("hardtanh", [True, False])
+def test_batchnorm_hardtanh_vs_oracle(F, M, C, hardtanh):
+    """Fused BatchNorm1d(+Hardtanh) (mnist-dist2.py:52-74) against the float64 oracle and torch."""
+    rng = np.random.default_rng(M + C)
+    x = (rng.integers(-40, 40, (M, C)) + rng.standard_normal(C) * 3).astype(np.float32)
+    gamma = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = rng.uniform(-0.2, 0.2, C).astype(np.float32)
+    g = rng.standard_normal((M, C)).astype(np.float32)
+    bn = torch.nn.BatchNorm1d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(dev(gamma))
+        bn.bias.copy_(dev(beta))
+    xt = dev(x).requires_grad_(True)
+    y = F.batch_norm_hardtanh(xt, bn, hardtanh)
+    y.backward(dev(g))
+    yr, cache, rm, rv = O.batchnorm_train(x, gamma, beta, np.zeros(C), np.ones(C))
+    yo = O.hardtanh(yr) if hardtanh else yr
+    assert rel_err(host(y), yo) < 1e-6
+    np.testing.assert_allclose(host(bn.running_mean), rm, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(host(bn.running_var), rv, rtol=1e-5, atol=1e-6)
+    assert int(bn.num_batches_tracked) == 1
+    gm = O.hardtanh_backward(yr, g) if hardtanh else g
+    dx, dgam, dbet = O.batchnorm_backward(cache, gm)
+    assert rel_err(host(xt.grad), dx) < GRAD_TOL
+    assert rel_err(host(bn.weight.grad), dgam) < GRAD_TOL
+    assert rel_err(host(bn.bias.grad), dbet) < GRAD_TOL
+    # eval mode uses the running statistics
+    bn.eval()
+    ye = F.batch_norm_hardtanh(dev(x), bn, hardtanh)
+    ref = torch.nn.functional.batch_norm(dev(x), bn.running_mean, bn.running_var, bn.weight, bn.bias, False,
+                                         0.0, bn.eps)
+    if hardtanh:
+        ref = ref.clamp(-1, 1)
+    assert rel_err(host(ye), host(ref)) < 1e-6
+
+
+def test_fused_mlp_step_matches_unfused(F):
+    """The build's trainer path (fused BN+Hardtanh, latent Adam) against the drop-in path
+    (torch BatchNorm1d/Hardtanh, torch Adam + .org protocol) on one step, dropout off."""
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    from bnn_amd.optim import LatentAdam, org_protocol_step
+    torch.manual_seed(3)
+    a = nets.MLP(256, 128, 64, p_drop=0.0).cuda()
+    b = nets.MLP(256, 128, 64, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    b.load_state_dict(a.state_dict())
+    x, y = synthetic_mnist(128, seed=11, device="cuda")
+    oa = torch.optim.Adam(a.parameters(), lr=0.01)
+    ob = LatentAdam(b.parameters(), lr=0.01, clamp_params=nets.binary_params(b))
+    la = torch.nn.functional.cross_entropy(a(x), y)
+    la.backward()
+    lb = torch.nn.functional.cross_entropy(b(x), y)
+    lb.backward()
+    assert abs(la.item() - lb.item()) < 1e-5
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert close(host(pa.grad), host(pb.grad), 1e-4, 1e-6), n
+    org_protocol_step(a, oa)
+    ob.step()
+    for k in ("fc1", "fc2", "fc3"):
+        wa = getattr(a, k).weight.org
+        wb = getattr(b, k).weight
+        assert close(host(wa), host(wb), 1e-4, 0.0), k
