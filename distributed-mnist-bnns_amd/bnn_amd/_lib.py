@@ -28,7 +28,7 @@ SIGNATURES = {
     "bnn_quant_cols_t": (I32, [P, I64, I64, I64, P, I64, I64, P, P, P, P]),
     "bnn_gemm_i8": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, I64, I64, I64, I64, P]),
     "bnn_gemm_set_variant": (I32, [I32]),
-    "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64]),
+    "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64, I64]),
     "bnn_gemm_xnor": (I32, [P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_conv2d_fwd": (I32, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_conv2d_bwd_data": (I32, [P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),

@@ -82,9 +82,9 @@ def _timed(name, ops=0.0, nbytes=0.0):
 GEMM_PAIRS = {(1, 1): 1, (3, 1): 3, (3, 3): 6}
 
 
-def gemm_kernel_name(a_digits, b_digits, M, N):
+def gemm_kernel_name(a_digits, b_digits, M, N, K):
     """The kernel instance libbnn launches for this GEMM (rocprofv3's name for it)."""
-    return L.lib().bnn_gemm_i8_kernel(a_digits, b_digits, M, N).decode()
+    return L.lib().bnn_gemm_i8_kernel(a_digits, b_digits, M, N, K).decode()
 
 
 def round_up(x, m=ALIGN):
@@ -198,7 +198,7 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
     cfg = (a_digits, b_digits)
     k_true = K if k_true is None else k_true
     ops = 2.0 * M * N * k_true * GEMM_PAIRS[cfg]
-    name = gemm_kernel_name(a_digits, b_digits, M, N) if _TIMER is not None else ""
+    name = gemm_kernel_name(a_digits, b_digits, M, N, K) if _TIMER is not None else ""
     with _timed(name, ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
         L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
                L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())

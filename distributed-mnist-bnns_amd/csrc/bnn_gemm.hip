@@ -239,16 +239,20 @@ __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
-  constexpr int A_ST = DA * BM * BK, B_ST = DB * BN * BK, ST = A_ST + B_ST;
-  constexpr int IA = DA * BM / 16, IB = DB * BN / 16;
+  constexpr int A_ST = DA * BM * BKT, B_ST = DB * BN * BKT, ST = A_ST + B_ST;
+  constexpr int RPI = 1024 / BKT;          // rows covered by one 1-KiB glds
+  constexpr int CPR = BKT / 16;            // 16-B chunks per row
+  constexpr int IA = DA * BM / RPI, IB = DB * BN / RPI;
   static_assert(IA % NW == 0 && IB % NW == 0, "glds instructions must split evenly over waves");
   constexpr int PER_WAVE = (IA + IB) / NW;
   constexpr int NC = Cfg<DA, DB>::NC;
   constexpr bool FLUSH = Cfg<DA, DB>::FLUSH;
+  constexpr int KSTEPS = BKT / 32;
+  constexpr int FLUSH_KT = Cfg<DA, DB>::FLUSH_KT * 64 / BKT;
   __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
 
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -257,23 +261,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   tile_of(blockIdx.x, p.gm, p.gn, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int srow = lane >> 2, sslot = lane & 3;
-  const int schunk = sslot ^ ((srow >> 2) & 3);
+  // chunk swizzle: BK=64 -> chunk ^ ((row>>2)&3); BK=128 -> chunk ^ ((row>>1)&7).  Applied to the
+  // global source (LDS image stays lane-linear) and to the ds_read address.
+  auto swz = [](int row) { return BKT == 64 ? ((row >> 2) & 3) : ((row >> 1) & 7); };
+  // lane -> (row srow of the 1-KiB piece, 16-B slot sslot); the swizzle uses the tile-local row
+  // (piece jr covers rows jr*RPI .. jr*RPI+RPI-1; with BK=128 bit 3 of the row comes from jr).
+  const int srow = lane / CPR, sslot = lane % CPR;
   auto stage = [&](int kt, int buf) {
     char* sA = smem + buf * ST;
     char* sB = sA + A_ST;
-    const int k0 = kt * BK + 16 * schunk;
 #pragma unroll
     for (int j = wave; j < IA; j += NW) {
-      const int d = j / (BM / 16), jr = j % (BM / 16);
-      const int row = min(m0 + jr * 16 + srow, p.M - 1);
-      glds16(p.A + d * p.a_plane + (int64_t)row * p.lda + k0, sA + d * BM * BK + jr * 1024);
+      const int d = j / (BM / RPI), jr = j % (BM / RPI);
+      const int lrow = jr * RPI + srow;
+      const int row = min(m0 + lrow, p.M - 1);
+      const int k0 = kt * BKT + 16 * (sslot ^ swz(lrow));
+      glds16(p.A + d * p.a_plane + (int64_t)row * p.lda + k0, sA + d * BM * BKT + jr * 1024);
     }
 #pragma unroll
     for (int j = wave; j < IB; j += NW) {
-      const int e = j / (BN / 16), jr = j % (BN / 16);
-      const int row = min(n0 + jr * 16 + srow, p.N - 1);
-      glds16(p.B + e * p.b_plane + (int64_t)row * p.ldb + k0, sB + e * BN * BK + jr * 1024);
+      const int e = j / (BN / RPI), jr = j % (BN / RPI);
+      const int lrow = jr * RPI + srow;
+      const int row = min(n0 + lrow, p.N - 1);
+      const int k0 = kt * BKT + 16 * (sslot ^ swz(lrow));
+      glds16(p.B + e * p.b_plane + (int64_t)row * p.ldb + k0, sB + e * BN * BKT + jr * 1024);
     }
   };
 
@@ -294,8 +305,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
         for (int i = 0; i < 16; ++i) facc[t][u][i] = 0.f;
   }
 
-  const int r = lane & 31, h = lane >> 5, sw = (r >> 2) & 3;
-  const int nk = p.K / BK;
+  const int r = lane & 31, h = lane >> 5, sw = swz(r);
+  const int nk = p.K / BKT;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s, s);
@@ -308,19 +319,19 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     const char* sA = smem + buf * ST;
     const char* sB = sA + A_ST;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KSTEPS; ++ks) {
       const int off = 16 * ((2 * ks + h) ^ sw);
       v4i a[DA][WM], b[DB][WN];
 #pragma unroll
       for (int d = 0; d < DA; ++d)
 #pragma unroll
         for (int t = 0; t < WM; ++t)
-          a[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BK + (wm * WM * 32 + t * 32 + r) * BK + off);
+          a[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * 32 + r) * BKT + off);
 #pragma unroll
       for (int e = 0; e < DB; ++e)
 #pragma unroll
         for (int u = 0; u < WN; ++u)
-          b[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BK + (wn * WN * 32 + u * 32 + r) * BK + off);
+          b[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * 32 + r) * BKT + off);
 #pragma unroll
       for (int t = 0; t < WM; ++t)
 #pragma unroll
@@ -343,7 +354,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
         }
     }
     if constexpr (FLUSH) {
-      if ((kt + 1) % Cfg<DA, DB>::FLUSH_KT == 0 || kt + 1 == nk) {
+      if ((kt + 1) % FLUSH_KT == 0 || kt + 1 == nk) {
 #pragma unroll
         for (int t = 0; t < WM; ++t)
 #pragma unroll
@@ -359,62 +370,78 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     }
   }
 
+  // ---- epilogue.  C/D map of the 32x32 MFMA: reg i -> tile row (i&3)+8(i>>2)+4h, col lane&31.
+  // Each 32x32 tile is finished in registers (combine digits, scales, bias), transposed through a
+  // per-wave 4 KiB LDS patch (16-B chunks XOR-swizzled by row: conflict-free both ways) and
+  // written as whole 128-B row segments with 16-B stores (4 per lane instead of 16 dword stores).
+  block_barrier();  // every wave is done reading the last operand stage
+  float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
+  const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
 #pragma unroll
-  for (int t = 0; t < WM; ++t)
+  for (int t = 0; t < WM; ++t) {
+    const int trow0 = m0 + wm * WM * 32 + t * 32;
 #pragma unroll
     for (int u = 0; u < WN; ++u) {
-      const int col = n0 + wn * WN * 32 + u * 32 + r;
-      if (col >= p.N) continue;
-      const float bs = p.b_scale ? p.b_scale[col] : 1.f;
-      const float bb = p.bias ? p.bias[col] : 0.f;
+      const int tcol0 = n0 + wn * WN * 32 + u * 32;
+      const int col = tcol0 + r;
+      const bool cin = col < p.N;
+      const float bb = (p.bias && cin) ? p.bias[col] : 0.f;
+      const double bs = (p.b_scale && cin) ? (double)p.b_scale[col] : 1.0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int row = m0 + wm * WM * 32 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        double v;
+        const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int row = min(trow0 + lr, p.M - 1);
+        float f;
         if constexpr (DA == 1 && DB == 1) {
-          v = (double)acc[0][t][u][i];
-        } else if constexpr (DB == 1) {
-          v = (double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 + (double)acc[0][t][u][i];
+          f = (float)acc[0][t][u][i];  // exact: |sum| <= K < 2^24
+          if (p.a_scale || p.b_scale)
+            f = (float)((double)f * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
         } else {
-          v = (double)facc[t][u][i] * 65536.0;
+          double v;
+          if constexpr (DB == 1) {
+            v = (double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 + (double)acc[0][t][u][i];
+          } else {
+            v = (double)facc[t][u][i] * 65536.0;
+          }
+          f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
         }
-        if (p.a_scale) v *= (double)p.a_scale[row];
-        v *= (double)bs;
-        float f = (float)v;
         if (p.bias) f += bb;
-        p.C[(int64_t)row * p.ldc + col] = f;
+        patch[lr * 32 + ((((r >> 2) ^ (lr & 7)) << 2) | (r & 3))] = f;
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int lr = (lane >> 3) + 8 * ps, c4 = lane & 7;
+        const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
+        const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
+        if (row >= p.M) continue;
+        float* dst = p.C + (int64_t)row * p.ldc + c0;
+        if (vec_ok && c0 + 3 < p.N) {
+          *reinterpret_cast<float4*>(dst) = v;
+        } else {
+          const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c0 + j < p.N) dst[j] = vs[j];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+  }
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT>
 int launch_v2(GemmParams p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
   const int64_t nblk = (int64_t)p.gm * p.gn;
-  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT>), dim3((unsigned)nblk),
                      dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   return check_launch("bnn_gemm_i8");
 }
 
 int g_variant = -1;  // tuning hook (bnn_gemm_set_variant); -1 = default table
-
-// Kernel choice per digit configuration and shape (tools/gemm_sweep.py on MI355X, round 1):
-// 256x256 (8 waves) / 256x128 tiles once the grid has >= 512 of them, smaller tiles otherwise.
-int pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N) {
-  const int v = g_variant;
-  if (a_digits == 1) {
-    if (v >= 0) return std::min(v, 3);
-    return ((M + 255) / 256) * ((N + 255) / 256) >= 512 ? 2 : 1;
-  }
-  if (b_digits == 1) {
-    if (v >= 0) return 10 + std::min(v, 3);
-    return ((M + 255) / 256) * ((N + 127) / 128) >= 512 ? 12 : 13;
-  }
-  return v == 0 ? 20 : 21;
-}
 
 template <int DA, int DB, int WM, int WN>
 int launch(GemmParams p, hipStream_t s) {
@@ -422,12 +449,64 @@ int launch(GemmParams p, hipStream_t s) {
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
   const int64_t nblk = (int64_t)p.gm * p.gn;
-  if (nblk > 0x7fffffff) {
-    set_error("bnn_gemm_i8: too many tiles");
-    return kErrInval;
-  }
   hipLaunchKernelGGL((gemm_i8_k<DA, DB, WM, WN>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   return check_launch("bnn_gemm_i8");
+}
+
+// Kernel table; the default choice per digit configuration and shape comes from
+// tools/gemm_sweep.py on MI355X (profiles/r01_gemm_sweep*.log).
+struct Variant {
+  int id;
+  const char* name;  // as rocprofv3 lists the instance
+  int (*fn)(GemmParams, hipStream_t);
+  int bk;
+};
+
+const Variant kVariants[] = {
+    {0, "gemm_i8_k<1, 1, 2, 2>", launch<1, 1, 2, 2>, 64},
+    {1, "gemm_i8_v2_k<1, 1, 2, 2, 2, 2, 3, 64>", launch_v2<1, 1, 2, 2, 2, 2, 3, 64>, 64},
+    {2, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 3, 64>", launch_v2<1, 1, 2, 4, 4, 2, 3, 64>, 64},
+    {3, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128>, 128},
+    {4, "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2, 64>", launch_v2<1, 1, 2, 2, 4, 4, 2, 64>, 64},
+    {10, "gemm_i8_k<3, 1, 2, 2>", launch<3, 1, 2, 2>, 64},
+    {11, "gemm_i8_v2_k<3, 1, 2, 2, 2, 2, 3, 64>", launch_v2<3, 1, 2, 2, 2, 2, 3, 64>, 64},
+    {12, "gemm_i8_v2_k<3, 1, 4, 2, 2, 2, 2, 64>", launch_v2<3, 1, 4, 2, 2, 2, 2, 64>, 64},
+    {13, "gemm_i8_v2_k<3, 1, 2, 4, 2, 1, 3, 64>", launch_v2<3, 1, 2, 4, 2, 1, 3, 64>, 64},
+    {14, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128>, 128},
+    {15, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 3, 64>", launch_v2<3, 1, 2, 4, 2, 2, 3, 64>, 64},
+    {20, "gemm_i8_k<3, 3, 2, 1>", launch<3, 3, 2, 1>, 64},
+    {21, "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2, 64>", launch_v2<3, 3, 2, 2, 2, 1, 2, 64>, 64},
+    {22, "gemm_i8_v2_k<3, 3, 2, 4, 2, 1, 2, 64>", launch_v2<3, 3, 2, 4, 2, 1, 2, 64>, 64},
+};
+
+const Variant* find_variant(int id) {
+  for (const Variant& v : kVariants)
+    if (v.id == id) return &v;
+  return nullptr;
+}
+
+const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int64_t K) {
+  const int base = a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20);
+  int id, alt;  // alt = the BK=64 sibling used when K % 128 != 0
+  if (g_variant >= 0) {
+    id = base + g_variant;
+    alt = base + 1;
+  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 0.41 of peak; 128x128 on small grids
+    const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
+    id = big ? 3 : 1;
+    alt = big ? 2 : 1;
+  } else if (b_digits == 1) {   // 128x256 BK128 8 waves: 0.46-0.49 of peak on dX / dW
+    const bool big = ((M + 127) / 128) * ((N + 255) / 256) >= 256;
+    id = big ? 14 : 13;
+    alt = big ? 15 : 13;
+  } else {
+    id = 22;
+    alt = 22;
+  }
+  const Variant* v = find_variant(id);
+  if (v == nullptr) v = find_variant(base + 1);
+  if (K % v->bk != 0) v = find_variant(alt);
+  return v;
 }
 
 }  // namespace
@@ -441,12 +520,13 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
                         int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
   const bool cfg_ok = (a_digits == 1 && b_digits == 1) || (a_digits == 3 && b_digits == 1) ||
                       (a_digits == 3 && b_digits == 3);
-  if (!A || !B || !C || !cfg_ok || M < 0 || N < 0 || K < 0 || K % BK != 0 || lda < K || ldb < K ||
+  if (!A || !B || !C || !cfg_ok || M < 0 || N < 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K ||
       lda % 16 != 0 || ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) ||
       M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff ||
       (a_digits > 1 && (a_plane < M * lda || a_plane % 16 != 0)) ||
       (b_digits > 1 && (b_plane < N * ldb || b_plane % 16 != 0))) {
-    set_error("bnn_gemm_i8: bad arguments (M=%lld N=%lld K=%lld lda=%lld ldb=%lld digits=%d,%d)",
+    set_error("bnn_gemm_i8: bad arguments (M=%lld N=%lld K=%lld lda=%lld ldb=%lld digits=%d,%d; "
+              "K must be a positive multiple of 64)",
               (long long)M, (long long)N, (long long)K, (long long)lda, (long long)ldb, a_digits,
               b_digits);
     return kErrInval;
@@ -454,40 +534,12 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
   if (M == 0 || N == 0) return 0;
   GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
                (int)M, (int)N, (int)K, 0, 0};
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (K == 0) {
-    // Empty reduction: C = bias (or 0).  Reuse the kernel with one zero k-tile is not possible
-    // without operand memory, so handle it here.
-    set_error("bnn_gemm_i8: K == 0 is not supported (pad K to 64 with zeros)");
-    return kErrInval;
-  }
-  switch (pick_kernel(a_digits, b_digits, M, N)) {
-    case 0: return launch<1, 1, 2, 2>(p, s);
-    case 1: return launch_v2<1, 1, 2, 2, 2, 2, 3>(p, s);
-    case 2: return launch_v2<1, 1, 2, 4, 4, 2, 3>(p, s);
-    case 3: return launch_v2<1, 1, 2, 2, 4, 4, 2>(p, s);
-    case 10: return launch<3, 1, 2, 2>(p, s);
-    case 11: return launch_v2<3, 1, 2, 2, 2, 2, 3>(p, s);
-    case 12: return launch_v2<3, 1, 4, 2, 2, 2, 2>(p, s);
-    case 13: return launch_v2<3, 1, 2, 4, 2, 1, 3>(p, s);
-    case 20: return launch<3, 3, 2, 1>(p, s);
-    default: return launch_v2<3, 3, 2, 2, 2, 1, 2>(p, s);
-  }
+  return pick_kernel(a_digits, b_digits, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 
-BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N) {
-  switch (pick_kernel(a_digits, b_digits, M, N)) {
-    case 0: return "gemm_i8_k<1, 1, 2, 2>";
-    case 1: return "gemm_i8_v2_k<1, 1, 2, 2, 2, 2, 3>";
-    case 2: return "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 3>";
-    case 3: return "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2>";
-    case 10: return "gemm_i8_k<3, 1, 2, 2>";
-    case 11: return "gemm_i8_v2_k<3, 1, 2, 2, 2, 2, 3>";
-    case 12: return "gemm_i8_v2_k<3, 1, 4, 2, 2, 2, 2>";
-    case 13: return "gemm_i8_v2_k<3, 1, 2, 4, 2, 1, 3>";
-    case 20: return "gemm_i8_k<3, 3, 2, 1>";
-    default: return "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2>";
-  }
+BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,
+                                       int64_t K) {
+  return pick_kernel(a_digits, b_digits, M, N, K)->name;
 }
 
 // Tuning hook: select a kernel variant for every later bnn_gemm_i8 call in this process

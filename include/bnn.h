@@ -95,7 +95,8 @@ int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
 int bnn_gemm_set_variant(int32_t variant);
 /* Name of the kernel instance bnn_gemm_i8 launches for this configuration (as rocprofv3 lists
  * it), so host-side HIP-event timings can be matched with profiles. */
-const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N);
+const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,
+                               int64_t K);
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row

@@ -286,3 +286,53 @@ def test_fused_mlp_step_matches_unfused(F):
         wa = getattr(a, k).weight.org
         wb = getattr(b, k).weight
         assert close(host(wa), host(wb), 1e-4, 0.0), k
+
+
+@pytest.mark.parametrize("cfg", [(1, 1), (3, 1), (3, 3)])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 256), (257, 520, 384), (64, 64, 64), (1000, 129, 1024)])
+def test_every_gemm_variant_is_exact(F, cfg, M, N, K):
+    """Every kernel in the bnn_gemm_i8 variant table (tools/gemm_sweep.py) against an exact int64
+    reference, including K not a multiple of 128 and ragged M, N."""
+    from bnn_amd import _lib
+    da, db = cfg
+    rng = np.random.default_rng(M + N + K + da + db)
+    A = rng.integers(-128, 128, (da, M, K)).astype(np.int8)
+    B = (rng.integers(-1, 2, (db, N, K)) if db == 1 else rng.integers(-128, 128, (db, N, K))).astype(np.int8)
+    if da == 3:
+        A[2] //= 2
+    if db == 3:
+        B[2] //= 2
+    bias = rng.standard_normal(N).astype(np.float32)
+    sa = np.exp2(rng.integers(-30, -10, M)).astype(np.float32) if da == 3 else None
+    sb = np.exp2(rng.integers(-30, -10, N)).astype(np.float32) if db == 3 else None
+    w = [1 << (8 * d) for d in range(3)]
+    acc = np.zeros((M, N), np.float64)
+    for i in range(da):
+        for j in range(db):
+            if da == 3 and db == 3 and i + j < 2:
+                continue                      # pairs the kernel drops (weight <= 2^-24 of the top)
+            acc += (w[i] if da == 3 else 1) * (w[j] if db == 3 else 1) * (
+                A[i].astype(np.int64) @ B[j].astype(np.int64).T).astype(np.float64)
+    if sa is not None:
+        acc *= sa[:, None]
+    if sb is not None:
+        acc *= sb[None, :]
+    ref = acc.astype(np.float32) + bias
+    At = dev(A if da == 3 else A[0])
+    Bt = dev(B if db == 3 else B[0])
+    names = set()
+    try:
+        for v in range(0, 6):
+            _lib.call("bnn_gemm_set_variant", v)
+            name = F.gemm_kernel_name(da, db, M, N, K)
+            if name in names:
+                continue
+            names.add(name)
+            C = host(F.gemm_i8(At, da, Bt, db, M, N, a_scale=dev(sa) if sa is not None else None,
+                               b_scale=dev(sb) if sb is not None else None, bias=dev(bias)))
+            if cfg == (1, 1):
+                assert np.array_equal(C, ref), name
+            else:
+                assert rel_err(C, ref) < 1e-6, name
+    finally:
+        _lib.call("bnn_gemm_set_variant", -1)

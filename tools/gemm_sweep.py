@@ -19,6 +19,7 @@ PEAK = 256 * 4 * 2048 * 2.4e9 / 1e12
 
 SHAPES = {  # name: (M, N, K, a_digits, b_digits)
     "fwd_fc2": (65536, 8192, 8192, 1, 1),
+    "fwd_k128": (65536, 8192, 128, 1, 1),
     "fc1_fwd": (65536, 8192, 832, 3, 1),
     "dx_fc2": (65536, 8192, 8192, 3, 1),
     "dw_fc2": (8192, 8192, 65536, 3, 1),
@@ -31,7 +32,7 @@ SHAPES = {  # name: (M, N, K, a_digits, b_digits)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="0,1,2,3,-1")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,-1")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -48,8 +49,13 @@ def main():
         sa = torch.ones(M, device="cuda") if da > 1 else None
         ref = None
         pairs = BF.GEMM_PAIRS[(da, db)]
+        seen = set()
         for v in (int(x) for x in args.variants.split(",")):
             L.call("bnn_gemm_set_variant", v)
+            kname = BF.gemm_kernel_name(da, db, M, N, K)
+            if kname in seen:
+                continue
+            seen.add(kname)
             C = BF.gemm_i8(A, da, B, db, M, N, a_scale=sa)
             torch.cuda.synchronize()
             same = True if ref is None else bool(torch.equal(C, ref))
@@ -63,7 +69,7 @@ def main():
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / args.reps
             tops = 2.0 * M * N * K * pairs / (ms * 1e-3) / 1e12
-            print(json.dumps({"shape": name, "variant": v, "kernel": BF.gemm_kernel_name(da, db, M, N),
+            print(json.dumps({"shape": name, "variant": v, "kernel": BF.gemm_kernel_name(da, db, M, N, K),
                               "ms": round(ms, 3), "tops": round(tops, 1),
                               "frac": round(tops / PEAK, 3), "matches_first": same}), flush=True)
         L.call("bnn_gemm_set_variant", -1)
