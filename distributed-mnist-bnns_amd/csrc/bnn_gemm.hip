@@ -214,23 +214,26 @@ __global__ __launch_bounds__(256) void gemm_i8_k(GemmParams p) {
 // v2: WAVES_M x WAVES_N waves, STAGES-deep LDS ring filled by global_load_lds, counted vmcnt
 // (the next STAGES-2 tiles stay in flight across the barrier), raw s_barrier (a __syncthreads()
 // would drain every in-flight LDS-DMA with vmcnt(0)).
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  // s_waitcnt simm16 (gfx9): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
-#define BNN_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14))
-  switch (n) {
-    case 0: BNN_VMCNT(0); break;
-    case 2: BNN_VMCNT(2); break;
-    case 3: BNN_VMCNT(3); break;
-    case 4: BNN_VMCNT(4); break;
-    case 6: BNN_VMCNT(6); break;
-    case 7: BNN_VMCNT(7); break;
-    case 8: BNN_VMCNT(8); break;
-    case 12: BNN_VMCNT(12); break;
-    case 14: BNN_VMCNT(14); break;
-    case 16: BNN_VMCNT(16); break;
-    default: BNN_VMCNT(0); break;
+// s_waitcnt simm16 (gfx9 encoding): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_c() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Wait until at most `ahead` stages (PER_WAVE loads each) of this wave's LDS-DMA remain in flight.
+template <int PER_WAVE, int MAX_AHEAD>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  if constexpr (MAX_AHEAD >= 3) {
+    if (ahead >= 3) { wait_vmcnt_c<3 * PER_WAVE>(); return; }
   }
-#undef BNN_VMCNT
+  if constexpr (MAX_AHEAD >= 2) {
+    if (ahead == 2) { wait_vmcnt_c<2 * PER_WAVE>(); return; }
+  }
+  if constexpr (MAX_AHEAD >= 1) {
+    if (ahead == 1) { wait_vmcnt_c<PER_WAVE>(); return; }
+  }
+  wait_vmcnt_c<0>();
 }
 
 __device__ __forceinline__ void block_barrier() {
@@ -239,7 +242,7 @@ __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
@@ -312,46 +315,67 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     if (s < nk) stage(s, s);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(STAGES - 2, nk - 1 - kt);
-    wait_vmcnt(PER_WAVE * ahead);
+    wait_stages<PER_WAVE, STAGES - 2>(ahead);
     block_barrier();
     if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const int buf = kt % STAGES;
     const char* sA = smem + buf * ST;
     const char* sB = sA + A_ST;
-#pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks) {
+    // fragments of k-step ks+1 are read from LDS while the MFMAs of k-step ks run (register
+    // double buffer; indices are compile-time after unrolling)
+    v4i a[2][DA][WM], b[2][DB][WN];
+    auto load_frags = [&](int ks, v4i (&fa)[DA][WM], v4i (&fb)[DB][WN]) {
       const int off = 16 * ((2 * ks + h) ^ sw);
-      v4i a[DA][WM], b[DB][WN];
 #pragma unroll
       for (int d = 0; d < DA; ++d)
 #pragma unroll
         for (int t = 0; t < WM; ++t)
-          a[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * 32 + r) * BKT + off);
+          fa[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * 32 + r) * BKT + off);
 #pragma unroll
       for (int e = 0; e < DB; ++e)
 #pragma unroll
         for (int u = 0; u < WN; ++u)
-          b[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * 32 + r) * BKT + off);
+          fb[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * 32 + r) * BKT + off);
+    };
+    load_frags(0, a[0], b[0]);
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      if (ks + 1 < KSTEPS) load_frags(ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+      const int cur = ks & 1;
 #pragma unroll
       for (int t = 0; t < WM; ++t)
 #pragma unroll
         for (int u = 0; u < WN; ++u) {
           if constexpr (DA == 1 && DB == 1) {
-            acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0][t], b[0][u], acc[0][t][u], 0, 0, 0);
+            acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][0][t], b[cur][0][u], acc[0][t][u], 0, 0, 0);
           } else if constexpr (DB == 1) {
 #pragma unroll
             for (int d = 0; d < DA; ++d)
-              acc[d][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[d][t], b[0][u], acc[d][t][u], 0, 0, 0);
+              acc[d][t][u] =
+                  __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][d][t], b[cur][0][u], acc[d][t][u], 0, 0, 0);
           } else {
 #pragma unroll
             for (int i = 0; i < DA; ++i)
 #pragma unroll
               for (int j = 0; j < DB; ++j)
                 if (i + j >= 2)
-                  acc[i + j - 2][t][u] =
-                      __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i][t], b[j][u], acc[i + j - 2][t][u], 0, 0, 0);
+                  acc[i + j - 2][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][i][t], b[cur][j][u],
+                                                                               acc[i + j - 2][t][u], 0, 0, 0);
           }
         }
+      if constexpr (IL == 1) {
+        // interleave: one MFMA of step ks, then one LDS fragment read of step ks+1
+        constexpr int NLD = DA * WM + DB * WN;
+        constexpr int NMF = WM * WN * (DA == 1 ? 1 : (DB == 1 ? DA : 6));
+        if (ks + 1 < KSTEPS) {
+#pragma unroll
+          for (int q = 0; q < NLD; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NMF - NLD, 0);
+        }
+      }
     }
     if constexpr (FLUSH) {
       if ((kt + 1) % FLUSH_KT == 0 || kt + 1 == nk) {
@@ -430,13 +454,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   }
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0>
 int launch_v2(GemmParams p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
   const int64_t nblk = (int64_t)p.gm * p.gn;
-  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL>), dim3((unsigned)nblk),
                      dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   return check_launch("bnn_gemm_i8");
 }
@@ -468,12 +492,15 @@ const Variant kVariants[] = {
     {2, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 3, 64>", launch_v2<1, 1, 2, 4, 4, 2, 3, 64>, 64},
     {3, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128>, 128},
     {4, "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2, 64>", launch_v2<1, 1, 2, 2, 4, 4, 2, 64>, 64},
+    {5, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 4, 64>", launch_v2<1, 1, 2, 4, 4, 2, 4, 64>, 64},
+    {6, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1>, 128},
     {10, "gemm_i8_k<3, 1, 2, 2>", launch<3, 1, 2, 2>, 64},
     {11, "gemm_i8_v2_k<3, 1, 2, 2, 2, 2, 3, 64>", launch_v2<3, 1, 2, 2, 2, 2, 3, 64>, 64},
     {12, "gemm_i8_v2_k<3, 1, 4, 2, 2, 2, 2, 64>", launch_v2<3, 1, 4, 2, 2, 2, 2, 64>, 64},
     {13, "gemm_i8_v2_k<3, 1, 2, 4, 2, 1, 3, 64>", launch_v2<3, 1, 2, 4, 2, 1, 3, 64>, 64},
     {14, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128>, 128},
     {15, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 3, 64>", launch_v2<3, 1, 2, 4, 2, 2, 3, 64>, 64},
+    {16, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 4, 64>", launch_v2<3, 1, 2, 4, 2, 2, 4, 64>, 64},
     {20, "gemm_i8_k<3, 3, 2, 1>", launch<3, 3, 2, 1>, 64},
     {21, "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2, 64>", launch_v2<3, 3, 2, 2, 2, 1, 2, 64>, 64},
     {22, "gemm_i8_v2_k<3, 3, 2, 4, 2, 1, 2, 64>", launch_v2<3, 3, 2, 4, 2, 1, 2, 64>, 64},
@@ -491,9 +518,9 @@ const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int
   if (g_variant >= 0) {
     id = base + g_variant;
     alt = base + 1;
-  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 0.41 of peak; 128x128 on small grids
+  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 interleaved 0.44 of peak; 128x128 on small grids
     const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
-    id = big ? 3 : 1;
+    id = big ? 6 : 1;
     alt = big ? 2 : 1;
   } else if (b_digits == 1) {   // 128x256 BK128 8 waves: 0.46-0.49 of peak on dX / dW
     const bool big = ((M + 127) / 128) * ((N + 255) / 256) >= 256;

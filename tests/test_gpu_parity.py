@@ -322,7 +322,7 @@ def test_every_gemm_variant_is_exact(F, cfg, M, N, K):
     Bt = dev(B if db == 3 else B[0])
     names = set()
     try:
-        for v in range(0, 6):
+        for v in range(0, 8):
             _lib.call("bnn_gemm_set_variant", v)
             name = F.gemm_kernel_name(da, db, M, N, K)
             if name in names:

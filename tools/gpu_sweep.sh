@@ -1,5 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread > gpurun_out/parity.log 2>&1; echo "PARITY EXIT $?"; tail -2 gpurun_out/parity.log
-timeout -k 10 400 python -u tools/gemm_sweep.py --reps 3 > gpurun_out/sweep.log 2>&1 || { echo SWEEP FAIL; tail -20 gpurun_out/sweep.log; exit 1; }
-cat gpurun_out/sweep.log | cut -c1-200
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread -k "variant" > gpurun_out/parity.log 2>&1; echo "PARITY EXIT $?"; tail -2 gpurun_out/parity.log
+timeout -k 10 400 python -u tools/gemm_sweep.py --reps 3 ${SWEEP_ARGS:-} > gpurun_out/sweep.log 2>&1 || { echo SWEEP FAIL; tail -20 gpurun_out/sweep.log; exit 1; }
+cut -c1-160 gpurun_out/sweep.log
