@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = config default)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--backend", default="mfma", choices=["mfma", "xnor"])
+    ap.add_argument("--backend", default="fp4", choices=["fp4", "mfma", "xnor"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -174,7 +174,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8-mfma (ternary operands, exact int32 sums; fp32 I/O)",
+        "dtype": "fp4/int8 MFMA (ternary operands as FP4 e2m1 / int8, fp32 digit planes as int8; exact integer sums; fp32 I/O)",
         "data": "synthetic MNIST-shaped (80.7% zero pixels, u8/255), random-init weights, resident in HBM",
         "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
@@ -182,7 +182,7 @@ def main():
     }
     if ksum:
         # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (logical 2MNK)
-        fwd = [v for k, v in ksum.items() if k.startswith("gemm_i8") and "<1, 1," in k]
+        fwd = [v for k, v in ksum.items() if k.startswith("gemm_i8") and "<1, 1," in k]   # ternary forms
         if fwd:
             ops, ms_ = sum(v["ops"] for v in fwd), sum(v["ms"] for v in fwd)
             result["binary_gemm_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)

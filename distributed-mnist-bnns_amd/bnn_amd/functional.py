@@ -20,6 +20,7 @@ from . import _lib as L
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
     "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "batch_norm_hardtanh",
+    "bn_hardtanh_binary_linear",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
 
@@ -134,6 +135,21 @@ def sign_pack(x, want_q=True, want_qt=False):
     return q, qt
 
 
+def sign_pack_fp4(x, want_qt=False):
+    """fp32 [M,K] -> (q4 uint8 [M, ldq4] FP4 e2m1 ternary nibbles, qt int8 [K, ldqt] or None).
+    ldq4 = round_up(K, 256) / 2 bytes (zero nibbles beyond K)."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    q4 = torch.empty((M, round_up(K, 256) // 2), dtype=torch.uint8, device=x.device)
+    qt = torch.empty((K, round_up(M)), dtype=torch.int8, device=x.device) if want_qt else None
+    nbytes = 4 * M * K + q4.numel() + (qt.numel() if qt is not None else 0)
+    with _timed("sign_pack_tile_k<1>", 0, nbytes):
+        L.call("bnn_sign_pack_fp4", L.ptr(x), M, K, K, L.ptr(q4), q4.shape[1], L.ptr(qt),
+               qt.shape[1] if qt is not None else 0, L.stream())
+    return q4, qt
+
+
 def sign_pack_bits(x, words=None):
     """fp32 [M,K] -> (sign bits, nonzero bits) int32 [M, words], words >= ceil(K/32)."""
     _check(x)
@@ -205,6 +221,20 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
     return C
 
 
+def gemm_fp4(A4, B4, M, N, bias=None, k_true=None):
+    """Ternary x ternary GEMM on FP4-packed operands (2 elements per byte): C = A.B^T + bias."""
+    Kb = A4.shape[-1]
+    assert B4.shape[-1] == Kb and Kb % ALIGN == 0
+    C = torch.empty((M, N), dtype=torch.float32, device=A4.device)
+    if M == 0 or N == 0:
+        return C
+    k_true = 2 * Kb if k_true is None else k_true
+    name = gemm_kernel_name(0, 0, M, N, Kb) if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * k_true, (M + N) * Kb + 4 * M * N):
+        L.call("bnn_gemm_fp4", L.ptr(A4), Kb, L.ptr(B4), Kb, L.ptr(bias), L.ptr(C), N, M, N, Kb, L.stream())
+    return C
+
+
 def gemm_xnor(a_bits, b_bits, M, N, bias=None):
     """XNOR-popcount GEMM on (sign, nonzero) bit-plane pairs; same result as the (1,1) int8 form."""
     (As, An), (Bs, Bn) = a_bits, b_bits
@@ -223,7 +253,7 @@ class BinaryLinearFunction(torch.autograd.Function):
     """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, binarize_input, backend="mfma"):
+    def forward(ctx, x, weight, bias, binarize_input, backend="fp4"):
         _check(x, weight, bias)
         M, K = x.shape
         N = weight.shape[0]
@@ -231,7 +261,11 @@ class BinaryLinearFunction(torch.autograd.Function):
         wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dx)
         b = bias.detach() if bias is not None else None
         if binarize_input:
-            if backend == "xnor":
+            if backend == "fp4":
+                x4, xqt = sign_pack_fp4(x, want_qt=need_dw)
+                w4, _ = sign_pack_fp4(weight)
+                y = gemm_fp4(x4, w4, M, N, bias=b, k_true=K)
+            elif backend == "xnor":
                 y = gemm_xnor(sign_pack_bits(x), sign_pack_bits(weight), M, N, bias=b)
                 xqt = sign_pack(x, want_q=False, want_qt=True)[1] if need_dw else None
             else:
@@ -269,7 +303,7 @@ class BinaryLinearFunction(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-def binary_linear(x, weight, bias=None, binarize_input=True, backend="mfma"):
+def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4"):
     """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened)."""
     lead = x.shape[:-1]
     y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend)
@@ -408,10 +442,8 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
                 None, None, None, None, None, None)
 
 
-def batch_norm_hardtanh(x, bn, hardtanh=True):
-    """Apply an ``nn.BatchNorm1d`` module (its parameters, buffers, momentum / eps /
-    track_running_stats semantics as in torch's ``_BatchNorm.forward``) followed by Hardtanh,
-    through libbnn."""
+def _bn_module_args(bn):
+    """torch _BatchNorm.forward bookkeeping: (running_mean, running_var, use_batch_stats, factor)."""
     factor = 0.0 if bn.momentum is None else bn.momentum
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
@@ -421,5 +453,96 @@ def batch_norm_hardtanh(x, bn, hardtanh=True):
     pass_stats = (not bn.training) or bn.track_running_stats
     rm = bn.running_mean if pass_stats else None
     rv = bn.running_var if pass_stats else None
+    return rm, rv, bn_training, factor
+
+
+def batch_norm_hardtanh(x, bn, hardtanh=True):
+    """Apply an ``nn.BatchNorm1d`` module (its parameters, buffers, momentum / eps /
+    track_running_stats semantics as in torch's ``_BatchNorm.forward``) followed by Hardtanh,
+    through libbnn."""
+    rm, rv, bn_training, factor = _bn_module_args(bn)
     return BatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
                                            hardtanh)
+
+
+class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
+    """fc(hardtanh(bn(z))) with fc a BinarizeLinear whose input is binarised (the hidden layers
+    of the reference Net, mnist-dist2.py:66-71): BatchNorm statistics, then ONE pass writes the
+    next GEMM's ternary operand (FP4 or int8 rows + int8 transpose) straight from z -- the fp32
+    hardtanh output the reference materialises is never written.  Backward: dh = dY.W_b and
+    dW = dY^T.sign(h) on the digit GEMM, then the fused BatchNorm+Hardtanh backward."""
+
+    @staticmethod
+    def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend):
+        _check(z, bn_w, bn_b, rm, rv, weight, bias)
+        z = _c2d(z)
+        M, C = z.shape
+        N = weight.shape[0]
+        gw = bn_w.detach() if bn_w is not None else None
+        gb = bn_b.detach() if bn_b is not None else None
+        if training:
+            mean = torch.empty((C,), dtype=torch.float32, device=z.device)
+            invstd = torch.empty_like(mean)
+            ws = _bn_ws(M, C, z.device)
+            with _timed("bn_fwd_stats", 0, 4 * M * C):
+                L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv),
+                       float(momentum if momentum is not None else -1.0), float(eps), L.ptr(mean),
+                       L.ptr(invstd), None, 1, L.ptr(ws), L.stream())
+        else:
+            mean = rm.contiguous()
+            invstd = (rv + eps).rsqrt()
+        need_dh = any(ctx.needs_input_grad[:3])
+        need_dw = ctx.needs_input_grad[8]
+        fp4 = backend == "fp4"
+        q = torch.empty((M, round_up(C, 256) // 2) if fp4 else (M, round_up(C)),
+                        dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
+        qt = torch.empty((C, round_up(M)), dtype=torch.int8, device=z.device) if need_dw else None
+        with _timed("bn_apply_pack", 0, 4 * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
+            L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(gw), L.ptr(gb),
+                   1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
+                   L.stream())
+        b = bias.detach() if bias is not None else None
+        if fp4:
+            w4, _ = sign_pack_fp4(weight)
+            wqt = sign_pack(weight, want_q=False, want_qt=True)[1] if need_dh else None
+            y = gemm_fp4(q, w4, M, N, bias=b, k_true=C)
+        else:
+            wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dh)
+            y = gemm_i8(q, 1, wq, 1, M, N, bias=b, k_true=C)
+        ctx.save_for_backward(z, gw, gb, mean, invstd, qt, wqt)
+        ctx.dims = (M, C, N)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, gw, gb, mean, invstd, qt, wqt = ctx.saved_tensors
+        M, C, N = ctx.dims
+        dy = _c2d(dy)
+        dz = dgw = dgb = dw = db = None
+        need_db = ctx.has_bias and ctx.needs_input_grad[9]
+        if ctx.needs_input_grad[8] or need_db:
+            dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)
+            if ctx.needs_input_grad[8]:
+                dw = gemm_i8(dt, 3, qt, 1, N, C, a_scale=sc, k_true=M)       # dY^T . sign(h)
+            db = cs
+        if any(ctx.needs_input_grad[:3]):
+            d, s = quant_rows(dy)
+            dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)             # dY . W_b
+            dz = torch.empty_like(z)
+            dgw = torch.empty((C,), dtype=torch.float32, device=z.device) if gw is not None else None
+            dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None
+            ws = _bn_ws(M, C, z.device)
+            with _timed("bn_bwd", 0, 16 * M * C):
+                L.call("bnn_bn_bwd", L.ptr(z), L.ptr(dh), M, C, L.ptr(gw), L.ptr(gb), L.ptr(mean),
+                       L.ptr(invstd), 1, L.ptr(dz), L.ptr(dgw), L.ptr(dgb), L.ptr(ws), L.stream())
+        return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, dw, db, None)
+
+
+def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4"):
+    """fc(hardtanh(bn(z))) through BNHardtanhBinaryLinearFunction (bn: nn.BatchNorm1d, fc: a
+    BinarizeLinear holding its latent weight, i.e. ``org_protocol = False``)."""
+    rm, rv, bn_training, factor = _bn_module_args(bn)
+    return BNHardtanhBinaryLinearFunction.apply(z, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
+                                                fc.weight, fc.bias, backend)

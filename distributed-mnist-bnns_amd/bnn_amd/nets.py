@@ -54,11 +54,18 @@ class MLP(nn.Module):
             return BF.batch_norm_hardtanh(x, bn)
         return ht(bn(x))
 
+    def _bnh_fc(self, bn, ht, fc, z):
+        """fc(ht(bn(z))); fused into one libbnn op (no fp32 hardtanh output) when the fc keeps
+        its latent weight in the Parameter and runs an MFMA backend."""
+        if (self.fused_bn and z.is_cuda and z.dim() == 2 and z.shape[1] % 4 == 0 and not fc.org_protocol
+                and fc.backend in ("fp4", "mfma")):
+            return BF.bn_hardtanh_binary_linear(z, bn, fc, fc.backend)
+        return fc(self._bnh(bn, ht, z))
+
     def forward(self, x):
         x = x.view(-1, 28 * 28)
-        x = self._bnh(self.bn1, self.htanh1, self.fc1(x))
-        x = self._bnh(self.bn2, self.htanh2, self.fc2(x))
-        x = self.fc3(x)
+        x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, self.fc1(x))
+        x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x)
         x = self.drop(x)
         x = self._bnh(self.bn3, self.htanh3, x)
         x = self.fc4(x)

@@ -84,7 +84,7 @@ def _apply_org_protocol(p):
 class BinarizeLinear(nn.Linear):
     org_protocol = True
     mutate_input = True
-    backend = "mfma"       # or "xnor" (VALU popcount path)
+    backend = "fp4"        # ternary GEMM engine: "fp4" (FP4 MFMA), "mfma" (int8 MFMA), "xnor" (VALU)
 
     def __init__(self, *kargs, **kwargs):
         super().__init__(*kargs, **kwargs)

@@ -241,7 +241,7 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
                              void* stream) {
-  if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !y || !work || !aligned16(y) ||
+  if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !work || !vec_ok(y) ||
       (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) || !vec_ok(beta) ||
       !aligned16(save_mean) || !aligned16(save_invstd)) {
     set_error("bnn_bn_fwd_train: bad arguments (M=%lld C=%lld; C must be a multiple of 4, M > 0)",
@@ -256,8 +256,9 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
                      nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
   hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, M, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd);
-  hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
-                     gamma, beta, hardtanh, y);
+  if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
+    hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
+                       gamma, beta, hardtanh, y);
   return check_launch("bnn_bn_fwd_train");
 }
 

@@ -167,6 +167,300 @@ int64_t filter_chunks(int64_t N, int64_t nelem) {
   return std::max<int64_t>(1, std::min<int64_t>({want, N, (int64_t)65535}));
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// LDS-tiled fast path (groups == 1, stride == 1, dilation == 1, pad <= K-1, one sample's planes
+// fit in LDS -- the MNIST-scale convolutions of the build CNN).  One workgroup per sample (fwd,
+// bwd_data) or per chunk of samples (bwd_filter); weights and the zero-padded sample staged in LDS
+// once; each thread keeps all output channels of its pixel in registers.
+//  * forward, binarised input: ternary activations and weights packed 4 channels per int32 word,
+//    v_dot4c_i32_i8 -> exact integer sums (bit-exact like the generic kernel);
+//  * forward, fp32 input (the C == 3 rule): fp32 FMAs;
+//  * backward data: fp32 dY x sign(W) FMAs; backward filter: fp32 dY x x_used FMAs, per-workgroup
+//    partial sums reduced in double in a fixed order.
+constexpr int TILE_T = 256;
+
+struct TileGeo {
+  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, Wp, C4;
+};
+
+constexpr int64_t kMaxTileLds = 160 * 1024;   // a single workgroup may own the CU's whole LDS
+
+inline bool tile_geom_ok(const ConvShape& s) {
+  return s.groups == 1 && s.stride == 1 && s.dil == 1 && s.pad <= s.KH - 1 && s.pad <= s.KW - 1 &&
+         s.Co <= 64 && s.C <= 64;
+}
+
+inline int pick_co(int64_t co) { return co <= 8 ? 8 : co <= 16 ? 16 : co <= 32 ? 32 : 64; }
+
+// Dynamic LDS bytes of each tiled kernel (must match the carve-up inside the kernels).
+inline int64_t fwd_tile_lds(const ConvShape& s, bool bin) {
+  const int64_t Hp = s.H + 2 * s.pad, Wp = s.W + 2 * s.pad, C4 = (s.C + 3) / 4, CO = pick_co(s.Co);
+  return bin ? (s.KH * s.KW * C4 * CO + Hp * Wp * C4) * 4 : (s.KH * s.KW * s.C * CO + s.C * Hp * Wp) * 4;
+}
+inline int64_t bwd_data_tile_lds(const ConvShape& s) {
+  const int64_t CI = pick_co(s.C);
+  return (s.KH * s.KW * s.Co * CI + s.Co * (s.OH + 2 * (s.KH - 1)) * (s.OW + 2 * (s.KW - 1))) * 4;
+}
+inline int64_t filter_tile_lds(const ConvShape& s) {
+  return ((s.H + 2 * s.pad) * (s.W + 2 * s.pad) * s.C + s.OH * s.OW * pick_co(s.Co)) * 4;
+}
+
+template <typename K>
+inline void allow_lds(K kernel, int64_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+}
+
+inline TileGeo geo(const ConvShape& s) {
+  return TileGeo{(int)s.C, (int)s.H, (int)s.W, (int)s.Co, (int)s.KH, (int)s.KW, (int)s.OH, (int)s.OW, s.pad,
+                 (int)(s.H + 2 * s.pad), (int)(s.W + 2 * s.pad), (int)((s.C + 3) / 4)};
+}
+
+template <int CO>
+__global__ __launch_bounds__(TILE_T) void conv_fwd_bin_tile_k(const float* __restrict__ x,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ y, TileGeo g) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  int* ws = lds;                                   // [KH][KW][C4][CO] packed signs
+  int* xs = lds + g.KH * g.KW * g.C4 * CO;         // [Hp][Wp][C4] packed signs
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int nw = g.KH * g.KW * g.C4 * CO, nx = g.Hp * g.Wp * g.C4;
+  for (int i = t; i < nw; i += TILE_T) {
+    const int co = i % CO, cg = (i / CO) % g.C4, kk = i / (CO * g.C4);
+    const int kh = kk / g.KW, kw = kk % g.KW;
+    int word = 0;
+    if (co < g.Co)
+      for (int j = 0; j < 4; ++j) {
+        const int ci = 4 * cg + j;
+        if (ci < g.C) word |= (tsign(w[((co * g.C + ci) * g.KH + kh) * g.KW + kw]) & 255) << (8 * j);
+      }
+    ws[i] = word;
+  }
+  for (int i = t; i < nx; i += TILE_T) xs[i] = 0;
+  __syncthreads();
+  int8_t* xs8 = reinterpret_cast<int8_t*>(xs);
+  const float* xn = x + (int64_t)n * g.C * g.H * g.W;
+  for (int i = t; i < g.C * g.H * g.W; i += TILE_T) {   // coalesced over the NCHW plane
+    const int iw = i % g.W, ih = (i / g.W) % g.H, c = i / (g.W * g.H);
+    xs8[((ih + g.pad) * g.Wp + (iw + g.pad)) * g.C4 * 4 + c] = (int8_t)tsign(xn[i]);
+  }
+  __syncthreads();
+  for (int p = t; p < g.OH * g.OW; p += TILE_T) {
+    const int oh = p / g.OW, ow = p % g.OW;
+    int acc[CO];
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[co] = 0;
+    for (int kh = 0; kh < g.KH; ++kh)
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int* xp = xs + ((oh + kh) * g.Wp + (ow + kw)) * g.C4;
+        const int* wp = ws + (kh * g.KW + kw) * g.C4 * CO;
+        for (int cg = 0; cg < g.C4; ++cg) {
+          const int xv = xp[cg];
+#pragma unroll
+          for (int co = 0; co < CO; ++co) acc[co] = __builtin_amdgcn_sdot4(xv, wp[cg * CO + co], acc[co], false);
+        }
+      }
+    float* yp = y + (int64_t)n * g.Co * g.OH * g.OW + p;
+#pragma unroll
+    for (int co = 0; co < CO; ++co)
+      if (co < g.Co) yp[(int64_t)co * g.OH * g.OW] = (float)acc[co] + (bias ? bias[co] : 0.f);
+  }
+}
+
+template <int CO>
+__global__ __launch_bounds__(TILE_T) void conv_fwd_f32_tile_k(const float* __restrict__ x,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ y, TileGeo g) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  float* ws = ldsf;                                // [KH][KW][C][CO] signs
+  float* xs = ldsf + g.KH * g.KW * g.C * CO;       // [C][Hp][Wp]
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int nw = g.KH * g.KW * g.C * CO, nx = g.C * g.Hp * g.Wp;
+  for (int i = t; i < nw; i += TILE_T) {
+    const int co = i % CO, ci = (i / CO) % g.C, kk = i / (CO * g.C);
+    ws[i] = co < g.Co ? (float)tsign(w[((co * g.C + ci) * g.KH + kk / g.KW) * g.KW + kk % g.KW]) : 0.f;
+  }
+  for (int i = t; i < nx; i += TILE_T) xs[i] = 0.f;
+  __syncthreads();
+  const float* xn = x + (int64_t)n * g.C * g.H * g.W;
+  for (int i = t; i < g.C * g.H * g.W; i += TILE_T) {
+    const int iw = i % g.W, ih = (i / g.W) % g.H, c = i / (g.W * g.H);
+    xs[(c * g.Hp + ih + g.pad) * g.Wp + iw + g.pad] = xn[i];
+  }
+  __syncthreads();
+  for (int p = t; p < g.OH * g.OW; p += TILE_T) {
+    const int oh = p / g.OW, ow = p % g.OW;
+    float acc[CO];
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[co] = 0.f;
+    for (int ci = 0; ci < g.C; ++ci)
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const float xv = xs[(ci * g.Hp + oh + kh) * g.Wp + ow + kw];
+          const float* wp = ws + ((kh * g.KW + kw) * g.C + ci) * CO;
+#pragma unroll
+          for (int co = 0; co < CO; ++co) acc[co] = fmaf(xv, wp[co], acc[co]);
+        }
+    float* yp = y + (int64_t)n * g.Co * g.OH * g.OW + p;
+#pragma unroll
+    for (int co = 0; co < CO; ++co)
+      if (co < g.Co) yp[(int64_t)co * g.OH * g.OW] = acc[co] + (bias ? bias[co] : 0.f);
+  }
+}
+
+// dX[ci][ih][iw] = sum_{co,kh,kw} dY[co][ih+pad-kh][iw+pad-kw] * sign(W[co][ci][kh][kw]).
+template <int CI>
+__global__ __launch_bounds__(TILE_T) void conv_bwd_data_tile_k(const float* __restrict__ dy,
+                                                               const float* __restrict__ w,
+                                                               float* __restrict__ dx, TileGeo g) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  const int PH = g.KH - 1, PW = g.KW - 1;
+  const int OHp = g.OH + 2 * PH, OWp = g.OW + 2 * PW;
+  float* ws = ldsf;                                // [KH][KW][Co][CI] signs
+  float* ds = ldsf + g.KH * g.KW * g.Co * CI;      // [Co][OHp][OWp], zero border
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int nw = g.KH * g.KW * g.Co * CI, nd = g.Co * OHp * OWp;
+  for (int i = t; i < nw; i += TILE_T) {
+    const int ci = i % CI, co = (i / CI) % g.Co, kk = i / (CI * g.Co);
+    ws[i] = ci < g.C ? (float)tsign(w[((co * g.C + ci) * g.KH + kk / g.KW) * g.KW + kk % g.KW]) : 0.f;
+  }
+  for (int i = t; i < nd; i += TILE_T) ds[i] = 0.f;
+  __syncthreads();
+  const float* dn = dy + (int64_t)n * g.Co * g.OH * g.OW;
+  for (int i = t; i < g.Co * g.OH * g.OW; i += TILE_T) {
+    const int ow = i % g.OW, oh = (i / g.OW) % g.OH, co = i / (g.OW * g.OH);
+    ds[(co * OHp + oh + PH) * OWp + ow + PW] = dn[i];
+  }
+  __syncthreads();
+  for (int p = t; p < g.H * g.W; p += TILE_T) {
+    const int ih = p / g.W, iw = p % g.W;
+    float acc[CI];
+#pragma unroll
+    for (int ci = 0; ci < CI; ++ci) acc[ci] = 0.f;
+    for (int co = 0; co < g.Co; ++co)
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw) {
+          // oh = ih + pad - kh  ->  padded row oh + PH
+          const float dv = ds[(co * OHp + ih + g.pad - kh + PH) * OWp + iw + g.pad - kw + PW];
+          const float* wp = ws + ((kh * g.KW + kw) * g.Co + co) * CI;
+#pragma unroll
+          for (int ci = 0; ci < CI; ++ci) acc[ci] = fmaf(dv, wp[ci], acc[ci]);
+        }
+    float* xp = dx + (int64_t)n * g.C * g.H * g.W + p;
+#pragma unroll
+    for (int ci = 0; ci < CI; ++ci)
+      if (ci < g.C) xp[(int64_t)ci * g.H * g.W] = acc[ci];
+  }
+}
+
+// Partial dW over a chunk of samples: thread -> (combo = (ci,kh,kw), pixel phase), CO accumulators.
+// part[(blockIdx.x * nphase + phase)][co * ncombo + combo]; bias partials in part[...][CO*ncombo + co].
+template <int CO>
+__global__ __launch_bounds__(TILE_T) void conv_bwd_filter_tile_k(const float* __restrict__ dy,
+                                                                 const float* __restrict__ x, int binarize,
+                                                                 float* __restrict__ part, int64_t N,
+                                                                 int spb, TileGeo g, int with_bias) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  float* xs = ldsf;                                // [C][Hp][Wp]
+  float* ds = ldsf + g.C * g.Hp * g.Wp;            // [OH*OW][CO]
+  const int ncombo = g.C * g.KH * g.KW;
+  const int nphase = TILE_T / ncombo > 0 ? TILE_T / ncombo : 1;
+  const int t = threadIdx.x;
+  const int phase = t / ncombo, combo0 = t % ncombo;
+  const int nelem = CO * ncombo + CO;
+  float acc[2][CO];  // a thread may own two combos when ncombo > 256
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[a][co] = 0.f;
+  float bacc = 0.f;
+  const int64_t n0 = (int64_t)blockIdx.x * spb, n1 = (n0 + spb < N) ? n0 + spb : N;
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();
+    for (int i = t; i < g.C * g.Hp * g.Wp; i += TILE_T) xs[i] = 0.f;
+    __syncthreads();
+    const float* xn = x + n * g.C * g.H * g.W;
+    for (int i = t; i < g.C * g.H * g.W; i += TILE_T) {
+      const int iw = i % g.W, ih = (i / g.W) % g.H, c = i / (g.W * g.H);
+      const float v = xn[i];
+      xs[(c * g.Hp + ih + g.pad) * g.Wp + iw + g.pad] = binarize ? (float)tsign(v) : v;
+    }
+    const float* dn = dy + n * g.Co * g.OH * g.OW;
+    for (int i = t; i < CO * g.OH * g.OW; i += TILE_T) {
+      const int co = i % CO, pp = i / CO;
+      ds[i] = co < g.Co ? dn[(int64_t)co * g.OH * g.OW + pp] : 0.f;
+    }
+    __syncthreads();
+    if (phase < nphase) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int combo = combo0 + a * TILE_T;
+        if (combo >= ncombo || (a == 1 && nphase > 1)) continue;
+        const int ci = combo / (g.KH * g.KW), kk = combo % (g.KH * g.KW), kh = kk / g.KW, kw = kk % g.KW;
+        for (int pp = phase; pp < g.OH * g.OW; pp += nphase) {
+          const int oh = pp / g.OW, ow = pp % g.OW;
+          const float xv = xs[(ci * g.Hp + oh + kh) * g.Wp + ow + kw];
+          const float* dp = ds + pp * CO;
+#pragma unroll
+          for (int co = 0; co < CO; ++co) acc[a][co] = fmaf(dp[co], xv, acc[a][co]);
+        }
+      }
+    }
+    if (with_bias && t < g.Co) {
+      float s = 0.f;
+      for (int pp = 0; pp < g.OH * g.OW; ++pp) s += ds[pp * CO + t];
+      bacc += s;
+    }
+  }
+  float* blk = part + (int64_t)blockIdx.x * nphase * nelem;
+  if (phase < nphase) {
+    float* pb = blk + (int64_t)phase * nelem;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int combo = combo0 + a * TILE_T;
+      if (combo >= ncombo || (a == 1 && nphase > 1)) continue;
+#pragma unroll
+      for (int co = 0; co < CO; ++co) pb[co * ncombo + combo] = acc[a][co];
+    }
+  }
+  if (t < CO) {  // the block's bias sums live in its phase-0 row; other rows' bias slots are zero
+    blk[CO * ncombo + t] = (with_bias && t < g.Co) ? bacc : 0.f;
+    for (int ph = 1; ph < nphase; ++ph) blk[(int64_t)ph * nelem + CO * ncombo + t] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_filter_tile_reduce_k(const float* __restrict__ part, int64_t nparts,
+                                                                 int CO, int ncombo, int Co,
+                                                                 float* __restrict__ dw, float* __restrict__ db) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nelem = (int64_t)CO * ncombo + CO;
+  if (e >= nelem) return;
+  double acc = 0.0;
+  for (int64_t q = 0; q < nparts; ++q) acc += (double)part[q * nelem + e];
+  if (e < (int64_t)CO * ncombo) {
+    const int64_t co = e / ncombo, combo = e % ncombo;
+    if (co < Co) dw[co * ncombo + combo] = (float)acc;
+  } else if (db) {
+    const int64_t co = e - (int64_t)CO * ncombo;
+    if (co < Co) db[co] = (float)acc;
+  }
+}
+
+// Launch a tiled kernel with `lds` dynamic bytes (lifting the 64 KiB default cap when needed).
+#define BNN_TILE_LAUNCH(KER, ...) \
+  do { allow_lds(KER, (int64_t)lds); hipLaunchKernelGGL(KER, __VA_ARGS__); } while (0)
+
+constexpr int FILTER_SPB = 8;  // samples per bwd_filter workgroup
+
+int64_t tile_filter_parts(const ConvShape& s) {
+  const int ncombo = (int)(s.C * s.KH * s.KW);
+  const int nphase = TILE_T / ncombo > 0 ? TILE_T / ncombo : 1;
+  return ((s.N + FILTER_SPB - 1) / FILTER_SPB) * nphase;
+}
 }  // namespace
 }  // namespace bnn
 
@@ -183,8 +477,29 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
   }
   const int64_t total = N * Co * s.OH * s.OW;
   if (total == 0) return 0;
-  hipLaunchKernelGGL(conv_fwd_k, dim3(grid_for(total)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), x, binarize_input, w_latent, bias, y, s);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (tile_geom_ok(s) && fwd_tile_lds(s, binarize_input != 0) <= kMaxTileLds) {
+    const TileGeo g = geo(s);
+    const int CO = pick_co(Co);
+    const size_t lds = (size_t)fwd_tile_lds(s, binarize_input != 0);
+    if (binarize_input) {
+      switch (CO) {
+        case 8: BNN_TILE_LAUNCH(conv_fwd_bin_tile_k<8>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        case 16: BNN_TILE_LAUNCH(conv_fwd_bin_tile_k<16>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        case 32: BNN_TILE_LAUNCH(conv_fwd_bin_tile_k<32>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        default: BNN_TILE_LAUNCH(conv_fwd_bin_tile_k<64>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+      }
+    } else {
+      switch (CO) {
+        case 8: BNN_TILE_LAUNCH(conv_fwd_f32_tile_k<8>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        case 16: BNN_TILE_LAUNCH(conv_fwd_f32_tile_k<16>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        case 32: BNN_TILE_LAUNCH(conv_fwd_f32_tile_k<32>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+        default: BNN_TILE_LAUNCH(conv_fwd_f32_tile_k<64>, dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g); break;
+      }
+    }
+    return check_launch("bnn_conv2d_fwd");
+  }
+  hipLaunchKernelGGL(conv_fwd_k, dim3(grid_for(total)), dim3(256), 0, st, x, binarize_input, w_latent, bias, y, s);
   return check_launch("bnn_conv2d_fwd");
 }
 
@@ -198,8 +513,20 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   }
   const int64_t total = N * C * H * W;
   if (total == 0) return 0;
-  hipLaunchKernelGGL(conv_bwd_data_k, dim3(grid_for(total)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), dy, w_latent, dx, s);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (tile_geom_ok(s) && bwd_data_tile_lds(s) <= kMaxTileLds) {
+    const TileGeo g = geo(s);
+    const int CI = pick_co(C);
+    const size_t lds = (size_t)bwd_data_tile_lds(s);
+    switch (CI) {
+      case 8: BNN_TILE_LAUNCH(conv_bwd_data_tile_k<8>, dim3(N), dim3(TILE_T), lds, st, dy, w_latent, dx, g); break;
+      case 16: BNN_TILE_LAUNCH(conv_bwd_data_tile_k<16>, dim3(N), dim3(TILE_T), lds, st, dy, w_latent, dx, g); break;
+      case 32: BNN_TILE_LAUNCH(conv_bwd_data_tile_k<32>, dim3(N), dim3(TILE_T), lds, st, dy, w_latent, dx, g); break;
+      default: BNN_TILE_LAUNCH(conv_bwd_data_tile_k<64>, dim3(N), dim3(TILE_T), lds, st, dy, w_latent, dx, g); break;
+    }
+    return check_launch("bnn_conv2d_bwd_data");
+  }
+  hipLaunchKernelGGL(conv_bwd_data_k, dim3(grid_for(total)), dim3(256), 0, st, dy, w_latent, dx, s);
   return check_launch("bnn_conv2d_bwd_data");
 }
 
@@ -207,7 +534,14 @@ BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co
                                                 int64_t KW, int32_t groups) {
   if (groups <= 0 || C % groups != 0) return 0;
   const int64_t nelem = Co * (C / groups) * KH * KW + Co;
-  return filter_chunks(std::max<int64_t>(N, 1), nelem) * nelem * (int64_t)sizeof(double);
+  const int64_t generic = filter_chunks(std::max<int64_t>(N, 1), nelem) * nelem * (int64_t)sizeof(double);
+  // tiled path: float partials [parts][CO*ncombo + CO]
+  const int CO = pick_co(Co);
+  const int ncombo = (int)(C * KH * KW);
+  const int nphase = TILE_T / ncombo > 0 ? TILE_T / ncombo : 1;
+  const int64_t parts = ((std::max<int64_t>(N, 1) + FILTER_SPB - 1) / FILTER_SPB) * nphase;
+  const int64_t tiled = parts * ((int64_t)CO * ncombo + CO) * (int64_t)sizeof(float);
+  return std::max(generic, tiled);
 }
 
 BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_input, float* dw,
@@ -223,6 +557,25 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   const int64_t nw = Co * (C / groups) * KH * KW;
   const int64_t nelem = nw + Co;
   const int64_t nchunks = filter_chunks(std::max<int64_t>(N, 1), nelem);
+  if (N > 0 && tile_geom_ok(s) && C * KH * KW <= 2 * TILE_T && filter_tile_lds(s) <= kMaxTileLds) {
+    const TileGeo g = geo(s);
+    const int CO = pick_co(Co);
+    const int ncombo = (int)(C * KH * KW);
+    const int64_t nblk = (N + FILTER_SPB - 1) / FILTER_SPB;
+    const int64_t parts = tile_filter_parts(s);
+    float* part = reinterpret_cast<float*>(work);
+    const size_t lds = (size_t)filter_tile_lds(s);
+    switch (CO) {
+      case 8: BNN_TILE_LAUNCH(conv_bwd_filter_tile_k<8>, dim3((unsigned)nblk), dim3(TILE_T), lds, st, dy, x, binarize_input, part, N, FILTER_SPB, g, db != nullptr); break;
+      case 16: BNN_TILE_LAUNCH(conv_bwd_filter_tile_k<16>, dim3((unsigned)nblk), dim3(TILE_T), lds, st, dy, x, binarize_input, part, N, FILTER_SPB, g, db != nullptr); break;
+      case 32: BNN_TILE_LAUNCH(conv_bwd_filter_tile_k<32>, dim3((unsigned)nblk), dim3(TILE_T), lds, st, dy, x, binarize_input, part, N, FILTER_SPB, g, db != nullptr); break;
+      default: BNN_TILE_LAUNCH(conv_bwd_filter_tile_k<64>, dim3((unsigned)nblk), dim3(TILE_T), lds, st, dy, x, binarize_input, part, N, FILTER_SPB, g, db != nullptr); break;
+    }
+    const int64_t nel = (int64_t)CO * ncombo + CO;
+    hipLaunchKernelGGL(conv_filter_tile_reduce_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, part,
+                       parts, CO, ncombo, (int)Co, dw, db);
+    return check_launch("bnn_conv2d_bwd_filter");
+  }
   double* part = reinterpret_cast<double*>(work);
   if (N == 0) {
     (void)hipMemsetAsync(part, 0, nchunks * nelem * sizeof(double), st);

@@ -15,6 +15,7 @@
 // ds_read_b128 fragment reads are bank-conflict free); two LDS buffers; XCD-aware bijective
 // block remap + grouped raster so blocks sharing an A panel run on one XCD's L2.
 #include <algorithm>
+#include <type_traits>
 
 #include "bnn_common.h"
 
@@ -242,8 +243,16 @@ __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
+          int DIAG = 0, int F4 = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
+  // F4 = 1: both operands are ternary FP4 (e2m1) nibbles, 2 per byte; K and the LDS tiles are
+  // counted in bytes (BKT bytes = 2*BKT elements); v_mfma_scale_f32_32x32x64_f8f6f4 with unit
+  // E8M0 scales (127) multiplies 64 k per instruction -- twice the int8 rate on half the bytes --
+  // and its fp32 accumulation of +-1 products is exact (|sum| < 2^24).
+  static_assert(!F4 || (DA == 1 && DB == 1), "FP4 mode is the ternary x ternary form");
+  using AccT = typename std::conditional<F4 != 0, v16f, v16i>::type;
+  // DIAG (timing-only builds, wrong results): 1 = no LDS fragment reads, 2 = no global->LDS staging
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   constexpr int A_ST = DA * BM * BKT, B_ST = DB * BN * BKT, ST = A_ST + B_ST;
@@ -271,6 +280,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   // (piece jr covers rows jr*RPI .. jr*RPI+RPI-1; with BK=128 bit 3 of the row comes from jr).
   const int srow = lane / CPR, sslot = lane % CPR;
   auto stage = [&](int kt, int buf) {
+    if constexpr (DIAG == 2) return;
     char* sA = smem + buf * ST;
     char* sB = sA + A_ST;
 #pragma unroll
@@ -291,13 +301,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     }
   };
 
-  v16i acc[NC][WM][WN];
+  AccT acc[NC][WM][WN];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int t = 0; t < WM; ++t)
 #pragma unroll
-      for (int u = 0; u < WN; ++u) acc[c][t][u] = v16i{0};
+      for (int u = 0; u < WN; ++u) acc[c][t][u] = AccT{0};
   float facc[FLUSH ? WM : 1][FLUSH ? WN : 1][16];
   if constexpr (FLUSH) {
 #pragma unroll
@@ -325,6 +335,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     // double buffer; indices are compile-time after unrolling)
     v4i a[2][DA][WM], b[2][DB][WN];
     auto load_frags = [&](int ks, v4i (&fa)[DA][WM], v4i (&fb)[DB][WN]) {
+      if constexpr (DIAG == 1) {
+#pragma unroll
+        for (int d = 0; d < DA; ++d)
+#pragma unroll
+          for (int t = 0; t < WM; ++t) fa[d][t] = v4i{lane + ks, d, t, kt};
+#pragma unroll
+        for (int e = 0; e < DB; ++e)
+#pragma unroll
+          for (int u = 0; u < WN; ++u) fb[e][u] = v4i{lane, e + ks, u, kt};
+        return;
+      }
       const int off = 16 * ((2 * ks + h) ^ sw);
 #pragma unroll
       for (int d = 0; d < DA; ++d)
@@ -346,7 +367,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
       for (int t = 0; t < WM; ++t)
 #pragma unroll
         for (int u = 0; u < WN; ++u) {
-          if constexpr (DA == 1 && DB == 1) {
+          if constexpr (F4) {
+            const v4i x = a[cur][0][t], y = b[cur][0][u];
+            const v8i xa = {x.x, x.y, x.z, x.w, 0, 0, 0, 0}, yb = {y.x, y.y, y.z, y.w, 0, 0, 0, 0};
+            acc[0][t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(xa, yb, acc[0][t][u], 4, 4, 0, 127,
+                                                                            0, 127);
+          } else if constexpr (DA == 1 && DB == 1) {
             acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][0][t], b[cur][0][u], acc[0][t][u], 0, 0, 0);
           } else if constexpr (DB == 1) {
 #pragma unroll
@@ -388,7 +414,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
               facc[t][u][i] += (float)((double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 +
                                        (double)acc[0][t][u][i]);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) acc[c][t][u] = v16i{0};
+            for (int c = 0; c < NC; ++c) acc[c][t][u] = AccT{0};
           }
       }
     }
@@ -454,13 +480,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   }
 }
 
-template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0>
+template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
+          int DIAG = 0, int F4 = 0>
 int launch_v2(GemmParams p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
   const int64_t nblk = (int64_t)p.gm * p.gn;
-  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, F4>), dim3((unsigned)nblk),
                      dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   return check_launch("bnn_gemm_i8");
 }
@@ -494,6 +521,8 @@ const Variant kVariants[] = {
     {4, "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2, 64>", launch_v2<1, 1, 2, 2, 4, 4, 2, 64>, 64},
     {5, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 4, 64>", launch_v2<1, 1, 2, 4, 4, 2, 4, 64>, 64},
     {6, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1>, 128},
+    {77, "diag: v6 without LDS fragment reads", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 1>, 128},
+    {78, "diag: v6 without global->LDS staging", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 2>, 128},
     {10, "gemm_i8_k<3, 1, 2, 2>", launch<3, 1, 2, 2>, 64},
     {11, "gemm_i8_v2_k<3, 1, 2, 2, 2, 2, 3, 64>", launch_v2<3, 1, 2, 2, 2, 2, 3, 64>, 64},
     {12, "gemm_i8_v2_k<3, 1, 4, 2, 2, 2, 2, 64>", launch_v2<3, 1, 4, 2, 2, 2, 2, 64>, 64},
@@ -501,7 +530,15 @@ const Variant kVariants[] = {
     {14, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128>, 128},
     {15, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 3, 64>", launch_v2<3, 1, 2, 4, 2, 2, 3, 64>, 64},
     {16, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 4, 64>", launch_v2<3, 1, 2, 4, 2, 2, 4, 64>, 64},
+    // timing-only diagnostics (wrong results; never picked by default)
+    {97, "diag: v14 without LDS fragment reads", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 0, 1>, 128},
+    {98, "diag: v14 without global->LDS staging", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 0, 2>, 128},
     {20, "gemm_i8_k<3, 3, 2, 1>", launch<3, 3, 2, 1>, 64},
+    // FP4 (e2m1) ternary x ternary forms (bnn_gemm_fp4): K in bytes, 2 elements per byte
+    {30, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1>, 128},
+    {31, "gemm_i8_v2_k<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 1>", launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 1>, 64},
+    {32, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 1>, 64},
+    {33, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1>, 128},
     {21, "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2, 64>", launch_v2<3, 3, 2, 2, 2, 1, 2, 64>, 64},
     {22, "gemm_i8_v2_k<3, 3, 2, 4, 2, 1, 2, 64>", launch_v2<3, 3, 2, 4, 2, 1, 2, 64>, 64},
 };
@@ -513,6 +550,14 @@ const Variant* find_variant(int id) {
 }
 
 const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int64_t K) {
+  if (a_digits == 0) {  // FP4 ternary form; K in bytes
+    const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
+    int id = g_variant >= 0 ? 30 + g_variant : (big ? 33 : 31);   // sweep r01: 33 = 0.40 of FP4 peak
+    const Variant* v = find_variant(id);
+    if (v == nullptr) v = find_variant(31);
+    if (K % v->bk != 0) v = find_variant(big ? 32 : 31);
+    return v;
+  }
   const int base = a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20);
   int id, alt;  // alt = the BK=64 sibling used when K % 128 != 0
   if (g_variant >= 0) {
@@ -562,6 +607,21 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
   GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
                (int)M, (int)N, (int)K, 0, 0};
   return pick_kernel(a_digits, b_digits, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
+                         float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+  if (!A || !B || !C || M < 0 || N < 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K || lda % 16 != 0 ||
+      ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) || M > 0x7fffffff || N > 0x7fffffff ||
+      K > 0x7fffffff) {
+    set_error("bnn_gemm_fp4: bad arguments (M=%lld N=%lld K=%lld bytes; K must be a positive multiple of 64)",
+              (long long)M, (long long)N, (long long)K);
+    return kErrInval;
+  }
+  if (M == 0 || N == 0) return 0;
+  GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
+               nullptr, nullptr, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0};
+  return pick_kernel(0, 0, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 
 BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,

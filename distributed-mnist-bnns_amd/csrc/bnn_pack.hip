@@ -41,11 +41,27 @@ __device__ __forceinline__ int pack4(int a, int b, int c, int d) {
   return (a & 255) | ((b & 255) << 8) | ((c & 255) << 16) | ((d & 255) << 24);
 }
 
-// One 64x64 tile of x -> ternary int8 rows (q) and/or the transposed tile (qt).
+// FP4 (e2m1) code of a ternary value: +1 = 0b0010, -1 = 0b1010, 0 = 0b0000.
+__device__ __forceinline__ uint32_t fp4_code(int s) { return s > 0 ? 0x2u : (s < 0 ? 0xAu : 0u); }
+
+// Optional per-column affine map applied before the sign: the BatchNorm output
+// y = (x - mean) * invstd * gamma + beta, computed exactly as bn_apply_k does (bnn_bn.hip), so the
+// fused BN -> Hardtanh -> sign path sees bit-identical y (Hardtanh does not change a sign).
+struct ColAffine {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;  // nullable
+  const float* beta;   // nullable
+  int vec;             // all four 16-B aligned -> float4 parameter loads
+};
+
+// One 64x64 tile of x -> ternary rows (q: FMT 0 = int8 per element, FMT 1 = FP4 e2m1 nibbles,
+// element k in byte k/2, low nibble for even k) and/or the transposed int8 tile (qt).
+template <int FMT, int AFF = 0>
 __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
                                                         int64_t K, int64_t ldx, int8_t* __restrict__ q,
                                                         int64_t ldq, int8_t* __restrict__ qt,
-                                                        int64_t ldqt, int vec) {
+                                                        int64_t ldqt, int vec, ColAffine af = {}) {
   __shared__ int tile[TILE][TILE + 1];
   const int64_t m0 = (int64_t)blockIdx.y * TILE, k0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
@@ -57,16 +73,55 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = 0.f;
   }
+  if (AFF) {
+    // per-column parameters for columns k0+c .. +15: float4 loads when the run is in range
+    float mu[16], is[16], ga[16], be[16];
+    const int64_t cb = k0 + c;
+    if (af.vec && cb + 16 <= K) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 a = *reinterpret_cast<const float4*>(af.mean + cb + 4 * i);
+        const float4 b = *reinterpret_cast<const float4*>(af.invstd + cb + 4 * i);
+        const float4 g = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb + 4 * i) : make_float4(1, 1, 1, 1);
+        const float4 e = af.beta ? *reinterpret_cast<const float4*>(af.beta + cb + 4 * i) : make_float4(0, 0, 0, 0);
+        mu[4 * i] = a.x; mu[4 * i + 1] = a.y; mu[4 * i + 2] = a.z; mu[4 * i + 3] = a.w;
+        is[4 * i] = b.x; is[4 * i + 1] = b.y; is[4 * i + 2] = b.z; is[4 * i + 3] = b.w;
+        ga[4 * i] = g.x; ga[4 * i + 1] = g.y; ga[4 * i + 2] = g.z; ga[4 * i + 3] = g.w;
+        be[4 * i] = e.x; be[4 * i + 1] = e.y; be[4 * i + 2] = e.z; be[4 * i + 3] = e.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const bool in = cb + j < K;
+        mu[j] = in ? af.mean[cb + j] : 0.f;
+        is[j] = in ? af.invstd[cb + j] : 0.f;
+        ga[j] = (in && af.gamma) ? af.gamma[cb + j] : 1.f;
+        be[j] = (in && af.beta) ? af.beta[cb + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      v[j] = (m < M && cb + j < K) ? fmaf((v[j] - mu[j]) * is[j], ga[j], be[j]) : 0.f;
+  }
   int s[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) s[j] = tsign(v[j]);
-  if (q != nullptr && m < M && k0 + c < ldq) {
+  if (FMT == 0 && q != nullptr && m < M && k0 + c < ldq) {
     v4i w;
     w.x = pack4(s[0], s[1], s[2], s[3]);
     w.y = pack4(s[4], s[5], s[6], s[7]);
     w.z = pack4(s[8], s[9], s[10], s[11]);
     w.w = pack4(s[12], s[13], s[14], s[15]);
     *reinterpret_cast<v4i*>(q + m * ldq + k0 + c) = w;
+  }
+  if (FMT == 1 && q != nullptr && m < M && (k0 + c) / 2 < ldq) {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lo |= fp4_code(s[j]) << (4 * j);
+      hi |= fp4_code(s[8 + j]) << (4 * j);
+    }
+    *reinterpret_cast<uint2*>(q + m * ldq + (k0 + c) / 2) = make_uint2(lo, hi);
   }
   if (qt != nullptr) {
 #pragma unroll
@@ -310,9 +365,39 @@ BNN_API int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, 
     set_error("bnn_sign_pack_i8: M too large for one launch (%lld)", (long long)M);
     return kErrInval;
   }
-  hipLaunchKernelGGL(sign_pack_tile_k, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x,
+  hipLaunchKernelGGL(sign_pack_tile_k<0>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x,
                      M, K, ldx, q, ldq, qt, ldqt, vec);
   return check_launch("bnn_sign_pack_i8");
+}
+
+BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
+                              int8_t* qt, int64_t ldqt, void* stream) {
+  if (!x || M < 0 || K < 0 || ldx < K || (!q4 && !qt)) {
+    set_error("bnn_sign_pack_fp4: bad arguments (M=%lld K=%lld ldx=%lld)", (long long)M, (long long)K,
+              (long long)ldx);
+    return kErrInval;
+  }
+  if (q4 && (ldq4 % 128 != 0 || 2 * ldq4 < round_up(K, 256) || !aligned16(q4))) {
+    set_error("bnn_sign_pack_fp4: ldq4=%lld bytes must be a multiple of 128 covering round_up(K,256)",
+              (long long)ldq4);
+    return kErrInval;
+  }
+  if (qt && (ldqt % TILE != 0 || ldqt < round_up(M, TILE) || !aligned16(qt))) {
+    set_error("bnn_sign_pack_fp4: ldqt=%lld must be a multiple of 64 >= round_up(M,64)", (long long)ldqt);
+    return kErrInval;
+  }
+  if (M == 0 && !qt) return 0;
+  const int vec = aligned16(x) && (ldx % 4 == 0);
+  const int64_t gx = q4 ? (2 * ldq4) / TILE : (K + TILE - 1) / TILE;
+  const int64_t gy = qt ? ldqt / TILE : (M + TILE - 1) / TILE;
+  if (gx == 0 || gy == 0) return 0;
+  if (gy > 65535) {
+    set_error("bnn_sign_pack_fp4: M too large for one launch (%lld)", (long long)M);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL(sign_pack_tile_k<1>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M, K,
+                     ldx, reinterpret_cast<int8_t*>(q4), ldq4, qt, ldqt, vec);
+  return check_launch("bnn_sign_pack_fp4");
 }
 
 BNN_API int bnn_sign_f32(const float* x, float* y, int64_t n, void* stream) {
@@ -391,4 +476,36 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
   hipLaunchKernelGGL(quant_cols_t_k, dim3((unsigned)((N + TILE - 1) / TILE), (unsigned)(ldqt / TILE)),
                      dim3(256), 0, S(stream), x, M, N, ldx, scale, digits_t, ldqt, plane, vec);
   return check_launch("bnn_quant_cols_t");
+}
+
+BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+                              const float* gamma, const float* beta, int32_t fmt, void* q, int64_t ldq,
+                              int8_t* qt, int64_t ldqt, void* stream) {
+  const int64_t need = fmt == 1 ? round_up(C, 256) / 2 : round_up(C, TILE);
+  if (!x || !mean || !invstd || M < 0 || C < 0 || (fmt != 0 && fmt != 1) || (!q && !qt) ||
+      (q && (ldq < need || ldq % (fmt == 1 ? 128 : TILE) != 0 || !aligned16(q))) ||
+      (qt && (ldqt % TILE != 0 || ldqt < round_up(M, TILE) || !aligned16(qt)))) {
+    set_error("bnn_bn_apply_pack: bad arguments (M=%lld C=%lld fmt=%d ldq=%lld ldqt=%lld)", (long long)M,
+              (long long)C, fmt, (long long)ldq, (long long)ldqt);
+    return kErrInval;
+  }
+  if (M == 0 && !qt) return 0;
+  const int vec = aligned16(x) && (C % 4 == 0);
+  const int64_t gx = q ? (fmt == 1 ? 2 * ldq : ldq) / TILE : (C + TILE - 1) / TILE;
+  const int64_t gy = qt ? ldqt / TILE : (M + TILE - 1) / TILE;
+  if (gx == 0 || gy == 0) return 0;
+  if (gy > 65535) {
+    set_error("bnn_bn_apply_pack: M too large for one launch (%lld)", (long long)M);
+    return kErrInval;
+  }
+  const ColAffine af{mean, invstd, gamma, beta,
+                     aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
+                         (!beta || aligned16(beta))};
+  if (fmt == 1)
+    hipLaunchKernelGGL((sign_pack_tile_k<1, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M,
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af);
+  else
+    hipLaunchKernelGGL((sign_pack_tile_k<0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M,
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af);
+  return check_launch("bnn_bn_apply_pack");
 }

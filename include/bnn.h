@@ -48,6 +48,12 @@ const char* bnn_last_error(void);
 int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* q, int64_t ldq,
                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
 
+/* FP4 form of the ternary rows for bnn_gemm_fp4: q4 [M][ldq4 bytes], ldq4 a multiple of 128 with
+ * 2*ldq4 >= round_up(K,256) (zero nibbles beyond K); qt as in bnn_sign_pack_i8 (int8, for the
+ * backward GEMMs). */
+int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
+                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+
 /* y[i] = sign(x[i]) as fp32 (the caller-visible `input.data = Binarize(input.data)` of :76/:95;
  * y may alias x). */
 int bnn_sign_f32(const float* x, float* y, int64_t n, bnn_stream_t stream);
@@ -90,11 +96,20 @@ int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
                 const float* a_scale, const float* b_scale, const float* bias, float* C,
                 int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
 
+/* Ternary x ternary GEMM on the FP4 (e2m1) block-scaled MFMA (unit scales): operands hold FP4
+ * codes (+1 = 0x2, -1 = 0xA, 0 = 0x0), two elements per byte (element k in byte k/2, low nibble
+ * for even k), rows of lda / ldb BYTES; K = padded reduction length in BYTES (multiple of 64,
+ * zero nibbles beyond the true length).  C = sum + bias[n], bit-exact like the (1,1) int8 form,
+ * at twice its MFMA rate on half the operand bytes.  Pack with bnn_sign_pack_fp4. */
+int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
+                 float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
+
 /* Tuning hook (not part of the stable contract): select the bnn_gemm_i8 kernel variant for all
  * later calls in this process; -1 restores the built-in default table (tools/gemm_sweep.py). */
 int bnn_gemm_set_variant(int32_t variant);
 /* Name of the kernel instance bnn_gemm_i8 launches for this configuration (as rocprofv3 lists
- * it), so host-side HIP-event timings can be matched with profiles. */
+ * it), so host-side HIP-event timings can be matched with profiles; a_digits = b_digits = 0
+ * names the bnn_gemm_fp4 kernel (K in bytes). */
 const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,
                                int64_t K);
 
@@ -132,7 +147,8 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
  * [-1,1] in forward, gradient masked by -1 < y < 1 in backward, y recomputed from x).
  * x, y, dy, dx fp32 [M][C] row-major, C % 4 == 0, 16-B aligned; gamma/beta nullable (affine off);
  * running_mean/var nullable in train mode (track_running_stats off; momentum < 0 skips the update).
- * `work` scratch of bnn_bn_workspace(M, C) bytes.  Deterministic (fixed-order reductions). */
+ * `work` scratch of bnn_bn_workspace(M, C) bytes.  Deterministic (fixed-order reductions).
+ * bnn_bn_fwd_train with y == NULL computes the statistics only (for bnn_bn_apply_pack). */
 int64_t bnn_bn_workspace(int64_t M, int64_t C);
 int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps,
@@ -144,6 +160,16 @@ int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, co
 int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
                float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
+
+/* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
+ * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = (x-mean)*invstd*gamma+beta exactly as
+ * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0
+ * (int8, ldq >= round_up(C,64)) or fmt 1 (FP4 nibbles, ldq bytes >= round_up(C,256)/2, multiple
+ * of 128) and/or the int8 transpose qt [C][ldqt] for the weight gradient; no fp32 activation is
+ * written (Hardtanh keeps the sign; its backward mask is recomputed from x by bnn_bn_bwd). */
+int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+                      const float* gamma, const float* beta, int32_t fmt, void* q, int64_t ldq,
+                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */

@@ -70,7 +70,7 @@ SHAPES = [(1, 64, 1), (3, 100, 37), (64, 256, 128), (100, 3072, 1536), (129, 100
 
 
 @pytest.mark.parametrize("M,K,N", SHAPES)
-@pytest.mark.parametrize("backend", ["mfma", "xnor"])
+@pytest.mark.parametrize("backend", ["mfma", "xnor", "fp4"])
 def test_linear_random_shapes(F, M, K, N, backend):
     rng = np.random.default_rng(M * 131 + K * 7 + N)
     x = rng.standard_normal((M, K)).astype(np.float32)
@@ -101,7 +101,33 @@ def test_mfma_and_xnor_agree_bitwise(F):
     b = dev(rng.standard_normal(200).astype(np.float32))
     y1 = F.binary_linear(x, w, b, True, "mfma")
     y2 = F.binary_linear(x, w, b, True, "xnor")
+    y3 = F.binary_linear(x, w, b, True, "fp4")
     assert torch.equal(y1, y2)
+    assert torch.equal(y1, y3)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 256), (257, 520, 1000), (64, 64, 64), (2048, 1024, 8192)])
+def test_every_fp4_variant_is_exact(F, M, N, K):
+    """FP4 (e2m1) ternary GEMM variants against exact integer products."""
+    from bnn_amd import _lib
+    rng = np.random.default_rng(M + N + K)
+    x = rng.integers(-1, 2, (M, K)).astype(np.float32)
+    w = rng.integers(-1, 2, (N, K)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    ref = (x.astype(np.int64) @ w.astype(np.int64).T).astype(np.float32) + bias
+    x4, _ = F.sign_pack_fp4(dev(x))
+    w4, _ = F.sign_pack_fp4(dev(w))
+    names = set()
+    try:
+        for v in range(0, 5):
+            _lib.call("bnn_gemm_set_variant", v)
+            name = F.gemm_kernel_name(0, 0, M, N, x4.shape[1])
+            if name in names:
+                continue
+            names.add(name)
+            assert np.array_equal(host(F.gemm_fp4(x4, w4, M, N, bias=dev(bias))), ref), name
+    finally:
+        _lib.call("bnn_gemm_set_variant", -1)
 
 
 def test_sign_pack_layouts(F):
@@ -181,6 +207,44 @@ def test_conv_cnn_shapes_vs_oracle(F):
     assert rel_err(host(xt.grad), dx64) < GRAD_TOL
     assert rel_err(host(wt.grad), dw64) < GRAD_TOL
     assert rel_err(host(bt.grad), db64) < GRAD_TOL
+
+
+@pytest.mark.parametrize("shape", [
+    # (N, C, H, W, Co, K, pad, bias, binarize) -- LDS-tiled fast path (stride 1, pad <= K-1) ...
+    (1, 1, 28, 28, 16, 5, 2, True, True),
+    (9, 16, 14, 14, 32, 5, 2, True, True),
+    (17, 3, 13, 11, 8, 3, 1, True, False),      # the C == 3 rule: fp32 input
+    (5, 7, 10, 9, 5, 3, 0, False, True),
+    (3, 33, 8, 8, 40, 3, 2, True, True),
+    (2, 64, 6, 7, 64, 1, 0, True, True),
+    (11, 3, 9, 12, 3, 7, 3, False, False),
+    (4, 20, 5, 5, 64, 5, 4, True, True),
+    # ... and shapes that take the generic kernels (stride 2 / pad > K-1 / C > 64)
+    (3, 4, 9, 9, 6, 3, 3, True, True),
+    (2, 80, 5, 5, 8, 3, 1, True, True),
+])
+def test_conv_tiled_and_generic_shapes_vs_oracle(F, shape):
+    N, C, H, W, Co, K, pad, has_bias, binarize = shape
+    rng = np.random.default_rng(N * 1000 + C)
+    x = np.where(rng.random((N, C, H, W)) < 0.2, 0, rng.standard_normal((N, C, H, W))).astype(np.float32)
+    w = np.where(rng.random((Co, C, K, K)) < 0.1, 0, rng.uniform(-1, 1, (Co, C, K, K))).astype(np.float32)
+    b = rng.standard_normal(Co).astype(np.float32) if has_bias else None
+    xt, wt = dev(x).requires_grad_(True), dev(w).requires_grad_(True)
+    bt = dev(b).requires_grad_(True) if has_bias else None
+    assert binarize == O.conv_binarizes_input(x)
+    y = F.binary_conv2d(xt, wt, bt, binarize, 1, pad, 1, 1)
+    y_ref, xu = O.conv2d_forward(x, w, b, 1, pad, 1, 1)   # float64 sums
+    if binarize:
+        assert np.array_equal(host(y), y_ref)
+    else:
+        assert rel_err(host(y), y_ref) < FP_FWD_TOL
+    dy = rng.standard_normal(tuple(y.shape)).astype(np.float32)
+    y.backward(dev(dy))
+    dx64, dw64, db64 = O.conv2d_backward(xu, w, dy, 1, pad, 1, 1)
+    assert rel_err(host(xt.grad), dx64) < GRAD_TOL
+    assert rel_err(host(wt.grad), dw64) < GRAD_TOL
+    if has_bias:
+        assert rel_err(host(bt.grad), db64) < GRAD_TOL
 
 
 def test_hardtanh_backward(F):
