@@ -83,6 +83,24 @@ def cpu_baseline(cfg, budget):
                       f"{secs:.1f} s"}
 
 
+def pmc_traffic(kernel):
+    """HBM/fabric bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench, gfx950-corrected).  None when no pass covers the kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    prefix = kernel.rstrip(">")
+    for f in reversed(files):
+        try:
+            ks = json.load(open(f))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, v in ks.items():
+            if name == kernel or (name.startswith(prefix) and name[len(prefix):len(prefix) + 1] in (",", ">")):
+                return v["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,6 +206,12 @@ def main():
             result["binary_gemm_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)
         result["kernels"] = {k: {"launches": v["launches"], "avg_us": round(v["avg_ms"] * 1e3, 1),
                                  "share": round(v["ms"] / (elapsed * 1e3), 4)} for k, v in ksum.items()}
+    if roofline is not None:
+        traffic, src = pmc_traffic(roofline["kernel"])
+        roofline["traffic"] = traffic
+        roofline["traffic_source"] = src
+        if traffic and d.get("avg_bytes"):
+            roofline["algorithmic_bytes"] = int(d["avg_bytes"])
     result["roofline"] = roofline
     result["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
