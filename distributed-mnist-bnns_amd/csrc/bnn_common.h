@@ -24,6 +24,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 // Ternary sign as used by the reference (models/binarized_modules.py:13, Tensor.sign()):
 // +1 for x>0, -1 for x<0, 0 for x==0 (NaN maps to 0 here; the reference would propagate NaN).

@@ -237,6 +237,14 @@ __device__ __forceinline__ void wait_stages(int ahead) {
   wait_vmcnt_c<0>();
 }
 
+template <int S16, typename Acc>
+__device__ __forceinline__ Acc mfma_i8(v4i a, v4i b, Acc c) {
+  if constexpr (S16)
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -244,14 +252,24 @@ __device__ __forceinline__ void block_barrier() {
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
-          int DIAG = 0, int F4 = 0>
+          int DIAG = 0, int F4 = 0, int S16 = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
   // F4 = 1: both operands are ternary FP4 (e2m1) nibbles, 2 per byte; K and the LDS tiles are
   // counted in bytes (BKT bytes = 2*BKT elements); v_mfma_scale_f32_32x32x64_f8f6f4 with unit
   // E8M0 scales (127) multiplies 64 k per instruction -- twice the int8 rate on half the bytes --
   // and its fp32 accumulation of +-1 products is exact (|sum| < 2^24).
+  // S16 = 1: the same WM x WN 32x32 wave tile computed as (2WM) x (2WN) 16x16 MFMA tiles
+  // (v_mfma_i32_16x16x64_i8 / v_mfma_scale_f32_16x16x128_f8f6f4, 64 bytes of K per instruction):
+  // equal cycles per op, but the chip holds a higher clock on the 16x16 shape under load
+  // (MI355X_MICROARCH.md, DVFS give-back item 7).  Needs BKT = 128 for conflict-free reads.
   static_assert(!F4 || (DA == 1 && DB == 1), "FP4 mode is the ternary x ternary form");
-  using AccT = typename std::conditional<F4 != 0, v16f, v16i>::type;
+  static_assert(!S16 || BKT == 128, "16x16 tiles use the BK=128 swizzle");
+  constexpr int TS = S16 ? 16 : 32;            // MFMA tile edge
+  constexpr int TM = S16 ? 2 * WM : WM, TN = S16 ? 2 * WN : WN;
+  constexpr int TR = TS * TS / 64;             // accumulator registers per tile
+  using AccT = typename std::conditional<
+      S16 != 0, typename std::conditional<F4 != 0, v4f, v4i>::type,
+      typename std::conditional<F4 != 0, v16f, v16i>::type>::type;
   // DIAG (timing-only builds, wrong results): 1 = no LDS fragment reads, 2 = no global->LDS staging
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
@@ -263,7 +281,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   constexpr int PER_WAVE = (IA + IB) / NW;
   constexpr int NC = Cfg<DA, DB>::NC;
   constexpr bool FLUSH = Cfg<DA, DB>::FLUSH;
-  constexpr int KSTEPS = BKT / 32;
+  constexpr int KSTEPS = BKT / (S16 ? 64 : 32);
   constexpr int FLUSH_KT = Cfg<DA, DB>::FLUSH_KT * 64 / BKT;
   __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
 
@@ -279,120 +297,177 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   // lane -> (row srow of the 1-KiB piece, 16-B slot sslot); the swizzle uses the tile-local row
   // (piece jr covers rows jr*RPI .. jr*RPI+RPI-1; with BK=128 bit 3 of the row comes from jr).
   const int srow = lane / CPR, sslot = lane % CPR;
+  // Each piece's address = a wave-uniform 64-bit base (SGPRs: operand, plane, tile row, k-tile)
+  // + a per-lane 32-bit offset (row in tile, clamped to the last valid row, and the swizzled
+  // chunk), so the LDS-DMA issues in its saddr form with one VGPR of address; the loops have
+  // compile-time trip counts (no branches between pieces).  The host guarantees BM*lda and
+  // BN*ldb < 2^31 (bnn_gemm_i8 falls back to the v1 kernel otherwise).
+  const int lim_a = p.M - 1 - m0, lim_b = p.N - 1 - n0;
   auto stage = [&](int kt, int buf) {
     if constexpr (DIAG == 2) return;
     char* sA = smem + buf * ST;
     char* sB = sA + A_ST;
 #pragma unroll
-    for (int j = wave; j < IA; j += NW) {
+    for (int i = 0; i < IA / NW; ++i) {
+      const int j = wave + i * NW;
       const int d = j / (BM / RPI), jr = j % (BM / RPI);
       const int lrow = jr * RPI + srow;
-      const int row = min(m0 + lrow, p.M - 1);
-      const int k0 = kt * BKT + 16 * (sslot ^ swz(lrow));
-      glds16(p.A + d * p.a_plane + (int64_t)row * p.lda + k0, sA + d * BM * BKT + jr * 1024);
+      const uint32_t voff = (uint32_t)min(lrow, lim_a) * (uint32_t)p.lda + 16u * (uint32_t)(sslot ^ swz(lrow));
+      const int8_t* base = p.A + d * p.a_plane + (int64_t)m0 * p.lda + (int64_t)kt * BKT;
+      glds16(base + voff, sA + d * BM * BKT + jr * 1024);
     }
 #pragma unroll
-    for (int j = wave; j < IB; j += NW) {
+    for (int i = 0; i < IB / NW; ++i) {
+      const int j = wave + i * NW;
       const int e = j / (BN / RPI), jr = j % (BN / RPI);
       const int lrow = jr * RPI + srow;
-      const int row = min(n0 + lrow, p.N - 1);
-      const int k0 = kt * BKT + 16 * (sslot ^ swz(lrow));
-      glds16(p.B + e * p.b_plane + (int64_t)row * p.ldb + k0, sB + e * BN * BKT + jr * 1024);
+      const uint32_t voff = (uint32_t)min(lrow, lim_b) * (uint32_t)p.ldb + 16u * (uint32_t)(sslot ^ swz(lrow));
+      const int8_t* base = p.B + e * p.b_plane + (int64_t)n0 * p.ldb + (int64_t)kt * BKT;
+      glds16(base + voff, sB + e * BN * BKT + jr * 1024);
     }
   };
 
-  AccT acc[NC][WM][WN];
+  AccT acc[NC][TM][TN];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int t = 0; t < WM; ++t)
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < WN; ++u) acc[c][t][u] = AccT{0};
-  float facc[FLUSH ? WM : 1][FLUSH ? WN : 1][16];
+      for (int u = 0; u < TN; ++u) acc[c][t][u] = AccT{0};
+  float facc[FLUSH ? TM : 1][FLUSH ? TN : 1][TR];
   if constexpr (FLUSH) {
 #pragma unroll
-    for (int t = 0; t < WM; ++t)
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < WN; ++u)
+      for (int u = 0; u < TN; ++u)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) facc[t][u][i] = 0.f;
+        for (int i = 0; i < TR; ++i) facc[t][u][i] = 0.f;
   }
 
-  const int r = lane & 31, h = lane >> 5, sw = swz(r);
+  // fragment lane map: 32x32 -> row lane&31, 16-B chunk (lane>>5) of a 32-B k-step;
+  //                    16x16 -> row lane&15, 16-B chunk (lane>>4) of a 64-B k-step
+  const int r = S16 ? (lane & 15) : (lane & 31), h = S16 ? (lane >> 4) : (lane >> 5), sw = swz(r);
   const int nk = p.K / BKT;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s, s);
   for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(STAGES - 2, nk - 1 - kt);
-    wait_stages<PER_WAVE, STAGES - 2>(ahead);
-    block_barrier();
-    if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    if constexpr (IL == 2) {
+      // IL = 2: the next stage is always issued (the last tile is re-loaded into the free buffer
+      // near the end), so STAGES-2 stages are always in flight, the loop body has no branch and
+      // its LDS-DMA pieces can be spread between the MFMAs by the schedule below.
+      wait_stages<PER_WAVE, STAGES - 2>(STAGES - 2);
+      block_barrier();
+      stage(min(kt + STAGES - 1, nk - 1), (kt + STAGES - 1) % STAGES);
+    } else {
+      const int ahead = min(STAGES - 2, nk - 1 - kt);
+      wait_stages<PER_WAVE, STAGES - 2>(ahead);
+      block_barrier();
+      if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    }
     const int buf = kt % STAGES;
     const char* sA = smem + buf * ST;
     const char* sB = sA + A_ST;
     // fragments of k-step ks+1 are read from LDS while the MFMAs of k-step ks run (register
     // double buffer; indices are compile-time after unrolling)
-    v4i a[2][DA][WM], b[2][DB][WN];
-    auto load_frags = [&](int ks, v4i (&fa)[DA][WM], v4i (&fb)[DB][WN]) {
+    v4i a[2][DA][TM], b[2][DB][TN];
+    auto load_frags = [&](int ks, v4i (&fa)[DA][TM], v4i (&fb)[DB][TN]) {
       if constexpr (DIAG == 1) {
 #pragma unroll
         for (int d = 0; d < DA; ++d)
 #pragma unroll
-          for (int t = 0; t < WM; ++t) fa[d][t] = v4i{lane + ks, d, t, kt};
+          for (int t = 0; t < TM; ++t) fa[d][t] = v4i{lane + ks, d, t, kt};
 #pragma unroll
         for (int e = 0; e < DB; ++e)
 #pragma unroll
-          for (int u = 0; u < WN; ++u) fb[e][u] = v4i{lane, e + ks, u, kt};
+          for (int u = 0; u < TN; ++u) fb[e][u] = v4i{lane, e + ks, u, kt};
         return;
       }
-      const int off = 16 * ((2 * ks + h) ^ sw);
+      const int off = S16 ? 16 * ((4 * ks + h) ^ sw) : 16 * ((2 * ks + h) ^ sw);
 #pragma unroll
       for (int d = 0; d < DA; ++d)
 #pragma unroll
-        for (int t = 0; t < WM; ++t)
-          fa[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * 32 + r) * BKT + off);
+        for (int t = 0; t < TM; ++t)
+          fa[d][t] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * TS + r) * BKT + off);
 #pragma unroll
       for (int e = 0; e < DB; ++e)
 #pragma unroll
-        for (int u = 0; u < WN; ++u)
-          fb[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * 32 + r) * BKT + off);
+        for (int u = 0; u < TN; ++u)
+          fb[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * TS + r) * BKT + off);
     };
+    if constexpr (S16 && DA == 3 && DB == 1 && DIAG == 0) {
+      // 16x16 digit form: a full register double buffer of 64-B k-steps would not fit beside the
+      // 192 accumulator registers, so B fragments are read once per k-step and A fragments are
+      // streamed one 16-row tile ahead of the MFMAs that use them.
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const int off = 16 * ((4 * ks + h) ^ sw);
+        v4i bf[TN], af[2][DA];
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          bf[u] = *reinterpret_cast<const v4i*>(sB + (wn * WN * 32 + u * TS + r) * BKT + off);
+        auto load_a = [&](int t, v4i (&fa)[DA]) {
+#pragma unroll
+          for (int d = 0; d < DA; ++d)
+            fa[d] = *reinterpret_cast<const v4i*>(sA + d * BM * BKT + (wm * WM * 32 + t * TS + r) * BKT + off);
+        };
+        load_a(0, af[0]);
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          if (t + 1 < TM) load_a(t + 1, af[(t + 1) & 1]);
+#pragma unroll
+          for (int u = 0; u < TN; ++u)
+#pragma unroll
+            for (int d = 0; d < DA; ++d) acc[d][t][u] = mfma_i8<S16>(af[t & 1][d], bf[u], acc[d][t][u]);
+          if constexpr (IL == 1) {
+            if (t + 1 < TM) {
+#pragma unroll
+              for (int q = 0; q < DA; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              }
+              __builtin_amdgcn_sched_group_barrier(0x008, TN * DA - DA, 0);
+            }
+          }
+        }
+      }
+    } else {
     load_frags(0, a[0], b[0]);
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       if (ks + 1 < KSTEPS) load_frags(ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
       const int cur = ks & 1;
 #pragma unroll
-      for (int t = 0; t < WM; ++t)
+      for (int t = 0; t < TM; ++t)
 #pragma unroll
-        for (int u = 0; u < WN; ++u) {
+        for (int u = 0; u < TN; ++u) {
           if constexpr (F4) {
             const v4i x = a[cur][0][t], y = b[cur][0][u];
             const v8i xa = {x.x, x.y, x.z, x.w, 0, 0, 0, 0}, yb = {y.x, y.y, y.z, y.w, 0, 0, 0, 0};
-            acc[0][t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(xa, yb, acc[0][t][u], 4, 4, 0, 127,
-                                                                            0, 127);
+            if constexpr (S16)
+              acc[0][t][u] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(xa, yb, acc[0][t][u], 4, 4, 0, 127,
+                                                                              0, 127);
+            else
+              acc[0][t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(xa, yb, acc[0][t][u], 4, 4, 0, 127,
+                                                                              0, 127);
           } else if constexpr (DA == 1 && DB == 1) {
-            acc[0][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][0][t], b[cur][0][u], acc[0][t][u], 0, 0, 0);
+            acc[0][t][u] = mfma_i8<S16>(a[cur][0][t], b[cur][0][u], acc[0][t][u]);
           } else if constexpr (DB == 1) {
 #pragma unroll
-            for (int d = 0; d < DA; ++d)
-              acc[d][t][u] =
-                  __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][d][t], b[cur][0][u], acc[d][t][u], 0, 0, 0);
+            for (int d = 0; d < DA; ++d) acc[d][t][u] = mfma_i8<S16>(a[cur][d][t], b[cur][0][u], acc[d][t][u]);
           } else {
 #pragma unroll
             for (int i = 0; i < DA; ++i)
 #pragma unroll
               for (int j = 0; j < DB; ++j)
                 if (i + j >= 2)
-                  acc[i + j - 2][t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cur][i][t], b[cur][j][u],
-                                                                               acc[i + j - 2][t][u], 0, 0, 0);
+                  acc[i + j - 2][t][u] = mfma_i8<S16>(a[cur][i][t], b[cur][j][u], acc[i + j - 2][t][u]);
           }
         }
       if constexpr (IL == 1) {
         // interleave: one MFMA of step ks, then one LDS fragment read of step ks+1
-        constexpr int NLD = DA * WM + DB * WN;
-        constexpr int NMF = WM * WN * (DA == 1 ? 1 : (DB == 1 ? DA : 6));
+        constexpr int NLD = DA * TM + DB * TN;
+        constexpr int NMF = TM * TN * (DA == 1 ? 1 : (DB == 1 ? DA : 6));
         if (ks + 1 < KSTEPS) {
 #pragma unroll
           for (int q = 0; q < NLD; ++q) {
@@ -402,15 +477,36 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
           __builtin_amdgcn_sched_group_barrier(0x008, NMF - NLD, 0);
         }
       }
+      if constexpr (IL == 2) {
+        // one MFMA, then one LDS fragment read of step ks+1 and one of this tile's PER_WAVE
+        // LDS-DMA pieces (spread evenly over the KSTEPS steps), then the remaining MFMAs
+        constexpr int NLD = DA * TM + DB * TN;
+        constexpr int NMF = TM * TN * (DA == 1 ? 1 : (DB == 1 ? DA : 6));
+        constexpr int NV = (PER_WAVE + KSTEPS - 1) / KSTEPS;
+        const int nv = min(NV, PER_WAVE - ks * NV);
+        const int nld = ks + 1 < KSTEPS ? NLD : 0;
+        if (ks == 0) __builtin_amdgcn_sched_group_barrier(0x100, NLD, 0);  // fragments of step 0
+        const int nq = max(nld, nv);
+        int used = 0;
+#pragma unroll
+        for (int q = 0; q < nq; ++q) {
+          if (used < NMF) { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); ++used; }
+          if (q < nld) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if (q < nv) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+        }
+#pragma unroll
+        for (int q = used; q < NMF; ++q) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
     }
     if constexpr (FLUSH) {
       if ((kt + 1) % FLUSH_KT == 0 || kt + 1 == nk) {
 #pragma unroll
-        for (int t = 0; t < WM; ++t)
+        for (int t = 0; t < TM; ++t)
 #pragma unroll
-          for (int u = 0; u < WN; ++u) {
+          for (int u = 0; u < TN; ++u) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
+            for (int i = 0; i < TR; ++i)
               facc[t][u][i] += (float)((double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 +
                                        (double)acc[0][t][u][i]);
 #pragma unroll
@@ -420,43 +516,56 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
     }
   }
 
-  // ---- epilogue.  C/D map of the 32x32 MFMA: reg i -> tile row (i&3)+8(i>>2)+4h, col lane&31.
-  // Each 32x32 tile is finished in registers (combine digits, scales, bias), transposed through a
-  // per-wave 4 KiB LDS patch (16-B chunks XOR-swizzled by row: conflict-free both ways) and
-  // written as whole 128-B row segments with 16-B stores (4 per lane instead of 16 dword stores).
+  // ---- epilogue.  C/D map of the 32x32 MFMA: reg i -> tile row (i&3)+8(i>>2)+4h, col lane&31;
+  // of the 16x16 MFMA: reg i -> tile row 4(lane>>4)+i, col lane&15.
+  // Each 32x32 output patch (one 32x32 tile or 2x2 16x16 tiles) is finished in registers
+  // (combine digits, scales, bias), transposed through a per-wave 4 KiB LDS patch (16-B chunks
+  // XOR-swizzled by row: conflict-free both ways) and written as whole 128-B row segments with
+  // 16-B stores (4 per lane instead of 16 dword stores).
+  wait_vmcnt_c<0>();  // no LDS-DMA piece may land in the epilogue's patches
   block_barrier();  // every wave is done reading the last operand stage
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
   const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
+  constexpr int SUB = S16 ? 2 : 1;   // MFMA tiles per patch edge
 #pragma unroll
   for (int t = 0; t < WM; ++t) {
     const int trow0 = m0 + wm * WM * 32 + t * 32;
 #pragma unroll
     for (int u = 0; u < WN; ++u) {
       const int tcol0 = n0 + wn * WN * 32 + u * 32;
-      const int col = tcol0 + r;
-      const bool cin = col < p.N;
-      const float bb = (p.bias && cin) ? p.bias[col] : 0.f;
-      const double bs = (p.b_scale && cin) ? (double)p.b_scale[col] : 1.0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const int row = min(trow0 + lr, p.M - 1);
-        float f;
-        if constexpr (DA == 1 && DB == 1) {
-          f = (float)acc[0][t][u][i];  // exact: |sum| <= K < 2^24
-          if (p.a_scale || p.b_scale)
-            f = (float)((double)f * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
-        } else {
-          double v;
-          if constexpr (DB == 1) {
-            v = (double)acc[2][t][u][i] * 65536.0 + (double)acc[1][t][u][i] * 256.0 + (double)acc[0][t][u][i];
-          } else {
-            v = (double)facc[t][u][i] * 65536.0;
+      for (int sb = 0; sb < SUB; ++sb) {
+        const int lc = sb * TS + r;    // patch column of this lane
+        const int col = tcol0 + lc;
+        const bool cin = col < p.N;
+        const float bb = (p.bias && cin) ? p.bias[col] : 0.f;
+        const double bs = (p.b_scale && cin) ? (double)p.b_scale[col] : 1.0;
+#pragma unroll
+        for (int sa = 0; sa < SUB; ++sa) {
+          const int ti = t * SUB + sa, ui = u * SUB + sb;
+#pragma unroll
+          for (int i = 0; i < TR; ++i) {
+            const int lr = S16 ? sa * 16 + 4 * h + i : (i & 3) + 8 * (i >> 2) + 4 * h;
+            const int row = min(trow0 + lr, p.M - 1);
+            float f;
+            if constexpr (DA == 1 && DB == 1) {
+              f = (float)acc[0][ti][ui][i];  // exact: |sum| <= K < 2^24
+              if (p.a_scale || p.b_scale)
+                f = (float)((double)f * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
+            } else {
+              double v;
+              if constexpr (DB == 1) {
+                v = (double)acc[2][ti][ui][i] * 65536.0 + (double)acc[1][ti][ui][i] * 256.0 +
+                    (double)acc[0][ti][ui][i];
+              } else {
+                v = (double)facc[ti][ui][i] * 65536.0;
+              }
+              f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
+            }
+            if (p.bias) f += bb;
+            patch[lr * 32 + ((((lc >> 2) ^ (lr & 7)) << 2) | (lc & 3))] = f;
           }
-          f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
         }
-        if (p.bias) f += bb;
-        patch[lr * 32 + ((((r >> 2) ^ (lr & 7)) << 2) | (r & 3))] = f;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -481,13 +590,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
-          int DIAG = 0, int F4 = 0>
+          int DIAG = 0, int F4 = 0, int S16 = 0>
 int launch_v2(GemmParams p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
   const int64_t nblk = (int64_t)p.gm * p.gn;
-  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, F4>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, F4, S16>), dim3((unsigned)nblk),
                      dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   return check_launch("bnn_gemm_i8");
 }
@@ -521,6 +630,17 @@ const Variant kVariants[] = {
     {4, "gemm_i8_v2_k<1, 1, 2, 2, 4, 4, 2, 64>", launch_v2<1, 1, 2, 2, 4, 4, 2, 64>, 64},
     {5, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 4, 64>", launch_v2<1, 1, 2, 4, 4, 2, 4, 64>, 64},
     {6, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1>, 128},
+    // 16x16 MFMA shape (S16) of variants 3/6, 14, 33 (DVFS: higher clock held on 16x16)
+    {7, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 0, 1>, 128},
+    {8, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 0, 1>, 128},
+    {17, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 0, 0, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 0, 0, 0, 1>, 128},
+    {18, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 1, 0, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 1, 0, 0, 1>, 128},
+    {34, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1, 1>, 128},
+    {35, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1, 1>, 128},
+    // IL = 2: LDS-DMA pieces spread between the MFMAs
+    {9, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 2>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2>, 128},
+    {19, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 2>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 2>, 128},
+    {36, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1>, 128},
     {77, "diag: v6 without LDS fragment reads", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 1>, 128},
     {78, "diag: v6 without global->LDS staging", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 2>, 128},
     {10, "gemm_i8_k<3, 1, 2, 2>", launch<3, 1, 2, 2>, 64},
@@ -552,7 +672,7 @@ const Variant* find_variant(int id) {
 const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int64_t K) {
   if (a_digits == 0) {  // FP4 ternary form; K in bytes
     const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
-    int id = g_variant >= 0 ? 30 + g_variant : (big ? 33 : 31);   // sweep r01: 33 = 0.40 of FP4 peak
+    int id = g_variant >= 0 ? 30 + g_variant : (big ? 36 : 31);   // sweep r01: 36 = 0.435 of FP4 peak
     const Variant* v = find_variant(id);
     if (v == nullptr) v = find_variant(31);
     if (K % v->bk != 0) v = find_variant(big ? 32 : 31);
@@ -563,13 +683,13 @@ const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int
   if (g_variant >= 0) {
     id = base + g_variant;
     alt = base + 1;
-  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 interleaved 0.44 of peak; 128x128 on small grids
+  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 16x16-MFMA 0.465 of peak; 128x128 on small grids
     const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
-    id = big ? 6 : 1;
+    id = big ? 7 : 1;
     alt = big ? 2 : 1;
-  } else if (b_digits == 1) {   // 128x256 BK128 8 waves: 0.46-0.49 of peak on dX / dW
+  } else if (b_digits == 1) {   // 128x256 BK128 8 waves 16x16-MFMA: 0.50-0.53 of peak on dX / dW
     const bool big = ((M + 127) / 128) * ((N + 255) / 256) >= 256;
-    id = big ? 14 : 13;
+    id = big ? 17 : 13;
     alt = big ? 15 : 13;
   } else {
     id = 22;
@@ -606,6 +726,9 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
   if (M == 0 || N == 0) return 0;
   GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
                (int)M, (int)N, (int)K, 0, 0};
+  // v2 kernels address a tile's rows with 32-bit per-lane offsets (< 256 rows x ld)
+  if (lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31))
+    return find_variant(a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20))->fn(p, reinterpret_cast<hipStream_t>(stream));
   return pick_kernel(a_digits, b_digits, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -613,8 +736,9 @@ BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_
                          float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
   if (!A || !B || !C || M < 0 || N < 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K || lda % 16 != 0 ||
       ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) || M > 0x7fffffff || N > 0x7fffffff ||
-      K > 0x7fffffff) {
-    set_error("bnn_gemm_fp4: bad arguments (M=%lld N=%lld K=%lld bytes; K must be a positive multiple of 64)",
+      K > 0x7fffffff || lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31)) {
+    set_error("bnn_gemm_fp4: bad arguments (M=%lld N=%lld K=%lld bytes; K must be a positive multiple of 64 "
+              "and below 2^23 bytes)",
               (long long)M, (long long)N, (long long)K);
     return kErrInval;
   }
@@ -626,6 +750,7 @@ BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_
 
 BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,
                                        int64_t K) {
+  if (round_up(K, 64) * 256 >= (1LL << 31)) return find_variant(a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20))->name;
   return pick_kernel(a_digits, b_digits, M, N, K)->name;
 }
 

@@ -119,7 +119,7 @@ def test_every_fp4_variant_is_exact(F, M, N, K):
     w4, _ = F.sign_pack_fp4(dev(w))
     names = set()
     try:
-        for v in range(0, 5):
+        for v in range(0, 7):
             _lib.call("bnn_gemm_set_variant", v)
             name = F.gemm_kernel_name(0, 0, M, N, x4.shape[1])
             if name in names:
@@ -386,7 +386,7 @@ def test_every_gemm_variant_is_exact(F, cfg, M, N, K):
     Bt = dev(B if db == 3 else B[0])
     names = set()
     try:
-        for v in range(0, 8):
+        for v in range(0, 10):
             _lib.call("bnn_gemm_set_variant", v)
             name = F.gemm_kernel_name(da, db, M, N, K)
             if name in names:

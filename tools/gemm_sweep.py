@@ -33,7 +33,7 @@ SHAPES = {  # name: (M, N, K, a_digits, b_digits)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,-1")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,-1")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
