@@ -42,6 +42,17 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// The same 16-B LDS-DMA in its saddr form: wave-uniform 64-bit base in SGPRs + per-lane 32-bit
+// offset (one VGPR), LDS destination through M0.  Written as asm because the compiler hoists
+// base+offset into a 64-bit VGPR pair per piece.  The explicit wait_vmcnt_c() counts cover it.
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, void* l) {
+  const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(l);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :
+               : "s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+
 // Bijective XCD remap (blocks b and b+8 share an XCD under round-robin dispatch: speed only)
 // followed by a grouped raster (8 tile-rows per group) so an XCD works on neighbouring tiles.
 __device__ __forceinline__ void tile_of(int bid, int gm, int gn, int& tm, int& tn) {
@@ -270,7 +281,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
   using AccT = typename std::conditional<
       S16 != 0, typename std::conditional<F4 != 0, v4f, v4i>::type,
       typename std::conditional<F4 != 0, v16f, v16i>::type>::type;
-  // DIAG (timing-only builds, wrong results): 1 = no LDS fragment reads, 2 = no global->LDS staging
+  // DIAG (timing-only builds, wrong results): 1 = no LDS fragment reads, 2 = no global->LDS staging;
+  // DIAG = 3 is not a diagnostic: the 16x16 digit form with B fragments prefetched a k-step ahead
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   constexpr int A_ST = DA * BM * BKT, B_ST = DB * BN * BKT, ST = A_ST + B_ST;
@@ -314,7 +326,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
       const int lrow = jr * RPI + srow;
       const uint32_t voff = (uint32_t)min(lrow, lim_a) * (uint32_t)p.lda + 16u * (uint32_t)(sslot ^ swz(lrow));
       const int8_t* base = p.A + d * p.a_plane + (int64_t)m0 * p.lda + (int64_t)kt * BKT;
-      glds16(base + voff, sA + d * BM * BKT + jr * 1024);
+      glds16_s(base, voff, sA + d * BM * BKT + jr * 1024);
     }
 #pragma unroll
     for (int i = 0; i < IB / NW; ++i) {
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
       const int lrow = jr * RPI + srow;
       const uint32_t voff = (uint32_t)min(lrow, lim_b) * (uint32_t)p.ldb + 16u * (uint32_t)(sslot ^ swz(lrow));
       const int8_t* base = p.B + e * p.b_plane + (int64_t)n0 * p.ldb + (int64_t)kt * BKT;
-      glds16(base + voff, sB + e * BN * BKT + jr * 1024);
+      glds16_s(base, voff, sB + e * BN * BKT + jr * 1024);
     }
   };
 
@@ -395,17 +407,25 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
         for (int u = 0; u < TN; ++u)
           fb[e][u] = *reinterpret_cast<const v4i*>(sB + e * BN * BKT + (wn * WN * 32 + u * TS + r) * BKT + off);
     };
-    if constexpr (S16 && DA == 3 && DB == 1 && DIAG == 0) {
+    if constexpr (S16 && DA == 3 && DB == 1 && (DIAG == 0 || DIAG == 3)) {
+      constexpr bool BPF = DIAG == 3;   // B fragments of the next k-step read during the last tiles
       // 16x16 digit form: a full register double buffer of 64-B k-steps would not fit beside the
       // 192 accumulator registers, so B fragments are read once per k-step and A fragments are
       // streamed one 16-row tile ahead of the MFMAs that use them.
+      v4i bfs[2][TN];
+      auto load_b = [&](int ks, v4i (&fb)[TN]) {
+        const int off = 16 * ((4 * ks + h) ^ sw);
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          fb[u] = *reinterpret_cast<const v4i*>(sB + (wn * WN * 32 + u * TS + r) * BKT + off);
+      };
+      if constexpr (BPF) load_b(0, bfs[0]);
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks) {
         const int off = 16 * ((4 * ks + h) ^ sw);
-        v4i bf[TN], af[2][DA];
-#pragma unroll
-        for (int u = 0; u < TN; ++u)
-          bf[u] = *reinterpret_cast<const v4i*>(sB + (wn * WN * 32 + u * TS + r) * BKT + off);
+        v4i(&bf)[TN] = bfs[BPF ? (ks & 1) : 0];
+        if constexpr (!BPF) load_b(ks, bf);
+        v4i af[2][DA];
         auto load_a = [&](int t, v4i (&fa)[DA]) {
 #pragma unroll
           for (int d = 0; d < DA; ++d)
@@ -415,6 +435,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
 #pragma unroll
         for (int t = 0; t < TM; ++t) {
           if (t + 1 < TM) load_a(t + 1, af[(t + 1) & 1]);
+          if (BPF && t == TM - 2 && ks + 1 < KSTEPS) load_b(ks + 1, bfs[(ks + 1) & 1]);
 #pragma unroll
           for (int u = 0; u < TN; ++u)
 #pragma unroll
@@ -427,6 +448,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
               }
               __builtin_amdgcn_sched_group_barrier(0x008, TN * DA - DA, 0);
+            }
+          }
+          if constexpr (IL == 2) {
+            // the k-tile's PER_WAVE LDS-DMA pieces spread over its KSTEPS*TM (k-step, tile) slots
+            constexpr int SLOTS = KSTEPS * TM;
+            const int slot = ks * TM + t;
+            const int nv = PER_WAVE * (slot + 1) / SLOTS - PER_WAVE * slot / SLOTS;
+            const int nld = t + 1 < TM ? DA : 0;
+            if (t == 0) __builtin_amdgcn_sched_group_barrier(0x100, TN + DA, 0);
+#pragma unroll
+            for (int q = 0; q < TN * DA; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              if (q < nld) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              if (q < nv) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
             }
           }
         }
@@ -634,12 +669,12 @@ const Variant kVariants[] = {
     {7, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 0, 1>, 128},
     {8, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 0, 1>, 128},
     {17, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 0, 0, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 0, 0, 0, 1>, 128},
-    {18, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 1, 0, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 1, 0, 0, 1>, 128},
+    {18, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 2, 0, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 2, 0, 0, 1>, 128},
     {34, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1, 1>, 128},
     {35, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 0, 1, 1>, 128},
-    // IL = 2: LDS-DMA pieces spread between the MFMAs
-    {9, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 2>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2>, 128},
-    {19, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 2>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 2>, 128},
+    // IL = 2: LDS-DMA pieces spread between the MFMAs (9, 18, 36: 16x16; 19: 16x16 + B prefetch)
+    {9, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 0, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 0, 1>, 128},
+    {19, "gemm_i8_v2_k<3, 1, 2, 4, 2, 2, 2, 128, 0, 3, 0, 1>", launch_v2<3, 1, 2, 4, 2, 2, 2, 128, 0, 3, 0, 1>, 128},
     {36, "gemm_i8_v2_k<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1>, 128},
     {77, "diag: v6 without LDS fragment reads", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 1>, 128},
     {78, "diag: v6 without global->LDS staging", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 1, 2>, 128},
@@ -683,13 +718,13 @@ const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int
   if (g_variant >= 0) {
     id = base + g_variant;
     alt = base + 1;
-  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 16x16-MFMA 0.465 of peak; 128x128 on small grids
+  } else if (a_digits == 1) {   // sweep r01: 256x256 BK128 16x16-MFMA + DMA spread 0.49 of peak; 128x128 on small grids
     const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
-    id = big ? 7 : 1;
+    id = big ? 9 : 1;
     alt = big ? 2 : 1;
-  } else if (b_digits == 1) {   // 128x256 BK128 8 waves 16x16-MFMA: 0.50-0.53 of peak on dX / dW
+  } else if (b_digits == 1) {   // 128x256 BK128 8 waves 16x16-MFMA + DMA spread: 0.51-0.56 of peak on dX / dW
     const bool big = ((M + 127) / 128) * ((N + 255) / 256) >= 256;
-    id = big ? 17 : 13;
+    id = big ? 18 : 13;
     alt = big ? 15 : 13;
   } else {
     id = 22;
