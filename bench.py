@@ -62,7 +62,7 @@ def build(cfg, backend):
     from bnn_amd import nets
     name = CONFIGS[cfg][0]
     if name == "cnn":
-        model = nets.BinCNN(org_protocol=False, mutate_input=False)
+        model = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True)
     else:
         model = nets.MODELS[name](org_protocol=False, mutate_input=False, backend=backend, fused_bn=True)
     return model

@@ -20,7 +20,7 @@ from . import _lib as L
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
     "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "batch_norm_hardtanh",
-    "bn_hardtanh_binary_linear",
+    "bn_hardtanh_binary_linear", "batch_norm2d_hardtanh_pool",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
 
@@ -463,6 +463,74 @@ def batch_norm_hardtanh(x, bn, hardtanh=True):
     rm, rv, bn_training, factor = _bn_module_args(bn)
     return BatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
                                            hardtanh)
+
+
+# ----------------------------------------------------------------------------- BatchNorm2d (+ Hardtanh + MaxPool2d)
+class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
+    """maxpool2(hardtanh(nn.BatchNorm2d(x))) on NCHW, fused (the block after each BinarizeConv2d of
+    the build's CNN; mnist-dist.py:31-51 template).  pool = 2 fuses MaxPool2d(2, 2) (argmax
+    recomputed in backward), pool = 0 leaves it out.  Running stats updated in place (train)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh, pool):
+        _check(x, weight, bias, running_mean, running_var)
+        x = x if x.is_contiguous() else x.contiguous()
+        N, C, H, W = x.shape
+        oh, ow = (H // 2, W // 2) if pool else (H, W)
+        y = torch.empty((N, C, oh, ow), dtype=torch.float32, device=x.device)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=x.device)
+        nel = N * C * H * W
+        if training:
+            mean = torch.empty((C,), dtype=torch.float32, device=x.device)
+            invstd = torch.empty_like(mean)
+            with _timed("bn2d_fwd_train", 0, 8 * nel + 4 * y.numel()):
+                L.call("bnn_bn2d_fwd_train", L.ptr(x), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                       L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
+                       L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
+        else:
+            mean = running_mean
+            invstd = (running_var + eps).rsqrt()
+            with _timed("bn2d_fwd_eval", 0, 4 * nel + 4 * y.numel()):
+                L.call("bnn_bn2d_fwd_eval", L.ptr(x), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                       L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
+        ctx.save_for_backward(x, w, b, mean, invstd)
+        ctx.hardtanh, ctx.pool = hardtanh, pool
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, mean, invstd = ctx.saved_tensors
+        dy = dy if dy.is_contiguous() else dy.contiguous()
+        N, C, H, W = x.shape
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
+        db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
+        ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=x.device)
+        nel = N * C * H * W
+        with _timed("bn2d_bwd", 0, 12 * nel + 8 * dy.numel()):
+            L.call("bnn_bn2d_bwd", L.ptr(x), L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(mean),
+                   L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
+                   L.stream())
+        return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, None)
+
+
+def bn2d_fusable(x, pool):
+    """Shapes the fused BatchNorm2d kernels take (else the caller runs the torch modules)."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32):
+        return False
+    H, W = x.shape[2], x.shape[3]
+    return (H * W) % 4 == 0 and (not pool or (H % 2 == 0 and W % 2 == 0))
+
+
+def batch_norm2d_hardtanh_pool(x, bn, hardtanh=True, pool=2):
+    """Apply an ``nn.BatchNorm2d`` module (torch ``_BatchNorm.forward`` semantics), then Hardtanh
+    and MaxPool2d(2, 2) (pool = 2) through libbnn."""
+    rm, rv, bn_training, factor = _bn_module_args(bn)
+    return BatchNorm2dHardtanhPoolFunction.apply(x, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
+                                                 hardtanh, pool)
 
 
 class BNHardtanhBinaryLinearFunction(torch.autograd.Function):

@@ -88,8 +88,11 @@ def WideNet(width=8192, **kw):
 
 
 class BinCNN(nn.Module):
-    def __init__(self, num_classes=10, org_protocol=True, mutate_input=True):
+    def __init__(self, num_classes=10, org_protocol=True, mutate_input=True, fused_bn=False):
         super().__init__()
+        # fused_bn: BatchNorm2d -> Hardtanh -> MaxPool2d of each layer run as one libbnn op (same
+        # parameters, buffers and math; the Sequential modules and state_dict are unchanged)
+        self.fused_bn = fused_bn
         self.layer1 = nn.Sequential(BinarizeConv2d(1, 16, kernel_size=5, stride=1, padding=2),
                                     nn.BatchNorm2d(16), nn.Hardtanh(), nn.MaxPool2d(kernel_size=2, stride=2))
         self.layer2 = nn.Sequential(BinarizeConv2d(16, 32, kernel_size=5, stride=1, padding=2),
@@ -98,8 +101,17 @@ class BinCNN(nn.Module):
         self.logsoftmax = nn.LogSoftmax(dim=1)
         _configure(self, org_protocol, mutate_input)
 
+    def _layer(self, seq, x):
+        conv, bn, ht, pool = seq
+        z = conv(x)
+        if (self.fused_bn and BF.bn2d_fusable(z, 2) and isinstance(bn, nn.BatchNorm2d)
+                and pool.kernel_size == 2 and pool.stride == 2 and pool.padding == 0 and not pool.ceil_mode
+                and ht.min_val == -1.0 and ht.max_val == 1.0):
+            return BF.batch_norm2d_hardtanh_pool(z, bn, hardtanh=True, pool=2)
+        return pool(ht(bn(z)))
+
     def forward(self, x):
-        out = self.layer2(self.layer1(x))
+        out = self._layer(self.layer2, self._layer(self.layer1, x))
         out = out.reshape(out.size(0), -1)
         return self.logsoftmax(self.fc(out))
 

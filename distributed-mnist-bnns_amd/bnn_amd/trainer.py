@@ -91,7 +91,7 @@ def train(gpu, args):
                                 device_id=device if args.backend == "nccl" else None)
     torch.cuda.manual_seed(args.seed)
     model = nets.MODELS[args.model](org_protocol=False, mutate_input=False,
-                                    **({} if args.model == "cnn" else {"fused_bn": True})).to(device)
+                                    fused_bn=True).to(device)
     exchange = GradExchange(model) if world > 1 else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=nets.binary_params(model))
     crit = torch.nn.CrossEntropyLoss()

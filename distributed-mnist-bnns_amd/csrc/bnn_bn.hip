@@ -110,13 +110,16 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
                                                       int64_t M, int64_t C, int64_t R, float momentum, float eps,
                                                       float* __restrict__ rmean, float* __restrict__ rvar,
                                                       float* __restrict__ save_mean,
-                                                      float* __restrict__ save_invstd) {
+                                                      float* __restrict__ save_invstd, int64_t chunk_rows,
+                                                      int64_t hw) {
+  // chunk r covers rows [r*chunk_rows, min((r+1)*chunk_rows, M)) of hw elements each (hw = 1 for
+  // BatchNorm1d; H*W for the NCHW BatchNorm2d of bnn_bn2d.hip)
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int64_t r = 0; r < R; ++r) {  // Chan et al. merge in a fixed order
-    const int64_t hi = ((r + 1) * BN_ROWS < M) ? (r + 1) * BN_ROWS : M;
-    const double nb = (double)(hi - r * BN_ROWS);
+    const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
+    const double nb = (double)((hi - r * chunk_rows) * hw);
     const double mb = p0[r * C + c], m2b = p1[r * C + c];
     const double nt = n + nb, delta = mb - mean;
     mean += delta * nb / nt;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
   save_mean[c] = (float)mean;
   save_invstd[c] = (float)(1.0 / std::sqrt(var + (double)eps));
   if (rmean != nullptr && momentum >= 0.f) {
-    const double unb = M > 1 ? m2 / (n - 1.0) : var;
+    const double unb = n > 1.0 ? m2 / (n - 1.0) : var;
     rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
     rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
   }
@@ -227,6 +230,278 @@ bool bn_args_ok(const float* x, int64_t M, int64_t C) {
 
 bool vec_ok(const float* p) { return p == nullptr || aligned16(p); }
 
+
+// ------------------------------------------------------------------ BatchNorm2d (+ Hardtanh, + MaxPool2d(2))
+// NCHW [N][C][H][W] activations of the binarized CNN (conv -> BatchNorm2d -> Hardtanh -> MaxPool2d(2),
+// the mnist-dist.py:31-51 template the build's BinCNN follows).  Per-channel statistics over N*H*W,
+// same math and merge order as the 1d kernels above (chunk = CR images of one channel, one workgroup).
+// pool = 2 fuses MaxPool2d(kernel 2, stride 2): forward writes only the pooled map; backward takes
+// the pooled gradient and recomputes the window's argmax (torch's rule: first strictly greater
+// value in (h, w) scan order, NaN wins), so neither the fp32 full-resolution output nor the
+// max-pool indices are ever stored.
+
+constexpr int BN2_T = 256;
+
+inline int64_t bn2_chunk_images(int64_t N, int64_t C) {
+  const int64_t R = std::max<int64_t>(1, std::min<int64_t>(N, (2048 + C - 1) / C));
+  return (N + R - 1) / R;
+}
+
+__device__ __forceinline__ void block_sum2(double& a, double& b) {
+  __shared__ double sa[BN2_T / 64], sb[BN2_T / 64];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sa[w] = a;
+    sb[w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ta = 0.0, tb = 0.0;
+    for (int i = 0; i < BN2_T / 64; ++i) {   // fixed order: deterministic
+      ta += sa[i];
+      tb += sb[i];
+    }
+    a = ta;
+    b = tb;
+  }
+}
+
+struct Bn2Chan {   // per-channel affine of the normalisation
+  float mu, is, ga, be;
+};
+
+__device__ __forceinline__ Bn2Chan bn2_chan(int64_t c, const float* mean, const float* invstd, const float* gamma,
+                                            const float* beta) {
+  return Bn2Chan{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f};
+}
+
+// One 2x2 pooling window: pre-activation y (before the clamp) of its 4 elements in torch scan
+// order (h, w), the max-pool output and the argmax slot.
+struct Win {
+  float xh[4], y[4];
+  float out;
+  int arg;
+};
+
+__device__ __forceinline__ Win bn2_window(float2 top, float2 bot, const Bn2Chan& k, int hardtanh) {
+  Win w;
+  const float xs[4] = {top.x, top.y, bot.x, bot.y};
+  float best = -__builtin_inff();
+  int arg = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w.xh[j] = (xs[j] - k.mu) * k.is;
+    w.y[j] = fmaf(w.xh[j], k.ga, k.be);
+    const float v = hardtanh ? fminf(fmaxf(w.y[j], -1.f), 1.f) : w.y[j];
+    if (v > best || v != v) {
+      best = v;
+      arg = j;
+    }
+  }
+  w.out = best;
+  w.arg = arg;
+  return w;
+}
+
+// MODE 0: chunk (mean, M2) of x.  MODE 1: chunk (sum g, sum g*xhat), g = masked full-resolution
+// gradient (POOL: routed to the window argmax from the pooled dy).
+template <int MODE, int POOL>
+__global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                       int64_t N, int64_t C, int H, int W, int64_t CR,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, int hardtanh,
+                                                       double* __restrict__ p0, double* __restrict__ p1) {
+  const int64_t c = blockIdx.x, r = blockIdx.y;
+  const int64_t n0 = r * CR, n1 = (n0 + CR < N) ? n0 + CR : N;
+  const int64_t HW = (int64_t)H * W;
+  double a = 0.0, b = 0.0;
+  float fa = 0.f, fb = 0.f;
+  int cnt = 0;
+  if (MODE == 0) {
+    const float shift = x[(n0 * C + c) * HW];
+    const int64_t hw4 = HW / 4, total = (n1 - n0) * hw4;
+    for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
+      const int64_t n = n0 + i / hw4, j = i - (i / hw4) * hw4;
+      const float4 v = ld4(x + (n * C + c) * HW + 4 * j);
+      const float d[4] = {v.x - shift, v.y - shift, v.z - shift, v.w - shift};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fa += d[q];
+        fb = fmaf(d[q], d[q], fb);
+      }
+      if (++cnt == 8) {
+        a += (double)fa;
+        b += (double)fb;
+        fa = fb = 0.f;
+        cnt = 0;
+      }
+    }
+    a += (double)fa;
+    b += (double)fb;
+    block_sum2(a, b);
+    if (threadIdx.x == 0) {
+      const double nb = (double)((n1 - n0) * HW), dm = a / nb;
+      p0[r * C + c] = (double)shift + dm;
+      p1[r * C + c] = b - a * dm;
+    }
+    return;
+  }
+  const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+  if (POOL) {
+    const int PH = H / 2, PW = W / 2;
+    const int64_t pp = (int64_t)PH * PW, total = (n1 - n0) * pp;
+    for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
+      const int64_t n = n0 + i / pp, p = i - (i / pp) * pp;
+      const int ph = (int)(p / PW), pw = (int)(p - (int64_t)ph * PW);
+      const float* xp = x + (n * C + c) * HW + (int64_t)(2 * ph) * W + 2 * pw;
+      const Win w = bn2_window(*reinterpret_cast<const float2*>(xp), *reinterpret_cast<const float2*>(xp + W),
+                               k, hardtanh);
+      const float yv = w.y[w.arg];
+      const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? dy[(n * C + c) * pp + p] : 0.f;
+      fa += g;
+      fb = fmaf(g, w.xh[w.arg], fb);
+      if (++cnt == 8) {
+        a += (double)fa;
+        b += (double)fb;
+        fa = fb = 0.f;
+        cnt = 0;
+      }
+    }
+  } else {
+    const int64_t hw4 = HW / 4, total = (n1 - n0) * hw4;
+    for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
+      const int64_t n = n0 + i / hw4, j = i - (i / hw4) * hw4;
+      const int64_t o = (n * C + c) * HW + 4 * j;
+      const float4 xv = ld4(x + o), gv = ld4(dy + o);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float xh = (xs[q] - k.mu) * k.is;
+        const float y = fmaf(xh, k.ga, k.be);
+        const float g = (!hardtanh || (y > -1.f && y < 1.f)) ? gs[q] : 0.f;
+        fa += g;
+        fb = fmaf(g, xh, fb);
+      }
+      if (++cnt == 8) {
+        a += (double)fa;
+        b += (double)fb;
+        fa = fb = 0.f;
+        cnt = 0;
+      }
+    }
+  }
+  a += (double)fa;
+  b += (double)fb;
+  block_sum2(a, b);
+  if (threadIdx.x == 0) {
+    p0[r * C + c] = a;
+    p1[r * C + c] = b;
+  }
+}
+
+// Forward apply: y = clamp((x-mean)*invstd*gamma+beta) (POOL: max over each 2x2 window).
+template <int POOL>
+__global__ __launch_bounds__(256) void bn2d_apply_k(const float* __restrict__ x, int64_t N, int64_t C, int H, int W,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ invstd,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, int hardtanh,
+                                                    float* __restrict__ y) {
+  const int64_t HW = (int64_t)H * W;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (POOL) {
+    const int PH = H / 2, PW = W / 2;
+    const int64_t pp = (int64_t)PH * PW, total = N * C * pp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+      const int64_t plane = i / pp, p = i - plane * pp;
+      const int ph = (int)(p / PW), pw = (int)(p - (int64_t)ph * PW);
+      const Bn2Chan k = bn2_chan(plane % C, mean, invstd, gamma, beta);
+      const float* xp = x + plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
+      y[i] = bn2_window(*reinterpret_cast<const float2*>(xp), *reinterpret_cast<const float2*>(xp + W), k,
+                        hardtanh).out;
+    }
+    return;
+  }
+  const int64_t n4 = N * C * HW / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const Bn2Chan k = bn2_chan(((4 * i) / HW) % C, mean, invstd, gamma, beta);
+    const float4 xv = ld4(x + 4 * i);
+    float v[4] = {fmaf((xv.x - k.mu) * k.is, k.ga, k.be), fmaf((xv.y - k.mu) * k.is, k.ga, k.be),
+                  fmaf((xv.z - k.mu) * k.is, k.ga, k.be), fmaf((xv.w - k.mu) * k.is, k.ga, k.be)};
+    if (hardtanh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fminf(fmaxf(v[j], -1.f), 1.f);
+    }
+    *reinterpret_cast<float4*>(y + 4 * i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// Backward apply: dx = gamma*invstd*(g - sum_g/n - xhat*sum_gxhat/n), g routed/masked as in reduce.
+template <int POOL>
+__global__ __launch_bounds__(256) void bn2d_bwd_apply_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                        int64_t N, int64_t C, int H, int W,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int hardtanh,
+                                                        const float* __restrict__ sg,
+                                                        const float* __restrict__ sgx, float* __restrict__ dx) {
+  const int64_t HW = (int64_t)H * W;
+  const float inv_n = (float)(1.0 / ((double)N * (double)HW));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (POOL) {
+    const int PH = H / 2, PW = W / 2;
+    const int64_t pp = (int64_t)PH * PW, total = N * C * pp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+      const int64_t plane = i / pp, p = i - plane * pp, c = plane % C;
+      const int ph = (int)(p / PW), pw = (int)(p - (int64_t)ph * PW);
+      const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+      const float m0 = sg[c] * inv_n, m1 = sgx[c] * inv_n, sc = k.ga * k.is;
+      const int64_t off = plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
+      const Win w = bn2_window(*reinterpret_cast<const float2*>(x + off),
+                               *reinterpret_cast<const float2*>(x + off + W), k, hardtanh);
+      const float gp = dy[i];
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = (j == w.arg && (!hardtanh || (w.y[j] > -1.f && w.y[j] < 1.f))) ? gp : 0.f;
+        o[j] = sc * (g - m0 - w.xh[j] * m1);
+      }
+      *reinterpret_cast<float2*>(dx + off) = make_float2(o[0], o[1]);
+      *reinterpret_cast<float2*>(dx + off + W) = make_float2(o[2], o[3]);
+    }
+    return;
+  }
+  const int64_t n4 = N * C * HW / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int64_t c = ((4 * i) / HW) % C;
+    const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+    const float m0 = sg[c] * inv_n, m1 = sgx[c] * inv_n, sc = k.ga * k.is;
+    const float4 xv = ld4(x + 4 * i), gv = ld4(dy + 4 * i);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (xs[j] - k.mu) * k.is;
+      const float yv = fmaf(xh, k.ga, k.be);
+      const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
+      o[j] = sc * (g - m0 - xh * m1);
+    }
+    *reinterpret_cast<float4*>(dx + 4 * i) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+bool bn2_args_ok(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int pool) {
+  if (!x || N <= 0 || C <= 0 || H <= 0 || W <= 0 || !aligned16(x) || C > 65535) return false;
+  if ((H * W) % 4 != 0) return false;
+  if (pool != 0 && (pool != 2 || H % 2 != 0 || W % 2 != 0)) return false;
+  return (N + bn2_chunk_images(N, C) - 1) / bn2_chunk_images(N, C) <= 65535;
+}
+
 }  // namespace
 }  // namespace bnn
 
@@ -255,7 +530,7 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
   hipLaunchKernelGGL(bn_reduce_k<0>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x,
                      nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
   hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, M, C, R,
-                     momentum, eps, running_mean, running_var, save_mean, save_invstd);
+                     momentum, eps, running_mean, running_var, save_mean, save_invstd, (int64_t)BN_ROWS, (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
     hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
                        gamma, beta, hardtanh, y);
@@ -302,4 +577,82 @@ BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
                        save_invstd, gamma, beta, hardtanh, k0, k1, dx);
   }
   return check_launch("bnn_bn_bwd");
+}
+
+BNN_API int64_t bnn_bn2d_workspace(int64_t N, int64_t C) {
+  const int64_t R = (std::max<int64_t>(N, 1) + bn2_chunk_images(std::max<int64_t>(N, 1), C) - 1) /
+                    bn2_chunk_images(std::max<int64_t>(N, 1), C);
+  return 2 * R * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
+}
+
+#define BN2_POOL_SWITCH(pool, ...) \
+  do { if (pool) { constexpr int P = 2; __VA_ARGS__; } else { constexpr int P = 0; __VA_ARGS__; } } while (0)
+
+BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, float momentum,
+                               float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
+                               int32_t pool, void* work, void* stream) {
+  if (!bn2_args_ok(x, N, C, H, W, pool) || !save_mean || !save_invstd || !work || !y ||
+      (running_mean == nullptr) != (running_var == nullptr)) {
+    set_error("bnn_bn2d_fwd_train: bad arguments (N=%lld C=%lld H=%lld W=%lld pool=%d; H*W must be a multiple "
+              "of 4, pool 0 or 2 with even H, W)", (long long)N, (long long)C, (long long)H, (long long)W, pool);
+    return kErrInval;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t CR = bn2_chunk_images(N, C), R = (N + CR - 1) / CR;
+  double* p0 = reinterpret_cast<double*>(work);
+  double* p1 = p0 + R * C;
+  hipLaunchKernelGGL((bn2d_reduce_k<0, 0>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s, x, nullptr, N, C,
+                     (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
+  hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, N, C, R,
+                     momentum, eps, running_mean, running_var, save_mean, save_invstd, CR, H * W);
+  const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
+  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
+                                           (int)W, save_mean, save_invstd, gamma, beta, hardtanh, y));
+  return check_launch("bnn_bn2d_fwd_train");
+}
+
+BNN_API int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+                              const float* beta, const float* running_mean, const float* running_var, float eps,
+                              float* y, int32_t hardtanh, int32_t pool, void* work, void* stream) {
+  if (!bn2_args_ok(x, N, C, H, W, pool) || !running_mean || !running_var || !y || !work) {
+    set_error("bnn_bn2d_fwd_eval: bad arguments");
+    return kErrInval;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* istd = reinterpret_cast<float*>(work);
+  hipLaunchKernelGGL(bn_invstd_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_var, istd, C, eps);
+  const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
+  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
+                                           (int)W, running_mean, istd, gamma, beta, hardtanh, y));
+  return check_launch("bnn_bn2d_fwd_eval");
+}
+
+BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+                         const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                         int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                         void* stream) {
+  if (!bn2_args_ok(x, N, C, H, W, pool) || !dy || !save_mean || !save_invstd || !work ||
+      (dx && !aligned16(dx)) || (!pool && !aligned16(dy))) {
+    set_error("bnn_bn2d_bwd: bad arguments");
+    return kErrInval;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t CR = bn2_chunk_images(N, C), R = (N + CR - 1) / CR;
+  double* p0 = reinterpret_cast<double*>(work);
+  double* p1 = p0 + R * C;
+  float* k0 = reinterpret_cast<float*>(p1 + R * C);
+  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
+  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
+                                           s, x, dy, N, C, (int)H, (int)W, CR, save_mean, save_invstd, gamma, beta,
+                                           hardtanh, p0, p1));
+  hipLaunchKernelGGL(bn_bwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, C, R, dgamma,
+                     dbeta, k0, k1);
+  if (dx) {
+    const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
+    BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_bwd_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, dy, N,
+                                             C, (int)H, (int)W, save_mean, save_invstd, gamma, beta, hardtanh, k0,
+                                             k1, dx));
+  }
+  return check_launch("bnn_bn2d_bwd");
 }

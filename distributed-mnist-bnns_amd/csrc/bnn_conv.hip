@@ -433,14 +433,41 @@ __global__ __launch_bounds__(TILE_T) void conv_bwd_filter_tile_k(const float* __
   }
 }
 
-__global__ __launch_bounds__(256) void conv_filter_tile_reduce_k(const float* __restrict__ part, int64_t nparts,
-                                                                 int CO, int ncombo, int Co,
-                                                                 float* __restrict__ dw, float* __restrict__ db) {
+// Partials -> dW / dB in two fixed-order stages (deterministic): stage 1 sums a contiguous slice of
+// the parts for 256 elements per workgroup (grid.y = slices, so the reduction is spread over the
+// chip instead of one serial walk per element); stage 2 folds the <= FILTER_SLICES slice sums.
+constexpr int FILTER_SLICES = 64;
+
+inline int64_t filter_slices(int64_t nparts) { return std::min<int64_t>(std::max<int64_t>(nparts, 1), FILTER_SLICES); }
+
+__global__ __launch_bounds__(256) void conv_filter_tile_reduce1_k(const float* __restrict__ part, int64_t nparts,
+                                                                  int64_t nelem, int64_t nslices,
+                                                                  double* __restrict__ slice) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nelem) return;
+  const int64_t q0 = blockIdx.y * nparts / nslices, q1 = (blockIdx.y + 1) * nparts / nslices;
+  double acc = 0.0;
+  int64_t q = q0;
+  for (; q + 4 <= q1; q += 4) {   // 4 independent loads in flight per thread
+    const float v0 = part[q * nelem + e], v1 = part[(q + 1) * nelem + e];
+    const float v2 = part[(q + 2) * nelem + e], v3 = part[(q + 3) * nelem + e];
+    acc += (double)v0;
+    acc += (double)v1;
+    acc += (double)v2;
+    acc += (double)v3;
+  }
+  for (; q < q1; ++q) acc += (double)part[q * nelem + e];
+  slice[blockIdx.y * nelem + e] = acc;
+}
+
+__global__ __launch_bounds__(256) void conv_filter_tile_reduce2_k(const double* __restrict__ slice, int64_t nslices,
+                                                                  int CO, int ncombo, int Co,
+                                                                  float* __restrict__ dw, float* __restrict__ db) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nelem = (int64_t)CO * ncombo + CO;
   if (e >= nelem) return;
   double acc = 0.0;
-  for (int64_t q = 0; q < nparts; ++q) acc += (double)part[q * nelem + e];
+  for (int64_t q = 0; q < nslices; ++q) acc += slice[q * nelem + e];
   if (e < (int64_t)CO * ncombo) {
     const int64_t co = e / ncombo, combo = e % ncombo;
     if (co < Co) dw[co * ncombo + combo] = (float)acc;
@@ -540,7 +567,9 @@ BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co
   const int ncombo = (int)(C * KH * KW);
   const int nphase = TILE_T / ncombo > 0 ? TILE_T / ncombo : 1;
   const int64_t parts = ((std::max<int64_t>(N, 1) + FILTER_SPB - 1) / FILTER_SPB) * nphase;
-  const int64_t tiled = parts * ((int64_t)CO * ncombo + CO) * (int64_t)sizeof(float);
+  const int64_t tnel = (int64_t)CO * ncombo + CO;
+  const int64_t tiled = round_up(parts * tnel * (int64_t)sizeof(float), 256) +
+                        filter_slices(parts) * tnel * (int64_t)sizeof(double);
   return std::max(generic, tiled);
 }
 
@@ -572,8 +601,13 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
       default: BNN_TILE_LAUNCH(conv_bwd_filter_tile_k<64>, dim3((unsigned)nblk), dim3(TILE_T), lds, st, dy, x, binarize_input, part, N, FILTER_SPB, g, db != nullptr); break;
     }
     const int64_t nel = (int64_t)CO * ncombo + CO;
-    hipLaunchKernelGGL(conv_filter_tile_reduce_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, part,
-                       parts, CO, ncombo, (int)Co, dw, db);
+    const int64_t nsl = filter_slices(parts);
+    double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                              round_up(parts * nel * (int64_t)sizeof(float), 256));
+    hipLaunchKernelGGL(conv_filter_tile_reduce1_k, dim3((unsigned)((nel + 255) / 256), (unsigned)nsl), dim3(256), 0,
+                       st, part, parts, nel, nsl, slice);
+    hipLaunchKernelGGL(conv_filter_tile_reduce2_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, slice,
+                       nsl, CO, ncombo, (int)Co, dw, db);
     return check_launch("bnn_conv2d_bwd_filter");
   }
   double* part = reinterpret_cast<double*>(work);

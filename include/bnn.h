@@ -161,6 +161,28 @@ int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const floa
                const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
                float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
 
+/* ---------------------------------------------------------------- BatchNorm2d (+ Hardtanh, + MaxPool2d(2))
+ * The block after each BinarizeConv2d of the build's CNN (conv -> nn.BatchNorm2d -> nn.Hardtanh ->
+ * nn.MaxPool2d(2, 2), the ConvNet template of mnist-dist.py:31-51 with the reference's BNN
+ * activation): per-channel statistics over N*H*W with the BatchNorm1d semantics above.  x, dx fp32
+ * NCHW [N][C][H][W], H*W % 4 == 0, 16-B aligned.  pool = 0: y, dy are [N][C][H][W]; pool = 2:
+ * y, dy are the max-pooled [N][C][H/2][W/2] (H, W even) and the backward recomputes each
+ * window's argmax (torch's rule: first strictly greater value in (h, w) order, NaN wins), so no
+ * full-resolution output or pooling indices are stored.  `work` scratch of
+ * bnn_bn2d_workspace(N, C) bytes.  Deterministic. */
+int64_t bnn_bn2d_workspace(int64_t N, int64_t C);
+int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+                       const float* beta, float* running_mean, float* running_var, float momentum,
+                       float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
+                       int32_t pool, void* work, bnn_stream_t stream);
+int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+                      const float* beta, const float* running_mean, const float* running_var, float eps,
+                      float* y, int32_t hardtanh, int32_t pool, void* work, bnn_stream_t stream);
+int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+                 const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                 int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                 bnn_stream_t stream);
+
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
  * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = (x-mean)*invstd*gamma+beta exactly as
  * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0

@@ -190,6 +190,43 @@ def batchnorm_backward(cache, g):
     return dx, dgamma, dbeta
 
 
+def batchnorm2d_train(x, gamma, beta, rmean, rvar, momentum=0.1, eps=1e-5):
+    """nn.BatchNorm2d in train mode (the block after each conv of the BinCNN; mnist-dist.py:33,39
+    template): per-channel statistics over (N, H, W) -- BatchNorm1d on the [N*H*W, C] view."""
+    x = np.asarray(x, F64)
+    n, c, h, w = x.shape
+    flat = x.transpose(0, 2, 3, 1).reshape(-1, c)
+    y, cache, rm, rv = batchnorm_train(flat, gamma, beta, rmean, rvar, momentum, eps)
+    return y.reshape(n, h, w, c).transpose(0, 3, 1, 2), cache, rm, rv
+
+
+def batchnorm2d_backward(cache, g):
+    g = np.asarray(g, F64)
+    n, c, h, w = g.shape
+    dx, dgamma, dbeta = batchnorm_backward(cache, g.transpose(0, 2, 3, 1).reshape(-1, c))
+    return dx.reshape(n, h, w, c).transpose(0, 3, 1, 2), dgamma, dbeta
+
+
+def maxpool2_forward(y):
+    """nn.MaxPool2d(kernel_size=2, stride=2) (mnist-dist.py:35,41 template) with torch's argmax
+    rule: the first strictly greater value in (h, w) scan order wins ties.  Returns the pooled
+    map and the window slot (0..3) of each maximum."""
+    y = np.asarray(y)
+    n, c, h, w = y.shape
+    win = y[:, :, :h - h % 2, :w - w % 2].reshape(n, c, h // 2, 2, w // 2, 2)
+    win = win.transpose(0, 1, 2, 4, 3, 5).reshape(n, c, h // 2, w // 2, 4)
+    arg = np.argmax(win, axis=-1)          # numpy's argmax also returns the first maximum
+    return np.take_along_axis(win, arg[..., None], -1)[..., 0], arg
+
+
+def maxpool2_backward(g, arg, shape):
+    n, c, h, w = shape
+    out = np.zeros((n, c, h // 2, w // 2, 4), F64)
+    np.put_along_axis(out, arg[..., None], np.asarray(g, F64)[..., None], -1)
+    out = out.reshape(n, c, h // 2, w // 2, 2, 2).transpose(0, 1, 2, 4, 3, 5).reshape(n, c, h, w)
+    return out
+
+
 def log_softmax(z):
     z = np.asarray(z, F64)
     zm = z - z.max(1, keepdims=True)

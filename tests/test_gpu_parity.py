@@ -324,6 +324,70 @@ def test_batchnorm_hardtanh_vs_oracle(F, M, C, hardtanh):
     assert rel_err(host(ye), host(ref)) < 1e-6
 
 
+@pytest.mark.parametrize("N,C,H,W", [(5, 16, 28, 28), (64, 32, 14, 14), (3, 8, 6, 10)])
+@pytest.mark.parametrize("pool", [2, 0])
+def test_batchnorm2d_hardtanh_pool_vs_oracle(F, N, C, H, W, pool):
+    """Fused BatchNorm2d -> Hardtanh -> MaxPool2d(2) (the BinCNN block) against the float64 oracle
+    (tie-free input so the argmax is unambiguous) and torch's modules in eval mode."""
+    rng = np.random.default_rng(N * C + H + pool)
+    x = (rng.standard_normal((N, C, H, W)) * 2 + rng.standard_normal((1, C, 1, 1))).astype(np.float32)
+    gamma = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = rng.uniform(-0.2, 0.2, C).astype(np.float32)
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(dev(gamma))
+        bn.bias.copy_(dev(beta))
+    xt = dev(x).requires_grad_(True)
+    y = F.batch_norm2d_hardtanh_pool(xt, bn, True, pool)
+    yr, cache, rm, rv = O.batchnorm2d_train(x, gamma, beta, np.zeros(C), np.ones(C))
+    h = O.hardtanh(yr)
+    if pool:
+        yo, arg = O.maxpool2_forward(h)
+    else:
+        yo = h
+    assert y.shape == yo.shape
+    assert rel_err(host(y), yo) < 1e-6
+    np.testing.assert_allclose(host(bn.running_mean), rm, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(host(bn.running_var), rv, rtol=1e-5, atol=1e-6)
+    g = rng.standard_normal(yo.shape).astype(np.float32)
+    y.backward(dev(g))
+    gf = O.maxpool2_backward(g, arg, x.shape) if pool else g
+    dx, dgam, dbet = O.batchnorm2d_backward(cache, O.hardtanh_backward(yr, gf))
+    assert rel_err(host(xt.grad), dx) < GRAD_TOL
+    assert rel_err(host(bn.weight.grad), dgam) < GRAD_TOL
+    assert rel_err(host(bn.bias.grad), dbet) < GRAD_TOL
+    bn.eval()
+    ye = F.batch_norm2d_hardtanh_pool(dev(x), bn, True, pool)
+    ref = torch.nn.functional.hardtanh(bn(dev(x)))
+    if pool:
+        ref = torch.nn.functional.max_pool2d(ref, 2, 2)
+    assert rel_err(host(ye), host(ref)) < 1e-6
+
+
+def test_fused_cnn_step_matches_torch_modules(F):
+    """BinCNN with the fused BatchNorm2d+Hardtanh+MaxPool2d op against the same net through torch's
+    BatchNorm2d / Hardtanh / MaxPool2d modules (integer-valued conv outputs: pooling ties resolved
+    by the same first-max rule), one forward + backward."""
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    torch.manual_seed(5)
+    a = nets.BinCNN(org_protocol=False, mutate_input=False).cuda()
+    b = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    b.load_state_dict(a.state_dict())
+    x, y = synthetic_mnist(96, seed=7, device="cuda")
+    la = torch.nn.functional.cross_entropy(a(x), y)
+    la.backward()
+    lb = torch.nn.functional.cross_entropy(b(x), y)
+    lb.backward()
+    assert abs(la.item() - lb.item()) < 1e-5
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        # a conv bias feeding BatchNorm has an exactly-zero true gradient (both sides are ~1e-8
+        # rounding noise), so it is compared absolutely
+        assert rel_err(host(pb.grad), host(pa.grad)) < 1e-4 or close(host(pb.grad), host(pa.grad), 0.0, 1e-6), n
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert close(host(ba), host(bb), 1e-5, 1e-6), n
+
+
 def test_fused_mlp_step_matches_unfused(F):
     """The build's trainer path (fused BN+Hardtanh, latent Adam) against the drop-in path
     (torch BatchNorm1d/Hardtanh, torch Adam + .org protocol) on one step, dropout off."""
