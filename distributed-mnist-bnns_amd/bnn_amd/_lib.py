@@ -37,6 +37,7 @@ SIGNATURES = {
     "bnn_conv2d_bwd_filter_workspace": (I64, [I64, I64, I64, I64, I64, I32]),
     "bnn_conv2d_bwd_filter": (I32, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32,
                                     I32, P]),
+    "bnn_conv_set_mfma": (I32, [I32]),
     "bnn_bn_workspace": (I64, [I64, I64]),
     "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, P, P]),
     "bnn_bn_fwd_eval": (I32, [P, I64, I64, P, P, P, P, F32, P, I32, P, P]),

@@ -477,6 +477,261 @@ __global__ __launch_bounds__(256) void conv_filter_tile_reduce2_k(const double* 
   }
 }
 
+// ------------------------------------------------------------------ f32-MFMA implicit-GEMM backward
+// Both backward convolutions as implicit GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 products,
+// f32 accumulation: the same numerics class as the fp32 reference's sgemm, at the f32 matrix
+// rate).  Operands are gathered from LDS images of one sample at a time (no im2col in HBM);
+// each workgroup walks IPB samples so the staged weights / accumulators amortise.
+//   16x16x4 lane map: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D col = l&15, row = 4*(l>>4)+r.
+// floor(i / d) for the staging loops through a float reciprocal: exact while i < 2^20 (the
+// fractional part of (i + 0.5) / d is >= 0.5 / d, far above the float rounding of the product).
+__device__ __forceinline__ int fdivi(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
+
+constexpr int MF_T = 256;        // 4 waves
+constexpr int MF_IPB = 8;        // samples per workgroup
+
+typedef float mf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ mf4 mfma16x4(float a, float b, mf4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Backward data: dX[ci][pix] = sum_k Wb[k][ci] * dYhalo[pix_base(pix) + koff(k)], k = (co, kh, kw).
+// GEMM per sample: M = ci (NT tiles of 16), N = pixels (tiles of 16, split over the 4 waves), K = Co*KH*KW.
+struct MfData {
+  int C, H, W, Co, KH, KW, OH, OW, pad, OHp, OWp, K, Kp, CIp, ntile_pix;
+};
+
+template <int NT, int MT>
+__global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __restrict__ dy,
+                                                             const float* __restrict__ w,
+                                                             float* __restrict__ dx, int64_t N, MfData g) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  unsigned short* wsb = reinterpret_cast<unsigned short*>(ldsf);            // bf16 signs [Kp][CIp]
+  int* koff = reinterpret_cast<int*>(wsb + g.Kp * g.CIp + (g.Kp * g.CIp & 1));   // [Kp]
+  float* ds = reinterpret_cast<float*>(koff + g.Kp);                          // [Co][OHp][OWp]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int hT = g.KH - 1 - g.pad, wT = g.KW - 1 - g.pad, KK = g.KH * g.KW;
+  for (int i = t; i < g.Kp * g.CIp; i += MF_T) {
+    const int k = i / g.CIp, ci = i - k * g.CIp;
+    int v = 0;
+    if (k < g.K && ci < g.C) {
+      const int co = k / KK, kk = k - co * KK;
+      v = tsign(w[(co * g.C + ci) * KK + kk]);
+    }
+    wsb[i] = v > 0 ? 0x3F80 : (v < 0 ? 0xBF80 : 0);   // +-1 / 0 as bf16 (exact)
+  }
+  for (int k = t; k < g.Kp; k += MF_T) {
+    int o = 0;
+    if (k < g.K) {
+      const int co = k / KK, kk = k - co * KK, kh = kk / g.KW, kw = kk - kh * g.KW;
+      o = co * g.OHp * g.OWp - kh * g.OWp - kw;
+    }
+    koff[k] = o;
+  }
+  const int nds = g.Co * g.OHp * g.OWp;
+  for (int i = t; i < nds; i += MF_T) ds[i] = 0.f;
+  // this wave's pixel tiles: wv, wv+4, ...; per lane the B column (pixel) base offset
+  const int HW = g.H * g.W;
+  int pbase[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    int pix = (wv + 4 * m) * 16 + (lane & 15);
+    if (pix >= HW) pix = 0;   // padded column: computed, never stored
+    const int ih = pix / g.W, iw = pix - ih * g.W;
+    pbase[m] = (ih + g.KH - 1) * g.OWp + iw + g.KW - 1;
+  }
+  const int my_tiles = (g.ntile_pix - wv + 3) / 4;
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  const int ohw = g.OH * g.OW;
+  const float inv_ow = 1.f / (float)g.OW, inv_oh = 1.f / (float)g.OH;
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();   // previous sample's reads of ds are done (and the set-up above on entry)
+    const float* dn = dy + n * g.Co * ohw;
+    for (int i = t; i < g.Co * ohw; i += MF_T) {
+      const int row = fdivi(i, inv_ow), ow = i - row * g.OW;   // row = co * OH + oh
+      const int co = fdivi(row, inv_oh), oh = row - co * g.OH;
+      ds[(co * g.OHp + oh + hT) * g.OWp + ow + wT] = dn[i];
+    }
+    __syncthreads();
+    mf4 acc[NT][MT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < g.Kp; k0 += 4) {
+      const int k = k0 + (lane >> 4);
+      const int ko = koff[k];
+      float av[NT];
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+        av[a] = __uint_as_float((unsigned)wsb[k * g.CIp + a * 16 + (lane & 15)] << 16);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if (m < my_tiles) {
+          const float bv = ds[pbase[m] + ko];
+#pragma unroll
+          for (int a = 0; a < NT; ++a) acc[a][m] = mfma16x4(av[a], bv, acc[a][m]);
+        }
+      }
+    }
+    float* xn = dx + n * g.C * HW;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m >= my_tiles) continue;
+      const int pix = (wv + 4 * m) * 16 + (lane & 15);
+      if (pix >= HW) continue;
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ci = a * 16 + 4 * (lane >> 4) + r;
+          if (ci < g.C) xn[(int64_t)ci * HW + pix] = acc[a][m][r];
+        }
+    }
+  }
+}
+
+// Backward filter: dW[co][combo] = sum_{n,p} dY[n][co][p] * Xs[n][combo][p], combo = (ci, kh, kw).
+// Tiles (co16, combo16) are dealt to WT wave groups; the remaining 4/WT factor splits the pixel
+// range (K), each (block, k-slice) writing one partial row for conv_filter_tile_reduce{1,2}_k.
+struct MfFilt {
+  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, Wp, P, Pp, Co16, ncombo, ntn, ntiles, WT, KS;
+};
+
+template <int MT>
+__global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __restrict__ dy,
+                                                               const float* __restrict__ x, int binarize,
+                                                               float* __restrict__ part, int64_t N,
+                                                               MfFilt g, int with_bias) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  float* xs = ldsf;                               // [C][Hp][Wp], zero border
+  float* dys = xs + ((g.C * g.Hp * g.Wp + 3) & ~3);   // [Co16][Pp], zero padded, 16-B aligned
+  int* poff = reinterpret_cast<int*>(dys + g.Co16 * g.Pp);   // [Pp]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int grp = wv % g.WT, ks = wv / g.WT;
+  const int KK = g.KH * g.KW;
+  for (int i = t; i < g.C * g.Hp * g.Wp; i += MF_T) xs[i] = 0.f;
+  for (int i = t; i < g.Co16 * g.Pp; i += MF_T) dys[i] = 0.f;
+  for (int p = t; p < g.Pp; p += MF_T) {
+    const int oh = p / g.OW, ow = p - oh * g.OW;
+    poff[p] = p < g.P ? oh * g.Wp + ow : 0;
+  }
+  // this wave's tiles t = grp + WT*m; per lane the B column (combo) offset and the A row (co)
+  int boff[MT], arow[MT];
+  const int my_tiles = (g.ntiles - grp + g.WT - 1) / g.WT;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int tt = grp + g.WT * m;
+    const int mt = tt / g.ntn, nt = tt - mt * g.ntn;
+    int combo = nt * 16 + (lane & 15);
+    if (combo >= g.ncombo) combo = 0;   // padded column: computed, never stored
+    const int ci = combo / KK, kk = combo - ci * KK, kh = kk / g.KW, kw = kk - kh * g.KW;
+    boff[m] = (ci * g.Hp + kh) * g.Wp + kw;
+    arow[m] = (mt * 16 + (lane & 15)) * g.Pp;   // A[i = co][k = p]
+  }
+  mf4 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = mf4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;
+  const int pslice = g.Pp / g.KS, p_lo = ks * pslice, p_hi = p_lo + pslice;
+  const float inv_w = 1.f / (float)g.W, inv_h = 1.f / (float)g.H, inv_p = 1.f / (float)g.P;
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();
+    const float* xn = x + n * g.C * g.H * g.W;
+    for (int i = t; i < g.C * g.H * g.W; i += MF_T) {
+      const int row = fdivi(i, inv_w), iw = i - row * g.W;   // row = c * H + ih
+      const int c = fdivi(row, inv_h), ih = row - c * g.H;
+      const float v = xn[i];
+      xs[(c * g.Hp + ih + g.pad) * g.Wp + iw + g.pad] = binarize ? (float)tsign(v) : v;
+    }
+    const float* dn = dy + n * g.Co * g.P;
+    if (g.Pp == g.P && ((g.Co * g.P) & 3) == 0) {   // dense rows: straight 16-B copy
+      for (int i = 4 * t; i < g.Co * g.P; i += 4 * MF_T)
+        *reinterpret_cast<float4*>(dys + i) = *reinterpret_cast<const float4*>(dn + i);
+    } else {
+      for (int i = t; i < g.Co * g.P; i += MF_T) {
+        const int co = fdivi(i, inv_p), p = i - co * g.P;
+        dys[co * g.Pp + p] = dn[i];
+      }
+    }
+    __syncthreads();
+    for (int p0 = p_lo; p0 < p_hi; p0 += 4) {
+      const int p = p0 + (lane >> 4);
+      const int po = poff[p];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        if (m < my_tiles) acc[m] = mfma16x4(dys[arow[m] + p], xs[boff[m] + po], acc[m]);
+    }
+    if (with_bias && t < g.Co) {
+      float sb = 0.f;
+      for (int p = 0; p < g.P; ++p) sb += dys[t * g.Pp + p];
+      bacc += sb;
+    }
+  }
+  const int64_t nelem = (int64_t)g.Co * g.ncombo + g.Co;
+  float* row = part + ((int64_t)blockIdx.x * g.KS + ks) * nelem;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m >= my_tiles) continue;
+    const int tt = grp + g.WT * m;
+    const int mt = tt / g.ntn, nt = tt - mt * g.ntn;
+    const int combo = nt * 16 + (lane & 15);
+    if (combo >= g.ncombo) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = mt * 16 + 4 * (lane >> 4) + r;
+      if (co < g.Co) row[(int64_t)co * g.ncombo + combo] = acc[m][r];
+    }
+  }
+  if (t < g.Co) {   // bias partial in k-slice 0's row, zero in the others
+    part[((int64_t)blockIdx.x * g.KS) * nelem + (int64_t)g.Co * g.ncombo + t] = with_bias ? bacc : 0.f;
+    for (int q = 1; q < g.KS; ++q) part[((int64_t)blockIdx.x * g.KS + q) * nelem + (int64_t)g.Co * g.ncombo + t] = 0.f;
+  }
+}
+
+inline bool mf_data_geom(const ConvShape& s, MfData* g, int64_t* lds) {
+  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.pad <= s.KH - 1 && s.pad <= s.KW - 1 && s.C <= 32))
+    return false;
+  MfData d;
+  d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
+  d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
+  d.OHp = d.OH + 2 * (d.KH - 1 - d.pad);
+  d.OWp = d.OW + 2 * (d.KW - 1 - d.pad);
+  d.K = d.Co * d.KH * d.KW;
+  d.Kp = (int)round_up(d.K, 4);
+  d.CIp = d.C <= 16 ? 16 : 32;
+  d.ntile_pix = (d.H * d.W + 15) / 16;
+  if ((d.ntile_pix + 3) / 4 > 16 || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
+  *lds = (int64_t)d.Kp * d.CIp * 2 + 4 + (int64_t)d.Kp * 4 + (int64_t)d.Co * d.OHp * d.OWp * 4;
+  *g = d;
+  return *lds <= kMaxTileLds;
+}
+
+inline bool mf_filt_geom(const ConvShape& s, MfFilt* g, int64_t* lds) {
+  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1)) return false;
+  MfFilt d;
+  d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
+  d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
+  d.Hp = d.H + 2 * d.pad; d.Wp = d.W + 2 * d.pad;
+  d.P = d.OH * d.OW;
+  d.Co16 = (int)round_up(d.Co, 16);
+  d.ncombo = d.C * d.KH * d.KW;
+  d.ntn = (d.ncombo + 15) / 16;
+  d.ntiles = (d.Co16 / 16) * d.ntn;
+  d.WT = d.ntiles >= 4 ? 4 : (d.ntiles >= 2 ? 2 : 1);
+  d.KS = 4 / d.WT;
+  d.Pp = (int)round_up(d.P, 4 * d.KS);
+  if ((d.ntiles + d.WT - 1) / d.WT > 16) return false;
+  if ((int64_t)d.C * d.H * d.W >= (1 << 20) || (int64_t)d.Co * d.P >= (1 << 20)) return false;
+  // every gathered x index stays inside the padded image: oh + kh < Hp, ow + kw < Wp
+  if (d.OH - 1 + d.KH - 1 >= d.Hp || d.OW - 1 + d.KW - 1 >= d.Wp) return false;
+  *lds = (round_up((int64_t)d.C * d.Hp * d.Wp, 4) + (int64_t)d.Co16 * d.Pp + d.Pp) * 4;
+  *g = d;
+  return *lds <= kMaxTileLds;
+}
+
 // Launch a tiled kernel with `lds` dynamic bytes (lifting the 64 KiB default cap when needed).
 #define BNN_TILE_LAUNCH(KER, ...) \
   do { allow_lds(KER, (int64_t)lds); hipLaunchKernelGGL(KER, __VA_ARGS__); } while (0)
@@ -492,6 +747,15 @@ int64_t tile_filter_parts(const ConvShape& s) {
 }  // namespace bnn
 
 using namespace bnn;
+
+// 1 (default): backward convolutions on the f32-MFMA implicit-GEMM kernels where the shape allows;
+// 0: the VALU LDS-tiled / generic kernels (kept as the cross-check in the parity tests).
+static int g_conv_mfma = 1;
+
+BNN_API int bnn_conv_set_mfma(int32_t on) {
+  g_conv_mfma = on != 0;
+  return 0;
+}
 
 BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* w_latent,
                            const float* bias, float* y, int64_t N, int64_t C, int64_t H, int64_t W,
@@ -541,6 +805,21 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   const int64_t total = N * C * H * W;
   if (total == 0) return 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  MfData md;
+  int64_t mlds = 0;
+  if (g_conv_mfma && mf_data_geom(s, &md, &mlds)) {
+    const size_t lds = (size_t)mlds;
+    const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
+    const bool small = (md.ntile_pix + 3) / 4 <= 4;
+    if (md.CIp == 16) {
+      if (small) BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<1, 4>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+      else BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<1, 16>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+    } else {
+      if (small) BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<2, 4>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+      else BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<2, 16>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+    }
+    return check_launch("bnn_conv2d_bwd_data");
+  }
   if (tile_geom_ok(s) && bwd_data_tile_lds(s) <= kMaxTileLds) {
     const TileGeo g = geo(s);
     const int CI = pick_co(C);
@@ -570,7 +849,11 @@ BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co
   const int64_t tnel = (int64_t)CO * ncombo + CO;
   const int64_t tiled = round_up(parts * tnel * (int64_t)sizeof(float), 256) +
                         filter_slices(parts) * tnel * (int64_t)sizeof(double);
-  return std::max(generic, tiled);
+  const int64_t mparts = ((std::max<int64_t>(N, 1) + MF_IPB - 1) / MF_IPB) * 4;
+  const int64_t mnel = Co * ncombo + Co;
+  const int64_t mfma = round_up(mparts * mnel * (int64_t)sizeof(float), 256) +
+                       filter_slices(mparts) * mnel * (int64_t)sizeof(double);
+  return std::max(std::max(generic, tiled), mfma);
 }
 
 BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_input, float* dw,
@@ -586,6 +869,27 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   const int64_t nw = Co * (C / groups) * KH * KW;
   const int64_t nelem = nw + Co;
   const int64_t nchunks = filter_chunks(std::max<int64_t>(N, 1), nelem);
+  MfFilt mf;
+  int64_t mlds = 0;
+  if (N > 0 && g_conv_mfma && mf_filt_geom(s, &mf, &mlds)) {
+    const int64_t nblk = (N + MF_IPB - 1) / MF_IPB;
+    const int64_t parts = nblk * mf.KS;
+    const int64_t nel = (int64_t)Co * mf.ncombo + Co;
+    float* part = reinterpret_cast<float*>(work);
+    const size_t lds = (size_t)mlds;
+    if ((mf.ntiles + mf.WT - 1) / mf.WT <= 4)
+      BNN_TILE_LAUNCH(conv_bwd_filter_mfma_k<4>, dim3((unsigned)nblk), dim3(MF_T), lds, st, dy, x, binarize_input, part, N, mf, db != nullptr);
+    else
+      BNN_TILE_LAUNCH(conv_bwd_filter_mfma_k<16>, dim3((unsigned)nblk), dim3(MF_T), lds, st, dy, x, binarize_input, part, N, mf, db != nullptr);
+    const int64_t nsl = filter_slices(parts);
+    double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                              round_up(parts * nel * (int64_t)sizeof(float), 256));
+    hipLaunchKernelGGL(conv_filter_tile_reduce1_k, dim3((unsigned)((nel + 255) / 256), (unsigned)nsl), dim3(256), 0,
+                       st, part, parts, nel, nsl, slice);
+    hipLaunchKernelGGL(conv_filter_tile_reduce2_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, slice,
+                       nsl, (int)Co, mf.ncombo, (int)Co, dw, db);
+    return check_launch("bnn_conv2d_bwd_filter");
+  }
   if (N > 0 && tile_geom_ok(s) && C * KH * KW <= 2 * TILE_T && filter_tile_lds(s) <= kMaxTileLds) {
     const TileGeo g = geo(s);
     const int CO = pick_co(Co);

@@ -247,6 +247,41 @@ def test_conv_tiled_and_generic_shapes_vs_oracle(F, shape):
         assert rel_err(host(bt.grad), db64) < GRAD_TOL
 
 
+@pytest.mark.parametrize("shape", [
+    (9, 16, 14, 14, 32, 5, 2, True),     # BinCNN conv2
+    (10, 1, 28, 28, 16, 5, 2, True),     # BinCNN conv1 (binarised C=1 input)
+    (5, 3, 12, 10, 8, 3, 1, False),      # C == 3: fp32 input
+    (3, 20, 9, 7, 40, 3, 0, True),
+    (2, 32, 6, 6, 64, 1, 0, True),
+])
+def test_conv_backward_mfma_matches_valu(F, shape):
+    """The f32-MFMA implicit-GEMM backward kernels against the float64 oracle and against the VALU
+    kernels (bnn_conv_set_mfma(0)) on the same inputs."""
+    from bnn_amd import _lib as L
+    N, C, H, W, Co, K, pad, binarize = shape
+    rng = np.random.default_rng(N + C + Co)
+    x = np.where(rng.random((N, C, H, W)) < 0.3, 0, rng.standard_normal((N, C, H, W))).astype(np.float32)
+    w = np.where(rng.random((Co, C, K, K)) < 0.1, 0, rng.uniform(-1, 1, (Co, C, K, K))).astype(np.float32)
+    b = rng.standard_normal(Co).astype(np.float32)
+    grads = []
+    try:
+        for on in (1, 0):
+            L.call("bnn_conv_set_mfma", on)
+            xt, wt, bt = dev(x).requires_grad_(True), dev(w).requires_grad_(True), dev(b).requires_grad_(True)
+            y = F.binary_conv2d(xt, wt, bt, binarize, 1, pad, 1, 1)
+            dy = np.random.default_rng(1).standard_normal(tuple(y.shape)).astype(np.float32)
+            y.backward(dev(dy))
+            grads.append((host(xt.grad), host(wt.grad), host(bt.grad)))
+    finally:
+        L.call("bnn_conv_set_mfma", 1)
+    _, xu = O.conv2d_forward(x, w, b, 1, pad, 1, 1)
+    dx64, dw64, db64 = O.conv2d_backward(xu, w, dy, 1, pad, 1, 1)
+    for g in grads:
+        assert rel_err(g[0], dx64) < GRAD_TOL
+        assert rel_err(g[1], dw64) < GRAD_TOL
+        assert rel_err(g[2], db64) < GRAD_TOL
+
+
 def test_hardtanh_backward(F):
     x = torch.tensor([-2.0, -1.0, -0.5, 0.0, 0.5, 1.0, 3.0] * 11, device="cuda")
     g = torch.randn_like(x)
