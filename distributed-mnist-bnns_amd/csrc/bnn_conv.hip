@@ -508,8 +508,7 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
                                                              float* __restrict__ dx, int64_t N, MfData g) {
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   unsigned short* wsb = reinterpret_cast<unsigned short*>(ldsf);            // bf16 signs [Kp][CIp]
-  int* koff = reinterpret_cast<int*>(wsb + g.Kp * g.CIp + (g.Kp * g.CIp & 1));   // [Kp]
-  float* ds = reinterpret_cast<float*>(koff + g.Kp);                          // [Co][OHp][OWp]
+  float* ds = reinterpret_cast<float*>(wsb + g.Kp * g.CIp);                   // [Co][OHp][OWp]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int hT = g.KH - 1 - g.pad, wT = g.KW - 1 - g.pad, KK = g.KH * g.KW;
   for (int i = t; i < g.Kp * g.CIp; i += MF_T) {
@@ -520,14 +519,6 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
       v = tsign(w[(co * g.C + ci) * KK + kk]);
     }
     wsb[i] = v > 0 ? 0x3F80 : (v < 0 ? 0xBF80 : 0);   // +-1 / 0 as bf16 (exact)
-  }
-  for (int k = t; k < g.Kp; k += MF_T) {
-    int o = 0;
-    if (k < g.K) {
-      const int co = k / KK, kk = k - co * KK, kh = kk / g.KW, kw = kk - kh * g.KW;
-      o = co * g.OHp * g.OWp - kh * g.OWp - kw;
-    }
-    koff[k] = o;
   }
   const int nds = g.Co * g.OHp * g.OWp;
   for (int i = t; i < nds; i += MF_T) ds[i] = 0.f;
@@ -545,6 +536,8 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
   const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
   const int ohw = g.OH * g.OW;
   const float inv_ow = 1.f / (float)g.OW, inv_oh = 1.f / (float)g.OH;
+  const float inv_kk = 1.f / (float)KK, inv_kw = 1.f / (float)g.KW;
+  const int ohwp = g.OHp * g.OWp;
   for (int64_t n = n0; n < n1; ++n) {
     __syncthreads();   // previous sample's reads of ds are done (and the set-up above on entry)
     const float* dn = dy + n * g.Co * ohw;
@@ -561,19 +554,23 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
       for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < g.Kp; k0 += 4) {
       const int k = k0 + (lane >> 4);
-      const int ko = koff[k];
-      float av[NT];
+      // koff(k) computed, not read: keeps the ds gather off a dependent LDS round trip.  k >= K
+      // (zero weights) is clamped to a valid address; no branch in the loop body.  (A register
+      // double-buffer of the operands made hipcc rotate the accumulators through AGPR copies
+      // every step -- slower; the plain loop is kept.)
+      const int kc = min(k, g.K - 1);
+      const int co = fdivi(kc, inv_kk), kk = kc - co * KK, kh = fdivi(kk, inv_kw), kw = kk - kh * g.KW;
+      const int ko = co * ohwp - kh * g.OWp - kw;
+      float av[NT], bv[MT];
 #pragma unroll
       for (int a = 0; a < NT; ++a)
         av[a] = __uint_as_float((unsigned)wsb[k * g.CIp + a * 16 + (lane & 15)] << 16);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        if (m < my_tiles) {
-          const float bv = ds[pbase[m] + ko];
+      for (int m = 0; m < MT; ++m) bv[m] = ds[pbase[m] + ko];   // all MT tiles: branch-free body
 #pragma unroll
-          for (int a = 0; a < NT; ++a) acc[a][m] = mfma16x4(av[a], bv, acc[a][m]);
-        }
-      }
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int a = 0; a < NT; ++a) acc[a][m] = mfma16x4(av[a], bv[m], acc[a][m]);
     }
     float* xn = dx + n * g.C * HW;
 #pragma unroll
@@ -622,7 +619,7 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
   const int my_tiles = (g.ntiles - grp + g.WT - 1) / g.WT;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int tt = grp + g.WT * m;
+    const int tt = min(grp + g.WT * m, g.ntiles - 1);   // past this wave's tiles: valid, unused
     const int mt = tt / g.ntn, nt = tt - mt * g.ntn;
     int combo = nt * 16 + (lane & 15);
     if (combo >= g.ncombo) combo = 0;   // padded column: computed, never stored
@@ -636,6 +633,7 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
   float bacc = 0.f;
   const int pslice = g.Pp / g.KS, p_lo = ks * pslice, p_hi = p_lo + pslice;
   const float inv_w = 1.f / (float)g.W, inv_h = 1.f / (float)g.H, inv_p = 1.f / (float)g.P;
+  const float inv_ow = 1.f / (float)g.OW;
   const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
   for (int64_t n = n0; n < n1; ++n) {
     __syncthreads();
@@ -657,12 +655,28 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
       }
     }
     __syncthreads();
-    for (int p0 = p_lo; p0 < p_hi; p0 += 4) {
+    auto gather = [&](int p0, float* av, float* bv) {
       const int p = p0 + (lane >> 4);
-      const int po = poff[p];
+      const int pc = min(p, g.P - 1);   // p >= P: zero dY column, any valid x address
+      const int oh = fdivi(pc, inv_ow), ow = pc - oh * g.OW;
+      const int po = oh * g.Wp + ow;
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        if (m < my_tiles) acc[m] = mfma16x4(dys[arow[m] + p], xs[boff[m] + po], acc[m]);
+      for (int m = 0; m < MT; ++m) {   // all MT tiles: branch-free body
+        av[m] = dys[arow[m] + p];
+        bv[m] = xs[boff[m] + po];
+      }
+    };
+    float av[MT], bv[MT], an[MT], bn[MT];
+    gather(p_lo, an, bn);
+    for (int p0 = p_lo; p0 < p_hi; p0 += 4) {   // software-pipelined as in the data kernel
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        av[m] = an[m];
+        bv[m] = bn[m];
+      }
+      gather(min(p0 + 4, p_hi - 4), an, bn);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma16x4(av[m], bv[m], acc[m]);
     }
     if (with_bias && t < g.Co) {
       float sb = 0.f;
@@ -704,7 +718,7 @@ inline bool mf_data_geom(const ConvShape& s, MfData* g, int64_t* lds) {
   d.CIp = d.C <= 16 ? 16 : 32;
   d.ntile_pix = (d.H * d.W + 15) / 16;
   if ((d.ntile_pix + 3) / 4 > 16 || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
-  *lds = (int64_t)d.Kp * d.CIp * 2 + 4 + (int64_t)d.Kp * 4 + (int64_t)d.Co * d.OHp * d.OWp * 4;
+  *lds = (int64_t)d.Kp * d.CIp * 2 + (int64_t)d.Co * d.OHp * d.OWp * 4;
   *g = d;
   return *lds <= kMaxTileLds;
 }
@@ -810,14 +824,16 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   if (g_conv_mfma && mf_data_geom(s, &md, &mlds)) {
     const size_t lds = (size_t)mlds;
     const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
-    const bool small = (md.ntile_pix + 3) / 4 <= 4;
+    const int per_wave = (md.ntile_pix + 3) / 4;
+#define BNN_MFD(NT_, MT_) BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<NT_, MT_>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md)
     if (md.CIp == 16) {
-      if (small) BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<1, 4>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
-      else BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<1, 16>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+      if (per_wave <= 1) BNN_MFD(1, 1); else if (per_wave <= 2) BNN_MFD(1, 2); else if (per_wave <= 4) BNN_MFD(1, 4);
+      else if (per_wave <= 8) BNN_MFD(1, 8); else if (per_wave <= 13) BNN_MFD(1, 13); else BNN_MFD(1, 16);
     } else {
-      if (small) BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<2, 4>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
-      else BNN_TILE_LAUNCH((conv_bwd_data_mfma_k<2, 16>), grid, dim3(MF_T), lds, st, dy, w_latent, dx, N, md);
+      if (per_wave <= 1) BNN_MFD(2, 1); else if (per_wave <= 2) BNN_MFD(2, 2); else if (per_wave <= 4) BNN_MFD(2, 4);
+      else if (per_wave <= 8) BNN_MFD(2, 8); else BNN_MFD(2, 16);
     }
+#undef BNN_MFD
     return check_launch("bnn_conv2d_bwd_data");
   }
   if (tile_geom_ok(s) && bwd_data_tile_lds(s) <= kMaxTileLds) {
@@ -877,10 +893,11 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
     const int64_t nel = (int64_t)Co * mf.ncombo + Co;
     float* part = reinterpret_cast<float*>(work);
     const size_t lds = (size_t)mlds;
-    if ((mf.ntiles + mf.WT - 1) / mf.WT <= 4)
-      BNN_TILE_LAUNCH(conv_bwd_filter_mfma_k<4>, dim3((unsigned)nblk), dim3(MF_T), lds, st, dy, x, binarize_input, part, N, mf, db != nullptr);
-    else
-      BNN_TILE_LAUNCH(conv_bwd_filter_mfma_k<16>, dim3((unsigned)nblk), dim3(MF_T), lds, st, dy, x, binarize_input, part, N, mf, db != nullptr);
+    const int per_wave = (mf.ntiles + mf.WT - 1) / mf.WT;
+#define BNN_MFF(MT_) BNN_TILE_LAUNCH(conv_bwd_filter_mfma_k<MT_>, dim3((unsigned)nblk), dim3(MF_T), lds, st, dy, x, binarize_input, part, N, mf, db != nullptr)
+    if (per_wave <= 1) BNN_MFF(1); else if (per_wave <= 2) BNN_MFF(2); else if (per_wave <= 4) BNN_MFF(4);
+    else if (per_wave <= 8) BNN_MFF(8); else if (per_wave <= 13) BNN_MFF(13); else BNN_MFF(16);
+#undef BNN_MFF
     const int64_t nsl = filter_slices(parts);
     double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
                                               round_up(parts * nel * (int64_t)sizeof(float), 256));
