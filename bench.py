@@ -39,7 +39,18 @@ CONFIGS = {
     "small": ("small", 4096, "binarized MLP 784-192x3-10 (mnist-dist3 Net)"),
     "cnn": ("cnn", 4096, "binarized CNN conv5(1-16)-conv5(16-32)-fc (BASELINE config 4)"),
 }
-CPU_WIDTHS = {"wide": (8192, 8192, 8192), "mlp": (3072, 1536, 768), "small": (192, 192, 192)}
+CPU_WIDTHS = {"wide": (8192, 8192, 8192), "mlp": (3072, 1536, 768), "small": (192, 192, 192), "cnn": "cnn"}
+MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
+MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
+
+
+def op_peak(kernel):
+    """(bound, peak TFLOP/s or TOPS, unit of the count) of an ops-counted kernel."""
+    if kernel.startswith("conv2d_bwd"):
+        return "mfma", MI355X_F32_MFMA_TFLOPS, "f32 MFMA flops (2*N*Co*OH*OW*C*KH*KW)"
+    if kernel.startswith("conv2d_fwd"):
+        return "valu", MI355X_DOT4_TOPS, "int8 dot4 ops (2*N*Co*OH*OW*C*KH*KW)"
+    return "mfma", MI355X_INT8_DENSE_TOPS, "int8 MFMA ops (2*M*N*K*digit_pairs)"
 
 
 def parse():
@@ -75,8 +86,8 @@ def cpu_baseline(cfg, budget):
     widths = CPU_WIDTHS.get(cfg)
     if widths is None:
         return None
-    batch = 512 if cfg == "wide" else 1024
-    sps, steps, secs = bnn_torch.time_training(widths, batch, threads, budget_s=budget)
+    batch = 512 if cfg == "wide" else (256 if cfg == "cnn" else 1024)
+    sps, steps, secs = bnn_torch.time_training(widths, batch, threads, budget_s=budget, max_steps=100000)
     return {"value": round(sps, 2), "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"{steps} fp32 torch-CPU train steps (oracle/bnn_torch.py restatement of the "
                       f"reference path, .org protocol + Adam) of the same net at batch {batch}, "
@@ -169,10 +180,11 @@ def main():
         d = ksum[dom]
         if d["avg_ops"] > 0:
             ach = d["avg_ops"] / (d["avg_ms"] * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(MI355X_INT8_DENSE_TOPS, 1),
-                        "unit": "TFLOP/s", "frac": round(ach / MI355X_INT8_DENSE_TOPS, 4), "traffic": None,
+            bound, peak, ops_unit = op_peak(dom)
+            roofline = {"bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1),
+                        "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
                         "kernel": dom, "launches_per_step": d["launches"] / args.steps,
-                        "avg_us": round(d["avg_ms"] * 1e3, 1), "ops_unit": "int8 MFMA ops (2*M*N*K*digit_pairs)"}
+                        "avg_us": round(d["avg_ms"] * 1e3, 1), "ops_unit": ops_unit}
         else:
             ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
             roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
@@ -200,7 +212,8 @@ def main():
     }
     if ksum:
         # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (logical 2MNK)
-        fwd = [v for k, v in ksum.items() if k.startswith("gemm_i8") and "<1, 1," in k]   # ternary forms
+        # ternary GEMM forms, and the binary convolutions' forward (im2col-free) for the CNN
+        fwd = [v for k, v in ksum.items() if (k.startswith("gemm_i8") and "<1, 1," in k) or k == "conv2d_fwd"]
         if fwd:
             ops, ms_ = sum(v["ops"] for v in fwd), sum(v["ms"] for v in fwd)
             result["binary_gemm_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)

@@ -331,8 +331,10 @@ class BinaryConv2dFunction(torch.autograd.Function):
         OW = (W + 2 * padding - dilation * (KW - 1) - 1) // stride + 1
         y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
         b = bias.detach() if bias is not None else None
-        L.call("bnn_conv2d_fwd", L.ptr(x), int(binarize_input), L.ptr(w), L.ptr(b), L.ptr(y),
-               N, C, H, W, Co, KH, KW, stride, padding, dilation, groups, L.stream())
+        macs = N * Co * OH * OW * (C // groups) * KH * KW
+        with _timed("conv2d_fwd", 2 * macs):
+            L.call("bnn_conv2d_fwd", L.ptr(x), int(binarize_input), L.ptr(w), L.ptr(b), L.ptr(y),
+                   N, C, H, W, Co, KH, KW, stride, padding, dilation, groups, L.stream())
         ctx.save_for_backward(x, w)
         ctx.conf = (binarize_input, stride, padding, dilation, groups)
         ctx.has_bias = bias is not None
@@ -346,19 +348,22 @@ class BinaryConv2dFunction(torch.autograd.Function):
         N, C, H, W = x.shape
         Co, _, KH, KW = w.shape
         dx = dw = db = None
+        macs = dy.numel() * (C // groups) * KH * KW
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            L.call("bnn_conv2d_bwd_data", L.ptr(dy), L.ptr(w), L.ptr(dx), N, C, H, W, Co, KH, KW,
-                   stride, padding, dilation, groups, L.stream())
+            with _timed("conv2d_bwd_data", 2 * macs):
+                L.call("bnn_conv2d_bwd_data", L.ptr(dy), L.ptr(w), L.ptr(dx), N, C, H, W, Co, KH, KW,
+                       stride, padding, dilation, groups, L.stream())
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or need_db:
             dw = torch.empty_like(w)
             db = torch.empty((Co,), dtype=torch.float32, device=x.device) if need_db else None
             ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
                              dtype=torch.uint8, device=x.device)
-            L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
-                   L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
-                   L.stream())
+            with _timed("conv2d_bwd_filter", 2 * macs):
+                L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
+                       L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
+                       L.stream())
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None, None

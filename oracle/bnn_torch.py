@@ -71,6 +71,23 @@ class RefMLP(nn.Module):
         return tF.log_softmax(self.fc4(x), dim=1)
 
 
+class RefCNN(nn.Module):
+    """The build's BinCNN (BASELINE config 4) with the reference's CPU layers: BinarizeConv2d
+    (binarized_modules.py:87-107) -> BatchNorm2d -> Hardtanh -> MaxPool2d(2), twice, then
+    Linear(1568, 10) and LogSoftmax (mnist-dist.py:31-51 ConvNet template)."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1, self.b1 = RefConv2d(1, 16, 5, padding=2), nn.BatchNorm2d(16)
+        self.c2, self.b2 = RefConv2d(16, 32, 5, padding=2), nn.BatchNorm2d(32)
+        self.fc = nn.Linear(7 * 7 * 32, 10)
+
+    def forward(self, x):
+        x = tF.max_pool2d(tF.hardtanh(self.b1(self.c1(x))), 2, 2)
+        x = tF.max_pool2d(tF.hardtanh(self.b2(self.c2(x))), 2, 2)
+        return tF.log_softmax(self.fc(x.reshape(x.size(0), -1)), dim=1)
+
+
 def train_step(model, opt, x, target, org_protocol=True):
     """mnist-dist2.py:122-137 (org protocol) or mnist-dist3.py:113-119 (without)."""
     opt.zero_grad()
@@ -98,12 +115,13 @@ def synthetic_batch(n, seed):
 
 
 def time_training(widths, batch, threads, budget_s=10.0, max_steps=50, min_steps=2, warmup=1):
-    """Time the CPU reference training step (fp32, torch on `threads` host threads).
+    """Time the CPU reference training step (fp32, torch on `threads` host threads); widths =
+    (h1, h2, h3) for the MLPs or "cnn" for RefCNN.
 
     Returns (samples_per_s, steps, seconds)."""
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    model = RefMLP(*widths)
+    model = RefCNN() if widths == "cnn" else RefMLP(*widths)
     model.train()
     opt = torch.optim.Adam(model.parameters(), lr=0.01)
     x, t = synthetic_batch(batch, 1234)
