@@ -25,6 +25,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from . import nets
+from .checkpoint import load_checkpoint, save_checkpoint
 from .data import read_idx, shard_indices, synthetic_mnist
 from .optim import LatentAdam
 from .parallel import GradExchange
@@ -61,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--max-steps", type=int, default=0, help="stop each epoch after this many steps")
     ap.add_argument("--no-lr-quirk", action="store_true", help="drop the per-batch lr*=0.1 at epoch%%40==0")
     ap.add_argument("--csv-prefix", default=None, help="write <prefix>_BATCH_TIME.csv / _EPOCH_TIME.csv")
+    ap.add_argument("--checkpoint", default=None, help="write a latent-weight checkpoint here after every epoch")
+    ap.add_argument("--resume", default=None, help="resume from a checkpoint written by --checkpoint")
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--master-addr", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
     ap.add_argument("--master-port", default=os.environ.get("MASTER_PORT", "23456"))
@@ -95,12 +98,15 @@ def train(gpu, args):
     exchange = GradExchange(model) if world > 1 else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=nets.binary_params(model))
     crit = torch.nn.CrossEntropyLoss()
+    first_epoch = 1
+    if args.resume:
+        first_epoch = load_checkpoint(args.resume, model, opt, map_location=device) + 1
     data, targets = load_dataset(args, device, rank)
     idx = torch.tensor(shard_indices(len(data), world, rank), device=device)
     nb = (len(idx) + args.batch_size - 1) // args.batch_size
     T, E = [], []
     starts = datetime.now()
-    for epoch in range(1, args.epochs + 1):
+    for epoch in range(first_epoch, args.epochs + 1):
         T.append(["epoch", epoch])
         start = datetime.now()
         meter = AverageMeter()
@@ -136,6 +142,8 @@ def train(gpu, args):
         if rank == 0:
             print("Training ", epoch, " : " + str(datetime.now() - start), flush=True)
         E.append([datetime.now() - start])
+        if args.checkpoint:
+            save_checkpoint(args.checkpoint, model, opt, epoch)
     if rank == 0:
         print("Training complete in: " + str(datetime.now() - starts), flush=True)
         if args.csv_prefix:
