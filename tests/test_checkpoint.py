@@ -8,6 +8,7 @@ import os
 import socket
 import sys
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -144,7 +145,7 @@ def test_rank0_save_barrier_load_gloo(tmp_path):
         assert ok, f"rank {rank}: {err}"
 
 
-@__import__("pytest").mark.gpu
+@pytest.mark.gpu
 def test_trainer_checkpoint_and_resume_on_gpu(tmp_path):
     """bnn_amd.trainer --checkpoint / --resume on one GPU: epoch 1 writes the latent weights and
     Adam state, the resumed run starts at epoch 2 from exactly those tensors."""
