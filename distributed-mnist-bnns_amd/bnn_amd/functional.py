@@ -114,6 +114,8 @@ def sign(x, out=None):
     _check(x)
     x = _c2d(x)
     y = torch.empty_like(x) if out is None else out
+    if x.numel() == 0:            # empty tensors have no device pointer; nothing to compute
+        return y
     L.call("bnn_sign_f32", L.ptr(x), L.ptr(y), x.numel(), L.stream())
     return y
 
@@ -257,6 +259,12 @@ class BinaryLinearFunction(torch.autograd.Function):
         _check(x, weight, bias)
         M, K = x.shape
         N = weight.shape[0]
+        ctx.dims = (M, K, N)
+        ctx.has_bias = bias is not None
+        if M == 0:                # empty batch: F.linear returns [0, N]; gradients are empty / zero
+            ctx.empty = True
+            return torch.empty((0, N), dtype=torch.float32, device=x.device)
+        ctx.empty = False
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dx)
         b = bias.detach() if bias is not None else None
@@ -283,8 +291,14 @@ class BinaryLinearFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xs, wqt = ctx.saved_tensors
         M, K, N = ctx.dims
+        if ctx.empty:
+            dev = dy.device
+            return (torch.empty((0, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None,
+                    torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
+                    torch.zeros((N,), dtype=torch.float32, device=dev)
+                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None)
+        xs, wqt = ctx.saved_tensors
         dy = _c2d(dy)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -331,6 +345,12 @@ class BinaryConv2dFunction(torch.autograd.Function):
         OW = (W + 2 * padding - dilation * (KW - 1) - 1) // stride + 1
         y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
         b = bias.detach() if bias is not None else None
+        ctx.empty = N == 0
+        if ctx.empty:             # empty batch: F.conv2d returns [0, Co, OH, OW]
+            ctx.save_for_backward(x, w)
+            ctx.conf = (binarize_input, stride, padding, dilation, groups)
+            ctx.has_bias = bias is not None
+            return y
         macs = N * Co * OH * OW * (C // groups) * KH * KW
         with _timed("conv2d_fwd", 2 * macs):
             L.call("bnn_conv2d_fwd", L.ptr(x), int(binarize_input), L.ptr(w), L.ptr(b), L.ptr(y),
@@ -347,6 +367,11 @@ class BinaryConv2dFunction(torch.autograd.Function):
         dy = _c2d(dy)
         N, C, H, W = x.shape
         Co, _, KH, KW = w.shape
+        if ctx.empty:
+            return (torch.empty_like(x) if ctx.needs_input_grad[0] else None,
+                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None,
+                    torch.zeros((Co,), dtype=torch.float32, device=x.device)
+                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None, None)
         dx = dw = db = None
         macs = dy.numel() * (C // groups) * KH * KW
         if ctx.needs_input_grad[0]:

@@ -499,3 +499,35 @@ def test_every_gemm_variant_is_exact(F, cfg, M, N, K):
                 assert rel_err(C, ref) < 1e-6, name
     finally:
         _lib.call("bnn_gemm_set_variant", -1)
+
+
+@pytest.mark.parametrize("backend", ["fp4", "mfma", "xnor"])
+def test_empty_and_single_sample_batches(F, backend):
+    """Edge batches through the drop-in path: an empty batch returns an empty output (as torch's
+    F.linear / F.conv2d do) with empty gradients, and a batch of one is exact."""
+    from models.binarized_modules import BinarizeConv2d, BinarizeLinear
+    torch.manual_seed(9)
+    lin = BinarizeLinear(256, 96).cuda()
+    lin.backend = backend
+    for m in (0, 1):
+        x = torch.randn(m, 256, device="cuda", requires_grad=True)
+        xr = x.detach().clone()
+        y = lin(x)
+        assert y.shape == (m, 96)
+        y.sum().backward()
+        assert x.grad.shape == (m, 256)
+        if m:
+            ref = torch.sign(xr) @ torch.sign(lin.weight.org).t() + lin.bias.detach()
+            assert torch.equal(y.detach(), ref)
+    conv = BinarizeConv2d(16, 32, kernel_size=5, padding=2).cuda()
+    for n in (0, 1):
+        x = torch.randn(n, 16, 14, 14, device="cuda", requires_grad=True)
+        xr = x.detach().clone()
+        y = conv(x)
+        assert y.shape == (n, 32, 14, 14)
+        y.sum().backward()
+        assert x.grad.shape == (n, 16, 14, 14)
+        if n:
+            ref = torch.nn.functional.conv2d(torch.sign(xr).double().cpu(), torch.sign(conv.weight.org).double().cpu(),
+                                             None, padding=2) + conv.bias.detach().double().cpu().view(1, -1, 1, 1)
+            assert torch.equal(y.detach().cpu(), ref.float())   # integer sum, then one fp32 bias add
