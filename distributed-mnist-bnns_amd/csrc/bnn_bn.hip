@@ -149,25 +149,39 @@ __device__ __forceinline__ float4 ld4_or(const float* p, int64_t c, float dflt) 
   return p ? ld4(p + c) : make_float4(dflt, dflt, dflt, dflt);
 }
 
+// Elementwise passes on a 2-D grid: blockIdx.x = 1024-column block (one float4 per thread),
+// blockIdx.y = APPLY_ROWS-row chunk.  Each thread keeps its 4 columns' parameters in registers and
+// walks the rows (per row the workgroup touches one contiguous 4 KiB segment): no per-element
+// index modulo and no per-element reloads of the column vectors.
+constexpr int APPLY_ROWS = 64;
+
+inline dim3 apply_grid(int64_t M, int64_t C) {
+  return dim3((unsigned)((C / 4 + 255) / 256), (unsigned)((M + APPLY_ROWS - 1) / APPLY_ROWS));
+}
+
 __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, int64_t M, int64_t C,
                                                   const float* __restrict__ mean,
                                                   const float* __restrict__ invstd,
                                                   const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int hardtanh,
                                                   float* __restrict__ y) {
-  const int64_t n4 = M * C / 4;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int64_t c = (i * 4) % C;
-    const float4 xv = ld4(x + i * 4), mv = ld4(mean + c), iv = ld4(invstd + c);
-    const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
-    float v[4] = {fmaf((xv.x - mv.x) * iv.x, gv.x, bv.x), fmaf((xv.y - mv.y) * iv.y, gv.y, bv.y),
-                  fmaf((xv.z - mv.z) * iv.z, gv.z, bv.z), fmaf((xv.w - mv.w) * iv.w, gv.w, bv.w)};
-    if (hardtanh) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
+  const float4 mv = ld4(mean + c), iv = ld4(invstd + c);
+  const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
+  const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
+  for (int64_t r = r0; r < r1; ++r) {
+    const float4 xv = ld4(x + r * C + c);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = fminf(fmaxf(v[j], -1.f), 1.f);
+    for (int j = 0; j < 4; ++j) {
+      v[j] = fmaf((xs[j] - mu[j]) * is[j], ga[j], be[j]);
+      if (hardtanh) v[j] = fminf(fmaxf(v[j], -1.f), 1.f);
     }
-    *reinterpret_cast<float4*>(y + i * 4) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(y + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -196,27 +210,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
                                                       const float* __restrict__ sg,
                                                       const float* __restrict__ sgx,
                                                       float* __restrict__ dx) {
-  const int64_t n4 = M * C / 4;
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
   const float inv_n = 1.f / (float)M;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int64_t c = (i * 4) % C;
-    const float4 xv = ld4(x + i * 4), gv = ld4(dy + i * 4);
-    const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
-    const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f);
+  const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
+  const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f);
+  const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
+  const float a0[4] = {s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n};
+  const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
+  for (int64_t r = r0; r < r1; ++r) {
+    const float4 xv = ld4(x + r * C + c), gv = ld4(dy + r * C + c);
     const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
-    const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
-    const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
-    const float a0[4] = {s0.x, s0.y, s0.z, s0.w}, a1[4] = {s1.x, s1.y, s1.z, s1.w};
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float xh = (xs[j] - ms[j]) * is[j];
-      const float y = fmaf(xh, ga[j], be[j]);
-      const float g = (!hardtanh || (y > -1.f && y < 1.f)) ? gs[j] : 0.f;
-      o[j] = ga[j] * is[j] * (g - a0[j] * inv_n - xh * (a1[j] * inv_n));
+      const float yv = fmaf(xh, ga[j], be[j]);
+      const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
+      o[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
     }
-    *reinterpret_cast<float4*>(dx + i * 4) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(dx + r * C + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -225,7 +240,8 @@ inline int grid_for(int64_t n) {
 }
 
 bool bn_args_ok(const float* x, int64_t M, int64_t C) {
-  return x && M > 0 && C > 0 && C % 4 == 0 && aligned16(x) && bn_chunks(M) <= 65535;
+  return x && M > 0 && C > 0 && C % 4 == 0 && aligned16(x) && bn_chunks(M) <= 65535 &&
+         (M + APPLY_ROWS - 1) / APPLY_ROWS <= 65535;
 }
 
 bool vec_ok(const float* p) { return p == nullptr || aligned16(p); }
@@ -532,7 +548,7 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
   hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, M, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, (int64_t)BN_ROWS, (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
-    hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
+    hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
                        gamma, beta, hardtanh, y);
   return check_launch("bnn_bn_fwd_train");
 }
@@ -548,7 +564,7 @@ BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* g
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* istd = reinterpret_cast<float*>(work);
   hipLaunchKernelGGL(bn_invstd_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_var, istd, C, eps);
-  hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, M, C, running_mean, istd, gamma,
+  hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, running_mean, istd, gamma,
                      beta, hardtanh, y);
   return check_launch("bnn_bn_fwd_eval");
 }
@@ -573,7 +589,7 @@ BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
   hipLaunchKernelGGL(bn_bwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
-    hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(M * C / 4)), dim3(256), 0, s, x, dy, M, C, save_mean,
+    hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean,
                        save_invstd, gamma, beta, hardtanh, k0, k1, dx);
   }
   return check_launch("bnn_bn_bwd");

@@ -258,6 +258,33 @@ __global__ __launch_bounds__(256) void colstats_k(const float* __restrict__ x, i
 }
 
 // Pass 2: reduce the chunks in a fixed order -> scale[n], colsum[n].
+// colstats_k with one float4 (4 adjacent columns) per thread: same per-column row order and
+// double accumulation (bit-identical results), a quarter of the load instructions.
+__global__ __launch_bounds__(256) void colstats4_k(const float* __restrict__ x, int64_t M, int64_t N,
+                                                   int64_t ldx, float* __restrict__ pmax,
+                                                   double* __restrict__ psum) {
+  const int64_t n = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * COL_ROWS;
+  if (n >= N) return;
+  const int64_t r1 = (M < r0 + COL_ROWS) ? M : r0 + COL_ROWS;
+  float amax[4] = {0.f, 0.f, 0.f, 0.f};
+  double sum[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t r = r0; r < r1; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ldx + n);
+    const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      amax[j] = absmax_acc(amax[j], vs[j]);
+      sum[j] += (double)vs[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pmax[blockIdx.y * N + n + j] = amax[j];
+    psum[blockIdx.y * N + n + j] = sum[j];
+  }
+}
+
 __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax,
                                                   const double* __restrict__ psum, int64_t N,
                                                   int64_t R, float* __restrict__ scale,
@@ -464,7 +491,10 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
   double* psum = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
                                            round_up(R * N * (int64_t)sizeof(float), 256));
   const unsigned gn = (unsigned)((N + 255) / 256);
-  if (M > 0) {
+  if (M > 0 && aligned16(x) && ldx % 4 == 0 && N % 4 == 0) {
+    hipLaunchKernelGGL(colstats4_k, dim3((unsigned)((N / 4 + 255) / 256), (unsigned)R), dim3(256), 0, S(stream), x,
+                       M, N, ldx, pmax, psum);
+  } else if (M > 0) {
     hipLaunchKernelGGL(colstats_k, dim3(gn, (unsigned)R), dim3(256), 0, S(stream), x, M, N, ldx, pmax,
                        psum);
   } else {
