@@ -48,8 +48,8 @@ def op_peak(kernel):
     """(bound, peak TFLOP/s or TOPS, unit of the count) of an ops-counted kernel."""
     if kernel.startswith("conv2d_bwd"):
         return "mfma", MI355X_F32_MFMA_TFLOPS, "f32 MFMA flops (2*N*Co*OH*OW*C*KH*KW)"
-    if kernel.startswith("conv2d_fwd"):
-        return "valu", MI355X_DOT4_TOPS, "int8 dot4 ops (2*N*Co*OH*OW*C*KH*KW)"
+    if kernel.startswith("conv2d_fwd"):   # C=1 layer on VALU dot4; C%16==0 layers on int8 MFMA (looser bound)
+        return "valu", MI355X_DOT4_TOPS, "int8 dot4 / MFMA ops (2*N*Co*OH*OW*C*KH*KW)"
     return "mfma", MI355X_INT8_DENSE_TOPS, "int8 MFMA ops (2*M*N*K*digit_pairs)"
 
 

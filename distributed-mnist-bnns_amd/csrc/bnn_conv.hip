@@ -705,6 +705,119 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
   }
 }
 
+// Forward binary conv as an implicit GEMM on v_mfma_i32_16x16x64_i8 (exact integer sums, so the
+// output equals the reference's F.conv2d on sign()ed operands bit for bit, + one fp32 bias add).
+// K order = (tap, 16-channel chunk): one lane's 16-byte fragment is 16 channels of one tap of one
+// pixel, a single ds_read_b128 from the channels-innermost int8 image xs[Hp][Wp][C].
+//   A[i = co][k]  = sign(W[co][ci][kh][kw])   (ws[co][KCp*16], zero for padded chunks)
+//   B[k][j = pix] = sign(x[ci][oh+kh-pad][ow+kw-pad])
+//   16x16x64 lane map: row/col = l&15, 16-byte chunk (l>>4) of the 64-byte k-step; D row 4(l>>4)+r.
+struct MfFwd {
+  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, Wp, CB, KC, KCp, ntile_pix;
+};
+
+template <int COT>
+__global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, float* __restrict__ y,
+                                                          int64_t N, MfFwd g) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  int8_t* ws = reinterpret_cast<int8_t*>(ldsf);                 // [COT*16][KCp*16]
+  int8_t* xs = ws + COT * 16 * g.KCp * 16;                      // [Hp][Wp][C]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int KK = g.KH * g.KW, rowb = g.KCp * 16;
+  for (int i = t; i < COT * 16 * rowb; i += MF_T) {
+    const int co = i / rowb, kb = i - co * rowb, ch = kb >> 4, ci16 = kb & 15;
+    int v = 0;
+    if (co < g.Co && ch < g.KC) {
+      const int tap = ch / g.CB, ci = (ch - tap * g.CB) * 16 + ci16;
+      v = tsign(w[(co * g.C + ci) * KK + tap]);
+    }
+    ws[i] = (int8_t)v;
+  }
+  const int nxs = g.Hp * g.Wp * g.C;
+  for (int i = t; i < nxs; i += MF_T) xs[i] = 0;
+  // this wave's pixel tiles wv, wv+4, wv+8, wv+12 (clamped: computed, never stored)
+  const int HW = g.H * g.W, OHW = g.OH * g.OW;
+  int pbase[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    int pix = (wv + 4 * m) * 16 + (lane & 15);
+    if (pix >= OHW) pix = 0;
+    const int oh = pix / g.OW, ow = pix - oh * g.OW;
+    pbase[m] = (oh * g.Wp + ow) * g.C;
+  }
+  const int my_tiles = (g.ntile_pix - wv + 3) / 4;
+  const int h = lane >> 4;
+  const float inv_w = 1.f / (float)g.W, inv_hw = 1.f / (float)HW;
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();
+    const float* xn = x + n * g.C * HW;
+    for (int i = t; i < g.C * HW; i += MF_T) {
+      const int c = fdivi(i, inv_hw), r = i - c * HW, ih = fdivi(r, inv_w), iw = r - ih * g.W;
+      xs[((ih + g.pad) * g.Wp + iw + g.pad) * g.C + c] = (int8_t)tsign(xn[i]);
+    }
+    __syncthreads();
+    v4i acc[COT][4];
+#pragma unroll
+    for (int a = 0; a < COT; ++a)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[a][m] = v4i{0, 0, 0, 0};
+    for (int ks = 0; ks < g.KCp / 4; ++ks) {
+      const int ch = min(4 * ks + h, g.KC - 1);   // padded chunks: zero weights, valid address
+      const int tap = ch / g.CB, cb = ch - tap * g.CB;
+      const int kh = tap / g.KW, kw = tap - kh * g.KW;
+      const int xo = (kh * g.Wp + kw) * g.C + cb * 16;
+      v4i av[COT], bv[4];
+#pragma unroll
+      for (int a = 0; a < COT; ++a)
+        av[a] = *reinterpret_cast<const v4i*>(ws + (a * 16 + (lane & 15)) * rowb + (4 * ks + h) * 16);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) bv[m] = *reinterpret_cast<const v4i*>(xs + pbase[m] + xo);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int a = 0; a < COT; ++a)
+          acc[a][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bv[m], acc[a][m], 0, 0, 0);
+    }
+    float* yn = y + n * g.Co * OHW;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      if (m >= my_tiles) continue;
+      const int pix = (wv + 4 * m) * 16 + (lane & 15);
+      if (pix >= OHW) continue;
+#pragma unroll
+      for (int a = 0; a < COT; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = a * 16 + 4 * h + r;
+          if (co < g.Co) yn[(int64_t)co * OHW + pix] = (float)acc[a][m][r] + (bias ? bias[co] : 0.f);
+        }
+    }
+  }
+}
+
+inline bool mf_fwd_geom(const ConvShape& s, MfFwd* g, int64_t* lds) {
+  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.C % 16 == 0 && s.C <= 64 && s.Co <= 64 &&
+        s.pad <= s.KH - 1 && s.pad <= s.KW - 1))
+    return false;
+  MfFwd d;
+  d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
+  d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
+  d.Hp = d.H + 2 * d.pad; d.Wp = d.W + 2 * d.pad;
+  d.CB = d.C / 16;
+  d.KC = d.KH * d.KW * d.CB;
+  d.KCp = (int)round_up(d.KC, 4);
+  d.ntile_pix = (d.OH * d.OW + 15) / 16;
+  if (d.ntile_pix > 16 || (int64_t)d.C * d.H * d.W >= (1 << 20)) return false;
+  // gathered pixel (oh + kh, ow + kw) stays inside the padded image
+  if (d.OH - 1 + d.KH - 1 >= d.Hp || d.OW - 1 + d.KW - 1 >= d.Wp) return false;
+  const int cot = (d.Co + 15) / 16;
+  *lds = (int64_t)(cot == 3 ? 4 : cot) * 16 * d.KCp * 16 + round_up((int64_t)d.Hp * d.Wp * d.C, 16);
+  *g = d;
+  return *lds <= kMaxTileLds;
+}
+
 inline bool mf_data_geom(const ConvShape& s, MfData* g, int64_t* lds) {
   if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.pad <= s.KH - 1 && s.pad <= s.KW - 1 && s.C <= 32))
     return false;
@@ -783,6 +896,17 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
   const int64_t total = N * Co * s.OH * s.OW;
   if (total == 0) return 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  MfFwd mf;
+  int64_t mlds = 0;
+  if (binarize_input && g_conv_mfma && mf_fwd_geom(s, &mf, &mlds)) {
+    const size_t lds = (size_t)mlds;
+    const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
+    const int cot = (mf.Co + 15) / 16;
+    if (cot == 1) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<1>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
+    else if (cot == 2) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<2>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
+    else BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<4>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
+    return check_launch("bnn_conv2d_fwd");
+  }
   if (tile_geom_ok(s) && fwd_tile_lds(s, binarize_input != 0) <= kMaxTileLds) {
     const TileGeo g = geo(s);
     const int CO = pick_co(Co);

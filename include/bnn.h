@@ -140,9 +140,10 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
                           int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
                           int32_t dil, int32_t groups, bnn_stream_t stream);
 
-/* Backward-convolution engine switch: 1 (default) = f32-MFMA implicit-GEMM kernels
- * (v_mfma_f32_16x16x4_f32, exact f32 products) for stride-1 ungrouped shapes; 0 = the VALU
- * LDS-tiled / generic kernels.  Process-global; for cross-checks and the kernel sweep. */
+/* Convolution engine switch: 1 (default) = MFMA implicit-GEMM kernels for stride-1 ungrouped
+ * shapes -- backward on v_mfma_f32_16x16x4_f32 (exact f32 products), forward with a binarised
+ * input and C % 16 == 0 on v_mfma_i32_16x16x64_i8 (exact integer sums); 0 = the VALU LDS-tiled /
+ * generic kernels.  Process-global; for cross-checks and the kernel sweep. */
 int bnn_conv_set_mfma(int32_t on);
 
 /* ---------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
