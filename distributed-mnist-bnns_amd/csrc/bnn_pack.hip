@@ -61,21 +61,16 @@ template <int FMT, int AFF = 0>
 __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
                                                         int64_t K, int64_t ldx, int8_t* __restrict__ q,
                                                         int64_t ldq, int8_t* __restrict__ qt,
-                                                        int64_t ldqt, int vec, ColAffine af = {}) {
+                                                        int64_t ldqt, int vec, ColAffine af = {},
+                                                        int rtiles = 1, int64_t ntiles_y = 0) {
+  // rtiles > 1: the workgroup walks rtiles vertically adjacent 64x64 tiles of its column block
+  // (the per-column BatchNorm parameters are loaded once per workgroup, not once per tile)
   __shared__ int tile[TILE][TILE + 1];
-  const int64_t m0 = (int64_t)blockIdx.y * TILE, k0 = (int64_t)blockIdx.x * TILE;
+  const int64_t k0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
-  const int64_t m = m0 + r;
-  float v[16];
-  if (m < M) {
-    load16(x + m * ldx, k0 + c, K, vec, v);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = 0.f;
-  }
+  float mu[16], is[16], ga[16], be[16];
   if (AFF) {
     // per-column parameters for columns k0+c .. +15: float4 loads when the run is in range
-    float mu[16], is[16], ga[16], be[16];
     const int64_t cb = k0 + c;
     if (af.vec && cb + 16 <= K) {
 #pragma unroll
@@ -99,6 +94,22 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
         be[j] = (in && af.beta) ? af.beta[cb + j] : 0.f;
       }
     }
+  }
+  for (int it = 0; it < rtiles; ++it) {
+  const int64_t ty = (int64_t)blockIdx.y * rtiles + it;
+  if (rtiles > 1 && ty >= ntiles_y) break;   // uniform per workgroup
+  if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
+  const int64_t m0 = ty * TILE;
+  const int64_t m = m0 + r;
+  float v[16];
+  if (m < M) {
+    load16(x + m * ldx, k0 + c, K, vec, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+  }
+  if (AFF) {
+    const int64_t cb = k0 + c;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       v[j] = (m < M && cb + j < K) ? fmaf((v[j] - mu[j]) * is[j], ga[j], be[j]) : 0.f;
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
       w.w = pack4(g[12], g[13], g[14], g[15]);
       *reinterpret_cast<v4i*>(qt + k * ldqt + m0 + mc) = w;
     }
+  }
   }
 }
 
@@ -531,11 +543,14 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   const ColAffine af{mean, invstd, gamma, beta,
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta))};
+  // 4 row tiles per workgroup when that still leaves >= 8K workgroups (amortised parameter loads)
+  const int rt = (gx * ((gy + 3) / 4) >= 8192) ? 4 : 1;
+  const unsigned gyr = (unsigned)((gy + rt - 1) / rt);
   if (fmt == 1)
-    hipLaunchKernelGGL((sign_pack_tile_k<1, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M,
-                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af);
+    hipLaunchKernelGGL((sign_pack_tile_k<1, 1>), dim3((unsigned)gx, gyr), dim3(256), 0, S(stream), x, M,
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy);
   else
-    hipLaunchKernelGGL((sign_pack_tile_k<0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M,
-                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af);
+    hipLaunchKernelGGL((sign_pack_tile_k<0, 1>), dim3((unsigned)gx, gyr), dim3(256), 0, S(stream), x, M,
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy);
   return check_launch("bnn_bn_apply_pack");
 }
