@@ -106,6 +106,13 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
   }
 }
 
+// Final merges: a workgroup owns 64 columns; its 4 waves each merge every 4th chunk (r = wave,
+// wave+4, ...) and wave 0 folds the 4 group results in order -- 4x the parallelism of one thread
+// per column walking all R chunks, still a fixed (deterministic) order.
+constexpr int FIN_COLS = 64, FIN_GROUPS = 4;
+
+inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + FIN_COLS - 1) / FIN_COLS)); }
+
 __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__ p0, const double* __restrict__ p1,
                                                       int64_t M, int64_t C, int64_t R, float momentum, float eps,
                                                       float* __restrict__ rmean, float* __restrict__ rvar,
@@ -113,17 +120,34 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
                                                       float* __restrict__ save_invstd, int64_t chunk_rows,
                                                       int64_t hw) {
   // chunk r covers rows [r*chunk_rows, min((r+1)*chunk_rows, M)) of hw elements each (hw = 1 for
-  // BatchNorm1d; H*W for the NCHW BatchNorm2d of bnn_bn2d.hip)
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  // BatchNorm1d; H*W for the NCHW BatchNorm2d)
+  __shared__ double sn[FIN_GROUPS][FIN_COLS], sm[FIN_GROUPS][FIN_COLS], sq[FIN_GROUPS][FIN_COLS];
+  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
+  const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int64_t r = 0; r < R; ++r) {  // Chan et al. merge in a fixed order
-    const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
-    const double nb = (double)((hi - r * chunk_rows) * hw);
-    const double mb = p0[r * C + c], m2b = p1[r * C + c];
-    const double nt = n + nb, delta = mb - mean;
+  if (c < C) {
+    for (int64_t r = grp; r < R; r += FIN_GROUPS) {  // Chan et al. merge, fixed order
+      const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
+      const double nb = (double)((hi - r * chunk_rows) * hw);
+      const double mb = p0[r * C + c], m2b = p1[r * C + c];
+      const double nt = n + nb, delta = mb - mean;
+      mean += delta * nb / nt;
+      m2 += m2b + delta * delta * n * nb / nt;
+      n = nt;
+    }
+  }
+  sn[grp][lc] = n;
+  sm[grp][lc] = mean;
+  sq[grp][lc] = m2;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int gI = 0; gI < FIN_GROUPS; ++gI) {
+    const double nb = sn[gI][lc];
+    if (nb == 0.0) continue;
+    const double nt = n + nb, delta = sm[gI][lc] - mean;
     mean += delta * nb / nt;
-    m2 += m2b + delta * delta * n * nb / nt;
+    m2 += sq[gI][lc] + delta * delta * n * nb / nt;
     n = nt;
   }
   double var = m2 / n;
@@ -189,13 +213,21 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
                                                       const double* __restrict__ p1, int64_t C, int64_t R,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       float* __restrict__ k0, float* __restrict__ k1) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ double sa[FIN_GROUPS][FIN_COLS], sb[FIN_GROUPS][FIN_COLS];
+  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
+  const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
   double s = 0.0, s2 = 0.0;
-  for (int64_t r = 0; r < R; ++r) {
-    s += p0[r * C + c];
-    s2 += p1[r * C + c];
-  }
+  if (c < C)
+    for (int64_t r = grp; r < R; r += FIN_GROUPS) {
+      s += p0[r * C + c];
+      s2 += p1[r * C + c];
+    }
+  sa[grp][lc] = s;
+  sb[grp][lc] = s2;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  s = sa[0][lc] + sa[1][lc] + sa[2][lc] + sa[3][lc];
+  s2 = sb[0][lc] + sb[1][lc] + sb[2][lc] + sb[3][lc];
   if (dbeta) dbeta[c] = (float)s;
   if (dgamma) dgamma[c] = (float)s2;
   k0[c] = (float)s;
@@ -545,7 +577,7 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
   double* p1 = p0 + R * C;
   hipLaunchKernelGGL(bn_reduce_k<0>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x,
                      nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
-  hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, M, C, R,
+  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, (int64_t)BN_ROWS, (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
     hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
@@ -586,7 +618,7 @@ BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
                      M, C, save_mean, save_invstd, gamma, beta, hardtanh, p0, p1);
-  hipLaunchKernelGGL(bn_bwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, C, R, dgamma,
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean,
@@ -620,7 +652,7 @@ BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, 
   double* p1 = p0 + R * C;
   hipLaunchKernelGGL((bn2d_reduce_k<0, 0>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s, x, nullptr, N, C,
                      (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
-  hipLaunchKernelGGL(bn_fwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, N, C, R,
+  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
   BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
@@ -662,7 +694,7 @@ BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, 
   BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
                                            s, x, dy, N, C, (int)H, (int)W, CR, save_mean, save_invstd, gamma, beta,
                                            hardtanh, p0, p1));
-  hipLaunchKernelGGL(bn_bwd_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, p1, C, R, dgamma,
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;

@@ -297,18 +297,29 @@ __global__ __launch_bounds__(256) void colstats4_k(const float* __restrict__ x, 
   }
 }
 
+// 64 columns x 4 chunk groups per workgroup (fixed-order fold of the groups): deterministic, 4x the
+// parallelism of one thread per column walking all R chunks.
 __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax,
                                                   const double* __restrict__ psum, int64_t N,
                                                   int64_t R, float* __restrict__ scale,
                                                   float* __restrict__ colsum) {
-  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  __shared__ float smx[4][64];
+  __shared__ double ssm[4][64];
+  const int lc = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + lc;
   float amax = 0.f;
   double sum = 0.0;
-  for (int64_t r = 0; r < R; ++r) {
-    amax = fmaxf(amax, pmax[r * N + n]);
-    sum += psum[r * N + n];
-  }
+  if (n < N)
+    for (int64_t r = grp; r < R; r += 4) {
+      amax = fmaxf(amax, pmax[r * N + n]);
+      sum += psum[r * N + n];
+    }
+  smx[grp][lc] = amax;
+  ssm[grp][lc] = sum;
+  __syncthreads();
+  if (grp != 0 || n >= N) return;
+  amax = fmaxf(fmaxf(smx[0][lc], smx[1][lc]), fmaxf(smx[2][lc], smx[3][lc]));
+  sum = ssm[0][lc] + ssm[1][lc] + ssm[2][lc] + ssm[3][lc];
   int shift;
   float s;
   digit_scale(amax, &shift, &s);
@@ -316,7 +327,6 @@ __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax
   if (colsum != nullptr) colsum[n] = (float)sum;
 }
 
-// Pass 3: quantise with the column scale and write the transposed digit planes.
 __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ x, int64_t M,
                                                       int64_t N, int64_t ldx,
                                                       const float* __restrict__ scale,
@@ -513,7 +523,8 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
     (void)hipMemsetAsync(pmax, 0, R * N * sizeof(float), S(stream));
     (void)hipMemsetAsync(psum, 0, R * N * sizeof(double), S(stream));
   }
-  hipLaunchKernelGGL(colfinal_k, dim3(gn), dim3(256), 0, S(stream), pmax, psum, N, R, scale, colsum);
+  hipLaunchKernelGGL(colfinal_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, S(stream), pmax, psum, N, R, scale,
+                     colsum);
   const int vec = aligned16(x) && (ldx % 4 == 0);
   hipLaunchKernelGGL(quant_cols_t_k, dim3((unsigned)((N + TILE - 1) / TILE), (unsigned)(ldqt / TILE)),
                      dim3(256), 0, S(stream), x, M, N, ldx, scale, digits_t, ldqt, plane, vec);
