@@ -20,7 +20,7 @@ from . import _lib as L
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
     "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "batch_norm_hardtanh",
-    "bn_hardtanh_binary_linear", "batch_norm2d_hardtanh_pool",
+    "bn_hardtanh_binary_linear", "batch_norm2d_hardtanh_pool", "dropout_batch_norm_hardtanh", "dropout_mask",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
 
@@ -470,6 +470,64 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
                    int(ctx.hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None)
+
+
+class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
+    """hardtanh(nn.BatchNorm1d(nn.Dropout(p)(x))) in training mode, fused (mnist-dist2.py:69-74:
+    fc3 -> drop -> bn3 -> htanh3).  The dropout mask is regenerated from ``seed`` by every pass
+    (bnn_bn_dropout_*), so neither the mask nor the dropped activation is written to HBM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, p, seed):
+        _check(x, weight, bias, running_mean, running_var)
+        x = _c2d(x)
+        M, C = x.shape
+        y = torch.empty_like(x)
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        ws = _bn_ws(M, C, x.device)
+        mean = torch.empty((C,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        with _timed("bn_dropout_fwd_train", 0, 12 * M * C):
+            L.call("bnn_bn_dropout_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                   L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
+                   L.ptr(mean), L.ptr(invstd), L.ptr(y), 1, float(p), int(seed), L.ptr(ws), L.stream())
+        ctx.save_for_backward(x, w, b, mean, invstd)
+        ctx.p, ctx.seed = p, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, mean, invstd = ctx.saved_tensors
+        dy = _c2d(dy)
+        M, C = x.shape
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
+        db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
+        ws = _bn_ws(M, C, x.device)
+        with _timed("bn_dropout_bwd", 0, 16 * M * C):
+            L.call("bnn_bn_dropout_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+                   1, float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+        return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None)
+
+
+def dropout_mask(n, p, seed, device="cuda"):
+    """The keep mask (scaled: 1/(1-p) or 0) the fused dropout passes use for elements 0..n-1."""
+    out = torch.empty((n,), dtype=torch.float32, device=device)
+    L.call("bnn_dropout_mask", n, float(p), int(seed), L.ptr(out), L.stream())
+    return out
+
+
+def dropout_batch_norm_hardtanh(x, p, bn, seed=None):
+    """nn.Dropout(p) -> nn.BatchNorm1d module (training mode) -> Hardtanh through libbnn.  The seed
+    is drawn from torch's CPU generator (so torch.manual_seed makes runs repeatable) unless given."""
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    rm, rv, bn_training, factor = _bn_module_args(bn)
+    if not bn_training:
+        raise ValueError("dropout_batch_norm_hardtanh is the training-mode fusion")
+    return DropoutBatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, factor, bn.eps, float(p), seed)
 
 
 def _bn_module_args(bn):

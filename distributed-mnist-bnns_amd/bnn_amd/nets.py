@@ -66,8 +66,13 @@ class MLP(nn.Module):
         x = x.view(-1, 28 * 28)
         x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, self.fc1(x))
         x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x)
-        x = self.drop(x)
-        x = self._bnh(self.bn3, self.htanh3, x)
+        if (self.fused_bn and self.training and self.drop.p > 0 and self.bn3.training and x.is_cuda
+                and x.dim() == 2 and x.shape[1] % 4 == 0):
+            # drop -> bn3 -> htanh3 as one libbnn op (mask regenerated in every pass, never stored)
+            x = BF.dropout_batch_norm_hardtanh(x, self.drop.p, self.bn3)
+        else:
+            x = self.drop(x)
+            x = self._bnh(self.bn3, self.htanh3, x)
         x = self.fc4(x)
         return self.logsoftmax(x)
 

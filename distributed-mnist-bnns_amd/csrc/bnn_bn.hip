@@ -24,6 +24,43 @@ inline int64_t bn_chunks(int64_t M) { return std::max<int64_t>(1, (M + BN_ROWS -
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// Fused nn.Dropout(p) in front of a BatchNorm (mnist-dist2.py:69-70: fc3 -> drop -> bn3).  The
+// keep mask is a counter-based hash of (seed, element index), so forward statistics, forward
+// apply and both backward passes regenerate the same mask without storing it; kept elements are
+// scaled by 1/(1-p) exactly as torch's dropout does (x * scale, grad * scale).
+struct Drop {
+  uint64_t seed;
+  uint32_t thresh;  // keep iff hash < thresh
+  int on;
+  float scale;      // 1 / (1 - p)
+};
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;   // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
+
+__device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4]) {
+  if (!d.on) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = drop_keep(d, i0 + j) ? v[j] * d.scale : 0.f;
+}
+
+inline Drop make_drop(float p, uint64_t seed) {
+  Drop d{seed, 0u, 0, 1.f};
+  if (p > 0.f && p < 1.f) {
+    const double t = (1.0 - (double)p) * 4294967296.0;
+    d.thresh = t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+    d.on = 1;
+    d.scale = 1.f / (1.f - p);
+  }
+  return d;
+}
+
 // MODE 0: per-chunk (mean, M2), accumulated as deviations from the chunk's first row so the
 //         float partials see deviations rather than raw magnitudes; merged with Chan's formula.
 // MODE 1: per-chunk (sum g, sum g*xhat) with g = dy*mask(y).
@@ -34,7 +71,8 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
                                                    const float* __restrict__ invstd,
                                                    const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, int hardtanh,
-                                                   double* __restrict__ p0, double* __restrict__ p1) {
+                                                   double* __restrict__ p0, double* __restrict__ p1,
+                                                   Drop dp = Drop{0, 0, 0, 1.f}) {
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
@@ -47,6 +85,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
     mu[1] = sv.y;
     mu[2] = sv.z;
     mu[3] = sv.w;
+    drop4(dp, (uint64_t)(r0 * C + c), mu);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -61,7 +100,8 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
     for (int64_t rr = r; rr < re; ++rr) {
       const float4 xv = ld4(x + rr * C + c);
-      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      drop4(dp, (uint64_t)(rr * C + c), xs);
       if (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -188,7 +228,7 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
                                                   const float* __restrict__ invstd,
                                                   const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int hardtanh,
-                                                  float* __restrict__ y) {
+                                                  float* __restrict__ y, Drop dp = Drop{0, 0, 0, 1.f}) {
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
@@ -198,7 +238,8 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
   const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
   for (int64_t r = r0; r < r1; ++r) {
     const float4 xv = ld4(x + r * C + c);
-    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    drop4(dp, (uint64_t)(r * C + c), xs);
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -241,7 +282,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
                                                       const float* __restrict__ beta, int hardtanh,
                                                       const float* __restrict__ sg,
                                                       const float* __restrict__ sgx,
-                                                      float* __restrict__ dx) {
+                                                      float* __restrict__ dx, Drop dp = Drop{0, 0, 0, 1.f}) {
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
@@ -254,7 +295,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
   const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
   for (int64_t r = r0; r < r1; ++r) {
     const float4 xv = ld4(x + r * C + c), gv = ld4(dy + r * C + c);
-    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    drop4(dp, (uint64_t)(r * C + c), xs);
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -263,6 +306,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
       const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
       o[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
     }
+    drop4(dp, (uint64_t)(r * C + c), o);   // dropout backward: grad * mask * scale
     *reinterpret_cast<float4*>(dx + r * C + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
@@ -560,10 +604,10 @@ BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
   return 2 * bn_chunks(M) * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
 }
 
-BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
-                             void* stream) {
+                             void* stream, Drop dp) {
   if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !work || !vec_ok(y) ||
       (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) || !vec_ok(beta) ||
       !aligned16(save_mean) || !aligned16(save_invstd)) {
@@ -576,13 +620,33 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   hipLaunchKernelGGL(bn_reduce_k<0>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x,
-                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
+                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, dp);
   hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, (int64_t)BN_ROWS, (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
     hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
-                       gamma, beta, hardtanh, y);
+                       gamma, beta, hardtanh, y, dp);
   return check_launch("bnn_bn_fwd_train");
+}
+
+BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+                             float* running_mean, float* running_var, float momentum, float eps,
+                             float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
+                             void* stream) {
+  return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
+                           y, hardtanh, work, stream, make_drop(0.f, 0));
+}
+
+BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+                                     float* running_mean, float* running_var, float momentum, float eps,
+                                     float* save_mean, float* save_invstd, float* y, int32_t hardtanh, float p,
+                                     uint64_t seed, void* work, void* stream) {
+  if (!(p >= 0.f && p < 1.f)) {
+    set_error("bnn_bn_dropout_fwd_train: p must be in [0, 1) (got %g)", (double)p);
+    return kErrInval;
+  }
+  return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
+                           y, hardtanh, work, stream, make_drop(p, seed));
 }
 
 BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -601,9 +665,9 @@ BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* g
   return check_launch("bnn_bn_fwd_eval");
 }
 
-BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
-                       float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
+                       float* dx, float* dgamma, float* dbeta, void* work, void* stream, Drop dp) {
   if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work ||
       (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
       !aligned16(save_invstd)) {
@@ -617,14 +681,52 @@ BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
-                     M, C, save_mean, save_invstd, gamma, beta, hardtanh, p0, p1);
+                     M, C, save_mean, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean,
-                       save_invstd, gamma, beta, hardtanh, k0, k1, dx);
+                       save_invstd, gamma, beta, hardtanh, k0, k1, dx, dp);
   }
   return check_launch("bnn_bn_bwd");
+}
+
+BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                       const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
+                       float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
+                     make_drop(0.f, 0));
+}
+
+BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                               const float* beta, const float* save_mean, const float* save_invstd,
+                               int32_t hardtanh, float p, uint64_t seed, float* dx, float* dgamma, float* dbeta,
+                               void* work, void* stream) {
+  if (!(p >= 0.f && p < 1.f)) {
+    set_error("bnn_bn_dropout_bwd: p must be in [0, 1) (got %g)", (double)p);
+    return kErrInval;
+  }
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
+                     make_drop(p, seed));
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d, float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = drop_keep(d, (uint64_t)i) ? d.scale : 0.f;
+}
+
+BNN_API int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, void* stream) {
+  if (n < 0 || (n > 0 && !out) || !(p >= 0.f && p < 1.f)) {
+    set_error("bnn_dropout_mask: bad arguments");
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  Drop d = make_drop(p, seed);
+  if (!d.on) d.thresh = 0xFFFFFFFFu, d.scale = 1.f;
+  hipLaunchKernelGGL(dropout_mask_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, d,
+                     out);
+  return check_launch("bnn_dropout_mask");
 }
 
 BNN_API int64_t bnn_bn2d_workspace(int64_t N, int64_t C) {

@@ -189,6 +189,21 @@ int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t 
                  int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                  bnn_stream_t stream);
 
+/* nn.Dropout(p) fused in front of BatchNorm1d (+ Hardtanh) (mnist-dist2.py:69-70: fc3 -> drop ->
+ * bn3): x is the pre-dropout input; the keep mask is a counter-based hash of (seed, row*C + col)
+ * regenerated by every pass (never stored), kept values scaled by 1/(1-p) as torch does; the
+ * backward's dx is the gradient w.r.t. the pre-dropout input.  p in [0, 1).  bnn_dropout_mask
+ * writes the mask the fused passes use (scale or 0 per element, n = M*C) for tests. */
+int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+                             float* running_mean, float* running_var, float momentum, float eps,
+                             float* save_mean, float* save_invstd, float* y, int32_t hardtanh, float p,
+                             uint64_t seed, void* work, bnn_stream_t stream);
+int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                       const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
+                       float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, void* work,
+                       bnn_stream_t stream);
+int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
+
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
  * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = (x-mean)*invstd*gamma+beta exactly as
  * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0

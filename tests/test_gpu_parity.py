@@ -532,3 +532,35 @@ def test_empty_and_single_sample_batches(F, backend):
             ref = torch.nn.functional.conv2d(torch.sign(xr).double().cpu(), torch.sign(conv.weight.org).double().cpu(),
                                              None, padding=2) + conv.bias.detach().double().cpu().view(1, -1, 1, 1)
             assert torch.equal(y.detach().cpu(), ref.float())   # integer sum, then one fp32 bias add
+
+
+@pytest.mark.parametrize("M,C,p", [(1000, 768, 0.3), (64, 12, 0.5)])
+def test_dropout_batchnorm_hardtanh_vs_explicit_mask(F, M, C, p):
+    """Fused Dropout -> BatchNorm1d -> Hardtanh (mnist-dist2.py:69-74) against torch's BatchNorm1d +
+    Hardtanh applied to x * mask, with the mask the fused passes regenerate (bnn_dropout_mask):
+    outputs, running stats and all gradients, and the keep fraction ~ 1 - p."""
+    torch.manual_seed(M + C)
+    x = (torch.randn(M, C, device="cuda") * 3 + torch.randn(C, device="cuda")).requires_grad_(True)
+    bn_a = torch.nn.BatchNorm1d(C).cuda()
+    with torch.no_grad():
+        bn_a.weight.uniform_(0.5, 1.5)
+        bn_a.bias.uniform_(-0.2, 0.2)
+    bn_b = torch.nn.BatchNorm1d(C).cuda()
+    bn_b.load_state_dict(bn_a.state_dict())
+    seed = 123456789 + M
+    y = F.dropout_batch_norm_hardtanh(x, p, bn_a, seed=seed)
+    g = torch.randn_like(y)
+    y.backward(g)
+    mask = F.dropout_mask(M * C, p, seed).view(M, C)
+    keep = (mask > 0).float().mean().item()
+    assert abs(keep - (1 - p)) < 0.02 + 3 / (M * C) ** 0.5
+    assert torch.all((mask == 0) | (mask == torch.tensor(1.0 / (1.0 - p), device="cuda")))
+    xr = x.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.hardtanh(bn_b(xr * mask))
+    yr.backward(g)
+    assert rel_err(host(y), host(yr)) < 1e-5
+    assert rel_err(host(x.grad), host(xr.grad)) < GRAD_TOL
+    assert rel_err(host(bn_a.weight.grad), host(bn_b.weight.grad)) < GRAD_TOL
+    assert rel_err(host(bn_a.bias.grad), host(bn_b.bias.grad)) < GRAD_TOL
+    assert close(host(bn_a.running_mean), host(bn_b.running_mean), 1e-5, 1e-6)
+    assert close(host(bn_a.running_var), host(bn_b.running_var), 1e-5, 1e-6)
