@@ -605,9 +605,11 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
   float* xs = ldsf;                               // [C][Hp][Wp], zero border
   float* dys = xs + ((g.C * g.Hp * g.Wp + 3) & ~3);   // [Co16][Pp], zero padded, 16-B aligned
   int* poff = reinterpret_cast<int*>(dys + g.Co16 * g.Pp);   // [Pp]
+  __shared__ float sbias[64];                     // per-channel dB of this workgroup's samples
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int grp = wv % g.WT, ks = wv / g.WT;
   const int KK = g.KH * g.KW;
+  if (t < 64) sbias[t] = 0.f;
   for (int i = t; i < g.C * g.Hp * g.Wp; i += MF_T) xs[i] = 0.f;
   for (int i = t; i < g.Co16 * g.Pp; i += MF_T) dys[i] = 0.f;
   for (int p = t; p < g.Pp; p += MF_T) {
@@ -678,12 +680,17 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_filter_mfma_k(const float* __re
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = mfma16x4(av[m], bv[m], acc[m]);
     }
-    if (with_bias && t < g.Co) {
-      float sb = 0.f;
-      for (int p = 0; p < g.P; ++p) sb += dys[t * g.Pp + p];
-      bacc += sb;
+    if (with_bias) {   // dB: wave w sums channels w, w+4, ... across its 64 lanes (not one serial lane)
+      for (int co = wv; co < g.Co; co += 4) {
+        float sb = 0.f;
+        for (int p = lane; p < g.P; p += 64) sb += dys[co * g.Pp + p];
+        const double tot = wave_sum((double)sb);
+        if (lane == 0) sbias[co] += (float)tot;
+      }
     }
   }
+  __syncthreads();
+  if (t < g.Co) bacc = sbias[t];
   const int64_t nelem = (int64_t)g.Co * g.ncombo + g.Co;
   float* row = part + ((int64_t)blockIdx.x * g.KS + ks) * nelem;
 #pragma unroll
@@ -837,7 +844,7 @@ inline bool mf_data_geom(const ConvShape& s, MfData* g, int64_t* lds) {
 }
 
 inline bool mf_filt_geom(const ConvShape& s, MfFilt* g, int64_t* lds) {
-  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1)) return false;
+  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.Co <= 64)) return false;
   MfFilt d;
   d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
   d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
