@@ -285,8 +285,6 @@ class BinaryLinearFunction(torch.autograd.Function):
             y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b, k_true=K)
             ctx.save_for_backward(x if need_dw else None, wqt)
         ctx.binarize_input = binarize_input
-        ctx.dims = (M, K, N)
-        ctx.has_bias = bias is not None
         return y
 
     @staticmethod

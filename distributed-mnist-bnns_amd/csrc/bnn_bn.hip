@@ -723,7 +723,10 @@ BNN_API int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, void
   }
   if (n == 0) return 0;
   Drop d = make_drop(p, seed);
-  if (!d.on) d.thresh = 0xFFFFFFFFu, d.scale = 1.f;
+  if (!d.on) {   // p == 0: every element kept
+    d.thresh = 0xFFFFFFFFu;
+    d.scale = 1.f;
+  }
   hipLaunchKernelGGL(dropout_mask_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, d,
                      out);
   return check_launch("bnn_dropout_mask");
