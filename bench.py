@@ -2,24 +2,35 @@
 """Training-step benchmark of the binarized-network hot path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config wide|mlp|cnn|small] [--batch B]
+                    [--exchange]
 
 N > 1 is launched by the driver as one process per GPU (torch.distributed.run, RCCL).
 A "step" = one training step of the reference loop (mnist-dist2.py:118-137) on one batch of
-synthetic MNIST-shaped input resident in HBM: forward through the libbnn layers (torch BatchNorm
-/ Hardtanh / Dropout / LogSoftmax in between, as the reference's Net), CrossEntropy, backward
-(libbnn STE GEMMs), bucketed RCCL gradient all-reduce overlapped with backward (N > 1), and the
-fused latent Adam + clamp update.  Per-GPU batch is fixed (weak scaling).
+synthetic MNIST-shaped input resident in HBM: forward through the libbnn layers (fused
+BatchNorm+Hardtanh, BN -> sign-pack -> FP4 GEMM between the binarized layers), CrossEntropy,
+backward (libbnn STE GEMMs), the bucketed RCCL gradient all-reduce overlapped with backward
+(N > 1, or --exchange at N = 1), and the fused latent Adam + clamp + weight re-pack.  Per-GPU
+batch is fixed (weak scaling).
 
 Default workload = BASELINE config 5 (the one the metric's 1/2/4/8-GPU curve is quoted on):
 wide binarized MLP 784-8192x3-10, batch 65536 per GPU.
 
-Prints ONE JSON line (rank 0) with the contract fields plus ``roofline`` (dominant libbnn
-kernel, HIP-event timed on its stream inside the timed region) and ``cpu_baseline`` (the
-oracle's torch-CPU restatement of the reference path on this box's host cores, N=1 only).
+Timing: W untimed warmup steps, then K steps between barrier + synchronize on both sides with
+NO per-kernel instrumentation (``value``); the max over ranks.  Afterwards (outside the timed
+region) a few instrumented steps time every libbnn launch with HIP events on its stream for the
+``roofline`` object, whose ``achieved`` is ALGORITHMIC work (2*M*N*K ops per GEMM launch,
+SURVEY §8(d); the digit passes that emulate fp32 operands on the int8 MFMA are not work) or
+algorithmic bytes (HBM-bound kernels) per launch over the average launch time.
+
+Prints ONE JSON line (rank 0) with the contract fields plus ``roofline``, ``cpu_baseline`` (the
+oracle's torch-CPU restatement of the reference path on this box's host cores, N = 1 only:
+the bench config itself, plus BASELINE configs 1 and 2) and ``gpu_torch_fp32`` (the same
+restatement run on this GPU with torch's fp32 kernels: the naive-GPU comparator).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -29,28 +40,44 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-mnist-bnns_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+# Dense MFMA peaks of MI355X (MI355X_MICROARCH.md § Matrix cores; 256 CUs x 4 SIMDs x 2.4 GHz):
 MI355X_INT8_DENSE_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12   # 32x32x32 i8 MFMA: 2048 ops/clk/SIMD
+MI355X_FP4_DENSE_TOPS = 256 * 4 * 4096 * 2.4e9 / 1e12    # 32x32x64 f8f6f4 MFMA (FP4/FP6): 4096 ops/clk/SIMD
+MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
+MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
 MI355X_HBM_GBS = 8000.0
 
 CONFIGS = {
-    # name: (model factory kwargs, default per-GPU batch, description)
+    # name: (model key, default per-GPU batch, description)
     "wide": ("wide", 65536, "wide binarized MLP 784-8192x3-10 (BASELINE config 5)"),
     "mlp": ("mlp", 4096, "binarized MLP 784-3072-1536-768-10 (mnist-dist2 Net, BASELINE config 3)"),
-    "small": ("small", 4096, "binarized MLP 784-192x3-10 (mnist-dist3 Net)"),
+    "small": ("small", 64, "binarized MLP 784-192x3-10 (mnist-dist3 Net: the published CSV config, batch 64)"),
     "cnn": ("cnn", 4096, "binarized CNN conv5(1-16)-conv5(16-32)-fc (BASELINE config 4)"),
 }
 CPU_WIDTHS = {"wide": (8192, 8192, 8192), "mlp": (3072, 1536, 768), "small": (192, 192, 192), "cnn": "cnn"}
-MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
-MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
+CPU_BATCH = {"wide": 512, "mlp": 1024, "small": 64, "cnn": 256}
+
+
+def digit_pairs(kernel):
+    """int8 MFMA passes per algorithmic MAC of a GEMM kernel instance (fp32 operands enter as 3
+    int8 digit planes: (3,1) = 3 passes, (3,3) = 6)."""
+    for tag, n in (("<3, 3,", 6), ("<3, 1,", 3)):
+        if tag in kernel:
+            return n
+    return 1
 
 
 def op_peak(kernel):
-    """(bound, peak TFLOP/s or TOPS, unit of the count) of an ops-counted kernel."""
+    """(bound, dense peak TOPS, what is counted) of an ops-counted kernel."""
     if kernel.startswith("conv2d_bwd"):
         return "mfma", MI355X_F32_MFMA_TFLOPS, "f32 MFMA flops (2*N*Co*OH*OW*C*KH*KW)"
     if kernel.startswith("conv2d_fwd"):   # C=1 layer on VALU dot4; C%16==0 layers on int8 MFMA (looser bound)
         return "valu", MI355X_DOT4_TOPS, "int8 dot4 / MFMA ops (2*N*Co*OH*OW*C*KH*KW)"
-    return "mfma", MI355X_INT8_DENSE_TOPS, "int8 MFMA ops (2*M*N*K*digit_pairs)"
+    if kernel.startswith("gemm_fp4"):
+        return "mfma", MI355X_FP4_DENSE_TOPS, "ternary GEMM ops 2*M*N*K on the FP4 MFMA"
+    if kernel.startswith("gemm_xnor"):   # SURVEY §8(d): VALU popcount bound with the nonzero-mask plane
+        return "valu", 840.0, "ternary popcount ops 2*M*N*K"
+    return "mfma", MI355X_INT8_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the int8 MFMA"
 
 
 def parse():
@@ -63,9 +90,13 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--backend", default="fp4", choices=["fp4", "mfma", "xnor"])
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the gradient-exchange bucket path at N=1 too (flat buckets, hooks)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work per config")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-gpu-torch", action="store_true", help="skip the torch-fp32-on-GPU comparator")
+    ap.add_argument("--timing-steps", type=int, default=3, help="instrumented steps for the roofline")
     return ap.parse_args()
 
 
@@ -79,19 +110,54 @@ def build(cfg, backend):
     return model
 
 
-def cpu_baseline(cfg, budget):
+def host_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+
+
+def cpu_baselines(cfg, budget):
+    """Reference semantics timed on this box's host cores (runs BEFORE this process touches the
+    GPU).  Returns (entry for the bench config, list of entries for BASELINE configs 1 and 2)."""
     sys.path.insert(0, ROOT)
     from oracle import bnn_torch
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = host_threads()
+    main = None
     widths = CPU_WIDTHS.get(cfg)
-    if widths is None:
-        return None
-    batch = 512 if cfg == "wide" else (256 if cfg == "cnn" else 1024)
+    batch = CPU_BATCH[cfg]
     sps, steps, secs = bnn_torch.time_training(widths, batch, threads, budget_s=budget, max_steps=100000)
-    return {"value": round(sps, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} fp32 torch-CPU train steps (oracle/bnn_torch.py restatement of the "
-                      f"reference path, .org protocol + Adam) of the same net at batch {batch}, "
-                      f"{secs:.1f} s"}
+    main = {"value": round(sps, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} fp32 torch-CPU train steps (oracle/bnn_torch.py restatement of the reference "
+                      f"path: .org protocol + Adam) of the same net at batch {batch}, {secs:.1f} s"}
+    extra = []
+    sps, steps, secs = bnn_torch.time_training((3072, 1536, 768), 100, threads, budget_s=budget, max_steps=100000)
+    extra.append({"config": "BASELINE config 1: MLP 784-3072-1536-768-10, batch 100, 1 process, CPU",
+                  "value": round(sps, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+                  "sample": f"{steps} steps, {secs:.1f} s"})
+    per_rank = max(1, threads // 2)
+    try:
+        out = subprocess.run([sys.executable, "-m", "oracle.bnn_torch", "gloo", "3072", "1536", "768", "100", "2",
+                              str(per_rank), str(budget)], cwd=ROOT, capture_output=True, text=True,
+                             timeout=300, check=True)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        extra.append({"config": "BASELINE config 2: same MLP, gloo DDP world_size 2 on CPU, batch 100 per rank",
+                      "value": round(r["samples_per_s"], 2), "unit": "samples/s (both ranks)",
+                      "cores": 2 * per_rank, "kind": "port",
+                      "sample": f"{r['steps']} steps, {r['seconds']:.1f} s, {per_rank} threads per rank"})
+    except (subprocess.SubprocessError, ValueError, IndexError, KeyError) as e:
+        extra.append({"config": "BASELINE config 2", "error": repr(e)[:200]})
+    return main, extra
+
+
+def gpu_torch_baseline(cfg, batch, budget=4.0):
+    """The reference semantics (oracle/bnn_torch.py: sign() + torch fp32 F.linear / F.conv2d,
+    BatchNorm, Adam, .org protocol) run with GPU tensors: what the reference would do on this
+    GPU without libbnn."""
+    sys.path.insert(0, ROOT)
+    from oracle import bnn_torch
+    widths = CPU_WIDTHS.get(cfg)
+    sps, steps, secs = bnn_torch.time_training(widths, batch, 1, budget_s=budget, max_steps=1000, device="cuda")
+    torch.cuda.empty_cache()
+    return {"value": round(sps, 2), "unit": "samples/s", "kind": "reference semantics, torch fp32 on this GPU",
+            "sample": f"{steps} steps at batch {batch}, {secs:.1f} s"}
 
 
 def pmc_traffic(kernel):
@@ -112,6 +178,30 @@ def pmc_traffic(kernel):
     return None, None
 
 
+def roofline_of(ksum, steps):
+    dom = max(ksum, key=lambda k: ksum[k]["ms"])
+    d = ksum[dom]
+    common = {"kernel": dom, "launches_per_step": d["launches"] / steps, "avg_us": round(d["avg_ms"] * 1e3, 1)}
+    if d["avg_ops"] > 0:
+        ach = d["avg_ops"] / (d["avg_ms"] * 1e-3) / 1e12
+        bound, peak, ops_unit = op_peak(dom)
+        r = {"bound": "mfma" if bound == "mfma" else bound, "achieved": round(ach, 2), "peak": round(peak, 1),
+             "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None, **common, "ops_unit": ops_unit}
+        pairs = digit_pairs(dom)
+        if pairs > 1:   # the int8 passes the fp32-operand emulation issues (secondary, not the work)
+            r["int8_pass_rate_tops"] = round(ach * pairs, 2)
+            r["int8_pass_frac"] = round(ach * pairs / peak, 4)
+    else:
+        ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
+        r = {"bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
+             "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": None, **common}
+    traffic, src = pmc_traffic(dom)
+    r["traffic"] = traffic
+    r["traffic_source"] = src
+    r["algorithmic_bytes_per_launch"] = int(d["avg_bytes"])
+    return r
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,10 +209,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    cpu_main, cpu_extra = None, []
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_main, cpu_extra = cpu_baselines(args.config, args.cpu_budget)   # before any GPU work
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    use_exchange = world > 1 or args.exchange
+    if use_exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     from bnn_amd import functional as BF
     from bnn_amd.data import synthetic_mnist
@@ -133,7 +229,7 @@ def main():
     batch = args.batch or CONFIGS[args.config][1]
     torch.manual_seed(0)
     model = build(args.config, args.backend).to(dev).train()
-    exchange = GradExchange(model, bucket_mb=args.bucket_mb) if world > 1 else None
+    exchange = GradExchange(model, bucket_mb=args.bucket_mb) if use_exchange else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model))
     x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev)
     crit = torch.nn.CrossEntropyLoss()
@@ -153,18 +249,15 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if use_exchange:
         dist.barrier()
     torch.cuda.synchronize()
 
-    timer = BF.KernelTimer()
-    ctx = BF.timing(timer) if not args.no_kernel_timing else BF.timing(None)
     t0 = time.perf_counter()
-    with ctx:
-        for _ in range(args.steps):
-            loss = step()
+    for _ in range(args.steps):
+        loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_exchange:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -173,23 +266,15 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.item())
 
-    ksum = timer.summary() if not args.no_kernel_timing else {}
-    roofline = None
-    if ksum:
-        dom = max(ksum, key=lambda k: ksum[k]["ms"])
-        d = ksum[dom]
-        if d["avg_ops"] > 0:
-            ach = d["avg_ops"] / (d["avg_ms"] * 1e-3) / 1e12
-            bound, peak, ops_unit = op_peak(dom)
-            roofline = {"bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1),
-                        "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-                        "kernel": dom, "launches_per_step": d["launches"] / args.steps,
-                        "avg_us": round(d["avg_ms"] * 1e3, 1), "ops_unit": ops_unit}
-        else:
-            ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": None, "kernel": dom,
-                        "launches_per_step": d["launches"] / args.steps, "avg_us": round(d["avg_ms"] * 1e3, 1)}
+    # instrumented steps (outside the timed region): per-launch HIP events -> roofline
+    ksum, tsteps = {}, 0
+    if not args.no_kernel_timing and args.timing_steps > 0:
+        timer = BF.KernelTimer()
+        with BF.timing(timer):
+            for _ in range(args.timing_steps):
+                step()
+        tsteps = args.timing_steps
+        ksum = timer.summary()
 
     ms = elapsed / args.steps * 1e3
     samples = batch * world * args.steps
@@ -204,36 +289,43 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp4/int8 MFMA (ternary operands as FP4 e2m1 / int8, fp32 digit planes as int8; exact integer sums; fp32 I/O)",
+        "dtype": "fp4/int8 MFMA (ternary operands as FP4 e2m1 / int8, fp32 operands as int8 digit planes; "
+                 "exact integer sums; fp32 I/O)",
         "data": "synthetic MNIST-shaped (80.7% zero pixels, u8/255), random-init weights, resident in HBM",
         "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
-                   "backend": args.backend, "loss_last_step": round(final_loss, 5)},
+                   "backend": args.backend, "exchange": bool(use_exchange), "loss_last_step": round(final_loss, 5)},
     }
     if ksum:
-        # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (logical 2MNK)
-        # ternary GEMM forms, and the binary convolutions' forward (im2col-free) for the CNN
-        fwd = [v for k, v in ksum.items() if (k.startswith("gemm_i8") and "<1, 1," in k) or k == "conv2d_fwd"]
+        # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (2*M*N*K) and the
+        # binary convolutions' forward for the CNN
+        fwd = [v for k, v in ksum.items()
+               if k.startswith("gemm_fp4") or (k.startswith("gemm_i8") and "<1, 1," in k) or k == "conv2d_fwd"
+               or k == "gemm_xnor_k"]
         if fwd:
             ops, ms_ = sum(v["ops"] for v in fwd), sum(v["ms"] for v in fwd)
             result["binary_gemm_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)
-        result["kernels"] = {k: {"launches": v["launches"], "avg_us": round(v["avg_ms"] * 1e3, 1),
-                                 "share": round(v["ms"] / (elapsed * 1e3), 4)} for k, v in ksum.items()}
-    if roofline is not None:
-        traffic, src = pmc_traffic(roofline["kernel"])
-        roofline["traffic"] = traffic
-        roofline["traffic_source"] = src
-        if traffic and d.get("avg_bytes"):
-            roofline["algorithmic_bytes"] = int(d["avg_bytes"])
-    result["roofline"] = roofline
-    result["cpu_baseline"] = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
-        if result["cpu_baseline"]:
-            result["speedup_vs_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        step_ms = sum(v["ms"] for v in ksum.values()) / tsteps
+        result["kernels"] = {k: {"launches_per_step": v["launches"] / tsteps, "avg_us": round(v["avg_ms"] * 1e3, 1),
+                                 "share_of_step": round(v["ms"] / tsteps / ms, 4)}
+                             for k, v in sorted(ksum.items(), key=lambda kv: -kv[1]["ms"])}
+        result["libbnn_kernel_ms_per_step"] = round(step_ms, 3)
+        result["roofline"] = roofline_of(ksum, tsteps)
+    else:
+        result["roofline"] = None
+    result["cpu_baseline"] = cpu_main
+    if cpu_main:
+        result["cpu_baselines_other"] = cpu_extra
+        result["speedup_vs_cpu"] = round(result["value"] / cpu_main["value"], 1)
+    if rank == 0 and world == 1 and not args.no_gpu_torch and args.config in CPU_WIDTHS:
+        try:
+            gb = min(batch, 16384) if args.config == "wide" else batch
+            result["gpu_torch_fp32"] = gpu_torch_baseline(args.config, gb)
+        except RuntimeError as e:        # e.g. out of memory: report, never fail the bench line
+            result["gpu_torch_fp32"] = {"error": repr(e)[:200]}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_exchange:
         dist.destroy_process_group()
 
 

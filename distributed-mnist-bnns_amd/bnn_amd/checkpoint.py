@@ -22,6 +22,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from . import functional as BF
 from .nn import BinarizeConv2d, BinarizeLinear
 
 FORMAT = "bnn_amd.checkpoint/1"
@@ -75,6 +76,8 @@ def load_checkpoint(path, model, optimizer=None, map_location=None):
     if blob.get("format") != FORMAT:
         raise ValueError(f"{path}: not a {FORMAT} checkpoint (format={blob.get('format')!r})")
     model.load_state_dict(blob["model"])
+    for prm in model.parameters():
+        BF.invalidate_packed(prm)
     latent = set(blob["latent"])
     for name, m in _binary_modules(model):
         key = f"{name}.weight" if name else "weight"

@@ -19,7 +19,8 @@ from . import _lib as L
 
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
-    "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "batch_norm_hardtanh",
+    "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "adam_clamp_pack_", "packed_weight",
+    "invalidate_packed", "batch_norm_hardtanh",
     "bn_hardtanh_binary_linear", "batch_norm2d_hardtanh_pool", "dropout_batch_norm_hardtanh", "dropout_mask",
     "BinaryLinearFunction", "BinaryConv2dFunction",
 ]
@@ -193,6 +194,64 @@ def quant_cols_t(x, want_colsum=False):
     return dg, sc, cs
 
 
+# ----------------------------------------------------------------------------- packed latent weights
+# The next forward's ternary weight operands, cached on the latent-weight Parameter of a layer
+# that keeps its latent weight in the Parameter (``org_protocol = False``).  The fused latent
+# update (``optim.LatentAdam`` -> bnn_adam_clamp_pack) rewrites them in place in the same pass
+# that updates the weight, so no forward re-packs the weight.  The cache is keyed
+# on (data_ptr, _version): torch in-place ops and load_state_dict bump the version; raw writes
+# through ``p.data`` do not -- code doing those calls ``invalidate_packed(p)``.
+def _pack_key(w):
+    return (w.data_ptr(), w._version)
+
+
+def invalidate_packed(w):
+    if hasattr(w, "_bnn_pack"):
+        del w._bnn_pack
+
+
+def packed_weight(weight, fmt, want_q, want_qt, cache=True):
+    """(q, qt) of sign(weight) [N,K]: q = FP4 rows (fmt "fp4") or int8 rows (fmt "i8"), qt = int8
+    transpose [K, round_up(N)].  With ``cache`` the operands are kept on the Parameter."""
+    ent = getattr(weight, "_bnn_pack", None) if cache else None
+    if ent is not None and ent["key"] == _pack_key(weight) and ent["fmt"] == fmt \
+            and (ent["q"] is not None or not want_q) and (ent["qt"] is not None or not want_qt):
+        return ent["q"], ent["qt"]
+    if ent is not None and ent["fmt"] == fmt:      # keep producing what earlier forwards needed
+        want_q = want_q or ent["q"] is not None
+        want_qt = want_qt or ent["qt"] is not None
+    if fmt == "fp4":
+        q, qt = sign_pack_fp4(weight, want_qt=want_qt) if want_q else sign_pack(weight, False, True)
+    else:
+        q, qt = sign_pack(weight, want_q=want_q, want_qt=want_qt)
+    if cache:
+        weight._bnn_pack = {"key": _pack_key(weight), "fmt": fmt, "q": q, "qt": qt}
+    return q, qt
+
+
+def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
+                     grad_scale=1.0, clamp=True):
+    """bnn_adam_clamp on a 2-D latent weight that also rewrites its cached packed operands (see
+    packed_weight).  Returns False (nothing done) when ``p`` has no valid cache."""
+    ent = getattr(p, "_bnn_pack", None)
+    if ent is None or ent["key"] != _pack_key(p) or p.dim() != 2:
+        return False
+    _check(p, grad, exp_avg, exp_avg_sq)
+    for t in (p, grad, exp_avg, exp_avg_sq):
+        if not t.is_contiguous():
+            raise ValueError("adam_clamp_pack_: tensors must be contiguous")
+    N, K = p.shape
+    q, qt = ent["q"], ent["qt"]
+    nbytes = 28 * N * K + (q.numel() if q is not None else 0) + (qt.numel() if qt is not None else 0)
+    with _timed("sign_pack_tile_k<adam>", 0, nbytes):
+        L.call("bnn_adam_clamp_pack", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
+               float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale), int(bool(clamp)),
+               1 if ent["fmt"] == "fp4" else 0, L.ptr(q), q.shape[1] if q is not None else 0,
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    ent["key"] = _pack_key(p)
+    return True
+
+
 # ----------------------------------------------------------------------------- (2) GEMMs
 def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=None, out=None,
             k_true=None):
@@ -213,9 +272,8 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
         if bias is not None:
             C += bias
         return C
-    cfg = (a_digits, b_digits)
     k_true = K if k_true is None else k_true
-    ops = 2.0 * M * N * k_true * GEMM_PAIRS[cfg]
+    ops = 2.0 * M * N * k_true          # algorithmic work; digit passes are not work
     name = gemm_kernel_name(a_digits, b_digits, M, N, K) if _TIMER is not None else ""
     with _timed(name, ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
         L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
@@ -255,7 +313,7 @@ class BinaryLinearFunction(torch.autograd.Function):
     """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, binarize_input, backend="fp4"):
+    def forward(ctx, x, weight, bias, binarize_input, backend="fp4", cache=False):
         _check(x, weight, bias)
         M, K = x.shape
         N = weight.shape[0]
@@ -266,21 +324,23 @@ class BinaryLinearFunction(torch.autograd.Function):
             return torch.empty((0, N), dtype=torch.float32, device=x.device)
         ctx.empty = False
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dx)
         b = bias.detach() if bias is not None else None
         if binarize_input:
             if backend == "fp4":
                 x4, xqt = sign_pack_fp4(x, want_qt=need_dw)
-                w4, _ = sign_pack_fp4(weight)
+                w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache)
                 y = gemm_fp4(x4, w4, M, N, bias=b, k_true=K)
             elif backend == "xnor":
                 y = gemm_xnor(sign_pack_bits(x), sign_pack_bits(weight), M, N, bias=b)
                 xqt = sign_pack(x, want_q=False, want_qt=True)[1] if need_dw else None
+                wqt = packed_weight(weight, "i8", False, need_dx, cache)[1] if need_dx else None
             else:
                 xq, xqt = sign_pack(x, want_q=True, want_qt=need_dw)
+                wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
                 y = gemm_i8(xq, 1, wq, 1, M, N, bias=b, k_true=K)
             ctx.save_for_backward(xqt, wqt)
         else:
+            wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
             xd, sx = quant_rows(x)
             y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b, k_true=K)
             ctx.save_for_backward(x if need_dw else None, wqt)
@@ -295,7 +355,7 @@ class BinaryLinearFunction(torch.autograd.Function):
             return (torch.empty((0, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None,
                     torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
                     torch.zeros((N,), dtype=torch.float32, device=dev)
-                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None)
+                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None)
         xs, wqt = ctx.saved_tensors
         dy = _c2d(dy)
         dx = dw = db = None
@@ -312,13 +372,14 @@ class BinaryLinearFunction(torch.autograd.Function):
                     xt, sxc, _ = quant_cols_t(xs)
                     dw = gemm_i8(dt, 3, xt, 3, N, K, a_scale=sc, b_scale=sxc, k_true=M)
             db = cs
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4"):
-    """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened)."""
+def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4", cache=False):
+    """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened).  ``cache``: the
+    weight is a latent weight whose packed operands are cached on it (packed_weight)."""
     lead = x.shape[:-1]
-    y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend)
+    y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend, cache)
     return y.reshape(*lead, weight.shape[0])
 
 
@@ -411,6 +472,7 @@ def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, 
                 grad_scale=1.0, clamp=True):
     """In-place fused Adam (torch formula) + clamp to [-1, 1] on a latent weight."""
     _check(p, grad, exp_avg, exp_avg_sq)
+    invalidate_packed(p)        # a raw in-place write: cached packed operands would go stale
     for t in (p, grad, exp_avg, exp_avg_sq):
         if not t.is_contiguous():
             raise ValueError("adam_clamp_: tensors must be contiguous")
@@ -452,6 +514,7 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
                        L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
         ctx.save_for_backward(x, w, b, mean, invstd)
         ctx.hardtanh = hardtanh
+        ctx.training = training
         return y
 
     @staticmethod
@@ -463,8 +526,9 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
         dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
         db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
         ws = _bn_ws(M, C, x.device)
+        # eval mode: the running statistics are constants (dx = gamma*invstd*g)
         with _timed("bn_bwd", 0, 16 * M * C):
-            L.call("bnn_bn_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+            L.call("bnn_bn_bwd" if ctx.training else "bnn_bn_bwd_eval", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                    int(ctx.hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None)
@@ -583,6 +647,7 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
                        L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
         ctx.save_for_backward(x, w, b, mean, invstd)
         ctx.hardtanh, ctx.pool = hardtanh, pool
+        ctx.training = training
         return y
 
     @staticmethod
@@ -596,7 +661,7 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
         ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=x.device)
         nel = N * C * H * W
         with _timed("bn2d_bwd", 0, 12 * nel + 8 * dy.numel()):
-            L.call("bnn_bn2d_bwd", L.ptr(x), L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(mean),
+            L.call("bnn_bn2d_bwd" if ctx.training else "bnn_bn2d_bwd_eval", L.ptr(x), L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(mean),
                    L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
                    L.stream())
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
@@ -656,14 +721,13 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                    1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
                    L.stream())
         b = bias.detach() if bias is not None else None
+        wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True)
         if fp4:
-            w4, _ = sign_pack_fp4(weight)
-            wqt = sign_pack(weight, want_q=False, want_qt=True)[1] if need_dh else None
-            y = gemm_fp4(q, w4, M, N, bias=b, k_true=C)
+            y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
-            wq, wqt = sign_pack(weight, want_q=True, want_qt=need_dh)
             y = gemm_i8(q, 1, wq, 1, M, N, bias=b, k_true=C)
         ctx.save_for_backward(z, gw, gb, mean, invstd, qt, wqt)
+        ctx.training = training
         ctx.dims = (M, C, N)
         ctx.has_bias = bias is not None
         return y
@@ -688,7 +752,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None
             ws = _bn_ws(M, C, z.device)
             with _timed("bn_bwd", 0, 16 * M * C):
-                L.call("bnn_bn_bwd", L.ptr(z), L.ptr(dh), M, C, L.ptr(gw), L.ptr(gb), L.ptr(mean),
+                L.call("bnn_bn_bwd" if ctx.training else "bnn_bn_bwd_eval", L.ptr(z), L.ptr(dh), M, C, L.ptr(gw), L.ptr(gb), L.ptr(mean),
                        L.ptr(invstd), 1, L.ptr(dz), L.ptr(dgw), L.ptr(dgb), L.ptr(ws), L.stream())
         return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, dw, db, None)

@@ -48,7 +48,9 @@ class HingeLoss(nn.Module):
         self.margin = 1.0
 
     def hinge_loss(self, input, target):
-        return torch.clamp(self.margin - input * target, min=0.0).mean()
+        # output[output.le(0)] = 0 (:27-29): relu zeroes the gradient where margin - x*t <= 0,
+        # ties included, and keeps NaN, as the masked assignment does
+        return torch.relu(self.margin - input * target).mean()
 
     def forward(self, input, target):
         return self.hinge_loss(input, target)
@@ -97,7 +99,8 @@ class BinarizeLinear(nn.Linear):
             _apply_org_protocol(self.weight)                    # :77-79
             if self.bias is not None:
                 self.bias.org = self.bias.data.clone()          # :82
-        return BF.binary_linear(input, self.weight, self.bias, binarize, self.backend)
+        return BF.binary_linear(input, self.weight, self.bias, binarize, self.backend,
+                                cache=not self.org_protocol)
 
 
 class BinarizeConv2d(nn.Conv2d):

@@ -12,7 +12,9 @@ The reference's protocol around ``torch.optim.Adam`` (mnist-dist2.py:91, :131-13
 ``LatentAdam`` is the fused form for models whose Parameters hold the latent weights directly
 (``org_protocol = False``): one libbnn kernel per tensor does Adam (torch's formula) and the clamp
 of the parameters the reference clamps, with an optional gradient scale (1/world_size when the
-gradient exchange summed instead of averaged).
+gradient exchange summed instead of averaged).  For a binarized layer's weight the same kernel
+also rewrites the next forward's packed ternary operands (bnn_adam_clamp_pack), replacing the
+per-forward sign-pack of the weight.
 """
 import torch
 
@@ -56,6 +58,10 @@ class LatentAdam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                BF.adam_clamp_(p.data, g, st["exp_avg"], st["exp_avg_sq"], st["step"], group["lr"],
-                               b1, b2, group["eps"], self.grad_scale, id(p) in self._clamp)
+                args = (g, st["exp_avg"], st["exp_avg_sq"], st["step"], group["lr"], b1, b2, group["eps"],
+                        self.grad_scale, id(p) in self._clamp)
+                # a binarized layer's weight also gets its next-forward ternary operands rewritten in
+                # the same pass (bnn_adam_clamp_pack); anything else: plain fused Adam + clamp
+                if not BF.adam_clamp_pack_(p, *args):
+                    BF.adam_clamp_(p, *args)
         return loss

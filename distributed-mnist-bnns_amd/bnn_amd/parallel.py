@@ -10,27 +10,45 @@ contract as DDP there:
   (DDP ``broadcast_buffers=True``); batch statistics themselves stay per rank (no SyncBN);
 * gradients are averaged across ranks, bucketed and overlapped with backward.
 
-MI355X design: every gradient lives inside a flat per-bucket buffer (``p.grad`` is a view, so
-there is no copy in or out); buckets follow reverse registration order (the order autograd
-produces gradients) and are capped at ``bucket_mb`` (64 MB default: xGMI rings are per-link
-bound, fewer larger collectives amortise launch cost while still overlapping); a
-post-accumulate-grad hook launches the bucket's async all-reduce on the process group's own
-stream as soon as its last gradient lands, strictly in bucket order on every rank.
-``finish()`` joins them before the optimizer.  With RCCL the reduction is ``ReduceOp.AVG``;
-gloo (CPU tests) has no AVG, so it sums and divides.
+MI355X design:
+
+* every gradient lives inside ONE flat buffer per (dtype, device) -- ``p.grad`` is a view, so
+  there is no copy in or out and zeroing is one memset;
+* buckets are contiguous slices of that buffer in reverse registration order (the order
+  autograd produces gradients), at most ``bucket_mb`` each (64 MB default: xGMI rings are
+  per-link bound, so fewer large collectives amortise launch cost while still overlapping);
+  a gradient larger than the cap (the wide MLP's 268 MB fc2 / fc3 weights) is split into
+  equal slices of at most the cap (SURVEY §5);
+* a post-accumulate-grad hook launches each bucket's async all-reduce on the process group's
+  own stream as soon as every gradient overlapping it has landed, strictly in bucket order on
+  every rank; ``finish()`` joins them before the optimizer.  With RCCL the reduction is
+  ``ReduceOp.AVG``; gloo (CPU tests) has no AVG, so it sums and divides;
+* DDP's per-forward buffer broadcast is ONE collective per device over a flat byte staging
+  buffer (not one per running_mean / running_var / num_batches_tracked).
 """
+import math
+
 import torch
 import torch.distributed as dist
 
+from . import functional as BF
+
+_ALIGN_BYTES = 256
+
 
 class _Bucket:
-    __slots__ = ("params", "flat", "pending", "work")
+    __slots__ = ("flat", "start", "end", "pending", "nparams", "work")
 
-    def __init__(self, params, flat):
-        self.params = params
+    def __init__(self, flat, start, end, nparams):
         self.flat = flat
-        self.pending = len(params)
+        self.start = start
+        self.end = end
+        self.nparams = nparams
+        self.pending = nparams
         self.work = None
+
+    def view(self):
+        return self.flat[self.start:self.end]
 
 
 class GradExchange:
@@ -44,91 +62,148 @@ class GradExchange:
         self.broadcast_buffers = broadcast_buffers
         self.use_avg = dist.get_backend(process_group) == "nccl"
         params = [p for p in module.parameters() if p.requires_grad]
+        self._flat_buffers = self._coalesce_buffers(module)
         if init_broadcast:
-            self._broadcast([p.data for p in params] + [b for b in module.buffers()])
-        self.buckets = self._build_buckets(list(reversed(params)), int(bucket_mb * 2 ** 20))
+            for p in params:
+                dist.broadcast(p.data, src=0, group=self.pg)
+                BF.invalidate_packed(p)     # written through .data: cached packed operands are stale
+            self.sync_buffers()
+        self.cap_bytes = max(1, int(bucket_mb * 2 ** 20))
+        self.buckets, self._param_buckets, self._flats = self._build_buckets(list(reversed(params)))
         self._next = 0
         self._handles = []
-        for bi, b in enumerate(self.buckets):
-            for p in b.params:
-                self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
+        for p in params:
+            self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(self._param_buckets[p])))
         if broadcast_buffers:
             self._handles.append(module.register_forward_pre_hook(lambda m, inp: self.sync_buffers()))
 
     # -------------------------------------------------------------- setup
-    def _build_buckets(self, params, cap_bytes):
-        buckets, cur, size = [], [], 0
-        for p in params:
-            nbytes = p.numel() * p.element_size()
-            if cur and (size + nbytes > cap_bytes or p.dtype != cur[0].dtype or p.device != cur[0].device):
-                buckets.append(cur)
-                cur, size = [], 0
-            cur.append(p)
-            size += nbytes
-        if cur:
-            buckets.append(cur)
-        out = []
-        for plist in buckets:
-            n = sum(p.numel() for p in plist)
-            flat = torch.zeros(n, dtype=plist[0].dtype, device=plist[0].device)
-            off = 0
-            for p in plist:
-                p.grad = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-            out.append(_Bucket(plist, flat))
-        return out
+    @staticmethod
+    def _coalesce_buffers(module):
+        """Staging for the per-forward buffer broadcast: one flat uint8 tensor per device with a
+        typed view per registered buffer.  (The buffers themselves are NOT re-homed as views of
+        it: views share a version counter, and torch's BatchNorm saves its running statistics
+        for backward, so an in-place update of one would invalidate the others.)"""
+        entries = [b for m in module.modules() for b in m._buffers.values() if b is not None]
+        by_dev = {}
+        for b in entries:
+            by_dev.setdefault(b.device, []).append(b)
+        groups = []
+        for device, bufs in by_dev.items():
+            offs, total = [], 0
+            for b in bufs:
+                offs.append(total)
+                total += -(-max(b.numel() * b.element_size(), 1) // _ALIGN_BYTES) * _ALIGN_BYTES
+            flat = torch.zeros(total, dtype=torch.uint8, device=device)
+            by_dtype = {}
+            for b, off in zip(bufs, offs):
+                v = flat[off:off + b.numel() * b.element_size()].view(b.dtype).view(b.shape)
+                src, dst = by_dtype.setdefault(b.dtype, ([], []))
+                src.append(b)
+                dst.append(v)
+            groups.append((flat, list(by_dtype.values())))
+        return groups
 
-    def _broadcast(self, tensors):
-        for t in tensors:
-            dist.broadcast(t, src=0, group=self.pg)
+    def _build_buckets(self, params):
+        """Flat gradient storage per (dtype, device) and the bucket slices over it."""
+        groups = {}
+        for p in params:
+            groups.setdefault((p.dtype, p.device), []).append(p)
+        buckets, param_buckets, flats = [], {}, []
+        for (dtype, device), plist in groups.items():
+            es = torch.empty((), dtype=dtype).element_size()
+            offsets, total = {}, 0
+            for p in plist:
+                offsets[p] = total
+                total += p.numel()
+            flat = torch.zeros(total, dtype=dtype, device=device)
+            flats.append((flat, plist, offsets))
+            cap = max(1, self.cap_bytes // es)
+            cur, cur_start, cur_n = [], 0, 0
+            for p in plist:
+                n, off = p.numel(), offsets[p]
+                if cur and (n > cap or cur_n + n > cap):
+                    self._close(buckets, param_buckets, flat, cur, cur_start, cur_n)
+                    cur, cur_n = [], 0
+                if n > cap:                                 # split into equal slices <= cap
+                    k = math.ceil(n / cap)
+                    step = -(-n // k)
+                    for i in range(k):
+                        a, b = off + i * step, min(off + n, off + (i + 1) * step)
+                        buckets.append(_Bucket(flat, a, b, 1))
+                        param_buckets.setdefault(p, []).append(len(buckets) - 1)
+                    continue
+                if not cur:
+                    cur_start = off
+                cur.append(p)
+                cur_n += n
+            if cur:
+                self._close(buckets, param_buckets, flat, cur, cur_start, cur_n)
+            self._bind(flat, plist, offsets)
+        return buckets, param_buckets, flats
+
+    @staticmethod
+    def _close(buckets, param_buckets, flat, cur, start, n):
+        buckets.append(_Bucket(flat, start, start + n, len(cur)))
+        for q in cur:
+            param_buckets.setdefault(q, []).append(len(buckets) - 1)
+
+    @staticmethod
+    def _bind(flat, plist, offsets):
+        for p in plist:
+            p.grad = flat[offsets[p]:offsets[p] + p.numel()].view_as(p)
 
     # -------------------------------------------------------------- per step
     def sync_buffers(self):
-        if self.world > 1:
-            self._broadcast(list(self.module.buffers()))
+        """DDP broadcast_buffers: rank 0's buffers to every rank -- packed into the staging
+        buffer (one multi-tensor copy per dtype), ONE collective per device, unpacked."""
+        if self.world <= 1:
+            return
+        root = dist.get_rank(self.pg) == 0 if self.pg is not None else dist.get_rank() == 0
+        for flat, lists in self._flat_buffers:
+            if root:
+                for bufs, views in lists:
+                    torch._foreach_copy_(views, bufs)
+            dist.broadcast(flat, src=0, group=self.pg)
+            if not root:
+                for bufs, views in lists:
+                    torch._foreach_copy_(bufs, views)
 
     def zero_grad(self):
-        """Zero every bucket (one memset each) and re-arm the hooks.  Gradients accumulate in
-        place into the bucket views, so they must start at zero, not None (an optimizer's
+        """Zero the flat gradient buffers (one memset each) and re-arm the hooks.  Gradients
+        accumulate in place into the views, so they must start at zero, not None (an optimizer's
         ``zero_grad(set_to_none=True)`` detaches them; they are re-bound here)."""
+        for flat, plist, offsets in self._flats:
+            if not all(self._is_view(p, flat) for p in plist):
+                self._bind(flat, plist, offsets)
+            flat.zero_()
         for b in self.buckets:
-            if not all(self._is_view(p, b) for p in b.params):
-                self._rebind(b)
-            b.flat.zero_()
-            b.pending = len(b.params)
+            b.pending = b.nparams
             b.work = None
         self._next = 0
 
     @staticmethod
-    def _is_view(p, b):
+    def _is_view(p, flat):
         g = p.grad
         if g is None:
             return False
-        start = b.flat.data_ptr()
-        end = start + b.flat.numel() * b.flat.element_size()
+        start = flat.data_ptr()
+        end = start + flat.numel() * flat.element_size()
         return start <= g.data_ptr() < end
 
-    @staticmethod
-    def _rebind(b):
-        off = 0
-        for p in b.params:
-            p.grad = b.flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
-
-    def _make_hook(self, bi):
+    def _make_hook(self, bucket_ids):
         def hook(p):
-            b = self.buckets[bi]
-            b.pending -= 1
-            if b.pending == 0:
-                self._launch_ready()
+            for bi in bucket_ids:
+                self.buckets[bi].pending -= 1
+            self._launch_ready()
         return hook
 
     def _launch_ready(self):
-        while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
             b = self.buckets[self._next]
             if self.world > 1:
                 op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
-                b.work = dist.all_reduce(b.flat, op=op, group=self.pg, async_op=True)
+                b.work = dist.all_reduce(b.view(), op=op, group=self.pg, async_op=True)
             self._next += 1
 
     def finish(self):
@@ -140,7 +215,7 @@ class GradExchange:
             if b.work is not None:
                 b.work.wait()
                 if not self.use_avg:
-                    b.flat.div_(self.world)
+                    b.view().div_(self.world)
                 b.work = None
 
     def remove(self):

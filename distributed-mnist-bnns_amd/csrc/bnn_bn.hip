@@ -281,12 +281,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int hardtanh,
                                                       const float* __restrict__ sg,
-                                                      const float* __restrict__ sgx,
+                                                      const float* __restrict__ sgx, float inv_n,
                                                       float* __restrict__ dx, Drop dp = Drop{0, 0, 0, 1.f}) {
+  // inv_n = 1/M with batch statistics (train); 0 in eval mode, where mean/invstd are the running
+  // statistics (constants): dx = gamma*invstd*g
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
-  const float inv_n = 1.f / (float)M;
   const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
   const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f);
   const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -541,9 +542,10 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_k(const float* __restrict_
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int hardtanh,
                                                         const float* __restrict__ sg,
-                                                        const float* __restrict__ sgx, float* __restrict__ dx) {
+                                                        const float* __restrict__ sgx, float inv_n,
+                                                        float* __restrict__ dx) {
+  // inv_n = 1/(N*H*W) with batch statistics; 0 in eval mode (running statistics: dx = gamma*invstd*g)
   const int64_t HW = (int64_t)H * W;
-  const float inv_n = (float)(1.0 / ((double)N * (double)HW));
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   if (POOL) {
     const int PH = H / 2, PW = W / 2;
@@ -667,7 +669,8 @@ BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* g
 
 static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
-                       float* dx, float* dgamma, float* dbeta, void* work, void* stream, Drop dp) {
+                       float* dx, float* dgamma, float* dbeta, void* work, void* stream, Drop dp,
+                       bool batch_stats) {
   if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work ||
       (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
       !aligned16(save_invstd)) {
@@ -686,7 +689,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
                      dbeta, k0, k1);
   if (dx) {
     hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean,
-                       save_invstd, gamma, beta, hardtanh, k0, k1, dx, dp);
+                       save_invstd, gamma, beta, hardtanh, k0, k1, batch_stats ? 1.f / (float)M : 0.f, dx, dp);
   }
   return check_launch("bnn_bn_bwd");
 }
@@ -695,7 +698,14 @@ BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
                        const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
                        float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
   return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
-                     make_drop(0.f, 0));
+                     make_drop(0.f, 0), true);
+}
+
+BNN_API int bnn_bn_bwd_eval(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                            const float* beta, const float* running_mean, const float* invstd, int32_t hardtanh,
+                            float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, running_mean, invstd, hardtanh, dx, dgamma, dbeta, work, stream,
+                     make_drop(0.f, 0), false);
 }
 
 BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
@@ -707,13 +717,13 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
     return kErrInval;
   }
   return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
-                     make_drop(p, seed));
+                     make_drop(p, seed), true);
 }
 
 __global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d, float* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    out[i] = drop_keep(d, (uint64_t)i) ? d.scale : 0.f;
+    out[i] = (!d.on || drop_keep(d, (uint64_t)i)) ? d.scale : 0.f;   // p == 0: the fused passes never mask
 }
 
 BNN_API int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, void* stream) {
@@ -722,11 +732,7 @@ BNN_API int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, void
     return kErrInval;
   }
   if (n == 0) return 0;
-  Drop d = make_drop(p, seed);
-  if (!d.on) {   // p == 0: every element kept
-    d.thresh = 0xFFFFFFFFu;
-    d.scale = 1.f;
-  }
+  const Drop d = make_drop(p, seed);   // p == 0: d.on = 0, scale 1 -> every element kept
   hipLaunchKernelGGL(dropout_mask_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, d,
                      out);
   return check_launch("bnn_dropout_mask");
@@ -781,10 +787,10 @@ BNN_API int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, i
   return check_launch("bnn_bn2d_fwd_eval");
 }
 
-BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+static int bn2d_bwd_impl(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
                          const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                          int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
-                         void* stream) {
+                         void* stream, bool batch_stats) {
   if (!bn2_args_ok(x, N, C, H, W, pool) || !dy || !save_mean || !save_invstd || !work ||
       (dx && !aligned16(dx)) || (!pool && !aligned16(dy))) {
     set_error("bnn_bn2d_bwd: bad arguments");
@@ -803,9 +809,26 @@ BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, 
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
+    const float inv_n = batch_stats ? (float)(1.0 / ((double)N * (double)(H * W))) : 0.f;
     BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_bwd_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, dy, N,
                                              C, (int)H, (int)W, save_mean, save_invstd, gamma, beta, hardtanh, k0,
-                                             k1, dx));
+                                             k1, inv_n, dx));
   }
   return check_launch("bnn_bn2d_bwd");
+}
+
+BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+                         const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                         int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                         void* stream) {
+  return bn2d_bwd_impl(x, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool, dx, dgamma, dbeta,
+                       work, stream, true);
+}
+
+BNN_API int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+                              const float* gamma, const float* beta, const float* running_mean, const float* invstd,
+                              int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                              void* stream) {
+  return bn2d_bwd_impl(x, dy, N, C, H, W, gamma, beta, running_mean, invstd, hardtanh, pool, dx, dgamma, dbeta,
+                       work, stream, false);
 }

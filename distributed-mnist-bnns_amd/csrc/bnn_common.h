@@ -81,4 +81,28 @@ __device__ __forceinline__ void digit_scale(float amax, int* shift, float* scale
   *scale = ldexpf(1.f, e - 22);
 }
 
+// torch.optim.Adam single-tensor math in fp32 (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_,
+// denom = sqrt(v)/sqrt(bc2) + eps, p.addcdiv_(m, denom, -lr/bc1)), then the latent clamp of
+// mnist-dist2.py:135-137.  Shared by bnn_adam_clamp and the fused bnn_adam_clamp_pack so both
+// produce bit-identical latent weights.
+struct AdamArgs {
+  const float* g;
+  float* m;
+  float* v;
+  float b1, b2, eps, step_size, bc2_sqrt, gscale;
+  int clamp;
+};
+
+void adam_bias_correction(float lr, float beta1, float beta2, int64_t step, float* step_size, float* bc2_sqrt);
+
+__device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v, const AdamArgs& a) {
+  const float gi = g * a.gscale;
+  m = m + (1.f - a.b1) * (gi - m);
+  v = fmaf((1.f - a.b2) * gi, gi, v * a.b2);
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  float pi = p - a.step_size * (m / denom);
+  if (a.clamp) pi = fminf(fmaxf(pi, -1.f), 1.f);
+  return pi;
+}
+
 }  // namespace bnn

@@ -55,14 +55,51 @@ struct ColAffine {
   int vec;             // all four 16-B aligned -> float4 parameter loads
 };
 
+// One 16-element run of a latent-weight row updated in place by Adam + clamp (ADAM mode of
+// sign_pack_tile_k: the fused latent update of mnist-dist2.py:131-137 that also writes the next
+// forward's ternary operands).  p, g, m, v share the row-major [M][K] layout (ldx = K).
+__device__ __forceinline__ void adam16(float* __restrict__ prow, int64_t off, int64_t k, int64_t K, bool vec,
+                                       const AdamArgs& a, float (&v)[16]) {
+  float g[16], mm[16], vv[16];
+  load16(prow, k, K, vec, v);
+  load16(a.g + off, k, K, vec, g);
+  load16(a.m + off, k, K, vec, mm);
+  load16(a.v + off, k, K, vec, vv);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = adam_elem(v[j], g[j], mm[j], vv[j], a);
+  if (vec && k + 16 <= K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<float4*>(prow + k + 4 * i) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+      *reinterpret_cast<float4*>(a.m + off + k + 4 * i) =
+          make_float4(mm[4 * i], mm[4 * i + 1], mm[4 * i + 2], mm[4 * i + 3]);
+      *reinterpret_cast<float4*>(a.v + off + k + 4 * i) =
+          make_float4(vv[4 * i], vv[4 * i + 1], vv[4 * i + 2], vv[4 * i + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (k + j < K) {
+        prow[k + j] = v[j];
+        a.m[off + k + j] = mm[j];
+        a.v[off + k + j] = vv[j];
+      } else {
+        v[j] = 0.f;
+      }
+    }
+  }
+}
+
 // One 64x64 tile of x -> ternary rows (q: FMT 0 = int8 per element, FMT 1 = FP4 e2m1 nibbles,
 // element k in byte k/2, low nibble for even k) and/or the transposed int8 tile (qt).
-template <int FMT, int AFF = 0>
+// ADAM = 1: x is a latent weight updated in place first (adam16), and its new sign is packed.
+template <int FMT, int AFF = 0, int ADAM = 0>
 __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
                                                         int64_t K, int64_t ldx, int8_t* __restrict__ q,
                                                         int64_t ldq, int8_t* __restrict__ qt,
                                                         int64_t ldqt, int vec, ColAffine af = {},
-                                                        int rtiles = 1, int64_t ntiles_y = 0) {
+                                                        int rtiles = 1, int64_t ntiles_y = 0,
+                                                        AdamArgs ad = {}) {
   // rtiles > 1: the workgroup walks rtiles vertically adjacent 64x64 tiles of its column block
   // (the per-column BatchNorm parameters are loaded once per workgroup, not once per tile)
   __shared__ int tile[TILE][TILE + 1];
@@ -102,7 +139,9 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
   const int64_t m0 = ty * TILE;
   const int64_t m = m0 + r;
   float v[16];
-  if (m < M) {
+  if (ADAM && m < M) {
+    adam16(const_cast<float*>(x) + m * ldx, m * ldx, k0 + c, K, vec, ad, v);
+  } else if (m < M) {
     load16(x + m * ldx, k0 + c, K, vec, v);
   } else {
 #pragma unroll
@@ -447,6 +486,46 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
   hipLaunchKernelGGL(sign_pack_tile_k<1>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M, K,
                      ldx, reinterpret_cast<int8_t*>(q4), ldq4, qt, ldqt, vec);
   return check_launch("bnn_sign_pack_fp4");
+}
+
+BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
+                                int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
+                                float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
+                                int64_t ldqt, void* stream) {
+  if (!p || !grad || !exp_avg || !exp_avg_sq || N <= 0 || K <= 0 || step < 1 || (fmt != 0 && fmt != 1) ||
+      (!q && !qt)) {
+    set_error("bnn_adam_clamp_pack: bad arguments (N=%lld K=%lld fmt=%d)", (long long)N, (long long)K, fmt);
+    return kErrInval;
+  }
+  if (q && (fmt == 0 ? (ldq % TILE != 0 || ldq < round_up(K, TILE))
+                     : (ldq % 128 != 0 || 2 * ldq < round_up(K, 256))) ) {
+    set_error("bnn_adam_clamp_pack: ldq=%lld does not cover K=%lld in fmt %d", (long long)ldq, (long long)K, fmt);
+    return kErrInval;
+  }
+  if ((q && !aligned16(q)) || (qt && (ldqt % TILE != 0 || ldqt < round_up(N, TILE) || !aligned16(qt)))) {
+    set_error("bnn_adam_clamp_pack: ldqt=%lld must be a multiple of 64 >= round_up(N,64), 16-B aligned",
+              (long long)ldqt);
+    return kErrInval;
+  }
+  // every element of p is visited exactly once: the grid spans K (and the q padding) x N (and
+  // the qt padding); tiles beyond K or N update nothing and only write zero padding
+  const int64_t gx = q ? (fmt == 0 ? ldq : 2 * ldq) / TILE : (K + TILE - 1) / TILE;
+  const int64_t gy = qt ? ldqt / TILE : (N + TILE - 1) / TILE;
+  if (gy > 65535 || gx > 0x7fffffff) {
+    set_error("bnn_adam_clamp_pack: N too large for one launch (%lld)", (long long)N);
+    return kErrInval;
+  }
+  float step_size, bc2_sqrt;
+  adam_bias_correction(lr, beta1, beta2, step, &step_size, &bc2_sqrt);
+  const AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bc2_sqrt, grad_scale, clamp};
+  const int vec = aligned16(p) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq) && (K % 4 == 0);
+  if (fmt == 0)
+    hipLaunchKernelGGL((sign_pack_tile_k<0, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
+                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a);
+  else
+    hipLaunchKernelGGL((sign_pack_tile_k<1, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
+                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a);
+  return check_launch("bnn_adam_clamp_pack");
 }
 
 BNN_API int bnn_sign_f32(const float* x, float* y, int64_t n, void* stream) {

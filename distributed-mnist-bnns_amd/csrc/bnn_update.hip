@@ -32,28 +32,28 @@ __global__ __launch_bounds__(256) void hardtanh_bwd_k(const float* __restrict__ 
   for (int64_t i = tail + i0; i < n; i += stride) out[i] = f(x[i], g[i]);
 }
 
-// torch.optim.Adam single-tensor math in fp32 (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_,
-// denom = sqrt(v)/sqrt(bc2) + eps, p.addcdiv_(m, denom, -lr/bc1)), then clamp.
-__global__ __launch_bounds__(256) void adam_clamp_k(float* __restrict__ p, const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v,
-                                                    int64_t n, float b1, float b2, float eps,
-                                                    float step_size, float bc2_sqrt, float gscale,
-                                                    int clamp) {
+// Adam + clamp over a flat tensor (math: adam_elem in bnn_common.h).
+__global__ __launch_bounds__(256) void adam_clamp_k(float* __restrict__ p, int64_t n, AdamArgs a) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float gi = g[i] * gscale;
-    float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);
-    float vi = v[i] * b2;
-    vi = fmaf((1.f - b2) * gi, gi, vi);
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    float pi = p[i] - step_size * (mi / denom);
-    if (clamp) pi = fminf(fmaxf(pi, -1.f), 1.f);
-    p[i] = pi;
-    m[i] = mi;
-    v[i] = vi;
+    float mi = a.m[i], vi = a.v[i];
+    p[i] = adam_elem(p[i], a.g[i], mi, vi, a);
+    a.m[i] = mi;
+    a.v[i] = vi;
   }
 }
+
+}  // namespace
+
+// torch computes the bias corrections as Python floats (double) from the step count.
+void adam_bias_correction(float lr, float beta1, float beta2, int64_t step, float* step_size, float* bc2_sqrt) {
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  *step_size = (float)((double)lr / bc1);
+  *bc2_sqrt = (float)std::sqrt(bc2);
+}
+
+namespace {
 
 inline int grid_for(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
@@ -84,13 +84,9 @@ BNN_API int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* e
     return kErrInval;
   }
   if (n == 0) return 0;
-  // torch computes the bias corrections as Python floats (double) from the step count.
-  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)std::sqrt(bc2);
-  hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), p, grad, exp_avg, exp_avg_sq, n, beta1,
-                     beta2, eps, step_size, bc2_sqrt, grad_scale, clamp);
+  float step_size, bc2_sqrt;
+  adam_bias_correction(lr, beta1, beta2, step, &step_size, &bc2_sqrt);
+  const AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bc2_sqrt, grad_scale, clamp};
+  hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, n, a);
   return check_launch("bnn_adam_clamp");
 }

@@ -166,6 +166,12 @@ int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, co
 int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
                float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
+/* Backward of the eval-mode forward (running statistics are constants, torch's
+ * batch_norm_backward with training=False): dx = gamma*invstd*g, dgamma = sum g*xhat,
+ * dbeta = sum g, with invstd = 1/sqrt(running_var + eps). */
+int bnn_bn_bwd_eval(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                    const float* beta, const float* running_mean, const float* invstd, int32_t hardtanh,
+                    float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- BatchNorm2d (+ Hardtanh, + MaxPool2d(2))
  * The block after each BinarizeConv2d of the build's CNN (conv -> nn.BatchNorm2d -> nn.Hardtanh ->
@@ -188,6 +194,11 @@ int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, int64_t 
                  const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                  int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                  bnn_stream_t stream);
+/* Eval-mode backward (running statistics), as bnn_bn_bwd_eval. */
+int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+                      const float* gamma, const float* beta, const float* running_mean, const float* invstd,
+                      int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                      bnn_stream_t stream);
 
 /* nn.Dropout(p) fused in front of BatchNorm1d (+ Hardtanh) (mnist-dist2.py:69-70: fc3 -> drop ->
  * bn3): x is the pre-dropout input; the keep mask is a counter-based hash of (seed, row*C + col)
@@ -224,6 +235,20 @@ int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_
 int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,
                    int32_t clamp, bnn_stream_t stream);
+
+/* The same update fused with the next forward's weight packing: p is a latent
+ * weight [N][K] row-major (ld = K; grad, exp_avg, exp_avg_sq alike), updated in place exactly as
+ * bnn_adam_clamp does (bit-identical p, m, v), and in the same pass sign(p_new) is written as the
+ * ternary rows q -- fmt 0: int8 [N][ldq] (ldq multiple of 64 >= round_up(K,64)); fmt 1: FP4
+ * nibbles [N][ldq bytes] (ldq multiple of 128, 2*ldq >= round_up(K,256)) -- and/or the int8
+ * transpose qt [K][ldqt] (ldqt multiple of 64 >= round_up(N,64)); padding zero-filled, as
+ * bnn_sign_pack_i8 / bnn_sign_pack_fp4 of p_new would write them.  q or qt may be NULL (not both).
+ * replaces: p.data.copy_(p.org); Adam.step(); p.org.copy_(p.data.clamp_(-1,1)) (mnist-dist2.py:
+ * 131-137) and the weight sign of the next forward (binarized_modules.py:79). */
+int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
+                        int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
+                        float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
+                        int64_t ldqt, bnn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -4,12 +4,18 @@ Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
 this module.  It is what the reference runs on a CPU: torch's fp32 ``F.linear`` / ``F.conv2d`` on
 sign()ed operands, ``BatchNorm1d``, ``Hardtanh``, ``torch.optim.Adam`` and the ``.org``
 protocol.  bench.py times it on the GPU box's host cores as the ``"port"`` CPU baseline
-(the reference source itself never travels there).  Pinned to the reference's outputs by
+(the reference source itself never travels there): configs 1 (single process) and 2 (gloo
+DDP, ``time_training_gloo``), and the bench config itself; run with GPU tensors it is the naive
+"reference semantics on torch fp32 GEMMs" comparator.  Pinned to the reference's outputs by
 tests/test_oracle_golden.py::test_torch_restatement_* against tests/golden/*.npz.
 
 Restated from: models/binarized_modules.py:11-13 (Binarize), :68-85 (BinarizeLinear),
 :87-107 (BinarizeConv2d); mnist-dist2.py:46-76 (Net), :118-137 (train step).
 """
+import json
+import os
+import socket
+import sys
 import time
 
 import torch
@@ -106,27 +112,30 @@ def train_step(model, opt, x, target, org_protocol=True):
     return loss.item()
 
 
-def synthetic_batch(n, seed):
+def synthetic_batch(n, seed, device="cpu"):
     g = torch.Generator().manual_seed(seed)
     u = torch.rand((n, 1, 28, 28), generator=g)
     v = torch.randint(1, 256, (n, 1, 28, 28), generator=g).float()
     x = torch.where(u < 0.807, torch.zeros_like(v), v) / 255.0
-    return x, torch.randint(0, 10, (n,), generator=g)
+    return x.to(device), torch.randint(0, 10, (n,), generator=g).to(device)
 
 
-def time_training(widths, batch, threads, budget_s=10.0, max_steps=50, min_steps=2, warmup=1):
-    """Time the CPU reference training step (fp32, torch on `threads` host threads); widths =
+def time_training(widths, batch, threads, budget_s=10.0, max_steps=50, min_steps=2, warmup=1, device="cpu"):
+    """Time the reference training step (fp32 torch; on `threads` host threads, or on a GPU with
+    device="cuda" -- the naive "reference semantics on torch fp32 GEMMs" comparator); widths =
     (h1, h2, h3) for the MLPs or "cnn" for RefCNN.
 
     Returns (samples_per_s, steps, seconds)."""
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    model = RefCNN() if widths == "cnn" else RefMLP(*widths)
+    model = (RefCNN() if widths == "cnn" else RefMLP(*widths)).to(device)
     model.train()
     opt = torch.optim.Adam(model.parameters(), lr=0.01)
-    x, t = synthetic_batch(batch, 1234)
+    x, t = synthetic_batch(batch, 1234, device)
+    sync = torch.cuda.synchronize if device != "cpu" else (lambda: None)
     for _ in range(warmup):
         train_step(model, opt, x.clone(), t)
+    sync()
     steps, t0 = 0, time.perf_counter()
     while steps < max_steps:
         train_step(model, opt, x.clone(), t)
@@ -134,5 +143,61 @@ def time_training(widths, batch, threads, budget_s=10.0, max_steps=50, min_steps
         el = time.perf_counter() - t0
         if steps >= min_steps and el >= budget_s:
             break
+    sync()
     el = time.perf_counter() - t0
     return batch * steps / el, steps, el
+
+
+# ----------------------------------------------------------------------------- gloo DDP (config 2)
+def _gloo_rank(rank, world, port, widths, batch, threads, budget_s, q):
+    """One rank of the reference's data-parallel loop: gloo process group, DDP over the CPU
+    restatement (mnist-dist2.py:83, :93), per-rank shard of the batch, .org protocol."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(threads)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.parallel.DistributedDataParallel(RefMLP(*widths))
+    opt = torch.optim.Adam(model.parameters(), lr=0.01)
+    x, t = synthetic_batch(batch, 1234 + rank)
+    train_step(model, opt, x.clone(), t)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        train_step(model, opt, x.clone(), t)
+        steps += 1
+        el = torch.tensor([time.perf_counter() - t0])
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)   # every rank agrees when to stop
+        if steps >= 2 and float(el) >= budget_s:
+            break
+    if rank == 0:
+        q.put((steps, float(el)))
+    dist.destroy_process_group()
+
+
+def time_training_gloo(widths, batch, world, threads_per_rank, budget_s=8.0):
+    """BASELINE config 2: the same MLP step under gloo DDP with `world` CPU ranks on this host
+    (threads split per rank).  `batch` is per rank; returns (total samples/s, steps, seconds)."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, widths, batch, threads_per_rank, budget_s, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    steps, el = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=60)
+    return batch * world * steps / el, steps, el
+
+
+if __name__ == "__main__":
+    # python -m oracle.bnn_torch gloo H1 H2 H3 BATCH WORLD THREADS BUDGET  -> one JSON line
+    if len(sys.argv) == 9 and sys.argv[1] == "gloo":
+        h1, h2, h3, b, w, th = (int(v) for v in sys.argv[2:8])
+        sps, n, secs = time_training_gloo((h1, h2, h3), b, w, th, float(sys.argv[8]))
+        print(json.dumps({"samples_per_s": sps, "steps": n, "seconds": secs}), flush=True)

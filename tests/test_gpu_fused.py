@@ -1,0 +1,281 @@
+"""GPU parity of the fused operators the benched trainer path runs, and of the wide (config 5)
+backward, against exact / float64 references.
+
+* ``bnn_bn_apply_pack`` (BatchNorm apply -> Hardtanh -> sign-pack, mnist-dist2.py:66-68): bit-exact
+  against sign(BN(z)) evaluated with the same fp32 formula (``(z - mean) * invstd`` rounded to
+  fp32, then one fused multiply-add with gamma, beta) from the same mean / invstd.  The sign of a
+  fused multiply-add equals the sign of the exact value, which float64 reproduces exactly.
+* ``BNHardtanhBinaryLinearFunction`` (bn -> htanh -> BinarizeLinear, mnist-dist2.py:66-71):
+  forward bit-exact, every gradient norm-wise <= 1e-5 against float64.
+* config 5 width: dX = dY.W_b and dW = dY^T.X_b at K = N = 8192 with heavy-tailed magnitudes
+  inside each dY row (the digit operands' per-row / per-column scale is the weak spot) against a
+  float64 GEMM, norm-wise <= 1e-5.
+* eval-mode BatchNorm backward (running statistics are constants): against torch autograd in
+  float64.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import bnn_np as O
+
+pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def F():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import functional
+    return functional
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def bn_sign_ref(z, mean, invstd, gamma, beta):
+    """sign(fmaf((z - mean) * invstd, gamma, beta)) with fp32 z - mean and fp32 product."""
+    t = (z.astype(np.float32) - mean.astype(np.float32)).astype(np.float32)
+    t = (t * invstd.astype(np.float32)).astype(np.float32)
+    y = t.astype(np.float64) * gamma.astype(np.float64) + beta.astype(np.float64)
+    return np.sign(y).astype(np.int8), y
+
+
+def decode_fp4(q4, K):
+    lo = (q4 & 0xF).astype(np.int16)
+    hi = (q4 >> 4).astype(np.int16)
+    codes = np.stack([lo, hi], axis=-1).reshape(q4.shape[0], -1)
+    out = np.zeros(codes.shape, np.int8)
+    out[codes == 0x2] = 1
+    out[codes == 0xA] = -1
+    assert np.isin(codes, [0x0, 0x2, 0xA]).all()
+    return out
+
+
+def bn_stats(F, z, C):
+    from bnn_amd import _lib as L
+    M = z.shape[0]
+    mean = torch.empty(C, device="cuda")
+    invstd = torch.empty(C, device="cuda")
+    ws = torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device="cuda")
+    L.call("bnn_bn_fwd_train", L.ptr(z), M, C, None, None, None, None, -1.0, 1e-5, L.ptr(mean), L.ptr(invstd),
+           None, 1, L.ptr(ws), L.stream())
+    return mean, invstd
+
+
+@pytest.mark.parametrize("M,C", [(300, 192), (1000, 1536), (77, 260), (4096, 768)])
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("with_qt", [True, False])
+def test_bn_apply_pack_bit_exact(F, M, C, fmt, with_qt):
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M * 7 + C + fmt)
+    # integer-valued pre-activations + a per-column bias (what a binarized GEMM produces): ties
+    # z == mean and exact zeros of BN(z) do occur
+    z = (rng.integers(-30, 31, (M, C)) + rng.uniform(-1, 1, C).astype(np.float32)).astype(np.float32)
+    z[:, 5] = 3.0                                        # constant columns: xhat = 0 exactly, so
+    z[:, 7] = -2.0                                       # BN(z) = beta (= 0 in column 7: sign 0)
+    gamma = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = rng.uniform(-0.3, 0.3, C).astype(np.float32)
+    beta[7] = 0.0
+    zt = dev(z)
+    mean, invstd = bn_stats(F, zt, C)
+    s_ref, _ = bn_sign_ref(z, host(mean), host(invstd), gamma, beta)
+    assert (s_ref == 0).any()                            # the ternary zero is exercised
+    if fmt == 1:
+        q = torch.full((M, F.round_up(C, 256) // 2), 0x55, dtype=torch.uint8, device="cuda")
+    else:
+        q = torch.full((M, F.round_up(C)), 9, dtype=torch.int8, device="cuda")
+    qt = torch.full((C, F.round_up(M)), 9, dtype=torch.int8, device="cuda") if with_qt else None
+    L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(dev(gamma)), L.ptr(dev(beta)),
+           fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    qh = host(q)
+    rows = decode_fp4(qh, C) if fmt == 1 else qh.astype(np.int8)
+    assert np.array_equal(rows[:, :C], s_ref)
+    assert not rows[:, C:].any()
+    if with_qt:
+        qth = host(qt)
+        assert np.array_equal(qth[:, :M], s_ref.T)
+        assert not qth[:, M:].any()
+
+
+@pytest.mark.parametrize("M,C,N", [(256, 192, 128), (1000, 1536, 768), (64, 96, 40)])
+@pytest.mark.parametrize("backend", ["fp4", "mfma"])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_hardtanh_binary_linear_vs_float64(F, M, C, N, backend, training):
+    """fc(hardtanh(bn(z))) fused: forward bit-exact, gradients <= 1e-5 norm-wise vs float64."""
+    rng = np.random.default_rng(M + C + N)
+    z = (rng.integers(-25, 26, (M, C)) + rng.uniform(-1, 1, C)).astype(np.float32)
+    w = rng.uniform(-1, 1, (N, C)).astype(np.float32)
+    w[rng.random((N, C)) < 0.01] = 0.0
+    b = rng.standard_normal(N).astype(np.float32)
+    gamma = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = rng.uniform(-0.3, 0.3, C).astype(np.float32)
+    dy = rng.standard_normal((M, N)).astype(np.float32)
+    bn = torch.nn.BatchNorm1d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(dev(gamma))
+        bn.bias.copy_(dev(beta))
+        if not training:
+            bn.running_mean.copy_(dev(rng.uniform(-3, 3, C).astype(np.float32)))
+            bn.running_var.copy_(dev(rng.uniform(50, 300, C).astype(np.float32)))
+    bn.train(training)
+    fc = torch.nn.Module()
+    fc.weight = torch.nn.Parameter(dev(w))
+    fc.bias = torch.nn.Parameter(dev(b))
+    zt = dev(z).requires_grad_(True)
+    if training:
+        mean, invstd = bn_stats(F, dev(z), C)       # the same reduction the fused op runs
+    else:
+        mean, invstd = bn.running_mean.clone(), (bn.running_var + bn.eps).rsqrt()
+    mean_h, inv_h = host(mean), host(invstd)
+    rm0 = host(bn.running_mean).astype(np.float64)
+    rv0 = host(bn.running_var).astype(np.float64)
+    y = F.bn_hardtanh_binary_linear(zt, bn, fc, backend)
+    # forward: sign(BN(z)) with the GPU's statistics -> exact integer GEMM -> one fp32 bias add
+    s, ybn = bn_sign_ref(z, mean_h, inv_h, gamma, beta)
+    y_ref = (s.astype(np.int64) @ np.sign(w).astype(np.int64).T).astype(np.float32) + b
+    assert np.array_equal(host(y), y_ref)
+    if training:
+        _, cache, rm, rv = O.batchnorm_train(z, gamma, beta, rm0, rv0)
+        assert rel_err(host(bn.running_mean), rm) < 1e-6
+        assert rel_err(host(bn.running_var), rv) < 1e-6
+    y.backward(dev(dy))
+    # backward in float64: dh = dY.W_b, hardtanh mask from the same fp32 y, BatchNorm backward
+    dh = dy.astype(np.float64) @ np.sign(w).astype(np.float64)
+    y32 = ybn.astype(np.float32)                 # the kernels compare the fp32-rounded BN output
+    mask = (y32 > -1.0) & (y32 < 1.0)
+    g = dh * mask
+    if training:
+        xhat = (z.astype(np.float64) - z.astype(np.float64).mean(0)) / np.sqrt(z.astype(np.float64).var(0) + 1e-5)
+        inv = 1.0 / np.sqrt(z.astype(np.float64).var(0) + 1e-5)
+        dz, dgam, dbet = O.batchnorm_backward((xhat, inv, gamma.astype(np.float64)), g)
+    else:
+        inv = 1.0 / np.sqrt(host(bn.running_var).astype(np.float64) + 1e-5)
+        xhat = (z.astype(np.float64) - host(bn.running_mean).astype(np.float64)) * inv
+        dz = g * gamma * inv
+        dgam, dbet = (g * xhat).sum(0), g.sum(0)
+    dw = dy.astype(np.float64).T @ s.astype(np.float64)
+    db = dy.astype(np.float64).sum(0)
+    assert rel_err(host(zt.grad), dz) < GRAD_TOL
+    assert rel_err(host(bn.weight.grad), dgam) < GRAD_TOL
+    assert rel_err(host(bn.bias.grad), dbet) < GRAD_TOL
+    assert rel_err(host(fc.weight.grad), dw) < GRAD_TOL
+    assert rel_err(host(fc.bias.grad), db) < GRAD_TOL
+
+
+@pytest.mark.parametrize("M", [1024, 2048])
+def test_wide_backward_heavy_tailed_vs_float64(F, M):
+    """Config 5 width (K = N = 8192): dX = dY.W_b and dW = dY^T.X_b with dY magnitudes spread
+    over e^+-9 inside every row and column, against float64 GEMMs (rocBLAS dgemm on the same
+    device: products of fp32 values and +-1/0 are exact in float64)."""
+    torch.manual_seed(M)
+    K = N = 8192
+    x = torch.randn(M, K, device="cuda")
+    x[torch.rand_like(x) < 0.02] = 0.0
+    w = torch.empty(N, K, device="cuda").uniform_(-1, 1)
+    w[torch.rand_like(w) < 0.001] = 0.0
+    dy = torch.randn(M, N, device="cuda") * torch.exp(torch.empty(M, N, device="cuda").uniform_(-9, 9))
+    xt = x.clone().requires_grad_(True)
+    wt = w.clone().requires_grad_(True)
+    y = F.binary_linear(xt, wt, None, True, "fp4")
+    y.backward(dy)
+    xb, wb = torch.sign(x).double(), torch.sign(w).double()
+    dx64 = dy.double() @ wb
+    dw64 = dy.double().t() @ xb
+    err_dx = float(torch.linalg.norm(xt.grad.double() - dx64) / torch.linalg.norm(dx64))
+    err_dw = float(torch.linalg.norm(wt.grad.double() - dw64) / torch.linalg.norm(dw64))
+    assert err_dx < GRAD_TOL, err_dx
+    assert err_dw < GRAD_TOL, err_dw
+    # per-row check too: the worst row of dX (each row has its own digit scale)
+    row_err = torch.linalg.norm(xt.grad.double() - dx64, dim=1) / torch.linalg.norm(dx64, dim=1)
+    assert float(row_err.max()) < 10 * GRAD_TOL, float(row_err.max())
+
+
+@pytest.mark.parametrize("hardtanh", [True, False])
+def test_batchnorm1d_eval_backward_vs_torch(F, hardtanh):
+    torch.manual_seed(3)
+    M, C = 300, 64
+    bn = torch.nn.BatchNorm1d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    bn.eval()
+    x = (torch.randn(M, C, device="cuda") * 1.5).requires_grad_(True)
+    g = torch.randn(M, C, device="cuda")
+    F.batch_norm_hardtanh(x, bn, hardtanh).backward(g)
+    bd = torch.nn.BatchNorm1d(C).double()
+    bd.load_state_dict({k: v.double().cpu() if v.is_floating_point() else v.cpu() for k, v in bn.state_dict().items()})
+    bd.eval()
+    xr = x.detach().double().cpu().requires_grad_(True)
+    yr = bd(xr)
+    if hardtanh:
+        yr = torch.nn.functional.hardtanh(yr)
+    yr.backward(g.double().cpu())
+    assert rel_err(host(x.grad), xr.grad.numpy()) < GRAD_TOL
+    assert rel_err(host(bn.weight.grad), bd.weight.grad.numpy()) < GRAD_TOL
+    assert rel_err(host(bn.bias.grad), bd.bias.grad.numpy()) < GRAD_TOL
+
+
+@pytest.mark.parametrize("pool", [2, 0])
+def test_batchnorm2d_eval_backward_vs_torch(F, pool):
+    torch.manual_seed(4)
+    N, C, H, W = 6, 16, 14, 14
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    bn.eval()
+    x = (torch.randn(N, C, H, W, device="cuda") * 1.5).requires_grad_(True)
+    y = F.batch_norm2d_hardtanh_pool(x, bn, True, pool)
+    g = torch.randn_like(y)
+    y.backward(g)
+    bd = torch.nn.BatchNorm2d(C).double()
+    bd.load_state_dict({k: v.double().cpu() if v.is_floating_point() else v.cpu() for k, v in bn.state_dict().items()})
+    bd.eval()
+    xr = x.detach().double().cpu().requires_grad_(True)
+    yr = torch.nn.functional.hardtanh(bd(xr))
+    if pool:
+        yr = torch.nn.functional.max_pool2d(yr, 2, 2)
+    yr.backward(g.double().cpu())
+    assert rel_err(host(x.grad), xr.grad.numpy()) < GRAD_TOL
+    assert rel_err(host(bn.weight.grad), bd.weight.grad.numpy()) < GRAD_TOL
+    assert rel_err(host(bn.bias.grad), bd.bias.grad.numpy()) < GRAD_TOL
+
+
+def test_eval_mode_net_input_gradient(F):
+    """An eval-mode MLP (frozen BN, e.g. input-gradient computation) through the fused ops vs the
+    drop-in ops with torch's BatchNorm1d: same input gradient."""
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    torch.manual_seed(8)
+    a = nets.MLP(256, 128, 64, p_drop=0.0, org_protocol=False, mutate_input=False).cuda()
+    b = nets.MLP(256, 128, 64, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    b.load_state_dict(a.state_dict())
+    x, y = synthetic_mnist(64, seed=3, device="cuda")
+    for m in (a, b):                      # give the running statistics non-trivial values
+        m.train()
+        with torch.no_grad():
+            m(x)
+        m.eval()
+    outs = []
+    for m in (a, b):
+        xi = x.clone().requires_grad_(True)
+        loss = torch.nn.functional.cross_entropy(m(xi), y)
+        loss.backward()
+        outs.append((loss.item(), host(xi.grad), host(m.bn2.weight.grad)))
+    assert abs(outs[0][0] - outs[1][0]) < 1e-5
+    assert rel_err(outs[1][1], outs[0][1]) < 1e-4
+    assert rel_err(outs[1][2], outs[0][2]) < 1e-4

@@ -89,6 +89,71 @@ def test_gradexchange_matches_torch_ddp_world2():
         np.testing.assert_array_equal(a, b)
 
 
+def _worker_chunks(rank, world, port, q):
+    """The build's own network (bnn_amd.nets.MLP; constructed on CPU, its forward needs libbnn)
+    under GradExchange with a bucket cap far below its largest gradients: chunked buckets,
+    gradients averaged exactly, coalesced buffer broadcast."""
+    try:
+        for p in (ROOT, PKG):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from bnn_amd import nets
+        from bnn_amd.parallel import GradExchange
+        torch.manual_seed(100 + rank)
+        model = nets.MLP(48, 32, 24, p_drop=0.0, org_protocol=False, mutate_input=False)
+        ex = GradExchange(model, bucket_mb=0.002)        # 524 floats: fc1.weight -> 72 slices
+        out = {"nbuckets": len(ex.buckets)}
+        sizes = [b.end - b.start for b in ex.buckets]
+        out["max_bucket"] = max(sizes)
+        out["fc1_slices"] = len(ex._param_buckets[model.fc1.weight])
+        params = list(model.parameters())
+        for step in range(2):
+            ex.zero_grad()
+            coefs = []
+            for r in range(world):
+                g = torch.Generator().manual_seed(1000 * step + 10 * r)
+                coefs.append([torch.randn(p.shape, generator=g) for p in params])
+            loss = sum((p * c).sum() for p, c in zip(params, coefs[rank]))
+            loss.backward()
+            ex.finish()
+            for i, p in enumerate(params):
+                want = sum(coefs[r][i] for r in range(world)) / world
+                assert torch.allclose(p.grad, want, rtol=1e-6, atol=1e-7), (step, i)
+        # one staging buffer (one broadcast) carries every running stat of every dtype
+        assert len(ex._flat_buffers) == 1
+        with torch.no_grad():
+            model.bn2.running_mean.fill_(float(rank + 1))
+            model.bn3.num_batches_tracked.fill_(7 + rank)
+        ex.sync_buffers()
+        assert torch.all(model.bn2.running_mean == 1.0) and int(model.bn3.num_batches_tracked) == 7
+        q.put((rank, out))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc()))
+
+
+def test_gradexchange_chunked_buckets_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_chunks, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert not isinstance(out[r], str), out[r]
+    assert out[0]["max_bucket"] * 4 <= 0.002 * 2 ** 20
+    assert out[0]["fc1_slices"] == 72
+    assert out[0]["nbuckets"] > 72
+
+
 def test_shard_indices_match_distributed_sampler_golden():
     from bnn_amd.data import shard_indices
     g = load_golden("sampler")
