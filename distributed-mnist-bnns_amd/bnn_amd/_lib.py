@@ -40,19 +40,19 @@ SIGNATURES = {
                                     I32, P]),
     "bnn_conv_set_mfma": (I32, [I32]),
     "bnn_bn_workspace": (I64, [I64, I64]),
-    "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, P, P]),
+    "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, P, P]),
     "bnn_bn_fwd_eval": (I32, [P, I64, I64, P, P, P, P, F32, P, I32, P, P]),
-    "bnn_bn_bwd": (I32, [P, P, I64, I64, P, P, P, P, I32, P, P, P, P, P]),
+    "bnn_bn_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, P, P]),
     "bnn_bn_bwd_eval": (I32, [P, P, I64, I64, P, P, P, P, I32, P, P, P, P, P]),
     "bnn_bn2d_workspace": (I64, [I64, I64]),
     "bnn_bn2d_fwd_train": (I32, [P, I64, I64, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P]),
     "bnn_bn2d_fwd_eval": (I32, [P, I64, I64, I64, I64, P, P, P, P, F32, P, I32, I32, P, P]),
     "bnn_bn2d_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "bnn_bn2d_bwd_eval": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
-    "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, F32, U64, P, P]),
-    "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
+    "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
+    "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
-    "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, I32, P, I64, P, I64, P]),
+    "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, P]),

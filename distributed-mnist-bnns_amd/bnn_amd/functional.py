@@ -486,6 +486,22 @@ def _bn_ws(M, C, device):
     return torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device=device)
 
 
+def _bn_stat_buffers(C, device):
+    """save_mean, save_invstd, save_mean_lo of a training-mode BatchNorm forward (bnn.h)."""
+    st = torch.empty((3, C), dtype=torch.float32, device=device)
+    return st[0], st[1], st[2]
+
+
+def _bn_bwd_call(training, x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, dx, dw, db, ws):
+    # eval mode: the running statistics are constants (dx = gamma*invstd*g)
+    if training:
+        L.call("bnn_bn_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd), L.ptr(mlo),
+               int(hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+    else:
+        L.call("bnn_bn_bwd_eval", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+               int(hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+
+
 class BatchNormHardtanhFunction(torch.autograd.Function):
     """nn.BatchNorm1d on [M, C] (train or eval) optionally followed by nn.Hardtanh, fused
     (mnist-dist2.py:52-74).  Running stats are updated in place in training mode."""
@@ -500,36 +516,33 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
         b = bias.detach() if bias is not None else None
         ws = _bn_ws(M, C, x.device)
         if training:
-            mean = torch.empty((C,), dtype=torch.float32, device=x.device)
-            invstd = torch.empty_like(mean)
+            mean, invstd, mlo = _bn_stat_buffers(C, x.device)
             with _timed("bn_fwd_train", 0, 12 * M * C):
                 L.call("bnn_bn_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                        L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
-                       L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
+                       L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
         else:
-            mean = running_mean
+            mean, mlo = running_mean, None
             invstd = (running_var + eps).rsqrt()
             with _timed("bn_fwd_eval", 0, 8 * M * C):
                 L.call("bnn_bn_fwd_eval", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                        L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), L.ptr(ws), L.stream())
-        ctx.save_for_backward(x, w, b, mean, invstd)
+        ctx.save_for_backward(x, w, b, mean, invstd, mlo)
         ctx.hardtanh = hardtanh
         ctx.training = training
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, b, mean, invstd = ctx.saved_tensors
+        x, w, b, mean, invstd, mlo = ctx.saved_tensors
         dy = _c2d(dy)
         M, C = x.shape
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
         db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
         ws = _bn_ws(M, C, x.device)
-        # eval mode: the running statistics are constants (dx = gamma*invstd*g)
         with _timed("bn_bwd", 0, 16 * M * C):
-            L.call("bnn_bn_bwd" if ctx.training else "bnn_bn_bwd_eval", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
-                   int(ctx.hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+            _bn_bwd_call(ctx.training, x, dy, M, C, w, b, mean, invstd, mlo, ctx.hardtanh, dx, dw, db, ws)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None)
 
@@ -548,19 +561,18 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         ws = _bn_ws(M, C, x.device)
-        mean = torch.empty((C,), dtype=torch.float32, device=x.device)
-        invstd = torch.empty_like(mean)
+        mean, invstd, mlo = _bn_stat_buffers(C, x.device)
         with _timed("bn_dropout_fwd_train", 0, 12 * M * C):
             L.call("bnn_bn_dropout_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                    L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
-                   L.ptr(mean), L.ptr(invstd), L.ptr(y), 1, float(p), int(seed), L.ptr(ws), L.stream())
-        ctx.save_for_backward(x, w, b, mean, invstd)
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(y), 1, float(p), int(seed), L.ptr(ws), L.stream())
+        ctx.save_for_backward(x, w, b, mean, invstd, mlo)
         ctx.p, ctx.seed = p, seed
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, b, mean, invstd = ctx.saved_tensors
+        x, w, b, mean, invstd, mlo = ctx.saved_tensors
         dy = _c2d(dy)
         M, C = x.shape
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
@@ -569,7 +581,8 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         ws = _bn_ws(M, C, x.device)
         with _timed("bn_dropout_bwd", 0, 16 * M * C):
             L.call("bnn_bn_dropout_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
-                   1, float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
+                   L.ptr(mlo), 1, float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
+                   L.stream())
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None)
 
@@ -700,15 +713,14 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         gw = bn_w.detach() if bn_w is not None else None
         gb = bn_b.detach() if bn_b is not None else None
         if training:
-            mean = torch.empty((C,), dtype=torch.float32, device=z.device)
-            invstd = torch.empty_like(mean)
+            mean, invstd, mlo = _bn_stat_buffers(C, z.device)
             ws = _bn_ws(M, C, z.device)
             with _timed("bn_fwd_stats", 0, 4 * M * C):
                 L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv),
                        float(momentum if momentum is not None else -1.0), float(eps), L.ptr(mean),
-                       L.ptr(invstd), None, 1, L.ptr(ws), L.stream())
+                       L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
         else:
-            mean = rm.contiguous()
+            mean, mlo = rm.contiguous(), None
             invstd = (rv + eps).rsqrt()
         need_dh = any(ctx.needs_input_grad[:3])
         need_dw = ctx.needs_input_grad[8]
@@ -717,7 +729,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
         qt = torch.empty((C, round_up(M)), dtype=torch.int8, device=z.device) if need_dw else None
         with _timed("bn_apply_pack", 0, 4 * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
-            L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(gw), L.ptr(gb),
+            L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
                    1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
                    L.stream())
         b = bias.detach() if bias is not None else None
@@ -726,7 +738,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
             y = gemm_i8(q, 1, wq, 1, M, N, bias=b, k_true=C)
-        ctx.save_for_backward(z, gw, gb, mean, invstd, qt, wqt)
+        ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, qt, wqt)
         ctx.training = training
         ctx.dims = (M, C, N)
         ctx.has_bias = bias is not None
@@ -734,7 +746,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        z, gw, gb, mean, invstd, qt, wqt = ctx.saved_tensors
+        z, gw, gb, mean, invstd, mlo, qt, wqt = ctx.saved_tensors
         M, C, N = ctx.dims
         dy = _c2d(dy)
         dz = dgw = dgb = dw = db = None
@@ -752,8 +764,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None
             ws = _bn_ws(M, C, z.device)
             with _timed("bn_bwd", 0, 16 * M * C):
-                L.call("bnn_bn_bwd" if ctx.training else "bnn_bn_bwd_eval", L.ptr(z), L.ptr(dh), M, C, L.ptr(gw), L.ptr(gb), L.ptr(mean),
-                       L.ptr(invstd), 1, L.ptr(dz), L.ptr(dgw), L.ptr(dgb), L.ptr(ws), L.stream())
+                _bn_bwd_call(ctx.training, z, dh, M, C, gw, gb, mean, invstd, mlo, True, dz, dgw, dgb, ws)
         return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, dw, db, None)
 

@@ -7,6 +7,11 @@
 // float4 elementwise pass.
 //
 // Forward (train): mean, biased var over the batch; y = (x-mean)*invstd*gamma + beta;
+// the mean is kept as an fp32 pair hi + lo of the batch sum taken in double (exact for the
+// integer-plus-bias pre-activations of the binarized layers), and x - mean is evaluated as
+// (x - hi) - lo, so the sign of a normalised value that sits within an ulp of the mean (a
+// BatchNorm near-tie: z_i ~ mean is common when z is integer-valued) is the sign of the exact
+// difference -- the next BinarizeLinear's sign() then agrees with exact arithmetic;
 // running_mean/var updated with the unbiased var (torch semantics); hardtanh -> clamp(y,-1,1).
 // Backward: with g = dy * (hardtanh ? (-1 < y < 1) : 1) (y recomputed from x, not stored),
 // dbeta = sum g, dgamma = sum g*xhat, dx = gamma*invstd*(g - dbeta/n - xhat*dgamma/n).
@@ -68,6 +73,7 @@ inline Drop make_drop(float p, uint64_t seed) {
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                    int64_t M, int64_t C, const float* __restrict__ mean,
+                                                   const float* __restrict__ mean_lo,
                                                    const float* __restrict__ invstd,
                                                    const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, int hardtanh,
@@ -77,8 +83,8 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
   const int64_t r1 = (M < r0 + BN_ROWS) ? M : r0 + BN_ROWS;
-  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-  float mu[4], is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+  float mu[4], lo[4] = {0, 0, 0, 0}, is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
   if (MODE == 0) {
     const float4 sv = ld4(x + r0 * C + c);
     mu[0] = sv.x;
@@ -90,6 +96,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       mu[j] = mean[c + j];
+      lo[j] = mean_lo ? mean_lo[c + j] : 0.f;
       is[j] = invstd[c + j];
       ga[j] = gamma ? gamma[c + j] : 1.f;
       be[j] = beta ? beta[c + j] : 0.f;
@@ -108,13 +115,14 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
           const float d = xs[j] - mu[j];
           fa[j] += d;
           fb[j] = fmaf(d, d, fb[j]);
+          sx[j] += (double)xs[j];      // exact batch sum (see file header)
         }
       } else {
         const float4 gv = ld4(dy + rr * C + c);
         const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float xh = (xs[j] - mu[j]) * is[j];
+          const float xh = ((xs[j] - mu[j]) - lo[j]) * is[j];
           const float y = fmaf(xh, ga[j], be[j]);
           const float g = (!hardtanh || (y > -1.f && y < 1.f)) ? gs[j] : 0.f;
           fa[j] += g;
@@ -134,8 +142,8 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const double dm = a[j] / n;
-      p0[o + j] = (double)mu[j] + dm;  // chunk mean
-      p1[o + j] = b[j] - a[j] * dm;    // chunk M2 = sum d^2 - (sum d)^2 / n
+      p0[o + j] = sx[j];               // chunk sum
+      p1[o + j] = b[j] - a[j] * dm;    // chunk M2 = sum d^2 - (sum d)^2 / n (about the chunk mean)
     }
   } else {
 #pragma unroll
@@ -157,31 +165,35 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
                                                       int64_t M, int64_t C, int64_t R, float momentum, float eps,
                                                       float* __restrict__ rmean, float* __restrict__ rvar,
                                                       float* __restrict__ save_mean,
-                                                      float* __restrict__ save_invstd, int64_t chunk_rows,
+                                                      float* __restrict__ save_invstd,
+                                                      float* __restrict__ save_mean_lo, int64_t chunk_rows,
                                                       int64_t hw) {
   // chunk r covers rows [r*chunk_rows, min((r+1)*chunk_rows, M)) of hw elements each (hw = 1 for
-  // BatchNorm1d; H*W for the NCHW BatchNorm2d)
-  __shared__ double sn[FIN_GROUPS][FIN_COLS], sm[FIN_GROUPS][FIN_COLS], sq[FIN_GROUPS][FIN_COLS];
+  // BatchNorm1d; H*W for the NCHW BatchNorm2d); p0 = chunk sum, p1 = chunk M2 about its mean
+  __shared__ double sn[FIN_GROUPS][FIN_COLS], sm[FIN_GROUPS][FIN_COLS], sq[FIN_GROUPS][FIN_COLS],
+      ss[FIN_GROUPS][FIN_COLS];
   const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
   const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+  double n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
   if (c < C) {
     for (int64_t r = grp; r < R; r += FIN_GROUPS) {  // Chan et al. merge, fixed order
       const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
       const double nb = (double)((hi - r * chunk_rows) * hw);
-      const double mb = p0[r * C + c], m2b = p1[r * C + c];
+      const double mb = p0[r * C + c] / nb, m2b = p1[r * C + c];
       const double nt = n + nb, delta = mb - mean;
       mean += delta * nb / nt;
       m2 += m2b + delta * delta * n * nb / nt;
       n = nt;
+      sum += p0[r * C + c];
     }
   }
   sn[grp][lc] = n;
   sm[grp][lc] = mean;
   sq[grp][lc] = m2;
+  ss[grp][lc] = sum;
   __syncthreads();
   if (grp != 0 || c >= C) return;
-  n = 0.0, mean = 0.0, m2 = 0.0;
+  n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
   for (int gI = 0; gI < FIN_GROUPS; ++gI) {
     const double nb = sn[gI][lc];
     if (nb == 0.0) continue;
@@ -189,10 +201,14 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
     mean += delta * nb / nt;
     m2 += sq[gI][lc] + delta * delta * n * nb / nt;
     n = nt;
+    sum += ss[gI][lc];
   }
   double var = m2 / n;
   if (var < 0.0) var = 0.0;
-  save_mean[c] = (float)mean;
+  mean = sum / n;                      // the exact batch sum / n: one rounding in double
+  const float mh = (float)mean;
+  save_mean[c] = mh;
+  if (save_mean_lo) save_mean_lo[c] = (float)(mean - (double)mh);
   save_invstd[c] = (float)(1.0 / std::sqrt(var + (double)eps));
   if (rmean != nullptr && momentum >= 0.f) {
     const double unb = n > 1.0 ? m2 / (n - 1.0) : var;
@@ -225,6 +241,7 @@ inline dim3 apply_grid(int64_t M, int64_t C) {
 
 __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, int64_t M, int64_t C,
                                                   const float* __restrict__ mean,
+                                                  const float* __restrict__ mean_lo,
                                                   const float* __restrict__ invstd,
                                                   const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int hardtanh,
@@ -232,9 +249,10 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
-  const float4 mv = ld4(mean + c), iv = ld4(invstd + c);
+  const float4 mv = ld4(mean + c), iv = ld4(invstd + c), lv = ld4_or(mean_lo, c, 0.f);
   const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
   const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
   const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
   for (int64_t r = r0; r < r1; ++r) {
     const float4 xv = ld4(x + r * C + c);
@@ -243,7 +261,7 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      v[j] = fmaf((xs[j] - mu[j]) * is[j], ga[j], be[j]);
+      v[j] = fmaf(((xs[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]);
       if (hardtanh) v[j] = fminf(fmaxf(v[j], -1.f), 1.f);
     }
     *reinterpret_cast<float4*>(y + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
@@ -277,6 +295,7 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                       int64_t M, int64_t C, const float* __restrict__ mean,
+                                                      const float* __restrict__ mean_lo,
                                                       const float* __restrict__ invstd,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int hardtanh,
@@ -289,8 +308,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
   if (c >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
   const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
-  const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f);
+  const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f), lv = ld4_or(mean_lo, c, 0.f);
   const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
   const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
   const float a0[4] = {s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n};
   const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
@@ -302,7 +322,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float xh = (xs[j] - ms[j]) * is[j];
+      const float xh = ((xs[j] - ms[j]) - lo[j]) * is[j];
       const float yv = fmaf(xh, ga[j], be[j]);
       const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
       o[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
@@ -438,7 +458,7 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__
     block_sum2(a, b);
     if (threadIdx.x == 0) {
       const double nb = (double)((n1 - n0) * HW), dm = a / nb;
-      p0[r * C + c] = (double)shift + dm;
+      p0[r * C + c] = (double)shift * nb + a;   // chunk sum
       p1[r * C + c] = b - a * dm;
     }
     return;
@@ -608,9 +628,9 @@ BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
 
 static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
-                             float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
-                             void* stream, Drop dp) {
-  if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !work || !vec_ok(y) ||
+                             float* save_mean, float* save_invstd, float* save_mean_lo, float* y,
+                             int32_t hardtanh, void* work, void* stream, Drop dp) {
+  if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !work || !vec_ok(y) || !vec_ok(save_mean_lo) ||
       (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) || !vec_ok(beta) ||
       !aligned16(save_mean) || !aligned16(save_invstd)) {
     set_error("bnn_bn_fwd_train: bad arguments (M=%lld C=%lld; C must be a multiple of 4, M > 0)",
@@ -621,34 +641,36 @@ static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* 
   const int64_t R = bn_chunks(M);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
+  // without a caller buffer the lo part of the mean lives in the workspace (the bwd's k0 slot)
+  float* lo = save_mean_lo ? save_mean_lo : reinterpret_cast<float*>(p1 + R * C);
   hipLaunchKernelGGL(bn_reduce_k<0>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x,
-                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, dp);
-  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R,
-                     momentum, eps, running_mean, running_var, save_mean, save_invstd, (int64_t)BN_ROWS, (int64_t)1);
+                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, dp);
+  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
+                     running_var, save_mean, save_invstd, lo, (int64_t)BN_ROWS, (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
-    hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, save_invstd,
+    hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, lo, save_invstd,
                        gamma, beta, hardtanh, y, dp);
   return check_launch("bnn_bn_fwd_train");
 }
 
 BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
-                             float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
-                             void* stream) {
+                             float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
+                             void* work, void* stream) {
   return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
-                           y, hardtanh, work, stream, make_drop(0.f, 0));
+                           save_mean_lo, y, hardtanh, work, stream, make_drop(0.f, 0));
 }
 
 BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                                      float* running_mean, float* running_var, float momentum, float eps,
-                                     float* save_mean, float* save_invstd, float* y, int32_t hardtanh, float p,
-                                     uint64_t seed, void* work, void* stream) {
+                                     float* save_mean, float* save_invstd, float* save_mean_lo, float* y,
+                                     int32_t hardtanh, float p, uint64_t seed, void* work, void* stream) {
   if (!(p >= 0.f && p < 1.f)) {
     set_error("bnn_bn_dropout_fwd_train: p must be in [0, 1) (got %g)", (double)p);
     return kErrInval;
   }
   return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
-                           y, hardtanh, work, stream, make_drop(p, seed));
+                           save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed));
 }
 
 BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -662,18 +684,19 @@ BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* g
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* istd = reinterpret_cast<float*>(work);
   hipLaunchKernelGGL(bn_invstd_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_var, istd, C, eps);
-  hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, running_mean, istd, gamma,
+  hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, running_mean, nullptr, istd, gamma,
                      beta, hardtanh, y);
   return check_launch("bnn_bn_fwd_eval");
 }
 
 static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
-                       const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
+                       const float* beta, const float* save_mean, const float* save_invstd,
+                       const float* save_mean_lo, int32_t hardtanh,
                        float* dx, float* dgamma, float* dbeta, void* work, void* stream, Drop dp,
                        bool batch_stats) {
   if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work ||
       (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
-      !aligned16(save_invstd)) {
+      !aligned16(save_invstd) || !vec_ok(save_mean_lo)) {
     set_error("bnn_bn_bwd: bad arguments");
     return kErrInval;
   }
@@ -684,40 +707,41 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
-                     M, C, save_mean, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
+                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
-    hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean,
+    hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo,
                        save_invstd, gamma, beta, hardtanh, k0, k1, batch_stats ? 1.f / (float)M : 0.f, dx, dp);
   }
   return check_launch("bnn_bn_bwd");
 }
 
 BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
-                       const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
-                       float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
-  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
-                     make_drop(0.f, 0), true);
+                       const float* beta, const float* save_mean, const float* save_invstd,
+                       const float* save_mean_lo, int32_t hardtanh, float* dx, float* dgamma, float* dbeta,
+                       void* work, void* stream) {
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dx, dgamma, dbeta,
+                     work, stream, make_drop(0.f, 0), true);
 }
 
 BNN_API int bnn_bn_bwd_eval(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                             const float* beta, const float* running_mean, const float* invstd, int32_t hardtanh,
                             float* dx, float* dgamma, float* dbeta, void* work, void* stream) {
-  return bn_bwd_impl(x, dy, M, C, gamma, beta, running_mean, invstd, hardtanh, dx, dgamma, dbeta, work, stream,
-                     make_drop(0.f, 0), false);
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, running_mean, invstd, nullptr, hardtanh, dx, dgamma, dbeta, work,
+                     stream, make_drop(0.f, 0), false);
 }
 
 BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                                const float* beta, const float* save_mean, const float* save_invstd,
-                               int32_t hardtanh, float p, uint64_t seed, float* dx, float* dgamma, float* dbeta,
-                               void* work, void* stream) {
+                               const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                               float* dgamma, float* dbeta, void* work, void* stream) {
   if (!(p >= 0.f && p < 1.f)) {
     set_error("bnn_bn_dropout_bwd: p must be in [0, 1) (got %g)", (double)p);
     return kErrInval;
   }
-  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, hardtanh, dx, dgamma, dbeta, work, stream,
-                     make_drop(p, seed), true);
+  return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dx, dgamma, dbeta,
+                     work, stream, make_drop(p, seed), true);
 }
 
 __global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d, float* __restrict__ out) {
@@ -764,7 +788,7 @@ BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, 
   hipLaunchKernelGGL((bn2d_reduce_k<0, 0>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s, x, nullptr, N, C,
                      (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
   hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
-                     momentum, eps, running_mean, running_var, save_mean, save_invstd, CR, H * W);
+                     momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
   BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
                                            (int)W, save_mean, save_invstd, gamma, beta, hardtanh, y));

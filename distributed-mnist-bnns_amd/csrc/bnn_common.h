@@ -96,6 +96,8 @@ struct AdamArgs {
 void adam_bias_correction(float lr, float beta1, float beta2, int64_t step, float* step_size, float* bc2_sqrt);
 
 __device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v, const AdamArgs& a) {
+  // no mul+add contraction: both kernels that inline this must round every step identically
+#pragma clang fp contract(off)
   const float gi = g * a.gscale;
   m = m + (1.f - a.b1) * (gi - m);
   v = fmaf((1.f - a.b2) * gi, gi, v * a.b2);

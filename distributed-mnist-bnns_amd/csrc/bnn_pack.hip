@@ -49,6 +49,7 @@ __device__ __forceinline__ uint32_t fp4_code(int s) { return s > 0 ? 0x2u : (s <
 // fused BN -> Hardtanh -> sign path sees bit-identical y (Hardtanh does not change a sign).
 struct ColAffine {
   const float* mean;
+  const float* mean_lo;  // nullable: the lo part of the batch mean (bnn_bn.hip), x - mean = (x - hi) - lo
   const float* invstd;
   const float* gamma;  // nullable
   const float* beta;   // nullable
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
   __shared__ int tile[TILE][TILE + 1];
   const int64_t k0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
-  float mu[16], is[16], ga[16], be[16];
+  float mu[16], lo[16], is[16], ga[16], be[16];
   if (AFF) {
     // per-column parameters for columns k0+c .. +15: float4 loads when the run is in range
     const int64_t cb = k0 + c;
@@ -116,7 +117,9 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
         const float4 b = *reinterpret_cast<const float4*>(af.invstd + cb + 4 * i);
         const float4 g = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb + 4 * i) : make_float4(1, 1, 1, 1);
         const float4 e = af.beta ? *reinterpret_cast<const float4*>(af.beta + cb + 4 * i) : make_float4(0, 0, 0, 0);
+        const float4 l = af.mean_lo ? *reinterpret_cast<const float4*>(af.mean_lo + cb + 4 * i) : make_float4(0, 0, 0, 0);
         mu[4 * i] = a.x; mu[4 * i + 1] = a.y; mu[4 * i + 2] = a.z; mu[4 * i + 3] = a.w;
+        lo[4 * i] = l.x; lo[4 * i + 1] = l.y; lo[4 * i + 2] = l.z; lo[4 * i + 3] = l.w;
         is[4 * i] = b.x; is[4 * i + 1] = b.y; is[4 * i + 2] = b.z; is[4 * i + 3] = b.w;
         ga[4 * i] = g.x; ga[4 * i + 1] = g.y; ga[4 * i + 2] = g.z; ga[4 * i + 3] = g.w;
         be[4 * i] = e.x; be[4 * i + 1] = e.y; be[4 * i + 2] = e.z; be[4 * i + 3] = e.w;
@@ -126,6 +129,7 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
       for (int j = 0; j < 16; ++j) {
         const bool in = cb + j < K;
         mu[j] = in ? af.mean[cb + j] : 0.f;
+        lo[j] = (in && af.mean_lo) ? af.mean_lo[cb + j] : 0.f;
         is[j] = in ? af.invstd[cb + j] : 0.f;
         ga[j] = (in && af.gamma) ? af.gamma[cb + j] : 1.f;
         be[j] = (in && af.beta) ? af.beta[cb + j] : 0.f;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
     const int64_t cb = k0 + c;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      v[j] = (m < M && cb + j < K) ? fmaf((v[j] - mu[j]) * is[j], ga[j], be[j]) : 0.f;
+      v[j] = (m < M && cb + j < K) ? fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]) : 0.f;
   }
   int s[16];
 #pragma unroll
@@ -611,7 +615,8 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
 }
 
 BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
-                              const float* gamma, const float* beta, int32_t fmt, void* q, int64_t ldq,
+                              const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
+                              int64_t ldq,
                               int8_t* qt, int64_t ldqt, void* stream) {
   const int64_t need = fmt == 1 ? round_up(C, 256) / 2 : round_up(C, TILE);
   if (!x || !mean || !invstd || M < 0 || C < 0 || (fmt != 0 && fmt != 1) || (!q && !qt) ||
@@ -630,9 +635,9 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
     set_error("bnn_bn_apply_pack: M too large for one launch (%lld)", (long long)M);
     return kErrInval;
   }
-  const ColAffine af{mean, invstd, gamma, beta,
+  const ColAffine af{mean, mean_lo, invstd, gamma, beta,
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
-                         (!beta || aligned16(beta))};
+                         (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
   // 4 row tiles per workgroup when that still leaves >= 8K workgroups (amortised parameter loads)
   const int rt = (gx * ((gy + 3) / 4) >= 8192) ? 4 : 1;
   const unsigned gyr = (unsigned)((gy + rt - 1) / rt);

@@ -154,18 +154,24 @@ int bnn_conv_set_mfma(int32_t on);
  * x, y, dy, dx fp32 [M][C] row-major, C % 4 == 0, 16-B aligned; gamma/beta nullable (affine off);
  * running_mean/var nullable in train mode (track_running_stats off; momentum < 0 skips the update).
  * `work` scratch of bnn_bn_workspace(M, C) bytes.  Deterministic (fixed-order reductions).
- * bnn_bn_fwd_train with y == NULL computes the statistics only (for bnn_bn_apply_pack). */
+ * bnn_bn_fwd_train with y == NULL computes the statistics only (for bnn_bn_apply_pack).
+ * The batch mean is the batch sum taken in double (exact for integer-plus-bias pre-activations)
+ * divided by M, returned as save_mean (fp32) + save_mean_lo (fp32, nullable: the rounding
+ * remainder); every pass that normalises computes x - mean as (x - save_mean) - save_mean_lo,
+ * so a value within an ulp of the mean (a BatchNorm near-tie, frequent when x is integer-valued)
+ * gets the sign of the exact difference, as the reference's (double-accumulated) CPU BatchNorm
+ * gives it.  Pass the same save_mean_lo to the backward / apply-pack calls (NULL = 0). */
 int64_t bnn_bn_workspace(int64_t M, int64_t C);
 int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps,
-                     float* save_mean, float* save_invstd, float* y, int32_t hardtanh, void* work,
-                     bnn_stream_t stream);
+                     float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
+                     void* work, bnn_stream_t stream);
 int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                     const float* running_mean, const float* running_var, float eps, float* y,
                     int32_t hardtanh, void* work, bnn_stream_t stream);
 int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
-               const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
-               float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
+               const float* beta, const float* save_mean, const float* save_invstd, const float* save_mean_lo,
+               int32_t hardtanh, float* dx, float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
 /* Backward of the eval-mode forward (running statistics are constants, torch's
  * batch_norm_backward with training=False): dx = gamma*invstd*g, dgamma = sum g*xhat,
  * dbeta = sum g, with invstd = 1/sqrt(running_var + eps). */
@@ -207,23 +213,23 @@ int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int
  * writes the mask the fused passes use (scale or 0 per element, n = M*C) for tests. */
 int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
-                             float* save_mean, float* save_invstd, float* y, int32_t hardtanh, float p,
-                             uint64_t seed, void* work, bnn_stream_t stream);
+                             float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
+                             float p, uint64_t seed, void* work, bnn_stream_t stream);
 int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
-                       const float* beta, const float* save_mean, const float* save_invstd, int32_t hardtanh,
-                       float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, void* work,
-                       bnn_stream_t stream);
+                       const float* beta, const float* save_mean, const float* save_invstd,
+                       const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                       float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
 
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
- * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = (x-mean)*invstd*gamma+beta exactly as
+ * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = ((x-mean)-mean_lo)*invstd*gamma+beta exactly as
  * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0
  * (int8, ldq >= round_up(C,64)) or fmt 1 (FP4 nibbles, ldq bytes >= round_up(C,256)/2, multiple
  * of 128) and/or the int8 transpose qt [C][ldqt] for the weight gradient; no fp32 activation is
  * written (Hardtanh keeps the sign; its backward mask is recomputed from x by bnn_bn_bwd). */
 int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
-                      const float* gamma, const float* beta, int32_t fmt, void* q, int64_t ldq,
-                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+                      const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
+                      int64_t ldq, int8_t* qt, int64_t ldqt, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */

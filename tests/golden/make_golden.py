@@ -125,6 +125,18 @@ def trace_case(name, gen, org_protocol, steps=3, batch=16, widths=(48, 32, 24), 
     opt = torch.optim.Adam(net.parameters(), lr=lr)
     crit = nn.CrossEntropyLoss()
     rec = {"init/" + k: v for k, v in init.items()}
+    # the reference's binarized hidden activations: BinarizeLinear leaves sign(input) in the
+    # caller's tensor (binarized_modules.py:75-76), recorded from fc2 / fc3 after each call, so a
+    # replay can tell BatchNorm near-tie resolutions (implementation rounding) from real errors
+    acts = {}
+
+    def keep(name):
+        def hook(mod, inp, out):
+            acts[name] = np32(inp[0]).astype(np.int8)
+        return hook
+
+    net.fc2.register_forward_hook(keep("fc2_in"))
+    net.fc3.register_forward_hook(keep("fc3_in"))
     net.train()
     for s in range(steps):
         x = mnist_like(gen, (batch, 1, 28, 28))
@@ -137,6 +149,8 @@ def trace_case(name, gen, org_protocol, steps=3, batch=16, widths=(48, 32, 24), 
         loss.backward()
         rec[f"s{s}/out"] = np32(out)
         rec[f"s{s}/loss"] = np.array(loss.item(), np.float64)
+        for k, v in acts.items():
+            rec[f"s{s}/act/{k}"] = v
         named = dict(net.named_parameters())
         for k in PARAM_NAMES:
             rec[f"s{s}/grad/{k}"] = np32(named[k].grad)

@@ -42,9 +42,12 @@ def host(t):
     return t.detach().cpu().numpy()
 
 
-def bn_sign_ref(z, mean, invstd, gamma, beta):
-    """sign(fmaf((z - mean) * invstd, gamma, beta)) with fp32 z - mean and fp32 product."""
+def bn_sign_ref(z, mean, invstd, gamma, beta, lo=None):
+    """sign(fmaf(((z - mean) - lo) * invstd, gamma, beta)), every step rounded to fp32 as the
+    kernels do (lo: the remainder of the double batch mean, bnn.h)."""
     t = (z.astype(np.float32) - mean.astype(np.float32)).astype(np.float32)
+    if lo is not None:
+        t = (t - lo.astype(np.float32)).astype(np.float32)
     t = (t * invstd.astype(np.float32)).astype(np.float32)
     y = t.astype(np.float64) * gamma.astype(np.float64) + beta.astype(np.float64)
     return np.sign(y).astype(np.int8), y
@@ -66,10 +69,11 @@ def bn_stats(F, z, C):
     M = z.shape[0]
     mean = torch.empty(C, device="cuda")
     invstd = torch.empty(C, device="cuda")
+    lo = torch.empty(C, device="cuda")
     ws = torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device="cuda")
     L.call("bnn_bn_fwd_train", L.ptr(z), M, C, None, None, None, None, -1.0, 1e-5, L.ptr(mean), L.ptr(invstd),
-           None, 1, L.ptr(ws), L.stream())
-    return mean, invstd
+           L.ptr(lo), None, 1, L.ptr(ws), L.stream())
+    return mean, invstd, lo
 
 
 @pytest.mark.parametrize("M,C", [(300, 192), (1000, 1536), (77, 260), (4096, 768)])
@@ -87,16 +91,19 @@ def test_bn_apply_pack_bit_exact(F, M, C, fmt, with_qt):
     beta = rng.uniform(-0.3, 0.3, C).astype(np.float32)
     beta[7] = 0.0
     zt = dev(z)
-    mean, invstd = bn_stats(F, zt, C)
-    s_ref, _ = bn_sign_ref(z, host(mean), host(invstd), gamma, beta)
+    mean, invstd, lo = bn_stats(F, zt, C)
+    s_ref, _ = bn_sign_ref(z, host(mean), host(invstd), gamma, beta, host(lo))
+    # the batch mean is the exact sum / M: hi + lo reproduce it to double precision
+    mean64 = z.astype(np.float64).mean(0)
+    assert np.abs(host(mean).astype(np.float64) + host(lo) - mean64).max() <= 1e-12 * np.abs(mean64).max()
     assert (s_ref == 0).any()                            # the ternary zero is exercised
     if fmt == 1:
         q = torch.full((M, F.round_up(C, 256) // 2), 0x55, dtype=torch.uint8, device="cuda")
     else:
         q = torch.full((M, F.round_up(C)), 9, dtype=torch.int8, device="cuda")
     qt = torch.full((C, F.round_up(M)), 9, dtype=torch.int8, device="cuda") if with_qt else None
-    L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(dev(gamma)), L.ptr(dev(beta)),
-           fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    gt, bt = dev(gamma), dev(beta)           # keep the device copies alive across the launch
+    L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo), L.ptr(gt), L.ptr(bt), fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
     qh = host(q)
     rows = decode_fp4(qh, C) if fmt == 1 else qh.astype(np.int8)
     assert np.array_equal(rows[:, :C], s_ref)
@@ -133,15 +140,17 @@ def test_bn_hardtanh_binary_linear_vs_float64(F, M, C, N, backend, training):
     fc.bias = torch.nn.Parameter(dev(b))
     zt = dev(z).requires_grad_(True)
     if training:
-        mean, invstd = bn_stats(F, dev(z), C)       # the same reduction the fused op runs
+        mean, invstd, lo = bn_stats(F, dev(z), C)       # the same reduction the fused op runs
+        lo_h = host(lo)
     else:
         mean, invstd = bn.running_mean.clone(), (bn.running_var + bn.eps).rsqrt()
+        lo_h = None
     mean_h, inv_h = host(mean), host(invstd)
     rm0 = host(bn.running_mean).astype(np.float64)
     rv0 = host(bn.running_var).astype(np.float64)
     y = F.bn_hardtanh_binary_linear(zt, bn, fc, backend)
     # forward: sign(BN(z)) with the GPU's statistics -> exact integer GEMM -> one fp32 bias add
-    s, ybn = bn_sign_ref(z, mean_h, inv_h, gamma, beta)
+    s, ybn = bn_sign_ref(z, mean_h, inv_h, gamma, beta, lo_h)
     y_ref = (s.astype(np.int64) @ np.sign(w).astype(np.int64).T).astype(np.float32) + b
     assert np.array_equal(host(y), y_ref)
     if training:
