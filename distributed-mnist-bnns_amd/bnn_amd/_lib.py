@@ -22,7 +22,7 @@ SIGNATURES = {
     "bnn_version": (I32, []),
     "bnn_last_error": (ctypes.c_char_p, []),
     "bnn_sign_pack_i8": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
-    "bnn_sign_pack_fp4": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
+    "bnn_sign_pack_fp4": (I32, [P, I64, I64, I64, P, I64, P, I64, I32, P]),
     "bnn_sign_f32": (I32, [P, P, I64, P]),
     "bnn_sign_pack_bits": (I32, [P, I64, I64, I64, P, P, I64, P]),
     "bnn_quant_rows": (I32, [P, I64, I64, I64, P, I64, I64, P, P]),
@@ -52,10 +52,18 @@ SIGNATURES = {
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
-    "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, P]),
+    "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
-    "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, P]),
+    "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,
+                                  P]),
+    "bnn_quant6_scale_rows": (I64, [I64]),
+    "bnn_quant6_rows": (I32, [P, I64, I64, I64, I64, P, P, P, P]),
+    "bnn_quant6_cols_workspace": (I64, [I64, I64]),
+    "bnn_quant6_cols_t": (I32, [P, I64, I64, I64, I64, P, P, P, P, P, P]),
+    "bnn_gemm_fp6": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_fp6_kernel": (ctypes.c_char_p, [I64, I64]),
+    "bnn_gemm_fp6_set_variant": (I32, [I32]),
 }
 
 _lib = None

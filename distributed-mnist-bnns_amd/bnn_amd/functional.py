@@ -19,6 +19,7 @@ from . import _lib as L
 
 __all__ = [
     "KernelTimer", "timing", "sign", "sign_pack", "sign_pack_bits", "quant_rows", "quant_cols_t", "gemm_i8", "gemm_xnor",
+    "quant6_rows", "quant6_cols_t", "gemm_fp6", "set_digit_gemm",
     "binary_linear", "binary_conv2d", "hardtanh_backward", "adam_clamp_", "adam_clamp_pack_", "packed_weight",
     "invalidate_packed", "batch_norm_hardtanh",
     "bn_hardtanh_binary_linear", "batch_norm2d_hardtanh_pool", "dropout_batch_norm_hardtanh", "dropout_mask",
@@ -138,18 +139,26 @@ def sign_pack(x, want_q=True, want_qt=False):
     return q, qt
 
 
-def sign_pack_fp4(x, want_qt=False):
-    """fp32 [M,K] -> (q4 uint8 [M, ldq4] FP4 e2m1 ternary nibbles, qt int8 [K, ldqt] or None).
-    ldq4 = round_up(K, 256) / 2 bytes (zero nibbles beyond K)."""
+def _qt_buffer(K, M, qt_fmt, device):
+    """The transposed ternary operand [K, .] of an [M, K] matrix: int8 (qt_fmt "i8") or FP4
+    nibbles (qt_fmt "fp4": round_up(M, 256) / 2 bytes per row, the B operand of gemm_fp6)."""
+    if qt_fmt == "fp4":
+        return torch.empty((K, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
+    return torch.empty((K, round_up(M)), dtype=torch.int8, device=device)
+
+
+def sign_pack_fp4(x, want_qt=False, qt_fmt="i8", want_q=True):
+    """fp32 [M,K] -> (q4 uint8 [M, ldq4] FP4 e2m1 ternary nibbles, qt [K, ldqt] or None).
+    ldq4 = round_up(K, 256) / 2 bytes (zero nibbles beyond K); qt as _qt_buffer."""
     _check(x)
     x = _c2d(x)
     M, K = x.shape
-    q4 = torch.empty((M, round_up(K, 256) // 2), dtype=torch.uint8, device=x.device)
-    qt = torch.empty((K, round_up(M)), dtype=torch.int8, device=x.device) if want_qt else None
-    nbytes = 4 * M * K + q4.numel() + (qt.numel() if qt is not None else 0)
+    q4 = torch.empty((M, round_up(K, 256) // 2), dtype=torch.uint8, device=x.device) if want_q else None
+    qt = _qt_buffer(K, M, qt_fmt, x.device) if want_qt else None
+    nbytes = 4 * M * K + (q4.numel() if q4 is not None else 0) + (qt.numel() if qt is not None else 0)
     with _timed("sign_pack_tile_k<1>", 0, nbytes):
-        L.call("bnn_sign_pack_fp4", L.ptr(x), M, K, K, L.ptr(q4), q4.shape[1], L.ptr(qt),
-               qt.shape[1] if qt is not None else 0, L.stream())
+        L.call("bnn_sign_pack_fp4", L.ptr(x), M, K, K, L.ptr(q4), q4.shape[1] if q4 is not None else 0,
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if qt_fmt == "fp4" else 0, L.stream())
     return q4, qt
 
 
@@ -210,22 +219,25 @@ def invalidate_packed(w):
         del w._bnn_pack
 
 
-def packed_weight(weight, fmt, want_q, want_qt, cache=True):
-    """(q, qt) of sign(weight) [N,K]: q = FP4 rows (fmt "fp4") or int8 rows (fmt "i8"), qt = int8
-    transpose [K, round_up(N)].  With ``cache`` the operands are kept on the Parameter."""
+def packed_weight(weight, fmt, want_q, want_qt, cache=True, qt_fmt="i8"):
+    """(q, qt) of sign(weight) [N,K]: q = FP4 rows (fmt "fp4") or int8 rows (fmt "i8"), qt = the
+    transpose [K, .] in qt_fmt ("i8" or "fp4", _qt_buffer).  With ``cache`` the operands are kept
+    on the Parameter."""
     ent = getattr(weight, "_bnn_pack", None) if cache else None
-    if ent is not None and ent["key"] == _pack_key(weight) and ent["fmt"] == fmt \
+    same = ent is not None and ent["fmt"] == fmt and ent["qt_fmt"] == qt_fmt
+    if same and ent["key"] == _pack_key(weight) \
             and (ent["q"] is not None or not want_q) and (ent["qt"] is not None or not want_qt):
         return ent["q"], ent["qt"]
-    if ent is not None and ent["fmt"] == fmt:      # keep producing what earlier forwards needed
+    if same:                                    # keep producing what earlier forwards needed
         want_q = want_q or ent["q"] is not None
         want_qt = want_qt or ent["qt"] is not None
-    if fmt == "fp4":
-        q, qt = sign_pack_fp4(weight, want_qt=want_qt) if want_q else sign_pack(weight, False, True)
+    if fmt == "fp4" or qt_fmt == "fp4":
+        assert fmt == "fp4" or not want_q, "int8 rows with an FP4 transpose are not a supported pairing"
+        q, qt = sign_pack_fp4(weight, want_qt=want_qt, qt_fmt=qt_fmt, want_q=want_q)
     else:
         q, qt = sign_pack(weight, want_q=want_q, want_qt=want_qt)
     if cache:
-        weight._bnn_pack = {"key": _pack_key(weight), "fmt": fmt, "q": q, "qt": qt}
+        weight._bnn_pack = {"key": _pack_key(weight), "fmt": fmt, "qt_fmt": qt_fmt, "q": q, "qt": qt}
     return q, qt
 
 
@@ -247,7 +259,7 @@ def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.
         L.call("bnn_adam_clamp_pack", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
                float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale), int(bool(clamp)),
                1 if ent["fmt"] == "fp4" else 0, L.ptr(q), q.shape[1] if q is not None else 0,
-               L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if ent["qt_fmt"] == "fp4" else 0, L.stream())
     ent["key"] = _pack_key(p)
     return True
 
@@ -308,6 +320,80 @@ def gemm_xnor(a_bits, b_bits, M, N, bias=None):
     return C
 
 
+# ----------------------------------------------------------------------------- fp32 x ternary on the FP6 MFMA
+# The fp32 operand (dY in both backward GEMMs, the pixels of the first layer) as 4 FP6 digit
+# planes with per-32-element block scales (bnn_gemm6.hip); the ternary operand as FP4.  "i8"
+# selects the int8 3-digit-plane form (bnn_gemm.hip) instead -- kept for cross-checks.
+DIGIT_GEMM = "fp6"
+
+
+def set_digit_gemm(kind):
+    global DIGIT_GEMM
+    if kind not in ("fp6", "i8"):
+        raise ValueError(kind)
+    DIGIT_GEMM = kind
+
+
+class Fp6Operand:
+    """4 FP6 digit planes of an fp32 matrix [rows, K] (blocks of 32 along K, padded to Kp)."""
+    __slots__ = ("lo", "hi", "sc", "rows", "Kp")
+
+    def __init__(self, lo, hi, sc, rows, Kp):
+        self.lo, self.hi, self.sc, self.rows, self.Kp = lo, hi, sc, rows, Kp
+
+
+def _fp6_buffers(rows, Kp, device):
+    nb = Kp // 32
+    lo = torch.empty((rows, nb * 64), dtype=torch.uint8, device=device)
+    hi = torch.empty((rows, nb * 32), dtype=torch.uint8, device=device)
+    sc = torch.zeros((Kp // 64, L.lib().bnn_quant6_scale_rows(rows), 2), dtype=torch.uint8, device=device)
+    return lo, hi, sc
+
+
+def quant6_rows(x):
+    """fp32 [M,K] -> Fp6Operand of its rows (Kp = round_up(K, 64))."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    Kp = round_up(K)
+    lo, hi, sc = _fp6_buffers(M, Kp, x.device)
+    with _timed("quant6_rows_k", 0, 4 * M * K + 3 * M * Kp + M * Kp // 32):
+        L.call("bnn_quant6_rows", L.ptr(x), M, K, K, Kp, L.ptr(lo), L.ptr(hi), L.ptr(sc), L.stream())
+    return Fp6Operand(lo, hi, sc, M, Kp)
+
+
+def quant6_cols_t(x, want_colsum=False):
+    """fp32 [M,N] -> (Fp6Operand of x^T [N, Mp], colsum [N] or None)."""
+    _check(x)
+    x = _c2d(x)
+    M, N = x.shape
+    Mp = round_up(M)
+    lo, hi, sc = _fp6_buffers(N, Mp, x.device)
+    cs = ws = None
+    if want_colsum:
+        cs = torch.empty((N,), dtype=torch.float32, device=x.device)
+        ws = torch.empty((L.lib().bnn_quant6_cols_workspace(M, N),), dtype=torch.uint8, device=x.device)
+    with _timed("quant6_cols_t_k", 0, 4 * M * N + 3 * N * Mp + N * Mp // 32):
+        L.call("bnn_quant6_cols_t", L.ptr(x), M, N, N, Mp, L.ptr(lo), L.ptr(hi), L.ptr(sc), L.ptr(cs), L.ptr(ws),
+               L.stream())
+    return Fp6Operand(lo, hi, sc, N, Mp), cs
+
+
+def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None):
+    """C[A.rows, N] = A . B4^T (+ bias): A an Fp6Operand, B4 FP4 nibbles [N, >= A.Kp/2 bytes]."""
+    M, K = A.rows, A.Kp
+    assert B4.dtype == torch.uint8 and B4.shape[0] == N and 2 * B4.shape[1] >= K
+    C = torch.empty((M, N), dtype=torch.float32, device=B4.device) if out is None else out
+    if M == 0 or N == 0:
+        return C
+    k_true = K if k_true is None else k_true
+    name = L.lib().bnn_gemm_fp6_kernel(M, N).decode() if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):
+        L.call("bnn_gemm_fp6", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
+               L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
+    return C
+
+
 # ----------------------------------------------------------------------------- linear
 class BinaryLinearFunction(torch.autograd.Function):
     """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
@@ -325,10 +411,12 @@ class BinaryLinearFunction(torch.autograd.Function):
         ctx.empty = False
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         b = bias.detach() if bias is not None else None
+        ctx.fp6 = backend == "fp4" and DIGIT_GEMM == "fp6"
+        qf = "fp4" if ctx.fp6 else "i8"
         if binarize_input:
             if backend == "fp4":
-                x4, xqt = sign_pack_fp4(x, want_qt=need_dw)
-                w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache)
+                x4, xqt = sign_pack_fp4(x, want_qt=need_dw, qt_fmt=qf)
+                w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache, qt_fmt=qf)
                 y = gemm_fp4(x4, w4, M, N, bias=b, k_true=K)
             elif backend == "xnor":
                 y = gemm_xnor(sign_pack_bits(x), sign_pack_bits(weight), M, N, bias=b)
@@ -339,6 +427,10 @@ class BinaryLinearFunction(torch.autograd.Function):
                 wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
                 y = gemm_i8(xq, 1, wq, 1, M, N, bias=b, k_true=K)
             ctx.save_for_backward(xqt, wqt)
+        elif ctx.fp6:                               # first layer: fp32 pixels x W_b on the FP6 MFMA
+            w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache, qt_fmt=qf)
+            y = gemm_fp6(quant6_rows(x), w4, N, bias=b, k_true=K)
+            ctx.save_for_backward(x if need_dw else None, wqt)
         else:
             wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
             xd, sx = quant_rows(x)
@@ -359,10 +451,22 @@ class BinaryLinearFunction(torch.autograd.Function):
         xs, wqt = ctx.saved_tensors
         dy = _c2d(dy)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            d, s = quant_rows(dy)                                   # [3, M, ldN]
-            dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.fp6 and (ctx.binarize_input or not ctx.needs_input_grad[1]):
+            if ctx.needs_input_grad[0]:
+                dx = gemm_fp6(quant6_rows(dy), wqt, K, k_true=N)               # dY . W_b
+            if ctx.needs_input_grad[1] or need_db:
+                dt, cs = quant6_cols_t(dy, want_colsum=need_db)
+                if ctx.needs_input_grad[1]:
+                    dw = gemm_fp6(dt, xs, K, k_true=M)                         # dY^T . X_b
+                db = cs
+            return dx, dw, db, None, None, None
+        if ctx.needs_input_grad[0]:
+            if ctx.fp6:
+                dx = gemm_fp6(quant6_rows(dy), wqt, K, k_true=N)
+            else:
+                d, s = quant_rows(dy)                                   # [3, M, ldN]
+                dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
         if ctx.needs_input_grad[1] or need_db:
             dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)      # [3, N, ldM]
             if ctx.needs_input_grad[1]:
@@ -725,15 +829,17 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         need_dh = any(ctx.needs_input_grad[:3])
         need_dw = ctx.needs_input_grad[8]
         fp4 = backend == "fp4"
+        ctx.fp6 = fp4 and DIGIT_GEMM == "fp6"
+        qf = "fp4" if ctx.fp6 else "i8"
         q = torch.empty((M, round_up(C, 256) // 2) if fp4 else (M, round_up(C)),
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
-        qt = torch.empty((C, round_up(M)), dtype=torch.int8, device=z.device) if need_dw else None
+        qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
         with _timed("bn_apply_pack", 0, 4 * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
             L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
                    1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
-                   L.stream())
+                   1 if qf == "fp4" else 0, L.stream())
         b = bias.detach() if bias is not None else None
-        wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True)
+        wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True, qt_fmt=qf)
         if fp4:
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
@@ -752,13 +858,21 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         dz = dgw = dgb = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[9]
         if ctx.needs_input_grad[8] or need_db:
-            dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)
-            if ctx.needs_input_grad[8]:
-                dw = gemm_i8(dt, 3, qt, 1, N, C, a_scale=sc, k_true=M)       # dY^T . sign(h)
+            if ctx.fp6:
+                dt, cs = quant6_cols_t(dy, want_colsum=need_db)
+                if ctx.needs_input_grad[8]:
+                    dw = gemm_fp6(dt, qt, C, k_true=M)                         # dY^T . sign(h)
+            else:
+                dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)
+                if ctx.needs_input_grad[8]:
+                    dw = gemm_i8(dt, 3, qt, 1, N, C, a_scale=sc, k_true=M)
             db = cs
         if any(ctx.needs_input_grad[:3]):
-            d, s = quant_rows(dy)
-            dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)             # dY . W_b
+            if ctx.fp6:
+                dh = gemm_fp6(quant6_rows(dy), wqt, C, k_true=N)               # dY . W_b
+            else:
+                d, s = quant_rows(dy)
+                dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)
             dz = torch.empty_like(z)
             dgw = torch.empty((C,), dtype=torch.float32, device=z.device) if gw is not None else None
             dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None

@@ -1,0 +1,535 @@
+// fp32-operand GEMMs of the binarized layers on the block-scaled FP6 MFMA.
+//
+// The straight-through backward of BinarizeLinear (models/binarized_modules.py:80; autograd:
+// dX = dY.W_b, dW = dY^T.X_b) and the first layer's forward (fp32 pixels x W_b) multiply an fp32
+// operand by a ternary one.  Here the fp32 operand enters v_mfma_scale_f32_32x32x64_f8f6f4 as FOUR
+// FP6 (e2m3) digit planes with one power-of-two scale per 32-element K-block (the instruction's
+// own E8M0 block scales), the ternary operand as FP4 (e2m1, unit scale):
+//
+//   block b of row r (32 consecutive k):  e = exponent with max|x| in [2^(e-1), 2^e)
+//   I = rint(x * 2^(19-e)), |I| <= 2^19, split into balanced base-32 digits
+//   I = d0 + 32 d1 + 1024 d2 + 32768 d3,  d0..d2 in [-16, 15], d3 in [-16, 16]
+//   plane j holds d_j / 8 (exact in e2m3: 0..15 in steps of 1/8 and 16/8 = 2.0) with block
+//   scale 2^(e - 19 + 5j + 3), so the MFMA sums d_j * 2^(e-19+5j) * (+-1 or 0).
+//
+// All four planes of a k-block accumulate into ONE fp32 accumulator.  |x - I*2^(e-19)| <=
+// 2^(e-20) <= max|x_block| * 2^-19, so the norm-wise relative error of a 32-element block is at
+// most sqrt(32) * 2^-19 / ... <= 5.4e-6 (each block's norm is >= its max), ~1e-6 typical; the fp32
+// accumulation over blocks rounds like an fp32 GEMM does (the reference's F.linear backward is
+// one).  Cost: 4 FP6 MFMA passes at the FP4/FP6 rate (2x the int8 rate) = 2 int8-equivalent
+// passes, against 3 for the int8 digit form (bnn_gemm.hip), with one accumulator instead of three.
+//
+// Operand layouts (K = padded reduction length, a multiple of 64; all rows 16-B aligned):
+//   A digits "lo": [rows][K/32][64 B]  -- per block, 16 B per plane: dwords 0..3 of the plane's
+//                                          6-dword MFMA operand (bits 0..127 of the 32 codes)
+//   A digits "hi": [rows][K/32][32 B]  -- per block, 8 B per plane: dwords 4..5 (bits 128..191)
+//   A scales:      [K/64][rows_pad][2] -- E8M0 byte of plane 0 (plane j adds 5j), per block
+//   B ternary:     [rows][ldb bytes]   -- FP4 nibbles, element k in byte k/2 (low nibble even k)
+// The MFMA operand map (checked by tools/probes/probe_fp6.hip on MI355X): lane l holds row l%32,
+// k-block l/32 of the 64-k step, element j at bits 6j..6j+5; the lane's scale byte scales its 32.
+#include <algorithm>
+#include <cmath>
+
+#include "bnn_common.h"
+
+namespace bnn {
+namespace {
+
+constexpr int QB = 32;        // elements per scale block
+constexpr int SCALE_BIAS = 111;  // E8M0 byte of plane 0 = e + 111 (= e - 19 + 3 + 127)
+
+// e2m3 code of the integer digit d in [-16, 16] read as d/8
+__device__ __forceinline__ uint32_t e2m3_code(int d) {
+  const uint32_t s = d < 0 ? 0x20u : 0u;
+  const uint32_t m = (uint32_t)(d < 0 ? -d : d);
+  return s | (m < 8 ? m : (m < 16 ? (0x8u | (m - 8)) : 0x10u));
+}
+
+// Block exponent from the block's |max|: e with amax in [2^(e-1), 2^e); returns the plane-0 E8M0
+// byte (255 = NaN for a non-finite block: its outputs become NaN, as the fp32 GEMM's would).
+__device__ __forceinline__ int block_scale(float amax, int* shift) {
+  if (!(amax == amax) || amax == __builtin_inff()) {
+    *shift = 0;
+    return 255;
+  }
+  int e = -111;
+  if (amax > 0.f) {
+    frexpf(amax, &e);
+    e = e < -111 ? -111 : e;     // blocks below 2^-112 quantise to ~0 (error < 2^-130)
+  }
+  *shift = 19 - e;
+  return e + SCALE_BIAS;
+}
+
+// 4 balanced base-32 digits of rint(x * 2^shift)
+__device__ __forceinline__ void digits4(float x, int shift, int (&d)[4]) {
+  int v = __float2int_rn(ldexpf(x, shift));
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int dj = ((v + 16) & 31) - 16;
+    d[j] = dj;
+    v = (v - dj) >> 5;
+  }
+  d[3] = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Row quantiser: x [M][K] (row stride ldx) -> lo, hi, scales; blocks beyond K are zero digits.
+// 8 lanes per block (4 elements each: one 16-B load per lane), lane j < 4 of the group packs and
+// writes plane j (lo 16 B + hi 8 B).  Grid: (rows, row blocks / 32); one wave = 8 blocks of a row.
+__global__ __launch_bounds__(256) void quant6_rows_k(const float* __restrict__ x, int64_t M, int64_t K,
+                                                     int64_t ldx, int64_t nblk, uint8_t* __restrict__ lo,
+                                                     uint8_t* __restrict__ hi, uint8_t* __restrict__ sc,
+                                                     int64_t sc_rows, int vec) {
+  const int lane = threadIdx.x & 63, q = lane & 7;
+  const int64_t row = blockIdx.x;
+  const int64_t blk = ((int64_t)blockIdx.y * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
+  if (blk >= nblk) return;   // whole 8-lane groups leave together
+  const int64_t k0 = blk * QB + 4 * q;
+  const float* xr = x + row * ldx;
+  float v[4];
+  if (vec && k0 + 4 <= K) {
+    const float4 f = *reinterpret_cast<const float4*>(xr + k0);
+    v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (k0 + j < K) ? xr[k0 + j] : 0.f;
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = fabsf(v[j]);
+    amax = (a == a) ? fmaxf(amax, a) : __builtin_inff();
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  int shift;
+  const int sbyte = block_scale(amax, &shift);
+  // this lane's 4 elements -> a 24-bit chunk per plane (element 4q+i at bits 6i of the chunk)
+  uint32_t chunk[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int d[4];
+    digits4(v[i], shift, d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) chunk[j] |= e2m3_code(d[j]) << (6 * i);
+  }
+  // lane j of the group assembles plane j: chunk of lane p sits at bits 24p..24p+23
+  const int plane = q & 3;
+  uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t cj = __shfl(chunk[j], (lane & ~7) | p, 64);
+      c = (plane == j) ? cj : c;
+    }
+    const int bit = 24 * p;
+    w[bit >> 5] |= c << (bit & 31);
+    if ((bit & 31) > 8) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+  }
+  if (q < 4) {
+    uint8_t* lo_p = lo + (row * nblk + blk) * 64 + plane * 16;
+    *reinterpret_cast<uint4*>(lo_p) = make_uint4(w[0], w[1], w[2], w[3]);
+    uint8_t* hi_p = hi + (row * nblk + blk) * 32 + plane * 8;
+    *reinterpret_cast<uint2*>(hi_p) = make_uint2(w[4], w[5]);
+  } else if (q == 4) {
+    sc[(blk >> 1) * sc_rows * 2 + row * 2 + (blk & 1)] = (uint8_t)sbyte;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Transposed column quantiser: x [M][N] -> the digits of x^T (rows n, k = m), blocks of 32
+// consecutive m; plus per-256-row partial column sums (double) for the bias gradient
+// dB = sum_B dY (binarized_modules.py:81-83).  Workgroup = 64 columns x 8 blocks (256 rows);
+// thread (column t%64, block t/64) reads its block's 32 values column-wise (each wave reads 64
+// consecutive columns of one row: 256 B) and writes the block's 96 digit bytes.
+constexpr int QC_COLS = 64, QC_BLKS = 8;
+
+__global__ __launch_bounds__(512) void quant6_cols_t_k(const float* __restrict__ x, int64_t M, int64_t N,
+                                                       int64_t ldx, int64_t nblk, uint8_t* __restrict__ lo,
+                                                       uint8_t* __restrict__ hi, uint8_t* __restrict__ sc,
+                                                       int64_t sc_rows, double* __restrict__ part) {
+  __shared__ double psum[QC_BLKS][QC_COLS];
+  const int tc = threadIdx.x & (QC_COLS - 1), tb = threadIdx.x / QC_COLS;
+  const int64_t n = (int64_t)blockIdx.x * QC_COLS + tc;
+  const int64_t blk = (int64_t)blockIdx.y * QC_BLKS + tb;
+  const int64_t m0 = blk * QB;
+  float v[QB];
+  float amax = 0.f;
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < QB; ++i) {
+    const int64_t m = m0 + i;
+    v[i] = (n < N && m < M) ? x[m * ldx + n] : 0.f;
+    const float a = fabsf(v[i]);
+    amax = (a == a) ? fmaxf(amax, a) : __builtin_inff();
+    s += (double)v[i];
+  }
+  psum[tb][tc] = s;
+  if (n < N && blk < nblk) {
+    int shift;
+    const int sbyte = block_scale(amax, &shift);
+    uint32_t w[4][6];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) w[j][i] = 0;
+#pragma unroll
+    for (int i = 0; i < QB; ++i) {
+      int d[4];
+      digits4(v[i], shift, d);
+      const int bit = 6 * i;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t c = e2m3_code(d[j]);
+        w[j][bit >> 5] |= c << (bit & 31);
+        if ((bit & 31) > 26) w[j][(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+      }
+    }
+    uint8_t* lo_p = lo + (n * nblk + blk) * 64;
+    uint8_t* hi_p = hi + (n * nblk + blk) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<uint4*>(lo_p + 16 * j) = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+    *reinterpret_cast<uint4*>(hi_p) = make_uint4(w[0][4], w[0][5], w[1][4], w[1][5]);
+    *reinterpret_cast<uint4*>(hi_p + 16) = make_uint4(w[2][4], w[2][5], w[3][4], w[3][5]);
+    sc[(blk >> 1) * sc_rows * 2 + n * 2 + (blk & 1)] = (uint8_t)sbyte;
+  }
+  __syncthreads();
+  if (part != nullptr && tb == 0 && n < N) {
+    double t = 0.0;
+#pragma unroll
+    for (int b = 0; b < QC_BLKS; ++b) t += psum[b][tc];   // fixed order: deterministic
+    part[(int64_t)blockIdx.y * N + n] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_k(const double* __restrict__ part, int64_t R, int64_t N,
+                                                      float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int64_t r = 0; r < R; ++r) s += part[r * N + n];
+  out[n] = (float)s;
+}
+
+// ------------------------------------------------------------------------------------------
+// GEMM: C[M][N] = sum_k A[m][k] B[n][k] (+ bias[n]); A = FP6 digits (lo, hi, scales), B = FP4.
+struct Gemm6Params {
+  const uint8_t* alo;   // [M][K/32][64]
+  const uint8_t* ahi;   // [M][K/32][32]
+  const uint8_t* asc;   // [K/64][asc_rows][2]
+  const uint8_t* b;     // [N][ldb]
+  int64_t ldb, asc_rows;
+  const float* bias;
+  float* C;
+  int64_t ldc;
+  int M, N, K;
+  int gm, gn;
+};
+
+__device__ __forceinline__ void glds16_6(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt6() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void barrier6() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Bijective XCD remap + grouped raster (as bnn_gemm.hip's tile_of).
+__device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int& tm, int& tn) {
+  const int nwg = gm * gn;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  constexpr int G = 8;
+  const int per_group = G * gn;
+  const int g = L / per_group, first = g * G;
+  const int gs = min(gm - first, G);
+  const int in = L - g * per_group;
+  tm = first + in % gs;
+  tn = in / gs;
+}
+
+// LDS stage (BK = 64 = one MFMA k-step, 2 scale blocks):
+//   A lo : BM rows x 128 B  (block 0: planes 0-3, block 1: planes 0-3), 16-B chunk c stored at
+//          chunk c ^ ((row >> 1) & 7)
+//   A hi : BM rows x  64 B  (block 0: planes 01, 23; block 1: ...), chunk c at c ^ ((row >> 2) & 3)
+//   A sc : BM x 2 B        (row-major, plane-0 bytes of blocks 0, 1)
+//   B    : BN rows x  32 B  (the 64 FP4 codes), chunk c at c ^ ((row >> 3) & 1)
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params p) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
+  constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_ST = BM * 2, B_ST = BN * 32;
+  constexpr int SC_PAD = (SC_ST + 1023) / 1024 * 1024;
+  constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST;
+  constexpr int I_LO = LO_ST / 1024, I_HI = HI_ST / 1024, I_SC = SC_PAD / 1024, I_B = B_ST / 1024;
+  constexpr int NPIECE = I_LO + I_HI + I_SC + I_B;
+  constexpr int PER_WAVE = (NPIECE + NW - 1) / NW;   // waves >= NPIECE % NW issue one piece less
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
+
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  int tm, tn;
+  tile6_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int64_t nblk = p.K / QB;
+  const int nk = p.K / 64;
+
+  // piece i of a stage (1 KiB = 64 lanes x 16 B): lo rows 8 per piece, hi rows 16, scales
+  // 512 rows (1 KiB of 2-B entries), B rows 32.  Source rows are clamped to the last valid row
+  // (their results are never stored); the XOR swizzles live on the source chunk (LDS stays linear).
+  auto stage = [&](int kt, int buf) {
+    char* base = smem + buf * ST;
+#pragma unroll
+    for (int ii = 0; ii < PER_WAVE; ++ii) {
+      const int i = wave + ii * NW;
+      if (i >= NPIECE) break;          // wave-uniform
+      if (i < I_LO) {
+        const int lrow = i * 8 + (lane >> 3), c = lane & 7;
+        const int row = min(m0 + lrow, p.M - 1);
+        const int src = c ^ ((lrow >> 1) & 7);
+        glds16_6(p.alo + ((int64_t)row * nblk + 2 * kt) * 64 + 16 * src, base + i * 1024);
+      } else if (i < I_LO + I_HI) {
+        const int j = i - I_LO;
+        const int lrow = j * 16 + (lane >> 2), c = lane & 3;
+        const int row = min(m0 + lrow, p.M - 1);
+        const int src = c ^ ((lrow >> 2) & 3);
+        glds16_6(p.ahi + ((int64_t)row * nblk + 2 * kt) * 32 + 16 * src, base + LO_ST + j * 1024);
+      } else if (i < I_LO + I_HI + I_SC) {
+        const int j = i - I_LO - I_HI;
+        // 2-byte entries, 8 rows per lane; rows beyond asc_rows are read from the padded tail
+        const int64_t off = (int64_t)kt * p.asc_rows * 2 + (int64_t)m0 * 2 + j * 1024 + lane * 16;
+        if (j * 1024 + lane * 16 < SC_ST)       // only this tile's BM rows (never past the slab)
+          glds16_6(p.asc + off, base + LO_ST + HI_ST + j * 1024);
+      } else {
+        const int j = i - I_LO - I_HI - I_SC;
+        const int lrow = j * 32 + (lane >> 1), c = lane & 1;
+        const int row = min(n0 + lrow, p.N - 1);
+        const int src = c ^ ((lrow >> 3) & 1);
+        glds16_6(p.b + (int64_t)row * p.ldb + (int64_t)kt * 32 + 16 * src, base + LO_ST + HI_ST + SC_PAD + j * 1024);
+      }
+    }
+  };
+
+  v16f acc[WM][WN];
+#pragma unroll
+  for (int t = 0; t < WM; ++t)
+#pragma unroll
+    for (int u = 0; u < WN; ++u) acc[t][u] = v16f{0};
+
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s);
+  // pieces this wave issues per stage (wave-uniform): the counted wait keeps the next stage in
+  // flight while retiring this one
+  const int mine = (NPIECE - wave + NW - 1) / NW;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(STAGES - 2, nk - 1 - kt);
+    if constexpr (STAGES >= 3) {
+      if (ahead >= 1 && mine == PER_WAVE) wait_vmcnt6<PER_WAVE>();
+      else if (ahead >= 1 && PER_WAVE > 1) wait_vmcnt6<(PER_WAVE > 1 ? PER_WAVE - 1 : 0)>();
+      else wait_vmcnt6<0>();
+    } else {
+      wait_vmcnt6<0>();
+    }
+    barrier6();
+    if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* base = smem + (kt % STAGES) * ST;
+    const char* sLo = base;
+    const char* sHi = base + LO_ST;
+    const uint8_t* sSc = reinterpret_cast<const uint8_t*>(base + LO_ST + HI_ST);
+    const char* sB = base + LO_ST + HI_ST + SC_PAD;
+    // B fragments: row n, 16 B = k-block h
+    v4i bf[WN];
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int lrow = wn * WN * 32 + u * 32 + r;
+      bf[u] = *reinterpret_cast<const v4i*>(sB + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
+    }
+#pragma unroll
+    for (int t = 0; t < WM; ++t) {
+      const int lrow = wm * WM * 32 + t * 32 + r;
+      v4i lo4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        lo4[j] = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + j) ^ ((lrow >> 1) & 7)));
+      const v4i hi01 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2) ^ ((lrow >> 2) & 3)));
+      const v4i hi23 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2 + 1) ^ ((lrow >> 2) & 3)));
+      const int sb = sSc[lrow * 2 + h];
+      const v8i a0 = {lo4[0].x, lo4[0].y, lo4[0].z, lo4[0].w, hi01.x, hi01.y, 0, 0};
+      const v8i a1 = {lo4[1].x, lo4[1].y, lo4[1].z, lo4[1].w, hi01.z, hi01.w, 0, 0};
+      const v8i a2 = {lo4[2].x, lo4[2].y, lo4[2].z, lo4[2].w, hi23.x, hi23.y, 0, 0};
+      const v8i a3 = {lo4[3].x, lo4[3].y, lo4[3].z, lo4[3].w, hi23.z, hi23.w, 0, 0};
+      // a NaN block (255) stays NaN in every plane; otherwise plane j scale = sb + 5j (<= 254)
+      const int s0 = sb, s1 = sb == 255 ? 255 : sb + 5, s2 = sb == 255 ? 255 : sb + 10, s3 = sb == 255 ? 255 : sb + 15;
+#pragma unroll
+      for (int u = 0; u < WN; ++u) {
+        const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a3, bb, acc[t][u], 2, 4, 0, s3, 0, 127);
+        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, acc[t][u], 2, 4, 0, s2, 0, 127);
+        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, acc[t][u], 2, 4, 0, s1, 0, 127);
+        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, acc[t][u], 2, 4, 0, s0, 0, 127);
+      }
+    }
+  }
+
+  // epilogue: C/D map of the 32x32 MFMA (reg i -> row (i&3)+8(i>>2)+4h, col lane&31), transposed
+  // through a per-wave LDS patch and written as 16-B row segments (as bnn_gemm.hip)
+  wait_vmcnt6<0>();
+  barrier6();
+  float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
+  const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
+#pragma unroll
+  for (int t = 0; t < WM; ++t) {
+    const int trow0 = m0 + wm * WM * 32 + t * 32;
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int tcol0 = n0 + wn * WN * 32 + u * 32;
+      const int col = tcol0 + r;
+      const float bb = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
+        float f = acc[t][u][i];
+        if (p.bias) f += bb;
+        patch[lr * 32 + ((((r >> 2) ^ (lr & 7)) << 2) | (r & 3))] = f;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int lr = (lane >> 3) + 8 * ps, c4 = lane & 7;
+        const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
+        const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
+        if (row >= p.M) continue;
+        float* dst = p.C + (int64_t)row * p.ldc + c0;
+        if (vec_ok && c0 + 3 < p.N) {
+          *reinterpret_cast<float4*>(dst) = v;
+        } else {
+          const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c0 + j < p.N) dst[j] = vs[j];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+}
+
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+int launch6(Gemm6Params p, hipStream_t s) {
+  constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
+  p.gm = (p.M + BM - 1) / BM;
+  p.gn = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES>), dim3((unsigned)((int64_t)p.gm * p.gn)),
+                     dim3(64 * WAVES_M * WAVES_N), 0, s, p);
+  return check_launch("bnn_gemm_fp6");
+}
+
+struct Variant6 {
+  int id;
+  const char* name;
+  int (*fn)(Gemm6Params, hipStream_t);
+  int bm;   // rows per tile (the scale array must hold round_up(M, bm) rows... see bnn_gemm_fp6)
+};
+
+const Variant6 kVariants6[] = {
+    {0, "gemm_fp6_k<2, 4, 4, 2, 2>", launch6<2, 4, 4, 2, 2>, 256},
+    {1, "gemm_fp6_k<2, 4, 2, 2, 3>", launch6<2, 4, 2, 2, 3>, 128},
+    {2, "gemm_fp6_k<2, 2, 2, 2, 3>", launch6<2, 2, 2, 2, 3>, 128},
+    {3, "gemm_fp6_k<4, 2, 2, 4, 2>", launch6<4, 2, 2, 4, 2>, 256},
+    {4, "gemm_fp6_k<2, 4, 2, 2, 4>", launch6<2, 4, 2, 2, 4>, 128},
+};
+
+int g_variant6 = -1;
+
+const Variant6* pick6(int64_t M, int64_t N) {
+  if (g_variant6 >= 0)
+    for (const Variant6& v : kVariants6)
+      if (v.id == g_variant6) return &v;
+  const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
+  return big ? &kVariants6[0] : &kVariants6[2];
+}
+
+inline hipStream_t S6(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+}  // namespace bnn
+
+using namespace bnn;
+
+BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return round_up(rows, 256); }
+
+BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
+                            uint8_t* sc, void* stream) {
+  if (!x || !lo || !hi || !sc || M < 0 || K < 0 || ldx < K || Kp < K || Kp % 64 != 0 || Kp == 0 || !aligned16(lo) ||
+      !aligned16(hi) || M > 0x7fffffff || (Kp / QB + 31) / 32 > 65535) {
+    set_error("bnn_quant6_rows: bad arguments (M=%lld K=%lld Kp=%lld)", (long long)M, (long long)K, (long long)Kp);
+    return kErrInval;
+  }
+  if (M == 0) return 0;
+  const int64_t nblk = Kp / QB;
+  const int vec = aligned16(x) && (ldx % 4 == 0);
+  hipLaunchKernelGGL(quant6_rows_k, dim3((unsigned)M, (unsigned)((nblk + 31) / 32)), dim3(256), 0, S6(stream), x, M,
+                     K, ldx, nblk, lo, hi, sc, round_up(M, 256), vec);
+  return check_launch("bnn_quant6_rows");
+}
+
+BNN_API int64_t bnn_quant6_cols_workspace(int64_t M, int64_t N) {
+  return ((M + 255) / 256) * N * (int64_t)sizeof(double);
+}
+
+BNN_API int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int64_t Mp, uint8_t* lo,
+                              uint8_t* hi, uint8_t* sc, float* colsum, void* work, void* stream) {
+  if (!x || !lo || !hi || !sc || M < 0 || N < 0 || ldx < N || Mp < M || Mp % 64 != 0 || Mp == 0 || !aligned16(lo) ||
+      !aligned16(hi) || (colsum && !work) || (Mp + 255) / 256 > 65535) {
+    set_error("bnn_quant6_cols_t: bad arguments (M=%lld N=%lld Mp=%lld)", (long long)M, (long long)N, (long long)Mp);
+    return kErrInval;
+  }
+  if (N == 0) return 0;
+  const int64_t nblk = Mp / QB;
+  const int64_t R = (nblk + QC_BLKS - 1) / QC_BLKS;
+  double* part = colsum ? reinterpret_cast<double*>(work) : nullptr;
+  hipLaunchKernelGGL(quant6_cols_t_k, dim3((unsigned)((N + QC_COLS - 1) / QC_COLS), (unsigned)R), dim3(512), 0,
+                     S6(stream), x, M, N, ldx, nblk, lo, hi, sc, round_up(N, 256), part);
+  if (colsum)
+    hipLaunchKernelGGL(colsum_final_k, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S6(stream), part, R, N,
+                       colsum);
+  return check_launch("bnn_quant6_cols_t");
+}
+
+BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
+                         int64_t N, int64_t K, void* stream) {
+  if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || ldb < K / 2 || ldb % 16 != 0 ||
+      ldc < N || asc_rows < round_up(M, 256) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
+      !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
+    set_error("bnn_gemm_fp6: bad arguments (M=%lld N=%lld K=%lld ldb=%lld asc_rows=%lld; K a positive multiple of "
+              "64, asc_rows a multiple of 256 >= round_up(M,256))",
+              (long long)M, (long long)N, (long long)K, (long long)ldb, (long long)asc_rows);
+    return kErrInval;
+  }
+  if (M == 0 || N == 0) return 0;
+  Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0};
+  return pick6(M, N)->fn(p, S6(stream));
+}
+
+BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, N)->name; }
+
+BNN_API int bnn_gemm_fp6_set_variant(int32_t v) {
+  g_variant6 = v;
+  return 0;
+}

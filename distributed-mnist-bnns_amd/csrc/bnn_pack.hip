@@ -100,7 +100,9 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
                                                         int64_t ldq, int8_t* __restrict__ qt,
                                                         int64_t ldqt, int vec, ColAffine af = {},
                                                         int rtiles = 1, int64_t ntiles_y = 0,
-                                                        AdamArgs ad = {}) {
+                                                        AdamArgs ad = {}, int qt4 = 0) {
+  // qt4 = 1: the transpose is written as FP4 nibbles (qt rows of ldqt BYTES, element m in byte
+  // m/2), the B operand of the FP6 digit GEMMs (bnn_gemm6.hip); else int8 (rows of ldqt elements)
   // rtiles > 1: the workgroup walks rtiles vertically adjacent 64x64 tiles of its column block
   // (the per-column BatchNorm parameters are loaded once per workgroup, not once per tile)
   __shared__ int tile[TILE][TILE + 1];
@@ -183,7 +185,17 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
     __syncthreads();
     const int kk = t >> 2, mc = (t & 3) * 16;
     const int64_t k = k0 + kk;
-    if (k < K && m0 + mc < ldqt) {
+    if (qt4) {
+      if (k < K && (m0 + mc) / 2 < ldqt) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          lo |= fp4_code(tile[mc + j][kk]) << (4 * j);
+          hi |= fp4_code(tile[mc + 8 + j][kk]) << (4 * j);
+        }
+        *reinterpret_cast<uint2*>(qt + k * ldqt + (m0 + mc) / 2) = make_uint2(lo, hi);
+      }
+    } else if (k < K && m0 + mc < ldqt) {
       int g[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][kk];
@@ -425,6 +437,18 @@ __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ 
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Transposed operand checks: int8 rows of ldqt elements (multiple of 64, >= round_up(M,64)) or
+// FP4 rows of ldqt bytes (multiple of 128, 2*ldqt >= round_up(M,256)); returns the number of
+// 64-row tiles the grid must cover so every padding element is written.
+bool qt_ok(const int8_t* qt, int64_t M, int64_t ldqt, int qt_fmt) {
+  if (!qt) return true;
+  if (!aligned16(qt) || (qt_fmt != 0 && qt_fmt != 1)) return false;
+  return qt_fmt == 1 ? (ldqt % 128 == 0 && 2 * ldqt >= round_up(M, 256))
+                     : (ldqt % TILE == 0 && ldqt >= round_up(M, TILE));
+}
+
+int64_t qt_tiles(int64_t ldqt, int qt_fmt) { return (qt_fmt == 1 ? 2 * ldqt : ldqt) / TILE; }
+
 inline int grid_cap(int64_t want) { return (int)std::max<int64_t>(1, std::min<int64_t>(want, 8192)); }
 
 }  // namespace
@@ -463,7 +487,7 @@ BNN_API int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, 
 }
 
 BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
-                              int8_t* qt, int64_t ldqt, void* stream) {
+                              int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
   if (!x || M < 0 || K < 0 || ldx < K || (!q4 && !qt)) {
     set_error("bnn_sign_pack_fp4: bad arguments (M=%lld K=%lld ldx=%lld)", (long long)M, (long long)K,
               (long long)ldx);
@@ -474,28 +498,30 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
               (long long)ldq4);
     return kErrInval;
   }
-  if (qt && (ldqt % TILE != 0 || ldqt < round_up(M, TILE) || !aligned16(qt))) {
-    set_error("bnn_sign_pack_fp4: ldqt=%lld must be a multiple of 64 >= round_up(M,64)", (long long)ldqt);
+  if (!qt_ok(qt, M, ldqt, qt_fmt)) {
+    set_error("bnn_sign_pack_fp4: ldqt=%lld does not cover M=%lld in qt_fmt %d", (long long)ldqt, (long long)M,
+              qt_fmt);
     return kErrInval;
   }
   if (M == 0 && !qt) return 0;
   const int vec = aligned16(x) && (ldx % 4 == 0);
   const int64_t gx = q4 ? (2 * ldq4) / TILE : (K + TILE - 1) / TILE;
-  const int64_t gy = qt ? ldqt / TILE : (M + TILE - 1) / TILE;
+  const int64_t gy = qt ? qt_tiles(ldqt, qt_fmt) : (M + TILE - 1) / TILE;
   if (gx == 0 || gy == 0) return 0;
   if (gy > 65535) {
     set_error("bnn_sign_pack_fp4: M too large for one launch (%lld)", (long long)M);
     return kErrInval;
   }
   hipLaunchKernelGGL(sign_pack_tile_k<1>, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), x, M, K,
-                     ldx, reinterpret_cast<int8_t*>(q4), ldq4, qt, ldqt, vec);
+                     ldx, reinterpret_cast<int8_t*>(q4), ldq4, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, AdamArgs{},
+                     qt_fmt);
   return check_launch("bnn_sign_pack_fp4");
 }
 
 BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
                                 int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
                                 float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
-                                int64_t ldqt, void* stream) {
+                                int64_t ldqt, int32_t qt_fmt, void* stream) {
   if (!p || !grad || !exp_avg || !exp_avg_sq || N <= 0 || K <= 0 || step < 1 || (fmt != 0 && fmt != 1) ||
       (!q && !qt)) {
     set_error("bnn_adam_clamp_pack: bad arguments (N=%lld K=%lld fmt=%d)", (long long)N, (long long)K, fmt);
@@ -506,15 +532,15 @@ BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, flo
     set_error("bnn_adam_clamp_pack: ldq=%lld does not cover K=%lld in fmt %d", (long long)ldq, (long long)K, fmt);
     return kErrInval;
   }
-  if ((q && !aligned16(q)) || (qt && (ldqt % TILE != 0 || ldqt < round_up(N, TILE) || !aligned16(qt)))) {
-    set_error("bnn_adam_clamp_pack: ldqt=%lld must be a multiple of 64 >= round_up(N,64), 16-B aligned",
-              (long long)ldqt);
+  if ((q && !aligned16(q)) || !qt_ok(qt, N, ldqt, qt_fmt)) {
+    set_error("bnn_adam_clamp_pack: ldqt=%lld does not cover N=%lld in qt_fmt %d", (long long)ldqt, (long long)N,
+              qt_fmt);
     return kErrInval;
   }
   // every element of p is visited exactly once: the grid spans K (and the q padding) x N (and
   // the qt padding); tiles beyond K or N update nothing and only write zero padding
   const int64_t gx = q ? (fmt == 0 ? ldq : 2 * ldq) / TILE : (K + TILE - 1) / TILE;
-  const int64_t gy = qt ? ldqt / TILE : (N + TILE - 1) / TILE;
+  const int64_t gy = qt ? qt_tiles(ldqt, qt_fmt) : (N + TILE - 1) / TILE;
   if (gy > 65535 || gx > 0x7fffffff) {
     set_error("bnn_adam_clamp_pack: N too large for one launch (%lld)", (long long)N);
     return kErrInval;
@@ -525,10 +551,10 @@ BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, flo
   const int vec = aligned16(p) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq) && (K % 4 == 0);
   if (fmt == 0)
     hipLaunchKernelGGL((sign_pack_tile_k<0, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
-                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a);
+                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a, qt_fmt);
   else
     hipLaunchKernelGGL((sign_pack_tile_k<1, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
-                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a);
+                       K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a, qt_fmt);
   return check_launch("bnn_adam_clamp_pack");
 }
 
@@ -616,12 +642,10 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
 
 BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                               const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
-                              int64_t ldq,
-                              int8_t* qt, int64_t ldqt, void* stream) {
+                              int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
   const int64_t need = fmt == 1 ? round_up(C, 256) / 2 : round_up(C, TILE);
   if (!x || !mean || !invstd || M < 0 || C < 0 || (fmt != 0 && fmt != 1) || (!q && !qt) ||
-      (q && (ldq < need || ldq % (fmt == 1 ? 128 : TILE) != 0 || !aligned16(q))) ||
-      (qt && (ldqt % TILE != 0 || ldqt < round_up(M, TILE) || !aligned16(qt)))) {
+      (q && (ldq < need || ldq % (fmt == 1 ? 128 : TILE) != 0 || !aligned16(q))) || !qt_ok(qt, M, ldqt, qt_fmt)) {
     set_error("bnn_bn_apply_pack: bad arguments (M=%lld C=%lld fmt=%d ldq=%lld ldqt=%lld)", (long long)M,
               (long long)C, fmt, (long long)ldq, (long long)ldqt);
     return kErrInval;
@@ -629,7 +653,7 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   if (M == 0 && !qt) return 0;
   const int vec = aligned16(x) && (C % 4 == 0);
   const int64_t gx = q ? (fmt == 1 ? 2 * ldq : ldq) / TILE : (C + TILE - 1) / TILE;
-  const int64_t gy = qt ? ldqt / TILE : (M + TILE - 1) / TILE;
+  const int64_t gy = qt ? qt_tiles(ldqt, qt_fmt) : (M + TILE - 1) / TILE;
   if (gx == 0 || gy == 0) return 0;
   if (gy > 65535) {
     set_error("bnn_bn_apply_pack: M too large for one launch (%lld)", (long long)M);
@@ -643,9 +667,9 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   const unsigned gyr = (unsigned)((gy + rt - 1) / rt);
   if (fmt == 1)
     hipLaunchKernelGGL((sign_pack_tile_k<1, 1>), dim3((unsigned)gx, gyr), dim3(256), 0, S(stream), x, M,
-                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy);
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy, AdamArgs{}, qt_fmt);
   else
     hipLaunchKernelGGL((sign_pack_tile_k<0, 1>), dim3((unsigned)gx, gyr), dim3(256), 0, S(stream), x, M,
-                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy);
+                       C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy, AdamArgs{}, qt_fmt);
   return check_launch("bnn_bn_apply_pack");
 }

@@ -49,10 +49,11 @@ int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* 
                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
 
 /* FP4 form of the ternary rows for bnn_gemm_fp4: q4 [M][ldq4 bytes], ldq4 a multiple of 128 with
- * 2*ldq4 >= round_up(K,256) (zero nibbles beyond K); qt as in bnn_sign_pack_i8 (int8, for the
- * backward GEMMs). */
+ * 2*ldq4 >= round_up(K,256) (zero nibbles beyond K).  qt = the transpose [K][ldqt] for the
+ * backward GEMMs: qt_fmt 0 = int8 as in bnn_sign_pack_i8; qt_fmt 1 = FP4 nibbles, ldqt BYTES (a
+ * multiple of 128, 2*ldqt >= round_up(M,256)), the B operand of bnn_gemm_fp6. */
 int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
-                      int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+                      int8_t* qt, int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
 
 /* y[i] = sign(x[i]) as fp32 (the caller-visible `input.data = Binarize(input.data)` of :76/:95;
  * y may alias x). */
@@ -112,6 +113,35 @@ int bnn_gemm_set_variant(int32_t variant);
  * names the bnn_gemm_fp4 kernel (K in bytes). */
 const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,
                                int64_t K);
+
+/* ---------------------------------------------------------------- fp32 x ternary on the FP6 MFMA
+ * The fp32 operand of the backward GEMMs (dY) and of the first layer's forward (pixels) as FOUR
+ * FP6 (e2m3) planes of balanced base-32 digits with one E8M0 scale per 32-element k-block
+ * (v_mfma_scale_f32_32x32x64_f8f6f4's own block scales), against the FP4 ternary operand:
+ * |x - x_q| <= max|x_block| * 2^-19 per element, accumulated in fp32.
+ * Layouts (Kp = padded reduction length, multiple of 64):
+ *   lo  [rows][Kp/32][64 B]   per block and plane j: dwords 0..3 of the plane's MFMA operand
+ *   hi  [rows][Kp/32][32 B]   per block: dwords 4..5 of planes 0,1,2,3
+ *   sc  [Kp/64][round_up(rows,256)][2]  E8M0 byte of plane 0 per block (plane j: +5j; 255 = NaN)
+ * replaces: the fp32 GEMMs of BinarizeLinear's autograd (dX = dY.W_b, dW = dY^T.X_b) and the
+ * first layer's F.linear(x, W_b) (models/binarized_modules.py:80). */
+int64_t bnn_quant6_scale_rows(int64_t rows);
+/* x [M][K] (row stride ldx) -> digits of its rows, blocks along K (zero digits for K..Kp-1). */
+int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
+                    uint8_t* sc, bnn_stream_t stream);
+/* x [M][N] -> digits of x^T (rows n, blocks along m, zero digits for M..Mp-1), plus colsum[n] =
+ * sum_m x[m][n] (nullable; fixed-order double sums, `work` of bnn_quant6_cols_workspace bytes):
+ * the bias gradient dB = sum_B dY (binarized_modules.py:81-83). */
+int64_t bnn_quant6_cols_workspace(int64_t M, int64_t N);
+int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int64_t Mp, uint8_t* lo, uint8_t* hi,
+                      uint8_t* sc, float* colsum, void* work, bnn_stream_t stream);
+/* C[m][n] = sum_k A[m][k] B[n][k] (+ bias[n]): A as above (asc_rows = the sc row pitch), B FP4
+ * nibbles [N][ldb bytes] (ldb multiple of 16, >= K/2; zero nibbles beyond the true length). */
+int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
+                 int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                 bnn_stream_t stream);
+const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
+int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row
@@ -229,7 +259,7 @@ int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t
  * written (Hardtanh keeps the sign; its backward mask is recomputed from x by bnn_bn_bwd). */
 int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                       const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
-                      int64_t ldq, int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+                      int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */
@@ -247,14 +277,15 @@ int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_s
  * bnn_adam_clamp does (bit-identical p, m, v), and in the same pass sign(p_new) is written as the
  * ternary rows q -- fmt 0: int8 [N][ldq] (ldq multiple of 64 >= round_up(K,64)); fmt 1: FP4
  * nibbles [N][ldq bytes] (ldq multiple of 128, 2*ldq >= round_up(K,256)) -- and/or the int8
- * transpose qt [K][ldqt] (ldqt multiple of 64 >= round_up(N,64)); padding zero-filled, as
+ * transpose qt [K][ldqt] (qt_fmt 0: int8, ldqt multiple of 64 >= round_up(N,64); qt_fmt 1: FP4
+ * nibbles, ldqt bytes as in bnn_sign_pack_fp4); padding zero-filled, as
  * bnn_sign_pack_i8 / bnn_sign_pack_fp4 of p_new would write them.  q or qt may be NULL (not both).
  * replaces: p.data.copy_(p.org); Adam.step(); p.org.copy_(p.data.clamp_(-1,1)) (mnist-dist2.py:
  * 131-137) and the weight sign of the next forward (binarized_modules.py:79). */
 int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
                         int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
                         float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
-                        int64_t ldqt, bnn_stream_t stream);
+                        int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,145 @@
+"""GPU parity of the FP6 digit GEMMs (csrc/bnn_gemm6.hip): fp32 operand x ternary operand on
+v_mfma_scale_f32_32x32x64_f8f6f4 -- the backward GEMMs of BinarizeLinear (dX = dY.W_b,
+dW = dY^T.X_b) and the first layer's forward (models/binarized_modules.py:80).
+
+Bars:
+* quantisers: decoded on the host, every element within max|x_block| * 2^-19 of x (the a-priori
+  bound), digits in range, padding zero, column sums to fp32 rounding of the double sum;
+* GEMM: against float64 products of the DECODED digits norm-wise <= 2e-6 (fp32 accumulation of
+  exact block partial sums), against the float64 product of x itself <= 1e-5 (the gradient bar).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def F():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import functional
+    return functional
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def _codes(lo, hi, rows, nblk):
+    """[rows, nblk, 4 planes, 32] e2m3 codes from the lo / hi byte arrays (element i of a plane
+    at bits 6i..6i+5 of its 6 dwords: 4 in lo, 2 in hi)."""
+    lo = lo.reshape(rows, nblk, 4, 16)
+    hi = hi.reshape(rows, nblk, 4, 8)
+    words = np.ascontiguousarray(np.concatenate([lo, hi], axis=-1)).view(np.uint32).astype(np.uint64)
+    codes = np.zeros(words.shape[:-1] + (32,), np.int64)
+    for i in range(32):
+        w, o = (6 * i) // 32, (6 * i) % 32
+        c = words[..., w] >> np.uint64(o)
+        if o > 26:
+            c |= words[..., w + 1] << np.uint64(32 - o)
+        codes[..., i] = (c & np.uint64(63)).astype(np.int64)
+    return codes
+
+
+def _e2m3_digit(c):
+    s = np.where(c & 0x20, -1, 1)
+    e = (c >> 3) & 3
+    m = c & 7
+    v8 = np.where(e == 0, m, (8 + m) << np.maximum(e - 1, 0))      # value * 8
+    return s * v8
+
+
+def decode(op, rows):
+    """Host decode of an Fp6Operand: [rows, Kp] float64 values and the digits."""
+    nblk = op.Kp // 32
+    d = _e2m3_digit(_codes(host(op.lo), host(op.hi), rows, nblk))     # [rows, nblk, 4, 32]
+    sc = host(op.sc)                                                  # [Kp/64, rows_pad, 2]
+    E = np.stack([sc[b // 2, :rows, b % 2] for b in range(nblk)], axis=1).astype(np.int64)   # [rows, nblk]
+    val = np.zeros((rows, nblk, 32))
+    for j in range(4):
+        val += d[:, :, j, :] * np.ldexp(1.0, (E + 5 * j - 130))[..., None]
+    return val.reshape(rows, nblk * 32), d, E
+
+
+def _check_quant(x, val, d, E):
+    rows, K = x.shape
+    nblk = val.shape[1] // 32
+    assert np.all(np.abs(d[..., :3, :]) <= 16) and np.all(np.abs(d[..., 3, :]) <= 16)
+    assert np.all(d[..., :3, :] < 16)                    # balanced: d0..d2 in [-16, 15]
+    xp = np.zeros((rows, nblk * 32))
+    xp[:, :K] = x
+    amax = np.abs(xp.reshape(rows, nblk, 32)).max(-1)
+    bound = np.repeat(amax * 2.0 ** -19, 32, axis=1)
+    assert np.all(np.abs(val - xp) <= bound + 1e-300)
+    assert not val[:, K:].any()
+    nz = amax > 0
+    e = E - 111
+    assert np.all((np.ldexp(1.0, e - 1) <= amax)[nz]) and np.all((amax < np.ldexp(1.0, e))[nz])
+
+
+@pytest.mark.parametrize("M,K", [(5, 64), (300, 1000), (64, 784), (1, 8192), (257, 33)])
+def test_quant6_rows_decodes_within_bound(F, M, K):
+    rng = np.random.default_rng(M + K)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-12, 12, (M, K)))).astype(np.float32)
+    x[:, ::7] = 0.0
+    if M > 3:
+        x[3] = 0.0
+    op = F.quant6_rows(torch.as_tensor(x).cuda())
+    val, d, E = decode(op, M)
+    _check_quant(x.astype(np.float64), val, d, E)
+
+
+@pytest.mark.parametrize("M,N", [(300, 200), (64, 8192), (1000, 37), (33, 64)])
+def test_quant6_cols_t_decodes_within_bound(F, M, N):
+    rng = np.random.default_rng(M * N)
+    x = (rng.standard_normal((M, N)) * np.exp(rng.uniform(-10, 10, (M, 1)))).astype(np.float32)
+    op, cs = F.quant6_cols_t(torch.as_tensor(x).cuda(), want_colsum=True)
+    val, d, E = decode(op, N)
+    _check_quant(x.T.astype(np.float64), val, d, E)
+    assert rel_err(host(cs), x.astype(np.float64).sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 256), (257, 520, 1000), (64, 64, 64), (1000, 129, 1024),
+                                   (2048, 1024, 8192), (3, 7, 784)])
+def test_gemm_fp6_every_variant(F, M, N, K):
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M + 3 * N + K)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-6, 6, (M, 1)))).astype(np.float32)
+    w = rng.integers(-1, 2, (N, K)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    xt = torch.as_tensor(x).cuda()
+    op = F.quant6_rows(xt)
+    w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
+    val, _, _ = decode(op, M)
+    exact_q = val[:, :K] @ w.astype(np.float64).T + bias        # what the MFMA sums (no rounding)
+    exact_x = x.astype(np.float64) @ w.astype(np.float64).T + bias
+    names = set()
+    try:
+        for v in range(0, 8):
+            L.call("bnn_gemm_fp6_set_variant", v)
+            name = L.lib().bnn_gemm_fp6_kernel(M, N).decode()
+            if name in names:
+                continue
+            names.add(name)
+            C = host(F.gemm_fp6(op, w4, N, bias=torch.as_tensor(bias).cuda()))
+            assert rel_err(C, exact_q) < 2e-6, (name, rel_err(C, exact_q))
+            assert rel_err(C, exact_x) < 1e-5, (name, rel_err(C, exact_x))
+    finally:
+        L.call("bnn_gemm_fp6_set_variant", -1)
+    assert len(names) >= 3
+
+
+def test_gemm_fp6_propagates_nan(F):
+    """A NaN in the fp32 operand makes its block's E8M0 scale NaN: every output that sums over it
+    is NaN (as the reference's fp32 GEMM gives), the others are unaffected."""
+    x = torch.randn(40, 128, device="cuda")
+    x[7, 100] = float("nan")
+    w = torch.randint(-1, 2, (24, 128), device="cuda").float()
+    C = F.gemm_fp6(F.quant6_rows(x), F.sign_pack_fp4(w)[0], 24)
+    isn = torch.isnan(C)
+    assert bool(isn[7].all()) and int(isn.sum()) == 24

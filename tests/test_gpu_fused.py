@@ -266,25 +266,27 @@ def test_batchnorm2d_eval_backward_vs_torch(F, pool):
 
 def test_eval_mode_net_input_gradient(F):
     """An eval-mode MLP (frozen BN, e.g. input-gradient computation) through the fused ops vs the
-    drop-in ops with torch's BatchNorm1d: same input gradient."""
+    drop-in ops with torch's BatchNorm1d, same weights and running statistics.  The two BN
+    implementations round (x - running_mean) * invstd differently, which can flip the sign of a
+    value next to the running mean, so the bar is loose (loss 1e-3, gradients 1e-2 norm-wise);
+    the train-mode formula applied in eval (the bug this guards against) is off by O(1)."""
     from bnn_amd import nets
     from bnn_amd.data import synthetic_mnist
     torch.manual_seed(8)
     a = nets.MLP(256, 128, 64, p_drop=0.0, org_protocol=False, mutate_input=False).cuda()
     b = nets.MLP(256, 128, 64, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True).cuda()
-    b.load_state_dict(a.state_dict())
     x, y = synthetic_mnist(64, seed=3, device="cuda")
-    for m in (a, b):                      # give the running statistics non-trivial values
-        m.train()
-        with torch.no_grad():
-            m(x)
-        m.eval()
+    b.train()
+    with torch.no_grad():                 # non-trivial running statistics
+        b(x)
+    a.load_state_dict(b.state_dict())
     outs = []
     for m in (a, b):
+        m.eval()
         xi = x.clone().requires_grad_(True)
         loss = torch.nn.functional.cross_entropy(m(xi), y)
         loss.backward()
         outs.append((loss.item(), host(xi.grad), host(m.bn2.weight.grad)))
-    assert abs(outs[0][0] - outs[1][0]) < 1e-5
-    assert rel_err(outs[1][1], outs[0][1]) < 1e-4
-    assert rel_err(outs[1][2], outs[0][2]) < 1e-4
+    assert abs(outs[0][0] - outs[1][0]) < 1e-3
+    assert rel_err(outs[1][1], outs[0][1]) < 1e-2
+    assert rel_err(outs[1][2], outs[0][2]) < 1e-2
