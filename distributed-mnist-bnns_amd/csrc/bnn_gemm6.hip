@@ -235,6 +235,16 @@ __device__ __forceinline__ void glds16_6(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// The same 16-B LDS-DMA in its saddr form: wave-uniform 64-bit base in SGPRs + per-lane 32-bit
+// offset, LDS destination through M0 (as bnn_gemm.hip's glds16_s).
+__device__ __forceinline__ void glds16_6s(const void* sbase, uint32_t voff, void* l) {
+  const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(l);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :
+               : "s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt6() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -267,16 +277,27 @@ __device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int& tm, int& 
 //   A hi : BM rows x  64 B  (block 0: planes 01, 23; block 1: ...), chunk c at c ^ ((row >> 2) & 3)
 //   A sc : BM x 2 B        (row-major, plane-0 bytes of blocks 0, 1)
 //   B    : BN rows x  32 B  (the 64 FP4 codes), chunk c at c ^ ((row >> 3) & 1)
-template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params p) {
+// DIAG (timing-only builds, wrong results): 1 = no global->LDS staging, 2 = no LDS fragment reads.
+// OCC = waves per SIMD the register allocation must allow (2: one 512-thread workgroup per CU;
+// 4: two, whose independent barriers let one's LDS-read phase overlap the other's MFMAs).
+// PP = 1 (WM = 2, STAGES = 3): software-pipelined k loop.  Each k-step's two A tiles are split
+// around a mid-step barrier: the MFMAs of tile 0 run while tile 1's fragments are read; then the
+// barrier retires the NEXT stage and its B and tile-0 fragments are read into the second register
+// set while tile 1's MFMAs run -- no k-step starts with the matrix pipe waiting on LDS.  All three
+// ring slots are in flight: stage kt+1 is waited for at step kt with stage kt+2 still landing
+// (two steps of cover), and stage kt+3 refills the slot stage kt has just left.
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6Params p) {
+  static_assert(PP != 1 || (WM == 2 && STAGES == 3 && DIAG == 0), "pipelined form 1: 2 tile rows, 3 stages");
+  static_assert(PP != 2 || (WM == 1 && WN % 2 == 0 && STAGES == 3 && DIAG == 0),
+                "pipelined form 2: 1 tile row, an even number of tile columns, 3 stages");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_ST = BM * 2, B_ST = BN * 32;
   constexpr int SC_PAD = (SC_ST + 1023) / 1024 * 1024;
   constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST;
   constexpr int I_LO = LO_ST / 1024, I_HI = HI_ST / 1024, I_SC = SC_PAD / 1024, I_B = B_ST / 1024;
-  constexpr int NPIECE = I_LO + I_HI + I_SC + I_B;
-  constexpr int PER_WAVE = (NPIECE + NW - 1) / NW;   // waves >= NPIECE % NW issue one piece less
+  constexpr int PER_WAVE = (I_LO + I_HI + I_B) / NW + 1;   // wave 0 also issues the scale piece
   __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
 
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -287,40 +308,51 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params
   const int64_t nblk = p.K / QB;
   const int nk = p.K / 64;
 
-  // piece i of a stage (1 KiB = 64 lanes x 16 B): lo rows 8 per piece, hi rows 16, scales
-  // 512 rows (1 KiB of 2-B entries), B rows 32.  Source rows are clamped to the last valid row
-  // (their results are never stored); the XOR swizzles live on the source chunk (LDS stays linear).
-  auto stage = [&](int kt, int buf) {
+  // One stage = I_LO + I_HI + I_SC + I_B LDS-DMA pieces of 1 KiB (64 lanes x 16 B): lo 8 rows per
+  // piece, hi 16 rows, scales 512 rows of 2-B entries (only this tile's BM rows are loaded), B 32
+  // rows.  Every wave issues the same compile-time number of lo / hi / B pieces (wave 0 also the
+  // scale piece); each piece's per-lane source offset (row clamped to the last valid row -- its
+  // results are never stored -- and the XOR-swizzled 16-B chunk: the LDS image stays linear) is
+  // k-invariant and computed once, so a stage is a wave-uniform base advance + the saddr-form DMA.
+  static_assert(I_LO % NW == 0 && I_HI % NW == 0 && I_B % NW == 0 && I_SC == 1, "piece split");
+  constexpr int P_LO = I_LO / NW, P_HI = I_HI / NW, P_B = I_B / NW;
+  uint32_t off_lo[P_LO], off_hi[P_HI], off_b[P_B];
+#pragma unroll
+  for (int ii = 0; ii < P_LO; ++ii) {
+    const int i = wave + ii * NW;
+    const int lrow = i * 8 + (lane >> 3), c = lane & 7;
+    off_lo[ii] = (uint32_t)min(lrow, p.M - 1 - m0) * (uint32_t)(nblk * 64) + 16u * (uint32_t)(c ^ ((lrow >> 1) & 7));
+  }
+#pragma unroll
+  for (int ii = 0; ii < P_HI; ++ii) {
+    const int i = wave + ii * NW;
+    const int lrow = i * 16 + (lane >> 2), c = lane & 3;
+    off_hi[ii] = (uint32_t)min(lrow, p.M - 1 - m0) * (uint32_t)(nblk * 32) + 16u * (uint32_t)(c ^ ((lrow >> 2) & 3));
+  }
+#pragma unroll
+  for (int ii = 0; ii < P_B; ++ii) {
+    const int i = wave + ii * NW;
+    const int lrow = i * 32 + (lane >> 1), c = lane & 1;
+    off_b[ii] = (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
+  }
+  const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64;
+  const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32;
+  const uint8_t* sc_base = p.asc + (int64_t)m0 * 2;
+  const uint8_t* b_base = p.b + (int64_t)n0 * p.ldb;
+  auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
+    if constexpr (DIAG == 1) return;
     char* base = smem + buf * ST;
 #pragma unroll
-    for (int ii = 0; ii < PER_WAVE; ++ii) {
-      const int i = wave + ii * NW;
-      if (i >= NPIECE) break;          // wave-uniform
-      if (i < I_LO) {
-        const int lrow = i * 8 + (lane >> 3), c = lane & 7;
-        const int row = min(m0 + lrow, p.M - 1);
-        const int src = c ^ ((lrow >> 1) & 7);
-        glds16_6(p.alo + ((int64_t)row * nblk + 2 * kt) * 64 + 16 * src, base + i * 1024);
-      } else if (i < I_LO + I_HI) {
-        const int j = i - I_LO;
-        const int lrow = j * 16 + (lane >> 2), c = lane & 3;
-        const int row = min(m0 + lrow, p.M - 1);
-        const int src = c ^ ((lrow >> 2) & 3);
-        glds16_6(p.ahi + ((int64_t)row * nblk + 2 * kt) * 32 + 16 * src, base + LO_ST + j * 1024);
-      } else if (i < I_LO + I_HI + I_SC) {
-        const int j = i - I_LO - I_HI;
-        // 2-byte entries, 8 rows per lane; rows beyond asc_rows are read from the padded tail
-        const int64_t off = (int64_t)kt * p.asc_rows * 2 + (int64_t)m0 * 2 + j * 1024 + lane * 16;
-        if (j * 1024 + lane * 16 < SC_ST)       // only this tile's BM rows (never past the slab)
-          glds16_6(p.asc + off, base + LO_ST + HI_ST + j * 1024);
-      } else {
-        const int j = i - I_LO - I_HI - I_SC;
-        const int lrow = j * 32 + (lane >> 1), c = lane & 1;
-        const int row = min(n0 + lrow, p.N - 1);
-        const int src = c ^ ((lrow >> 3) & 1);
-        glds16_6(p.b + (int64_t)row * p.ldb + (int64_t)kt * 32 + 16 * src, base + LO_ST + HI_ST + SC_PAD + j * 1024);
-      }
-    }
+    for (int ii = 0; ii < P_LO; ++ii)
+      glds16_6s(lo_base + (int64_t)kt * 128, off_lo[ii], base + (wave + ii * NW) * 1024);
+#pragma unroll
+    for (int ii = 0; ii < P_HI; ++ii)
+      glds16_6s(hi_base + (int64_t)kt * 64, off_hi[ii], base + LO_ST + (wave + ii * NW) * 1024);
+#pragma unroll
+    for (int ii = 0; ii < P_B; ++ii)
+      glds16_6s(b_base + (int64_t)kt * 32, off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
+    if (wave == 0)   // a whole 1-KiB piece (512 rows): the scale array has 512 rows of tail padding
+      glds16_6(sc_base + (int64_t)kt * p.asc_rows * 2 + lane * 16, base + LO_ST + HI_ST);
   };
 
   v16f acc[WM][WN];
@@ -330,12 +362,174 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params
     for (int u = 0; u < WN; ++u) acc[t][u] = v16f{0};
 
   const int r = lane & 31, h = lane >> 5;
+  // pieces this wave issues per stage (wave-uniform): the counted waits keep later stages in
+  // flight while retiring one
+  const int mine = wave == 0 ? PER_WAVE : PER_WAVE - 1;
+
+  struct AFrag {      // the 4 planes' 6-dword MFMA operands (elements 6, 7 unused) + scale byte
+    v8i a0, a1, a2, a3;
+    int sb;
+  };
+  auto read_a = [&](const char* base, int t, AFrag& f) __attribute__((always_inline)) {
+    const int lrow = wm * WM * 32 + t * 32 + r;
+    const char* sLo = base;
+    const char* sHi = base + LO_ST;
+    const uint8_t* sSc = reinterpret_cast<const uint8_t*>(base + LO_ST + HI_ST);
+    const int sw = (lrow >> 1) & 7;
+    const v4i l0 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 0) ^ sw));
+    const v4i l1 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 1) ^ sw));
+    const v4i l2 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 2) ^ sw));
+    const v4i l3 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 3) ^ sw));
+    const v4i h01 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2) ^ ((lrow >> 2) & 3)));
+    const v4i h23 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2 + 1) ^ ((lrow >> 2) & 3)));
+    f.a0 = v8i{l0.x, l0.y, l0.z, l0.w, h01.x, h01.y, 0, 0};
+    f.a1 = v8i{l1.x, l1.y, l1.z, l1.w, h01.z, h01.w, 0, 0};
+    f.a2 = v8i{l2.x, l2.y, l2.z, l2.w, h23.x, h23.y, 0, 0};
+    f.a3 = v8i{l3.x, l3.y, l3.z, l3.w, h23.z, h23.w, 0, 0};
+    f.sb = sSc[lrow * 2 + h];
+  };
+  // B fragments: row n, 16 B = k-block h
+  auto read_b = [&](const char* base, v4i (&bf)[WN]) __attribute__((always_inline)) {
+    const char* sB = base + LO_ST + HI_ST + SC_PAD;
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int lrow = wn * WN * 32 + u * 32 + r;
+      bf[u] = *reinterpret_cast<const v4i*>(sB + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
+    }
+  };
+  // MFMAs of one A fragment against B fragments u0 .. u1-1
+  auto mma_cols = [&](const AFrag& f, const v4i (&bf)[WN], v16f (&ac)[WN], int u0, int u1) __attribute__((always_inline)) {
+    const v8i a0 = f.a0, a1 = f.a1, a2 = f.a2, a3 = f.a3;
+    const int sb = f.sb;
+    const int s0 = sb, s1 = sb == 255 ? 255 : sb + 5, s2 = sb == 255 ? 255 : sb + 10, s3 = sb == 255 ? 255 : sb + 15;
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      if (u < u0 || u >= u1) continue;
+      const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a3, bb, ac[u], 2, 4, 0, s3, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, ac[u], 2, 4, 0, s2, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, ac[u], 2, 4, 0, s1, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, ac[u], 2, 4, 0, s0, 0, 127);
+    }
+  };
+  // B fragments u0 .. u1-1
+  auto read_b_cols = [&](const char* base, v4i (&bf)[WN], int u0, int u1) __attribute__((always_inline)) {
+    const char* sB = base + LO_ST + HI_ST + SC_PAD;
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      if (u < u0 || u >= u1) continue;
+      const int lrow = wn * WN * 32 + u * 32 + r;
+      bf[u] = *reinterpret_cast<const v4i*>(sB + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
+    }
+  };
+  auto mma_tile = [&](const AFrag& f, const v4i (&bf)[WN], v16f (&ac)[WN]) __attribute__((always_inline)) {
+    const v8i a0 = f.a0, a1 = f.a1, a2 = f.a2, a3 = f.a3;
+    // a NaN block (255) stays NaN in every plane; otherwise plane j scale = sb + 5j (<= 254)
+    const int sb = f.sb;
+    const int s0 = sb, s1 = sb == 255 ? 255 : sb + 5, s2 = sb == 255 ? 255 : sb + 10, s3 = sb == 255 ? 255 : sb + 15;
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a3, bb, ac[u], 2, 4, 0, s3, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, ac[u], 2, 4, 0, s2, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, ac[u], 2, 4, 0, s1, 0, 127);
+      ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, ac[u], 2, 4, 0, s0, 0, 127);
+    }
+  };
+
+  if constexpr (PP == 2) {
+    // form 2: one A fragment per k-step; its MFMAs against B columns [0, WN/2) run while the
+    // columns [WN/2, WN) are read, then the barrier retires the next stage and its A fragment and
+    // first-half B columns are read while the second-half MFMAs run
+    constexpr int HN = WN / 2;
+    auto buf_of = [&](int kt) __attribute__((always_inline)) { return smem + (kt % STAGES) * ST; };
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s)
+      if (s < nk) stage(s, s);
+    if (nk >= 3) {
+      if (mine == PER_WAVE) wait_vmcnt6<2 * PER_WAVE>(); else wait_vmcnt6<2 * (PER_WAVE - 1)>();
+    } else if (nk == 2) {
+      if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();
+    } else {
+      wait_vmcnt6<0>();
+    }
+    barrier6();
+    v4i b0[WN], b1[WN];
+    AFrag f0, f1;
+    read_b_cols(buf_of(0), b0, 0, HN);
+    read_a(buf_of(0), 0, f0);
+#define BNN_FP6_STEP2(KT, BC, FC, BN, FN)                                                             \
+  {                                                                                                  \
+    read_b_cols(buf_of(KT), BC, HN, WN);                                                             \
+    mma_cols(FC, BC, acc[0], 0, HN);                                                                 \
+    if ((KT) + 1 < nk) {                                                                             \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                             \
+      if ((KT) + 2 < nk) {                                                                           \
+        if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();             \
+      } else {                                                                                       \
+        wait_vmcnt6<0>();                                                                            \
+      }                                                                                              \
+      barrier6();                                                                                    \
+      if ((KT) + 3 < nk) stage((KT) + 3, ((KT) + 3) % STAGES);                                       \
+      read_b_cols(buf_of((KT) + 1), BN, 0, HN);                                                      \
+      read_a(buf_of((KT) + 1), 0, FN);                                                               \
+    }                                                                                                \
+    mma_cols(FC, BC, acc[0], HN, WN);                                                                \
+  }
+    for (int kt = 0; kt < nk; kt += 2) {
+      BNN_FP6_STEP2(kt, b0, f0, b1, f1)
+      if (kt + 1 < nk) BNN_FP6_STEP2(kt + 1, b1, f1, b0, f0)
+    }
+#undef BNN_FP6_STEP2
+  } else if constexpr (PP == 1) {
+    auto buf_of = [&](int kt) __attribute__((always_inline)) { return smem + (kt % STAGES) * ST; };
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s)
+      if (s < nk) stage(s, s);
+    // stage 0 ready, stages 1 and 2 may still be landing
+    if (nk >= 3) {
+      if (mine == PER_WAVE) wait_vmcnt6<2 * PER_WAVE>(); else wait_vmcnt6<2 * (PER_WAVE - 1)>();
+    } else if (nk == 2) {
+      if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();
+    } else {
+      wait_vmcnt6<0>();
+    }
+    barrier6();
+    v4i b0[WN], b1[WN];
+    AFrag f0, f1;
+    read_b(buf_of(0), b0);
+    read_a(buf_of(0), 0, f0);
+    // one k-step (written out twice so each register set keeps a fixed name): (BC, FC) hold this
+    // step's B and tile-0 fragments, (BN, FN) receive the next step's
+#define BNN_FP6_STEP(KT, BC, FC, BN, FN)                                                              \
+  {                                                                                                  \
+    AFrag ft;                                                                                        \
+    read_a(buf_of(KT), 1, ft);                                                                       \
+    mma_tile(FC, BC, acc[0]);                                                                        \
+    if ((KT) + 1 < nk) {                                                                             \
+      /* tile 1's reads of this slot are complete before any wave may refill it */                   \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                             \
+      if ((KT) + 2 < nk) {                                                                           \
+        if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();             \
+      } else {                                                                                       \
+        wait_vmcnt6<0>();                                                                            \
+      }                                                                                              \
+      barrier6();                                                                                    \
+      if ((KT) + 3 < nk) stage((KT) + 3, ((KT) + 3) % STAGES);                                       \
+      read_b(buf_of((KT) + 1), BN);                                                                  \
+      read_a(buf_of((KT) + 1), 0, FN);                                                               \
+    }                                                                                                \
+    mma_tile(ft, BC, acc[1]);                                                                        \
+  }
+    for (int kt = 0; kt < nk; kt += 2) {
+      BNN_FP6_STEP(kt, b0, f0, b1, f1)
+      if (kt + 1 < nk) BNN_FP6_STEP(kt + 1, b1, f1, b0, f0)
+    }
+#undef BNN_FP6_STEP
+  } else {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s, s);
-  // pieces this wave issues per stage (wave-uniform): the counted wait keeps the next stage in
-  // flight while retiring this one
-  const int mine = (NPIECE - wave + NW - 1) / NW;
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(STAGES - 2, nk - 1 - kt);
     if constexpr (STAGES >= 3) {
@@ -348,42 +542,23 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params
     barrier6();
     if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const char* base = smem + (kt % STAGES) * ST;
-    const char* sLo = base;
-    const char* sHi = base + LO_ST;
-    const uint8_t* sSc = reinterpret_cast<const uint8_t*>(base + LO_ST + HI_ST);
-    const char* sB = base + LO_ST + HI_ST + SC_PAD;
-    // B fragments: row n, 16 B = k-block h
     v4i bf[WN];
-#pragma unroll
-    for (int u = 0; u < WN; ++u) {
-      const int lrow = wn * WN * 32 + u * 32 + r;
-      bf[u] = *reinterpret_cast<const v4i*>(sB + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
-    }
+    read_b(base, bf);
 #pragma unroll
     for (int t = 0; t < WM; ++t) {
-      const int lrow = wm * WM * 32 + t * 32 + r;
-      v4i lo4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        lo4[j] = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + j) ^ ((lrow >> 1) & 7)));
-      const v4i hi01 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2) ^ ((lrow >> 2) & 3)));
-      const v4i hi23 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2 + 1) ^ ((lrow >> 2) & 3)));
-      const int sb = sSc[lrow * 2 + h];
-      const v8i a0 = {lo4[0].x, lo4[0].y, lo4[0].z, lo4[0].w, hi01.x, hi01.y, 0, 0};
-      const v8i a1 = {lo4[1].x, lo4[1].y, lo4[1].z, lo4[1].w, hi01.z, hi01.w, 0, 0};
-      const v8i a2 = {lo4[2].x, lo4[2].y, lo4[2].z, lo4[2].w, hi23.x, hi23.y, 0, 0};
-      const v8i a3 = {lo4[3].x, lo4[3].y, lo4[3].z, lo4[3].w, hi23.z, hi23.w, 0, 0};
-      // a NaN block (255) stays NaN in every plane; otherwise plane j scale = sb + 5j (<= 254)
-      const int s0 = sb, s1 = sb == 255 ? 255 : sb + 5, s2 = sb == 255 ? 255 : sb + 10, s3 = sb == 255 ? 255 : sb + 15;
-#pragma unroll
-      for (int u = 0; u < WN; ++u) {
-        const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
-        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a3, bb, acc[t][u], 2, 4, 0, s3, 0, 127);
-        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, acc[t][u], 2, 4, 0, s2, 0, 127);
-        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, acc[t][u], 2, 4, 0, s1, 0, 127);
-        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, acc[t][u], 2, 4, 0, s0, 0, 127);
+      AFrag f;
+      if constexpr (DIAG == 2) {
+        f.a0 = v8i{lane, t, kt, 1, lane, t, 0, 0};
+        f.a1 = v8i{t, lane, kt, 2, kt, lane, 0, 0};
+        f.a2 = v8i{kt, t, lane, 3, t, kt, 0, 0};
+        f.a3 = v8i{lane, kt, t, 4, lane, kt, 0, 0};
+        f.sb = 100 + (lane & 7);
+      } else {
+        read_a(base, t, f);
       }
+      mma_tile(f, bf, acc[t]);
     }
+  }
   }
 
   // epilogue: C/D map of the 32x32 MFMA (reg i -> row (i&3)+8(i>>2)+4h, col lane&31), transposed
@@ -429,12 +604,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp6_k(Gemm6Params
   }
 }
 
-template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES>
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0>
 int launch6(Gemm6Params p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES>), dim3((unsigned)((int64_t)p.gm * p.gn)),
+  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES, DIAG, OCC, PP>), dim3((unsigned)((int64_t)p.gm * p.gn)),
                      dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   return check_launch("bnn_gemm_fp6");
 }
@@ -452,16 +627,41 @@ const Variant6 kVariants6[] = {
     {2, "gemm_fp6_k<2, 2, 2, 2, 3>", launch6<2, 2, 2, 2, 3>, 128},
     {3, "gemm_fp6_k<4, 2, 2, 4, 2>", launch6<4, 2, 2, 4, 2>, 256},
     {4, "gemm_fp6_k<2, 4, 2, 2, 4>", launch6<2, 4, 2, 2, 4>, 128},
+    // tall-N tiles: the FP6 operand costs 3 B/element against 0.5 for FP4, so BM x BN = 128 x 512
+    // moves 29% fewer bytes per MAC than 256 x 256 and leaves room for a third stage
+    {5, "gemm_fp6_k<2, 4, 2, 4, 3>", launch6<2, 4, 2, 4, 3>, 128},
+    {6, "gemm_fp6_k<1, 8, 4, 2, 3>", launch6<1, 8, 4, 2, 3>, 128},
+    {7, "gemm_fp6_k<2, 4, 2, 4, 2>", launch6<2, 4, 2, 4, 2>, 128},
+    // two workgroups per CU (OCC 4: <= 128 registers per lane)
+    {8, "gemm_fp6_k<2, 4, 2, 2, 2, 0, 4>", launch6<2, 4, 2, 2, 2, 0, 4>, 128},
+    // software-pipelined k loop (PP): 128 x 512 and 128 x 256 tiles
+    {10, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 1>", launch6<2, 4, 2, 4, 3, 0, 2, 1>, 128},
+    {11, "gemm_fp6_k<2, 4, 2, 2, 3, 0, 2, 1>", launch6<2, 4, 2, 2, 3, 0, 2, 1>, 128},
+    // pipelined form 2: 128 x 512 tile, every wave 32 rows x 256 columns (4 x 2 waves)
+    {12, "gemm_fp6_k<4, 2, 1, 8, 3, 0, 2, 2>", launch6<4, 2, 1, 8, 3, 0, 2, 2>, 128},
+    {13, "gemm_fp6_k<4, 1, 1, 8, 3, 0, 2, 2>", launch6<4, 1, 1, 8, 3, 0, 2, 2>, 128},
+    // timing-only diagnostics of variant 5 (wrong results; never picked by default)
+    {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128},
+    {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128},
 };
 
 int g_variant6 = -1;
 
+const Variant6* find6(int id) {
+  for (const Variant6& v : kVariants6)
+    if (v.id == id) return &v;
+  return &kVariants6[0];      // unknown id: the first entry (the sweep skips repeated names)
+}
+
+// Default per shape (tools/gpu_fp6_sweep.py, profiles/r02_fp6_*.log): the 128 x 512 tile (the
+// FP6 operand is 6x the bytes of the FP4 one per row, so tall-N tiles move the fewest bytes per
+// MAC) when the grid still fills the chip several times over, else 128 x 256 / 128 x 128.
 const Variant6* pick6(int64_t M, int64_t N) {
-  if (g_variant6 >= 0)
-    for (const Variant6& v : kVariants6)
-      if (v.id == g_variant6) return &v;
-  const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
-  return big ? &kVariants6[0] : &kVariants6[2];
+  if (g_variant6 >= 0) return find6(g_variant6);
+  const int64_t t512 = ((M + 127) / 128) * ((N + 511) / 512), t256 = ((M + 127) / 128) * ((N + 255) / 256);
+  if (t512 >= 1024) return find6(7);
+  if (t256 >= 512) return find6(1);
+  return find6(2);
 }
 
 inline hipStream_t S6(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -471,7 +671,9 @@ inline hipStream_t S6(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 using namespace bnn;
 
-BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return round_up(rows, 256); }
+// scale-array row pitch: rows rounded up to 256, plus 512 rows of padding so the GEMM's per-stage
+// 1-KiB scale piece (512 rows from the tile's first row) never reads past the slab
+BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return round_up(rows, 256) + 512; }
 
 BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
                             uint8_t* sc, void* stream) {
@@ -484,7 +686,7 @@ BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, i
   const int64_t nblk = Kp / QB;
   const int vec = aligned16(x) && (ldx % 4 == 0);
   hipLaunchKernelGGL(quant6_rows_k, dim3((unsigned)M, (unsigned)((nblk + 31) / 32)), dim3(256), 0, S6(stream), x, M,
-                     K, ldx, nblk, lo, hi, sc, round_up(M, 256), vec);
+                     K, ldx, nblk, lo, hi, sc, bnn_quant6_scale_rows(M), vec);
   return check_launch("bnn_quant6_rows");
 }
 
@@ -504,7 +706,7 @@ BNN_API int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx,
   const int64_t R = (nblk + QC_BLKS - 1) / QC_BLKS;
   double* part = colsum ? reinterpret_cast<double*>(work) : nullptr;
   hipLaunchKernelGGL(quant6_cols_t_k, dim3((unsigned)((N + QC_COLS - 1) / QC_COLS), (unsigned)R), dim3(512), 0,
-                     S6(stream), x, M, N, ldx, nblk, lo, hi, sc, round_up(N, 256), part);
+                     S6(stream), x, M, N, ldx, nblk, lo, hi, sc, bnn_quant6_scale_rows(N), part);
   if (colsum)
     hipLaunchKernelGGL(colsum_final_k, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S6(stream), part, R, N,
                        colsum);
@@ -515,10 +717,10 @@ BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
                          const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
                          int64_t N, int64_t K, void* stream) {
   if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || ldb < K / 2 || ldb % 16 != 0 ||
-      ldc < N || asc_rows < round_up(M, 256) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
+      ldc < N || asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
       !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
     set_error("bnn_gemm_fp6: bad arguments (M=%lld N=%lld K=%lld ldb=%lld asc_rows=%lld; K a positive multiple of "
-              "64, asc_rows a multiple of 256 >= round_up(M,256))",
+              "64, asc_rows a multiple of 256 >= bnn_quant6_scale_rows(M))",
               (long long)M, (long long)N, (long long)K, (long long)ldb, (long long)asc_rows);
     return kErrInval;
   }

@@ -122,7 +122,8 @@ const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, in
  * Layouts (Kp = padded reduction length, multiple of 64):
  *   lo  [rows][Kp/32][64 B]   per block and plane j: dwords 0..3 of the plane's MFMA operand
  *   hi  [rows][Kp/32][32 B]   per block: dwords 4..5 of planes 0,1,2,3
- *   sc  [Kp/64][round_up(rows,256)][2]  E8M0 byte of plane 0 per block (plane j: +5j; 255 = NaN)
+ *   sc  [Kp/64][bnn_quant6_scale_rows(rows)][2]  E8M0 byte of plane 0 per block (plane j: +5j;
+ *       255 = NaN); the row pitch carries 512 rows of tail padding the GEMM may read
  * replaces: the fp32 GEMMs of BinarizeLinear's autograd (dX = dY.W_b, dW = dY^T.X_b) and the
  * first layer's F.linear(x, W_b) (models/binarized_modules.py:80). */
 int64_t bnn_quant6_scale_rows(int64_t rows);

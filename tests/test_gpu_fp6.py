@@ -120,7 +120,7 @@ def test_gemm_fp6_every_variant(F, M, N, K):
     exact_x = x.astype(np.float64) @ w.astype(np.float64).T + bias
     names = set()
     try:
-        for v in range(0, 8):
+        for v in range(0, 16):
             L.call("bnn_gemm_fp6_set_variant", v)
             name = L.lib().bnn_gemm_fp6_kernel(M, N).decode()
             if name in names:
