@@ -59,8 +59,11 @@ CPU_BATCH = {"wide": 512, "mlp": 1024, "small": 64, "cnn": 256}
 
 
 def digit_pairs(kernel):
-    """int8 MFMA passes per algorithmic MAC of a GEMM kernel instance (fp32 operands enter as 3
-    int8 digit planes: (3,1) = 3 passes, (3,3) = 6)."""
+    """MFMA passes per algorithmic MAC of a GEMM kernel instance: fp32 operands enter as digit
+    planes -- 3 int8 planes on gemm_i8 ((3,1) = 3 passes, (3,3) = 6), 4 FP6 e2m3 planes against
+    an FP4 ternary operand on gemm_fp6 (4 passes)."""
+    if kernel.startswith("gemm_fp6"):
+        return 4
     for tag, n in (("<3, 3,", 6), ("<3, 1,", 3)):
         if tag in kernel:
             return n
@@ -75,6 +78,8 @@ def op_peak(kernel):
         return "valu", MI355X_DOT4_TOPS, "int8 dot4 / MFMA ops (2*N*Co*OH*OW*C*KH*KW)"
     if kernel.startswith("gemm_fp4"):
         return "mfma", MI355X_FP4_DENSE_TOPS, "ternary GEMM ops 2*M*N*K on the FP4 MFMA"
+    if kernel.startswith("gemm_fp6"):   # same f8f6f4 MFMA, FP6 x FP4 issues at the FP4 rate
+        return "mfma", MI355X_FP4_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the FP6 x FP4 MFMA (4 digit planes)"
     if kernel.startswith("gemm_xnor"):   # VALU popcount bound with the nonzero-mask plane
         return "valu", 840.0, "ternary popcount ops 2*M*N*K"
     return "mfma", MI355X_INT8_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the int8 MFMA"
@@ -188,9 +193,9 @@ def roofline_of(ksum, steps):
         r = {"bound": "mfma" if bound == "mfma" else bound, "achieved": round(ach, 2), "peak": round(peak, 1),
              "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None, **common, "ops_unit": ops_unit}
         pairs = digit_pairs(dom)
-        if pairs > 1:   # the int8 passes the fp32-operand emulation issues (secondary, not the work)
-            r["int8_pass_rate_tops"] = round(ach * pairs, 2)
-            r["int8_pass_frac"] = round(ach * pairs / peak, 4)
+        if pairs > 1:   # the MFMA passes the fp32-operand emulation issues (secondary, not the work)
+            r["mfma_pass_rate_tops"] = round(ach * pairs, 2)
+            r["mfma_pass_frac"] = round(ach * pairs / peak, 4)
     else:
         ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
         r = {"bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
@@ -289,8 +294,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp4/int8 MFMA (ternary operands as FP4 e2m1 / int8, fp32 operands as int8 digit planes; "
-                 "exact integer sums; fp32 I/O)",
+        "dtype": "fp4/fp6/int8 MFMA (ternary operands as FP4 e2m1, fp32 operands as 4 FP6 e2m3 digit planes "
+                 "with E8M0 block scales (backward) or 3 int8 digit planes (first layer); fp32 accumulate, fp32 I/O)",
         "data": "synthetic MNIST-shaped (80.7% zero pixels, u8/255), random-init weights, resident in HBM",
         "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",

@@ -411,7 +411,10 @@ class BinaryLinearFunction(torch.autograd.Function):
         ctx.empty = False
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         b = bias.detach() if bias is not None else None
-        ctx.fp6 = backend == "fp4" and DIGIT_GEMM == "fp6"
+        # the FP6 digit GEMMs carry 20-bit block-scaled operands: used for the backward GEMMs of a
+        # layer with a ternary input (gradient bar 1e-5); the first layer's fp32-input forward
+        # keeps the 24-bit int8 digit form (forward bar 1e-6)
+        ctx.fp6 = backend == "fp4" and DIGIT_GEMM == "fp6" and binarize_input
         qf = "fp4" if ctx.fp6 else "i8"
         if binarize_input:
             if backend == "fp4":
@@ -427,10 +430,6 @@ class BinaryLinearFunction(torch.autograd.Function):
                 wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
                 y = gemm_i8(xq, 1, wq, 1, M, N, bias=b, k_true=K)
             ctx.save_for_backward(xqt, wqt)
-        elif ctx.fp6:                               # first layer: fp32 pixels x W_b on the FP6 MFMA
-            w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache, qt_fmt=qf)
-            y = gemm_fp6(quant6_rows(x), w4, N, bias=b, k_true=K)
-            ctx.save_for_backward(x if need_dw else None, wqt)
         else:
             wq, wqt = packed_weight(weight, "i8", True, need_dx, cache)
             xd, sx = quant_rows(x)
@@ -452,7 +451,7 @@ class BinaryLinearFunction(torch.autograd.Function):
         dy = _c2d(dy)
         dx = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
-        if ctx.fp6 and (ctx.binarize_input or not ctx.needs_input_grad[1]):
+        if ctx.fp6:
             if ctx.needs_input_grad[0]:
                 dx = gemm_fp6(quant6_rows(dy), wqt, K, k_true=N)               # dY . W_b
             if ctx.needs_input_grad[1] or need_db:
@@ -462,11 +461,8 @@ class BinaryLinearFunction(torch.autograd.Function):
                 db = cs
             return dx, dw, db, None, None, None
         if ctx.needs_input_grad[0]:
-            if ctx.fp6:
-                dx = gemm_fp6(quant6_rows(dy), wqt, K, k_true=N)
-            else:
-                d, s = quant_rows(dy)                                   # [3, M, ldN]
-                dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
+            d, s = quant_rows(dy)                                   # [3, M, ldN]
+            dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
         if ctx.needs_input_grad[1] or need_db:
             dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)      # [3, N, ldM]
             if ctx.needs_input_grad[1]:

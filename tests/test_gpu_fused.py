@@ -78,8 +78,9 @@ def bn_stats(F, z, C):
 
 @pytest.mark.parametrize("M,C", [(300, 192), (1000, 1536), (77, 260), (4096, 768)])
 @pytest.mark.parametrize("fmt", [0, 1])
-@pytest.mark.parametrize("with_qt", [True, False])
+@pytest.mark.parametrize("with_qt", [None, 0, 1])
 def test_bn_apply_pack_bit_exact(F, M, C, fmt, with_qt):
+    """with_qt: no transpose, an int8 transpose (0) or an FP4 transpose (1, the FP6 GEMMs' B)."""
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M * 7 + C + fmt)
     # integer-valued pre-activations + a per-column bias (what a binarized GEMM produces): ties
@@ -101,15 +102,20 @@ def test_bn_apply_pack_bit_exact(F, M, C, fmt, with_qt):
         q = torch.full((M, F.round_up(C, 256) // 2), 0x55, dtype=torch.uint8, device="cuda")
     else:
         q = torch.full((M, F.round_up(C)), 9, dtype=torch.int8, device="cuda")
-    qt = torch.full((C, F.round_up(M)), 9, dtype=torch.int8, device="cuda") if with_qt else None
+    if with_qt == 1:
+        qt = torch.full((C, F.round_up(M, 256) // 2), 0x55, dtype=torch.uint8, device="cuda")
+    elif with_qt == 0:
+        qt = torch.full((C, F.round_up(M)), 9, dtype=torch.int8, device="cuda")
+    else:
+        qt = None
     gt, bt = dev(gamma), dev(beta)           # keep the device copies alive across the launch
-    L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo), L.ptr(gt), L.ptr(bt), fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo), L.ptr(gt), L.ptr(bt), fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0, with_qt or 0, L.stream())
     qh = host(q)
     rows = decode_fp4(qh, C) if fmt == 1 else qh.astype(np.int8)
     assert np.array_equal(rows[:, :C], s_ref)
     assert not rows[:, C:].any()
-    if with_qt:
-        qth = host(qt)
+    if with_qt is not None:
+        qth = decode_fp4(host(qt), M) if with_qt == 1 else host(qt)
         assert np.array_equal(qth[:, :M], s_ref.T)
         assert not qth[:, M:].any()
 

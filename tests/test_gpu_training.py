@@ -265,7 +265,8 @@ def test_fused_trainer_uses_repacked_weights(nets):
 
 @pytest.mark.parametrize("N,K", [(300, 1000), (64, 784), (8192, 784), (100, 37)])
 @pytest.mark.parametrize("fmt", [0, 1])
-def test_adam_clamp_pack_matches_unfused(nets, N, K, fmt):
+@pytest.mark.parametrize("qt_fmt", [0, 1])
+def test_adam_clamp_pack_matches_unfused(nets, N, K, fmt, qt_fmt):
     """bnn_adam_clamp_pack: p, m, v bit-identical to bnn_adam_clamp; q / qt bit-identical to
     sign-packing the updated weight (padding zero)."""
     from bnn_amd import _lib as L
@@ -283,14 +284,18 @@ def test_adam_clamp_pack_matches_unfused(nets, N, K, fmt):
         q = torch.full((N, F.round_up(K, 256) // 2), 0x77, dtype=torch.uint8, device="cuda")
     else:
         q = torch.full((N, F.round_up(K)), 7, dtype=torch.int8, device="cuda")
-    qt = torch.full((K, F.round_up(N)), 7, dtype=torch.int8, device="cuda")
+    if qt_fmt == 1:
+        qt = torch.full((K, F.round_up(N, 256) // 2), 0x77, dtype=torch.uint8, device="cuda")
+    else:
+        qt = torch.full((K, F.round_up(N)), 7, dtype=torch.int8, device="cuda")
     L.call("bnn_adam_clamp_pack", L.ptr(b[0]), L.ptr(g), L.ptr(b[1]), L.ptr(b[2]), N, K, 0.01, 0.9, 0.999, 1e-8,
-           3, 1.0, 1, fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], L.stream())
+           3, 1.0, 1, fmt, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], qt_fmt, L.stream())
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     if fmt == 1:
-        q_ref, qt_ref = F.sign_pack_fp4(a[0], want_qt=True)
+        q_ref, _ = F.sign_pack_fp4(a[0])
     else:
-        q_ref, qt_ref = F.sign_pack(a[0], True, True)
+        q_ref, _ = F.sign_pack(a[0], True, False)
+    _, qt_ref = F.sign_pack_fp4(a[0], want_qt=True, qt_fmt="fp4" if qt_fmt == 1 else "i8", want_q=False)
     assert torch.equal(q, q_ref)
     assert torch.equal(qt, qt_ref)
