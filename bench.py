@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--backend", default="fp4", choices=["fp4", "mfma", "xnor"])
     ap.add_argument("--exchange", action="store_true",
                     help="run the gradient-exchange bucket path at N=1 too (flat buckets, hooks)")
+    ap.add_argument("--fp32-input", action="store_true",
+                    help="feed fp32 images (u/255) instead of the u8 pixels the MLPs' fc1 consumes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work per config")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -236,7 +238,8 @@ def main():
     model = build(args.config, args.backend).to(dev).train()
     exchange = GradExchange(model, bucket_mb=args.bucket_mb) if use_exchange else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model))
-    x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev)
+    as_u8 = args.config != "cnn" and not args.fp32_input
+    x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev, as_u8=as_u8)
     crit = torch.nn.CrossEntropyLoss()
 
     def step():
@@ -296,7 +299,9 @@ def main():
         "vs_baseline": None,
         "dtype": "fp4/fp6/int8 MFMA (ternary operands as FP4 e2m1, fp32 operands as 4 FP6 e2m3 digit planes "
                  "with E8M0 block scales (backward) or 3 int8 digit planes (first layer); fp32 accumulate, fp32 I/O)",
-        "data": "synthetic MNIST-shaped (80.7% zero pixels, u8/255), random-init weights, resident in HBM",
+        "data": ("synthetic MNIST-shaped (80.7% zero pixels), resident in HBM as "
+                 + ("u8 pixels (fc1 applies ToTensor on the bytes)" if as_u8 else "fp32 u8/255 images")
+                 + ", random-init weights"),
         "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
                    "backend": args.backend, "exchange": bool(use_exchange), "loss_last_step": round(final_loss, 5)},
@@ -305,7 +310,7 @@ def main():
         # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (2*M*N*K) and the
         # binary convolutions' forward for the CNN
         fwd = [v for k, v in ksum.items()
-               if k.startswith("gemm_fp4") or (k.startswith("gemm_i8") and "<1, 1," in k) or k == "conv2d_fwd"
+               if k.startswith("gemm_fp4") or (k.startswith("gemm_i8") and "<1, 1," in k and "[pixels]" not in k) or k == "conv2d_fwd"
                or k == "gemm_xnor_k"]
         if fwd:
             ops, ms_ = sum(v["ops"] for v in fwd), sum(v["ms"] for v in fwd)

@@ -28,7 +28,12 @@ SIGNATURES = {
     "bnn_quant_rows": (I32, [P, I64, I64, I64, P, I64, I64, P, P]),
     "bnn_quant_cols_workspace": (I64, [I64, I64]),
     "bnn_quant_cols_t": (I32, [P, I64, I64, I64, P, I64, I64, P, P, P, P]),
+    "bnn_quant_cols_t_dsum": (I32, [P, I64, I64, I64, P, I64, I64, P, P, P, P, P]),
     "bnn_gemm_i8": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_i8_affine": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, P, ctypes.c_double, P, I64,
+                                 I64, I64, I64, P]),
+    "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
+    "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_gemm_set_variant": (I32, [I32]),
     "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64, I64]),

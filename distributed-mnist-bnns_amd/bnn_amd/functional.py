@@ -94,15 +94,15 @@ def round_up(x, m=ALIGN):
     return (x + m - 1) // m * m
 
 
-def _check(*ts):
+def _check(*ts, dtype=torch.float32):
     for t in ts:
         if t is None:
             continue
         if not t.is_cuda:
             raise RuntimeError("bnn_amd: libbnn runs on ROCm (cuda) tensors only; "
                                f"got a {t.device} tensor (there is no CPU fallback)")
-        if t.dtype != torch.float32:
-            raise TypeError(f"bnn_amd: expected float32, got {t.dtype}")
+        if t.dtype != dtype:
+            raise TypeError(f"bnn_amd: expected {dtype}, got {t.dtype}")
 
 
 def _c2d(x):
@@ -187,8 +187,9 @@ def quant_rows(x):
     return dg, sc
 
 
-def quant_cols_t(x, want_colsum=False):
-    """fp32 [M,N] -> (digits_t int8 [3, N, ldqt], scale [N], colsum [N] or None)."""
+def quant_cols_t(x, want_colsum=False, want_dsum=False):
+    """fp32 [M,N] -> (digits_t int8 [3, N, ldqt], scale [N], colsum [N] or None), plus the exact
+    int64 digit column sums [N] when ``want_dsum`` (bnn_quant_cols_t_dsum)."""
     _check(x)
     x = _c2d(x)
     M, N = x.shape
@@ -196,11 +197,12 @@ def quant_cols_t(x, want_colsum=False):
     dg = torch.empty((3, N, ldqt), dtype=torch.int8, device=x.device)
     sc = torch.empty((N,), dtype=torch.float32, device=x.device)
     cs = torch.empty((N,), dtype=torch.float32, device=x.device) if want_colsum else None
+    ds = torch.empty((N,), dtype=torch.int64, device=x.device) if want_dsum else None
     ws = torch.empty((L.lib().bnn_quant_cols_workspace(M, N),), dtype=torch.uint8, device=x.device)
     with _timed("quant_cols_t", 0, 4 * M * N + dg.numel() + 8 * N):
-        L.call("bnn_quant_cols_t", L.ptr(x), M, N, N, L.ptr(dg), ldqt, N * ldqt, L.ptr(sc), L.ptr(cs),
-               L.ptr(ws), L.stream())
-    return dg, sc, cs
+        L.call("bnn_quant_cols_t_dsum", L.ptr(x), M, N, N, L.ptr(dg), ldqt, N * ldqt, L.ptr(sc), L.ptr(cs),
+               L.ptr(ds), L.ptr(ws), L.stream())
+    return (dg, sc, cs, ds) if want_dsum else (dg, sc, cs)
 
 
 # ----------------------------------------------------------------------------- packed latent weights
@@ -290,6 +292,31 @@ def gemm_i8(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=Non
     with _timed(name, ops, a_digits * M * K + b_digits * N * K + 4 * M * N):
         L.call("bnn_gemm_i8", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
                L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
+    return C
+
+
+def gemm_i8_affine(A, a_digits, B, b_digits, M, N, a_scale=None, b_scale=None, bias=None, row_off=None,
+                   col_off=None, off_mul=0.0, k_true=None, label=None):
+    """gemm_i8 with exact integer offsets: C = (sums + off_mul*(row_off[m] + col_off[n])) * a_scale[m]
+    * b_scale[n] + bias[n] (bnn_gemm_i8_affine; row_off / col_off int64)."""
+    K = A.shape[-1]
+    assert B.shape[-1] == K and K % ALIGN == 0
+    for o in (row_off, col_off):
+        assert o is None or o.dtype == torch.int64
+    lda, ldb = A.shape[-1], B.shape[-1]
+    a_plane = A.shape[-2] * lda if a_digits > 1 else 0
+    b_plane = B.shape[-2] * ldb if b_digits > 1 else 0
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if M == 0 or N == 0:
+        return C
+    k_true = K if k_true is None else k_true
+    name = gemm_kernel_name(a_digits, b_digits, M, N, K) if _TIMER is not None else ""
+    if label and name:
+        name = f"{name} [{label}]"
+    with _timed(name, 2.0 * M * N * k_true, a_digits * M * K + b_digits * N * K + 4 * M * N):
+        L.call("bnn_gemm_i8_affine", L.ptr(A), lda, a_plane, a_digits, L.ptr(B), ldb, b_plane, b_digits,
+               L.ptr(a_scale), L.ptr(b_scale), L.ptr(bias), L.ptr(row_off), L.ptr(col_off), float(off_mul),
+               L.ptr(C), C.stride(0), M, N, K, L.stream())
     return C
 
 
@@ -480,6 +507,118 @@ def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4", cach
     weight is a latent weight whose packed operands are cached on it (packed_weight)."""
     lead = x.shape[:-1]
     y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend, cache)
+    return y.reshape(*lead, weight.shape[0])
+
+
+# ----------------------------------------------------------------------------- u8 pixels (fc1)
+# The reference's loader hands fc1 x = ToTensor(u8) = u/255, optionally Normalize((m,), (s,))
+# (mnist-dist2.py:96-99, mnist-distributed-BNNS2.py:82).  Kept as bytes in HBM and fed to fc1 as
+# v = u - 128 (int8): x = a*v + c exactly, so fc1 and its weight gradient are one-pass int8 MFMA
+# sums with the offset folded back in as an integer (bnn_pixels.hip, DESIGN.md §3).
+def pixel_affine(normalize=None):
+    """(a, s0) with x = a * (v + s0), v = u - 128: ToTensor (s0 = 128) or ToTensor + Normalize."""
+    m, sd = normalize if normalize is not None else (0.0, 1.0)
+    return 1.0 / (255.0 * sd), 128.0 - 255.0 * m
+
+
+def pixels_to_float(u, normalize=None):
+    """The fp32 tensor the reference's transform produces from the same bytes (reference
+    semantics; for the CPU/oracle paths and comparisons)."""
+    x = u.float() / 255.0
+    if normalize is not None:
+        x = (x - normalize[0]) / normalize[1]
+    return x
+
+
+def pixels_pack(u, want_q=True, want_qt=False):
+    """u8 [M, K] -> (int8 rows v [M, round_up(K)], int8 v^T [K, round_up(M)]) (either None)."""
+    _check(u, dtype=torch.uint8)
+    u = u if u.is_contiguous() else u.contiguous()
+    M, K = u.shape
+    q = torch.empty((M, round_up(K)), dtype=torch.int8, device=u.device) if want_q else None
+    qt = torch.empty((K, round_up(M)), dtype=torch.int8, device=u.device) if want_qt else None
+    if (q is None and qt is None) or M == 0:
+        return q, qt
+    with _timed("pixels_pack_k", 0, M * K + (q.numel() if q is not None else 0) + (qt.numel() if qt is not None else 0)):
+        L.call("bnn_pixels_pack", L.ptr(u), M, K, K, L.ptr(q), q.shape[1] if q is not None else 0,
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, L.stream())
+    return q, qt
+
+
+def row_sums(q, K):
+    """Exact int64 row sums of an int8 matrix's first K columns (bnn_row_sums)."""
+    N = q.shape[0]
+    out = torch.empty((N,), dtype=torch.int64, device=q.device)
+    L.call("bnn_row_sums", L.ptr(q), N, K, q.shape[1], L.ptr(out), L.stream())
+    return out
+
+
+_CONST = {}
+
+
+def _const_vec(val, n, device):
+    key = (float(val), int(n), str(device))
+    t = _CONST.get(key)
+    if t is None:
+        t = torch.full((n,), float(val), dtype=torch.float32, device=device)
+        _CONST[key] = t
+    return t
+
+
+class BinaryLinearPixelsFunction(torch.autograd.Function):
+    """fc1 on u8 pixels: y = F.linear(x, sign(w)) + b with x = a*(u - 128 + s0), the reference's
+    first BinarizeLinear (models/binarized_modules.py:68-85 with size(1) == 784: input not
+    binarised) fed by ToTensor[/Normalize].  No gradient flows to the pixels."""
+
+    @staticmethod
+    def forward(ctx, u, weight, bias, a, s0, cache=False):
+        _check(u, dtype=torch.uint8)
+        _check(weight, bias)
+        M, K = u.shape
+        N = weight.shape[0]
+        ctx.dims = (M, K, N)
+        ctx.has_bias = bias is not None
+        ctx.a, ctx.s0 = a, s0
+        need_dw = ctx.needs_input_grad[1]
+        q, qt = pixels_pack(u, want_q=M > 0, want_qt=need_dw and M > 0)
+        if M == 0:
+            ctx.save_for_backward(None)
+            return torch.empty((0, N), dtype=torch.float32, device=u.device)
+        wq, _ = packed_weight(weight, "i8", True, False, cache)
+        R = row_sums(wq, K)
+        y = gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=_const_vec(a, N, u.device),
+                           bias=bias.detach() if bias is not None else None, col_off=R, off_mul=s0, k_true=K,
+                           label="pixels")
+        ctx.save_for_backward(qt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        M, K, N = ctx.dims
+        (qt,) = ctx.saved_tensors
+        dev = dy.device
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        dw = db = None
+        if M == 0:
+            return (None, torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
+                    torch.zeros((N,), dtype=torch.float32, device=dev) if need_db else None, None, None, None)
+        dy = _c2d(dy)
+        if ctx.needs_input_grad[1] or need_db:
+            dt, sc, cs, ds = quant_cols_t(dy, want_colsum=need_db, want_dsum=True)   # dY^T digits, T[n]
+            if ctx.needs_input_grad[1]:
+                dw = gemm_i8_affine(dt, 3, qt, 1, N, K, a_scale=sc, b_scale=_const_vec(ctx.a, K, dev),
+                                    row_off=ds, off_mul=ctx.s0, k_true=M, label="pixels")
+            db = cs
+        return None, dw, db, None, None, None
+
+
+def binary_linear_pixels(u, weight, bias=None, normalize=None, cache=False):
+    """fc1 on u8 pixels [.., K] (leading dims flattened); ``normalize`` = (mean, std) or None."""
+    if u.dtype != torch.uint8:
+        raise TypeError("binary_linear_pixels: expects uint8 pixels")
+    a, s0 = pixel_affine(normalize)
+    lead = u.shape[:-1]
+    y = BinaryLinearPixelsFunction.apply(u.reshape(-1, u.shape[-1]), weight, bias, a, s0, cache)
     return y.reshape(*lead, weight.shape[0])
 
 

@@ -5,6 +5,8 @@
   fc4 = nn.Linear, LogSoftmax.
 * ``SmallNet`` -- mnist-dist3.py:40-70 (64r = 192 wide; the source of the published CSVs).
 * ``WideNet`` -- BASELINE config 5: 784-8192x3-10, same topology.
+* Inputs: fp32 images (what the reference's transform yields) or the uint8 pixels themselves
+  (``data.synthetic_mnist(..., as_u8=True)``, ``data.U8Dataset``): fc1 then works on the bytes.
 * ``BinCNN`` -- BASELINE config 4 (build-defined; the reference never instantiates
   BinarizeConv2d): the ConvNet template of mnist-dist.py:31-51 with binarised convolutions and
   Hardtanh in place of ReLU: conv5x5(1->16,p2)-BN-Hardtanh-MaxPool2, conv5x5(16->32,p2)-BN-
@@ -30,7 +32,7 @@ class MLP(nn.Module):
     """mnist-dist2.py:46-76 with explicit widths."""
 
     def __init__(self, h1, h2, h3, p_drop=0.3, org_protocol=True, mutate_input=True, backend=None,
-                 fused_bn=False):
+                 fused_bn=False, normalize=None):
         super().__init__()
         # fused_bn: bn_i -> htanh_i run as one libbnn BatchNorm+Hardtanh pass (same parameters,
         # buffers and math; replaces torch's BatchNorm1d kernels, DESIGN.md)
@@ -47,6 +49,8 @@ class MLP(nn.Module):
         self.fc4 = nn.Linear(h3, 10)
         self.logsoftmax = nn.LogSoftmax(dim=1)
         self.drop = nn.Dropout(p_drop)
+        # uint8 pixel batches: fc1 applies ToTensor (+ Normalize(*normalize)) on the bytes
+        self.fc1.pixel_normalize = normalize
         _configure(self, org_protocol, mutate_input, backend)
 
     def _bnh(self, bn, ht, x):

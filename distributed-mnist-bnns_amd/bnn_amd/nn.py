@@ -20,6 +20,11 @@ Two class attributes switch behaviour for the build's own trainer:
   ``org_protocol = False`` keeps the latent weight in the Parameter itself (no ``.org``,
   binarised on the fly inside the kernel; pair it with ``bnn_amd.optim.LatentAdam``), and
   ``mutate_input = False`` skips materialising ``sign(input)`` in fp32 (nothing reads it).
+
+A ``uint8`` input to a 784-input ``BinarizeLinear`` is taken as the raw pixels the reference's
+loader would turn into ``ToTensor()`` (``u/255``), followed by ``Normalize(*pixel_normalize)``
+when that attribute is set: the layer then runs on the bytes (functional.binary_linear_pixels),
+with the same output as on the fp32 tensor the transform would have produced.
 """
 import torch
 import torch.nn as nn
@@ -91,8 +96,19 @@ class BinarizeLinear(nn.Linear):
     def __init__(self, *kargs, **kwargs):
         super().__init__(*kargs, **kwargs)
 
+    pixel_normalize = None   # (mean, std) of a Normalize after ToTensor, for uint8 inputs
+
     def forward(self, input):
         binarize = input.size(1) != 784                       # :75
+        if input.dtype == torch.uint8:
+            if binarize:
+                raise TypeError("BinarizeLinear: uint8 (pixel) input is only defined for the 784-input layer")
+            if self.org_protocol:
+                _apply_org_protocol(self.weight)
+                if self.bias is not None:
+                    self.bias.org = self.bias.data.clone()
+            return BF.binary_linear_pixels(input, self.weight, self.bias, self.pixel_normalize,
+                                           cache=not self.org_protocol)
         if binarize and self.mutate_input:
             input.data = BF.sign(input.data)                    # :76
         if self.org_protocol:

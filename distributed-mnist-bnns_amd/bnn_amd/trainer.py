@@ -26,7 +26,7 @@ import torch.multiprocessing as mp
 
 from . import nets
 from .checkpoint import load_checkpoint, save_checkpoint
-from .data import read_idx, shard_indices, synthetic_mnist
+from .data import load_idx_dataset, shard_indices, synthetic_mnist
 from .optim import LatentAdam
 from .parallel import GradExchange
 
@@ -59,6 +59,8 @@ def parse(argv=None):
     ap.add_argument("--dataset-size", type=int, default=60000, help="synthetic training set size")
     ap.add_argument("--idx-images", default=None)
     ap.add_argument("--idx-labels", default=None)
+    ap.add_argument("--fp32-input", action="store_true", help="keep the dataset as fp32 images (u/255) "
+                    "instead of u8 pixels")
     ap.add_argument("--max-steps", type=int, default=0, help="stop each epoch after this many steps")
     ap.add_argument("--no-lr-quirk", action="store_true", help="drop the per-batch lr*=0.1 at epoch%%40==0")
     ap.add_argument("--csv-prefix", default=None, help="write <prefix>_BATCH_TIME.csv / _EPOCH_TIME.csv")
@@ -70,13 +72,14 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def load_dataset(args, device, rank):
+def load_dataset(args, device, rank, as_u8=True):
+    """Resident training set: u8 pixels (fc1 applies ToTensor on the bytes) unless the model
+    needs the fp32 images (the CNN) or --fp32-input asks for them."""
     if args.idx_images:
-        imgs = torch.from_numpy(read_idx(args.idx_images).copy()).float().div_(255.0).unsqueeze(1)
-        labels = torch.from_numpy(read_idx(args.idx_labels).astype("int64"))
-        return imgs.to(device), labels.to(device)
+        imgs, labels = load_idx_dataset(args.idx_images, args.idx_labels, device)
+        return (imgs if as_u8 else imgs.float().div_(255.0)), labels
     # identical synthetic set on every rank (seed 1234); the sampler shards it
-    return synthetic_mnist(args.dataset_size, seed=1234, device=device)
+    return synthetic_mnist(args.dataset_size, seed=1234, device=device, as_u8=as_u8)
 
 
 def train(gpu, args):
@@ -101,7 +104,7 @@ def train(gpu, args):
     first_epoch = 1
     if args.resume:
         first_epoch = load_checkpoint(args.resume, model, opt, map_location=device) + 1
-    data, targets = load_dataset(args, device, rank)
+    data, targets = load_dataset(args, device, rank, as_u8=args.model != "cnn" and not args.fp32_input)
     idx = torch.tensor(shard_indices(len(data), world, rank), device=device)
     nb = (len(idx) + args.batch_size - 1) // args.batch_size
     T, E = [], []

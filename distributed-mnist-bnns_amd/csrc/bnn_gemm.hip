@@ -35,7 +35,19 @@ struct GemmParams {
   int64_t ldc;
   int M, N, K;
   int gm, gn;
+  // optional integer offsets added to the raw sum before scaling (u8 pixel operands,
+  // bnn_pixels.hip): sum + off_mul * (row_off[m] + col_off[n]), in double
+  const int64_t* row_off;
+  const int64_t* col_off;
+  double off_mul;
 };
+
+__device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
+  double o = 0.0;
+  if (p.row_off) o += (double)p.row_off[row];
+  if (p.col_off) o += (double)p.col_off[col];
+  return o * p.off_mul;
+}
 
 __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -213,6 +225,7 @@ __global__ __launch_bounds__(256) void gemm_i8_k(GemmParams p) {
         } else {
           v = (double)facc[t][u][i] * 65536.0;
         }
+        if (p.row_off || p.col_off) v += int_offset(p, row, col);
         if (p.a_scale) v *= (double)p.a_scale[row];
         v *= (double)bs;
         float f = (float)v;
@@ -585,7 +598,10 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
             float f;
             if constexpr (DA == 1 && DB == 1) {
               f = (float)acc[0][ti][ui][i];  // exact: |sum| <= K < 2^24
-              if (p.a_scale || p.b_scale)
+              if (p.row_off || p.col_off)
+                f = (float)(((double)acc[0][ti][ui][i] + int_offset(p, row, min(col, p.N - 1))) *
+                            (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
+              else if (p.a_scale || p.b_scale)
                 f = (float)((double)f * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
             } else {
               double v;
@@ -595,6 +611,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
               } else {
                 v = (double)facc[ti][ui][i] * 65536.0;
               }
+              if (p.row_off || p.col_off) v += int_offset(p, row, min(col, p.N - 1));
               f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
             }
             if (p.bias) f += bb;
@@ -761,10 +778,11 @@ const Variant* pick_kernel(int a_digits, int b_digits, int64_t M, int64_t N, int
 
 using namespace bnn;
 
-BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
-                        const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
-                        const float* a_scale, const float* b_scale, const float* bias, float* C,
-                        int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+BNN_API int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
+                               const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
+                               const float* a_scale, const float* b_scale, const float* bias,
+                               const int64_t* row_off, const int64_t* col_off, double off_mul, float* C,
+                               int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
   const bool cfg_ok = (a_digits == 1 && b_digits == 1) || (a_digits == 3 && b_digits == 1) ||
                       (a_digits == 3 && b_digits == 3);
   if (!A || !B || !C || !cfg_ok || M < 0 || N < 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K ||
@@ -772,7 +790,7 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
       M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff ||
       (a_digits > 1 && (a_plane < M * lda || a_plane % 16 != 0)) ||
       (b_digits > 1 && (b_plane < N * ldb || b_plane % 16 != 0))) {
-    set_error("bnn_gemm_i8: bad arguments (M=%lld N=%lld K=%lld lda=%lld ldb=%lld digits=%d,%d; "
+    set_error("bnn_gemm_i8_affine: bad arguments (M=%lld N=%lld K=%lld lda=%lld ldb=%lld digits=%d,%d; "
               "K must be a positive multiple of 64)",
               (long long)M, (long long)N, (long long)K, (long long)lda, (long long)ldb, a_digits,
               b_digits);
@@ -780,11 +798,19 @@ BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a
   }
   if (M == 0 || N == 0) return 0;
   GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
-               (int)M, (int)N, (int)K, 0, 0};
+               (int)M, (int)N, (int)K, 0, 0, row_off, col_off, off_mul};
   // v2 kernels address a tile's rows with 32-bit per-lane offsets (< 256 rows x ld)
   if (lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31))
     return find_variant(a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20))->fn(p, reinterpret_cast<hipStream_t>(stream));
   return pick_kernel(a_digits, b_digits, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
+                        const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
+                        const float* a_scale, const float* b_scale, const float* bias, float* C,
+                        int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+  return bnn_gemm_i8_affine(A, lda, a_plane, a_digits, B, ldb, b_plane, b_digits, a_scale, b_scale, bias,
+                            nullptr, nullptr, 0.0, C, ldc, M, N, K, stream);
 }
 
 BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
@@ -799,7 +825,7 @@ BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_
   }
   if (M == 0 || N == 0) return 0;
   GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
-               nullptr, nullptr, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0};
+               nullptr, nullptr, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, nullptr, nullptr, 0.0};
   return pick_kernel(0, 0, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void colstats4_k(const float* __restrict__ x, 
 __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax,
                                                   const double* __restrict__ psum, int64_t N,
                                                   int64_t R, float* __restrict__ scale,
-                                                  float* __restrict__ colsum) {
+                                                  float* __restrict__ colsum, int64_t* __restrict__ dsum) {
   __shared__ float smx[4][64];
   __shared__ double ssm[4][64];
   const int lc = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -380,13 +380,14 @@ __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax
   digit_scale(amax, &shift, &s);
   scale[n] = s;
   if (colsum != nullptr) colsum[n] = (float)sum;
+  if (dsum != nullptr) dsum[n] = 0;   // quant_cols_t_k accumulates the digit sums into it
 }
 
 __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ x, int64_t M,
                                                       int64_t N, int64_t ldx,
                                                       const float* __restrict__ scale,
                                                       int8_t* __restrict__ dt, int64_t ldqt,
-                                                      int64_t plane, int vec) {
+                                                      int64_t plane, int vec, int64_t* __restrict__ dsum) {
   __shared__ int tile[TILE][TILE + 1];
   __shared__ int sh[TILE];
   const int64_t n0 = (int64_t)blockIdx.x * TILE, m0 = (int64_t)blockIdx.y * TILE;
@@ -432,6 +433,22 @@ __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ 
       w.w = pack4(g[12] >> sh8, g[13] >> sh8, g[14] >> sh8, g[15] >> sh8);
       *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc) = w;
     }
+  }
+  if (dsum != nullptr) {
+    // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22
+    // each, so 64 of them fit an int); the 4 lanes sharing n are adjacent
+    int part = 0;
+    if (n < N && m0 + mc < ldqt) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int g = tile[mc + j][nn];
+        part += (int)(int8_t)(g & 255) + 256 * (int)(int8_t)((g >> 8) & 255) + 65536 * (int)(int8_t)((g >> 16) & 255);
+      }
+    }
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    if ((t & 3) == 0 && n < N && part != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n), (unsigned long long)(long long)part);
   }
 }
 
@@ -603,9 +620,9 @@ BNN_API int64_t bnn_quant_cols_workspace(int64_t M, int64_t N) {
   return round_up(R * N * (int64_t)sizeof(float), 256) + R * N * (int64_t)sizeof(double);
 }
 
-BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
-                             int64_t ldqt, int64_t plane, float* scale, float* colsum, void* work,
-                             void* stream) {
+BNN_API int bnn_quant_cols_t_dsum(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
+                                  int64_t ldqt, int64_t plane, float* scale, float* colsum, int64_t* dsum,
+                                  void* work, void* stream) {
   if (!x || !digits_t || !scale || !work || M < 0 || N < 0 || ldx < N || ldqt % TILE != 0 ||
       ldqt < round_up(M, TILE) || plane < N * ldqt || (plane % 16) != 0 || !aligned16(digits_t)) {
     set_error("bnn_quant_cols_t: bad arguments (M=%lld N=%lld ldqt=%lld plane=%lld)", (long long)M,
@@ -633,11 +650,17 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
     (void)hipMemsetAsync(psum, 0, R * N * sizeof(double), S(stream));
   }
   hipLaunchKernelGGL(colfinal_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, S(stream), pmax, psum, N, R, scale,
-                     colsum);
+                     colsum, dsum);
   const int vec = aligned16(x) && (ldx % 4 == 0);
   hipLaunchKernelGGL(quant_cols_t_k, dim3((unsigned)((N + TILE - 1) / TILE), (unsigned)(ldqt / TILE)),
-                     dim3(256), 0, S(stream), x, M, N, ldx, scale, digits_t, ldqt, plane, vec);
+                     dim3(256), 0, S(stream), x, M, N, ldx, scale, digits_t, ldqt, plane, vec, dsum);
   return check_launch("bnn_quant_cols_t");
+}
+
+BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
+                             int64_t ldqt, int64_t plane, float* scale, float* colsum, void* work,
+                             void* stream) {
+  return bnn_quant_cols_t_dsum(x, M, N, ldx, digits_t, ldqt, plane, scale, colsum, nullptr, work, stream);
 }
 
 BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,

@@ -81,6 +81,11 @@ int64_t bnn_quant_cols_workspace(int64_t M, int64_t N);
 int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
                      int64_t ldqt, int64_t plane, float* scale, float* colsum, void* work,
                      bnn_stream_t stream);
+/* bnn_quant_cols_t that also writes dsum[n] = sum_m (d2*2^16 + d1*2^8 + d0)[n][m], the exact
+ * integer column sum of the digits (the T[n] of bnn_gemm_i8_affine's row_off); dsum nullable. */
+int bnn_quant_cols_t_dsum(const float* x, int64_t M, int64_t N, int64_t ldx, int8_t* digits_t,
+                          int64_t ldqt, int64_t plane, float* scale, float* colsum, int64_t* dsum,
+                          void* work, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (2) forward GEMM, int8 MFMA
  * C[m][n] = cvt( sum_{i,j} 2^(8(i+j)) * sum_k A_i[m][k]*B_j[n][k] ) * a_scale[m] * b_scale[n]
@@ -96,6 +101,32 @@ int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
                 const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
                 const float* a_scale, const float* b_scale, const float* bias, float* C,
                 int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
+
+/* bnn_gemm_i8 with integer offsets folded into the raw sum before any rounding:
+ * C[m][n] = (combine(sums) + off_mul * (row_off[m] + col_off[n])) * a_scale[m] * b_scale[n]
+ *           + bias[n]        (the bracket and products in double, one rounding to fp32)
+ * row_off / col_off nullable int64 (NULL both: this IS bnn_gemm_i8).  For u8 pixels
+ * (bnn_pixels_pack, v = u - 128, off_mul = 128 for ToTensor): fc1 with col_off = R (bnn_row_sums
+ * of the weight), dW1 with row_off = T (bnn_quant_cols_t_dsum of dY), so both are exact integer
+ * sums over u before scaling. */
+int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
+                       const int8_t* B, int64_t ldb, int64_t b_plane, int32_t b_digits,
+                       const float* a_scale, const float* b_scale, const float* bias,
+                       const int64_t* row_off, const int64_t* col_off, double off_mul, float* C,
+                       int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
+
+/* ---------------------------------------------------------------- u8 pixels (first layer)
+ * Replaces the fp32 pixel tensor the reference's loader builds (ToTensor = u8/255, optionally
+ * Normalize; mnist-dist2.py:96-99, mnist-distributed-BNNS2.py:82) as the operand of fc1
+ * (models/binarized_modules.py:80, input kept because size(1) == 784): x = a*v + c with
+ * v = u - 128 stored as int8, so fc1 and its weight gradient are exact int8 MFMA sums.
+ * bnn_pixels_pack: x [M][ldx] bytes -> q [M][ldq] int8 rows v (zero for k >= K; ldq >=
+ * round_up(K,64)) and/or qt [K][ldqt] = v^T (zero for m >= M; ldqt >= round_up(M,64)); either
+ * output may be NULL, ld's multiples of 16, outputs 16-B aligned. */
+int bnn_pixels_pack(const uint8_t* x, int64_t M, int64_t K, int64_t ldx, int8_t* q, int64_t ldq,
+                    int8_t* qt, int64_t ldqt, bnn_stream_t stream);
+/* out[n] = sum_{k<K} q[n][k] (exact int64): R[n] of the packed ternary weight rows. */
+int bnn_row_sums(const int8_t* q, int64_t N, int64_t K, int64_t ldq, int64_t* out, bnn_stream_t stream);
 
 /* Ternary x ternary GEMM on the FP4 (e2m1) block-scaled MFMA (unit scales): operands hold FP4
  * codes (+1 = 0x2, -1 = 0xA, 0 = 0x0), two elements per byte (element k in byte k/2, low nibble

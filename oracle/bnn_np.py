@@ -30,6 +30,17 @@ F64 = np.float64
 
 
 # --------------------------------------------------------------------------- binarize
+def to_tensor(u, normalize=None):
+    """The reference loader's transform on u8 pixels (mnist-dist2.py:96-99
+    ``transforms.ToTensor()`` = ``u.float().div(255)`` in fp32; mnist-distributed-BNNS2.py:82 adds
+    ``Normalize((m,), (s,))`` = ``(x - m) / s`` in fp32)."""
+    x = (np.asarray(u).astype(F32) / F32(255.0)).astype(F32)
+    if normalize is not None:
+        m, sd = normalize
+        x = ((x - F32(m)) / F32(sd)).astype(F32)
+    return x
+
+
 def binarize(x):
     """``Binarize(tensor, 'det')`` -- models/binarized_modules.py:11-13.  sign(0) = 0."""
     return np.sign(x).astype(x.dtype, copy=False)

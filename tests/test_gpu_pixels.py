@@ -1,0 +1,177 @@
+"""GPU parity of fc1 on u8 pixels (bnn_pixels.hip + bnn_gemm_i8_affine): the reference's first
+BinarizeLinear (models/binarized_modules.py:68-85, input kept since size(1) == 784) fed by
+ToTensor (mnist-dist2.py:96-99) or ToTensor + Normalize (mnist-distributed-BNNS2.py:82).
+
+Bars:
+* pixels_pack, row sums, digit column sums, the offset GEMM: exact (integers);
+* forward against float64 of the reference's fp32 pixels: norm-wise <= 1e-6 (its only roundings
+  are the scale by a and the fp32 bias add, both after the exact integer sum);
+* dW, db against float64: <= 1e-5 (the dY digits); a pixel column that is zero across the batch
+  gets an exactly zero weight gradient, as the reference's fp32 GEMM gives (ToTensor).
+Real pixels: the MNIST test images the reference ships (tests/golden, a fixture).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_err
+from oracle import bnn_np as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def F():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import functional
+    return functional
+
+
+@pytest.fixture(scope="module")
+def t10k():
+    from bnn_amd.data import read_idx
+    return read_idx(os.path.join(GOLDEN, "t10k-images-idx3-ubyte.gz")).reshape(10000, 784)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def _pixels(rng, M, K):
+    u = rng.integers(1, 256, (M, K)).astype(np.uint8)
+    u[rng.random((M, K)) < 0.807] = 0
+    return u
+
+
+@pytest.mark.parametrize("M,K", [(5, 784), (300, 784), (64, 784), (1000, 100), (7, 33), (0, 784)])
+@pytest.mark.parametrize("which", ["both", "q", "qt"])
+def test_pixels_pack_exact(F, M, K, which):
+    rng = np.random.default_rng(M * 7 + K)
+    u = _pixels(rng, M, K)
+    q, qt = F.pixels_pack(torch.as_tensor(u).cuda(), want_q=which != "qt", want_qt=which != "q")
+    v = u.astype(np.int16) - 128
+    if which != "qt":
+        qh = host(q)
+        assert qh.shape == (M, F.round_up(K)) and np.array_equal(qh[:, :K], v) and not qh[:, K:].any()
+    if which != "q":
+        th = host(qt)
+        assert th.shape == (K, F.round_up(M)) and np.array_equal(th[:, :M], v.T) and not th[:, M:].any()
+
+
+def test_row_sums_exact(F):
+    rng = np.random.default_rng(3)
+    q = rng.integers(-1, 2, (1000, 832)).astype(np.int8)
+    q[:, 784:] = 0
+    out = host(F.row_sums(torch.as_tensor(q).cuda(), 784))
+    assert out.dtype == np.int64 and np.array_equal(out, q[:, :784].sum(1, dtype=np.int64))
+
+
+@pytest.mark.parametrize("M,N", [(300, 200), (1000, 37), (64, 8192), (4096, 64)])
+def test_quant_cols_t_digit_sums_exact(F, M, N):
+    rng = np.random.default_rng(M + N)
+    x = (rng.standard_normal((M, N)) * np.exp(rng.uniform(-8, 8, (1, N)))).astype(np.float32)
+    x[:, 3] = 0.0
+    dg, sc, cs, ds = F.quant_cols_t(torch.as_tensor(x).cuda(), want_colsum=True, want_dsum=True)
+    d = host(dg).astype(np.int64)
+    comb = d[2] * 65536 + d[1] * 256 + d[0]
+    assert np.array_equal(host(ds), comb.sum(1))
+    assert host(ds)[3] == 0
+
+
+def test_gemm_i8_affine_offsets_exact(F):
+    """(1,1) with col_off and (3,1) with row_off against the int64 formula, scales of 1."""
+    rng = np.random.default_rng(11)
+    M, N, K = 300, 200, 832
+    A = rng.integers(-128, 128, (M, K)).astype(np.int8)
+    B = rng.integers(-1, 2, (N, K)).astype(np.int8)
+    co = rng.integers(-784, 785, N).astype(np.int64)
+    ro = rng.integers(-2 ** 30, 2 ** 30, M).astype(np.int64)
+    dv = lambda a: torch.as_tensor(a).cuda()   # noqa: E731
+    C = host(F.gemm_i8_affine(dv(A), 1, dv(B), 1, M, N, col_off=dv(co), off_mul=128.0))
+    exact = A.astype(np.int64) @ B.astype(np.int64).T + 128 * co[None, :]
+    assert np.array_equal(C, exact.astype(np.float32))
+    A3 = rng.integers(-128, 128, (3, M, K)).astype(np.int8)
+    C3 = host(F.gemm_i8_affine(dv(A3), 3, dv(B), 1, M, N, row_off=dv(ro), off_mul=128.0))
+    comb = (A3[2].astype(np.int64) * 65536 + A3[1].astype(np.int64) * 256 + A3[0]) @ B.astype(np.int64).T
+    exact3 = comb + 128 * ro[:, None]
+    assert np.array_equal(C3, exact3.astype(np.float64).astype(np.float32))
+
+
+def _layer(F, u, w, b, normalize, want_grad=True):
+    ut = torch.as_tensor(u).cuda()
+    wt = torch.as_tensor(w).cuda().requires_grad_(want_grad)
+    bt = torch.as_tensor(b).cuda().requires_grad_(want_grad)
+    y = F.binary_linear_pixels(ut, wt, bt, normalize)
+    return y, wt, bt
+
+
+@pytest.mark.parametrize("normalize", [None, (0.1307, 0.3081)])
+@pytest.mark.parametrize("M,N", [(512, 3072), (64, 192), (2048, 1000), (1, 10)])
+def test_fc1_pixels_forward_backward(F, t10k, normalize, M, N):
+    rng = np.random.default_rng(M + N)
+    u = t10k[rng.choice(10000, M, replace=False)]
+    w = rng.uniform(-1, 1, (N, 784)).astype(np.float32)
+    w[:, ::97] = 0.0                                               # ternary zeros
+    b = rng.standard_normal(N).astype(np.float32)
+    y, wt, bt = _layer(F, u, w, b, normalize)
+    x = O.to_tensor(u, normalize).astype(np.float64)                # the reference's fp32 pixels
+    wb = np.sign(w).astype(np.float64)
+    ref = x @ wb.T + b
+    assert rel_err(host(y), ref) <= 1e-6
+    dy = rng.standard_normal((M, N)).astype(np.float32) * np.exp(rng.uniform(-4, 4, (1, N))).astype(np.float32)
+    y.backward(torch.as_tensor(dy).cuda())
+    dw_ref = dy.astype(np.float64).T @ x
+    assert rel_err(host(wt.grad), dw_ref) <= 1e-5
+    assert rel_err(host(bt.grad), dy.astype(np.float64).sum(0)) <= 1e-6
+    if normalize is None:
+        dead = ~u.any(0)                                           # pixel columns dark in the whole batch
+        assert dead.any()
+        assert not host(wt.grad)[:, dead].any()                     # exactly zero, as fp32 GEMM gives
+
+
+def test_fc1_pixels_matches_fp32_path(F, t10k):
+    """The u8 path and the fp32-pixel path (int8 digit planes of u/255) agree to the bar."""
+    rng = np.random.default_rng(5)
+    u = t10k[:256]
+    w = rng.uniform(-1, 1, (512, 784)).astype(np.float32)
+    b = rng.standard_normal(512).astype(np.float32)
+    y8 = host(F.binary_linear_pixels(torch.as_tensor(u).cuda(), torch.as_tensor(w).cuda(), torch.as_tensor(b).cuda()))
+    yf = host(F.binary_linear(torch.as_tensor(O.to_tensor(u)).cuda(), torch.as_tensor(w).cuda(),
+                              torch.as_tensor(b).cuda(), binarize_input=False))
+    assert rel_err(y8, yf) <= 2e-6
+
+
+def test_fc1_pixels_empty_batch(F):
+    w = torch.randn(16, 784, device="cuda", requires_grad=True)
+    b = torch.randn(16, device="cuda", requires_grad=True)
+    y = F.binary_linear_pixels(torch.zeros((0, 784), dtype=torch.uint8, device="cuda"), w, b)
+    assert y.shape == (0, 16)
+    y.sum().backward()
+    assert not w.grad.any() and not b.grad.any()
+
+
+def test_net_on_pixels_drop_in(F, t10k):
+    """nets.MLP given the bytes equals the same MLP given ToTensor(bytes) at fc1, and a training
+    step of the fused trainer path runs on them (loss finite, dead-pixel weights unchanged)."""
+    from bnn_amd import nets
+    from bnn_amd.optim import LatentAdam
+    torch.manual_seed(0)
+    m = nets.MLP(256, 128, 64, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+    u = torch.as_tensor(t10k[:512].reshape(512, 1, 28, 28)).cuda()
+    y = torch.randint(0, 10, (512,), device="cuda")
+    h8 = m.fc1(u.view(-1, 784))
+    hf = m.fc1(torch.as_tensor(O.to_tensor(t10k[:512])).cuda())
+    assert rel_err(host(h8), host(hf)) <= 2e-6
+    w0 = host(m.fc1.weight).copy()
+    opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=nets.binary_params(m))
+    loss = torch.nn.CrossEntropyLoss()(m(u), y)
+    loss.backward()
+    opt.step()
+    assert np.isfinite(float(loss))
+    dead = ~t10k[:512].any(0)
+    w1 = host(m.fc1.weight)
+    assert np.array_equal(w1[:, dead], w0[:, dead]) and not np.array_equal(w1, w0)
