@@ -588,6 +588,8 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         const bool cin = col < p.N;
         const float bb = (p.bias && cin) ? p.bias[col] : 0.f;
         const double bs = (p.b_scale && cin) ? (double)p.b_scale[col] : 1.0;
+        const bool offs = p.row_off || p.col_off;
+        const double coff = (p.col_off && cin) ? (double)p.col_off[col] * p.off_mul : 0.0;
 #pragma unroll
         for (int sa = 0; sa < SUB; ++sa) {
           const int ti = t * SUB + sa, ui = u * SUB + sb;
@@ -598,10 +600,11 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
             float f;
             if constexpr (DA == 1 && DB == 1) {
               f = (float)acc[0][ti][ui][i];  // exact: |sum| <= K < 2^24
-              if (p.row_off || p.col_off)
-                f = (float)(((double)acc[0][ti][ui][i] + int_offset(p, row, min(col, p.N - 1))) *
-                            (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
-              else if (p.a_scale || p.b_scale)
+              if (offs) {
+                double v = (double)acc[0][ti][ui][i] + coff;
+                if (p.row_off) v += (double)p.row_off[row] * p.off_mul;
+                f = (float)(v * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
+              } else if (p.a_scale || p.b_scale)
                 f = (float)((double)f * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
             } else {
               double v;
@@ -611,7 +614,10 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
               } else {
                 v = (double)facc[ti][ui][i] * 65536.0;
               }
-              if (p.row_off || p.col_off) v += int_offset(p, row, min(col, p.N - 1));
+              if (offs) {
+                v += coff;
+                if (p.row_off) v += (double)p.row_off[row] * p.off_mul;
+              }
               f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
             }
             if (p.bias) f += bb;
