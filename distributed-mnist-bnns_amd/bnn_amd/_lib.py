@@ -56,6 +56,8 @@ SIGNATURES = {
     "bnn_bn2d_bwd_eval": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
+    "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
+                            P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),

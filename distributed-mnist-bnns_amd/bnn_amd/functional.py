@@ -463,6 +463,8 @@ class BinaryLinearFunction(torch.autograd.Function):
             y = gemm_i8(xd, 3, wq, 1, M, N, a_scale=sx, bias=b, k_true=K)
             ctx.save_for_backward(x if need_dw else None, wqt)
         ctx.binarize_input = binarize_input
+        if ctx.fp6:
+            setattr(y, _Q6_WANT, True)
         return y
 
     @staticmethod
@@ -479,13 +481,14 @@ class BinaryLinearFunction(torch.autograd.Function):
         dx = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.fp6:
+            pre = _q6_take(dy)                      # digits of dy from the BatchNorm backward
             if ctx.needs_input_grad[0]:
-                dx = gemm_fp6(quant6_rows(dy), wqt, K, k_true=N)               # dY . W_b
+                dx = gemm_fp6(pre[0] if pre is not None else quant6_rows(dy), wqt, K, k_true=N)   # dY . W_b
             if ctx.needs_input_grad[1] or need_db:
-                dt, cs = quant6_cols_t(dy, want_colsum=need_db)
+                dt, cs = (pre[1], pre[2]) if pre is not None else quant6_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[1]:
                     dw = gemm_fp6(dt, xs, K, k_true=M)                         # dY^T . X_b
-                db = cs
+                db = cs if need_db else None
             return dx, dw, db, None, None, None
         if ctx.needs_input_grad[0]:
             d, s = quant_rows(dy)                                   # [3, M, ldN]
@@ -741,6 +744,53 @@ def _bn_bwd_call(training, x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, dx, d
                int(hardtanh), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
 
 
+# FP6 digits of a gradient, handed from the BatchNorm backward that produces it to the
+# BinarizeLinear backward that consumes it (bnn_bn_bwd_q6: dz is quantised in the pass that
+# computes it, never re-read).  A forward output whose gradient an FP6-backward linear will
+# quantise carries _Q6_WANT; the BatchNorm function that takes it as input then emits the digits
+# on its gradient (_Q6_ATTR, keyed on the tensor's storage / version / shape, taken once).
+_Q6_ATTR = "_bnn_q6"
+_Q6_WANT = "_bnn_q6_consumer"
+
+
+def _q6_key(t):
+    return (t.data_ptr(), t._version, tuple(t.shape))
+
+
+Q6_HANDOFF = True        # False: every FP6 linear backward quantises its dy itself (cross-checks)
+
+
+def _q6_wanted(x, C, training=True):
+    return (Q6_HANDOFF and bool(getattr(x, _Q6_WANT, False)) and training and DIGIT_GEMM == "fp6"
+            and C % 64 == 0)
+
+
+def _q6_take(dy):
+    """(rows Fp6Operand, cols Fp6Operand, colsum) attached to ``dy`` by bnn_bn_bwd_q6, or None."""
+    ent = getattr(dy, _Q6_ATTR, None)
+    if ent is None:
+        return None
+    delattr(dy, _Q6_ATTR)
+    return ent[1:] if ent[0] == _q6_key(dy) else None
+
+
+def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name):
+    """BatchNorm(+Dropout) backward that also quantises dz (returned, with the digits attached)."""
+    dev = x.device
+    dx = torch.empty_like(x)
+    rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
+    Mp = round_up(M)
+    cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
+    cs = torch.empty((C,), dtype=torch.float32, device=dev)
+    with _timed(name, 0, 16 * M * C + 4 * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
+        L.call("bnn_bn_bwd_q6", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+               L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
+               L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws),
+               L.stream())
+    setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
+    return dx
+
+
 class BatchNormHardtanhFunction(torch.autograd.Function):
     """nn.BatchNorm1d on [M, C] (train or eval) optionally followed by nn.Hardtanh, fused
     (mnist-dist2.py:52-74).  Running stats are updated in place in training mode."""
@@ -748,6 +798,7 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh):
         _check(x, weight, bias, running_mean, running_var)
+        ctx.q6 = _q6_wanted(x, x.shape[-1], training)
         x = _c2d(x)
         M, C = x.shape
         y = torch.empty_like(x)
@@ -780,8 +831,11 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
         dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
         db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
         ws = _bn_ws(M, C, x.device)
-        with _timed("bn_bwd", 0, 16 * M * C):
-            _bn_bwd_call(ctx.training, x, dy, M, C, w, b, mean, invstd, mlo, ctx.hardtanh, dx, dw, db, ws)
+        if ctx.q6 and dx is not None:
+            dx = _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, ctx.hardtanh, 0.0, 0, dw, db, ws, "bn_bwd_q6")
+        else:
+            with _timed("bn_bwd", 0, 16 * M * C):
+                _bn_bwd_call(ctx.training, x, dy, M, C, w, b, mean, invstd, mlo, ctx.hardtanh, dx, dw, db, ws)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None)
 
@@ -794,6 +848,7 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, p, seed):
         _check(x, weight, bias, running_mean, running_var)
+        ctx.q6 = _q6_wanted(x, x.shape[-1])
         x = _c2d(x)
         M, C = x.shape
         y = torch.empty_like(x)
@@ -818,6 +873,11 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
         db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
         ws = _bn_ws(M, C, x.device)
+        if ctx.q6 and dx is not None:
+            dx = _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, True, ctx.p, ctx.seed, dw, db, ws,
+                            "bn_dropout_bwd_q6")
+            return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                    None, None, None, None, None, None)
         with _timed("bn_dropout_bwd", 0, 16 * M * C):
             L.call("bnn_bn_dropout_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                    L.ptr(mlo), 1, float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
@@ -946,6 +1006,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend):
         _check(z, bn_w, bn_b, rm, rv, weight, bias)
+        ctx.q6 = _q6_wanted(z, z.shape[-1], training)
         z = _c2d(z)
         M, C = z.shape
         N = weight.shape[0]
@@ -983,6 +1044,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         ctx.training = training
         ctx.dims = (M, C, N)
         ctx.has_bias = bias is not None
+        if ctx.fp6:
+            setattr(y, _Q6_WANT, True)
         return y
 
     @staticmethod
@@ -992,8 +1055,13 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         dy = _c2d(dy)
         dz = dgw = dgb = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[9]
+        pre = _q6_take(dy) if ctx.fp6 else None       # digits of dy from the BatchNorm backward
         if ctx.needs_input_grad[8] or need_db:
-            if ctx.fp6:
+            if pre is not None:
+                dt, cs = pre[1], (pre[2] if need_db else None)
+                if ctx.needs_input_grad[8]:
+                    dw = gemm_fp6(dt, qt, C, k_true=M)
+            elif ctx.fp6:
                 dt, cs = quant6_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[8]:
                     dw = gemm_fp6(dt, qt, C, k_true=M)                         # dY^T . sign(h)
@@ -1004,16 +1072,20 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             db = cs
         if any(ctx.needs_input_grad[:3]):
             if ctx.fp6:
-                dh = gemm_fp6(quant6_rows(dy), wqt, C, k_true=N)               # dY . W_b
+                dh = gemm_fp6(pre[0] if pre is not None else quant6_rows(dy), wqt, C, k_true=N)   # dY . W_b
             else:
                 d, s = quant_rows(dy)
                 dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)
-            dz = torch.empty_like(z)
+            del pre
             dgw = torch.empty((C,), dtype=torch.float32, device=z.device) if gw is not None else None
             dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None
             ws = _bn_ws(M, C, z.device)
-            with _timed("bn_bwd", 0, 16 * M * C):
-                _bn_bwd_call(ctx.training, z, dh, M, C, gw, gb, mean, invstd, mlo, True, dz, dgw, dgb, ws)
+            if ctx.q6:
+                dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6")
+            else:
+                dz = torch.empty_like(z)
+                with _timed("bn_bwd", 0, 16 * M * C):
+                    _bn_bwd_call(ctx.training, z, dh, M, C, gw, gb, mean, invstd, mlo, True, dz, dgw, dgb, ws)
         return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, dw, db, None)
 

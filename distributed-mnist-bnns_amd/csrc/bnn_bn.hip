@@ -19,6 +19,7 @@
 #include <cmath>
 
 #include "bnn_common.h"
+#include "bnn_fp6.h"
 
 namespace bnn {
 namespace {
@@ -330,6 +331,119 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
     drop4(dp, (uint64_t)(r * C + c), o);   // dropout backward: grad * mask * scale
     *reinterpret_cast<float4*>(dx + r * C + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
+}
+
+// ------------------------------------------------------------------ fused backward apply + FP6 quantise
+// The apply pass of the BatchNorm backward whose output dz is the upstream gradient dY of the
+// BinarizeLinear that produced z (mnist-dist2.py:66-71: fc -> bn -> htanh -> fc).  That layer's
+// backward multiplies dY twice on the FP6 MFMA (dX = dY.W_b, dW = dY^T.X_b, bnn_gemm6.hip), so
+// this pass writes, besides dz itself (optional), both FP6 digit forms of dz straight from
+// registers -- the rows (blocks of 32 columns) and the transpose (blocks of 32 rows, through an
+// LDS tile) -- and the per-256-row partial column sums of dz (the bias gradient): dz is never
+// re-read.  Bit-identical digits to bnn_quant6_rows / bnn_quant6_cols_t of the same dz.
+// Workgroup: 256 rows x 64 columns, walked as 4 sub-tiles of 64 rows; C % 64 == 0.  Per sub-tile
+// all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
+// the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
+constexpr int Q6T_ROWS = 256, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
+
+struct Q6Out {
+  float* dx;                       // [M][C] or null
+  uint8_t *rlo, *rhi, *rsc;        // rows of dz: [M][C/32][64], [M][C/32][32], [C/64][rsc_rows][2]
+  int64_t rsc_rows;
+  uint8_t *clo, *chi, *csc;        // dz^T: [C][Mp/32][64], [C][Mp/32][32], [Mp/64][csc_rows][2]
+  int64_t csc_rows, nblk_m;        // nblk_m = Mp / 32
+  double* part;                    // [M/256 chunks][C] partial column sums, or null
+};
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int64_t M, int64_t C, const float* __restrict__ mean,
+                                                         const float* __restrict__ mean_lo,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, int hardtanh,
+                                                         const float* __restrict__ sg,
+                                                         const float* __restrict__ sgx, float inv_n, Q6Out o,
+                                                         Drop dp) {
+  __shared__ __attribute__((aligned(16))) float tile[Q6T_SUB * Q6T_LD];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * Q6T_COLS;
+  const int64_t mbase = (int64_t)blockIdx.y * Q6T_ROWS;
+  const int64_t nblk_c = C / QB;
+  // elementwise mapping: float4 f = t + 256 i of a 64 x 64 sub-tile: row f / 16, columns 4 (f % 16)
+  const int cq = 4 * (t & 15);
+  const int64_t c = c0 + cq;
+  const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
+  const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f), lv = ld4_or(mean_lo, c, 0.f);
+  const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+  const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
+  const float a0[4] = {s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n};
+  const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
+  double csum = 0.0;                      // waves 2-3: column lane, rows of block wave-2 of each sub-tile
+  const int64_t mp = o.nblk_m * QB;
+  for (int sub = 0; sub < Q6T_ROWS / Q6T_SUB; ++sub) {
+    const int64_t m0 = mbase + sub * Q6T_SUB;
+    if (m0 >= mp) break;                       // block-uniform
+#pragma unroll
+    for (int i = 0; i < Q6T_SUB / 16; ++i) {
+      const int rr = (t >> 4) + 16 * i;
+      const int64_t r = m0 + rr;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < M) {
+        const float4 xv = ld4(x + r * C + c), gv = ld4(dy + r * C + c);
+        float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+        drop4(dp, (uint64_t)(r * C + c), xs);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = ((xs[j] - ms[j]) - lo[j]) * is[j];
+          const float yv = fmaf(xh, ga[j], be[j]);
+          const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
+          v[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
+        }
+        drop4(dp, (uint64_t)(r * C + c), v);
+        if (o.dx) *reinterpret_cast<float4*>(o.dx + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    if (wave < 2) {
+      // row block (row m0 + lane, columns c0 + 32 wave ..)
+      const int rr = lane, b = wave;
+      const int64_t r = m0 + rr;
+      const int64_t rs = r < M ? r : 0;
+      const int64_t blk = c0 / QB + b;
+      q6_block_store_lds<1>(tile + rr * Q6T_LD + QB * b, r < M, o.rlo + (rs * nblk_c + blk) * 64,
+                            o.rhi + (rs * nblk_c + blk) * 32, o.rsc + (blk >> 1) * o.rsc_rows * 2 + rs * 2 + (blk & 1));
+    } else {
+      // column block (column c0 + lane, rows m0 + 32 (wave - 2) ..): rows beyond M are zeros
+      const int b = wave - 2;
+      const float* col = tile + QB * b * Q6T_LD + lane;
+#pragma unroll
+      for (int k = 0; k < QB; ++k) csum += (double)col[k * Q6T_LD];
+      const int64_t n = c0 + lane;
+      const int64_t mblk = m0 / QB + b;
+      q6_block_store_lds<Q6T_LD>(col, true, o.clo + (n * o.nblk_m + mblk) * 64, o.chi + (n * o.nblk_m + mblk) * 32,
+                                 o.csc + (mblk >> 1) * o.csc_rows * 2 + n * 2 + (mblk & 1));
+    }
+    __syncthreads();
+  }
+  if (o.part != nullptr) {
+    // fixed-order fold of the two column waves' sums: deterministic
+    __shared__ double cs[Q6T_COLS];
+    if (wave == 3) cs[lane] = csum;
+    __syncthreads();
+    if (wave == 2) o.part[(int64_t)blockIdx.y * C + c0 + lane] = csum + cs[lane];
+  }
+}
+
+__global__ __launch_bounds__(256) void q6_colsum_final_k(const double* __restrict__ part, int64_t R, int64_t N,
+                                                         float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int64_t r = 0; r < R; ++r) s += part[r * N + n];
+  out[n] = (float)s;
 }
 
 inline int grid_for(int64_t n) {
@@ -742,6 +856,41 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
   }
   return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dx, dgamma, dbeta,
                      work, stream, make_drop(p, seed), true);
+}
+
+BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                          const float* beta, const float* save_mean, const float* save_invstd,
+                          const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
+  if (!bn_args_ok(x, M, C) || C % Q6T_COLS != 0 || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work ||
+      (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
+      !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !rlo || !rhi || !rsc || !clo || !chi || !csc ||
+      !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) || !(p >= 0.f && p < 1.f) ||
+      (M + Q6T_ROWS - 1) / Q6T_ROWS > 65535) {
+    set_error("bnn_bn_bwd_q6: bad arguments (M=%lld C=%lld; C must be a multiple of 64, 0 <= p < 1)", (long long)M,
+              (long long)C);
+    return kErrInval;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Drop dp = make_drop(p, seed);
+  const int64_t R = bn_chunks(M);
+  double* p0 = reinterpret_cast<double*>(work);
+  double* p1 = p0 + R * C;
+  float* k0 = reinterpret_cast<float*>(p1 + R * C);
+  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
+  hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
+                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
+  const int64_t mp = round_up(M, 64);
+  Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
+  hipLaunchKernelGGL(bn_bwd_apply_q6_k, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
+                     dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, k0,
+                     k1, 1.f / (float)M, o, dp);
+  if (colsum)
+    hipLaunchKernelGGL(q6_colsum_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, R, C, colsum);
+  return check_launch("bnn_bn_bwd_q6");
 }
 
 __global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d, float* __restrict__ out) {

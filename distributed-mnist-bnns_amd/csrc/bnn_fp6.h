@@ -1,0 +1,148 @@
+// FP6 (e2m3) digit-plane quantisation of fp32 operands, shared by the FP6 GEMM's quantisers
+// (bnn_gemm6.hip) and the fused BatchNorm-backward + quantise pass (bnn_bn.hip).  The scheme and
+// the operand layouts are described at the top of bnn_gemm6.hip.
+#pragma once
+#include "bnn_common.h"
+
+namespace bnn {
+
+constexpr int QB = 32;           // elements per scale block
+constexpr int SCALE_BIAS = 111;  // E8M0 byte of plane 0 = e + 111 (= e - 19 + 3 + 127)
+
+// e2m3 code of the integer digit d in [-16, 16] read as d/8.  For |d| <= 16 the code of |d|/8 IS
+// |d|: 0..7 are the subnormals m/8 (exponent field 0), 8..15 are 1.mmm (exponent 1, mantissa
+// |d| - 8), 16 is 2.0 (exponent 2, mantissa 0) = 0b010000; the sign is bit 5.
+__device__ __forceinline__ uint32_t e2m3_code(int d) {
+  return d < 0 ? (0x20u | (uint32_t)(-d)) : (uint32_t)d;
+}
+
+// Block exponent from the block's |max|: e with amax in [2^(e-1), 2^e); returns the plane-0 E8M0
+// byte (255 = NaN for a non-finite block: its outputs become NaN, as the fp32 GEMM's would).
+__device__ __forceinline__ int block_scale(float amax, int* shift) {
+  if (!(amax == amax) || amax == __builtin_inff()) {
+    *shift = 0;
+    return 255;
+  }
+  int e = -111;
+  if (amax > 0.f) {
+    frexpf(amax, &e);
+    e = e < -111 ? -111 : e;     // blocks below 2^-112 quantise to ~0 (error < 2^-130)
+  }
+  *shift = 19 - e;
+  return e + SCALE_BIAS;
+}
+
+// 4 balanced base-32 digits of rint(x * 2^shift)
+__device__ __forceinline__ void digits4(float x, int shift, int (&d)[4]) {
+  int v = __float2int_rn(ldexpf(x, shift));
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int dj = ((v + 16) & 31) - 16;
+    d[j] = dj;
+    v = (v - dj) >> 5;
+  }
+  d[3] = v;
+}
+
+__device__ __forceinline__ float absmax_nan(float amax, float x) {
+  const float a = fabsf(x);
+  return (a == a) ? fmaxf(amax, a) : __builtin_inff();
+}
+
+// One 32-element block held by 8 consecutive lanes (q = lane & 7 holds elements 4q..4q+3):
+// quantise it and store its record -- lanes q < 4 write plane q (16 B at lo_blk + 16q, 8 B at
+// hi_blk + 8q), lane 4 the plane-0 scale byte.  Every lane of the wave must call it (shuffles);
+// store = false suppresses this group's writes.
+__device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bool store, uint8_t* lo_blk,
+                                               uint8_t* hi_blk, uint8_t* sc_byte) {
+  const int q = lane & 7;
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) amax = absmax_nan(amax, v[j]);
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  int shift;
+  const int sbyte = block_scale(amax, &shift);
+  // this lane's 4 elements -> a 24-bit chunk per plane (element 4q+i at bits 6i of the chunk)
+  uint32_t chunk[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int d[4];
+    digits4(v[i], shift, d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) chunk[j] |= e2m3_code(d[j]) << (6 * i);
+  }
+  // lane j of the group assembles plane j: chunk of lane p sits at bits 24p..24p+23
+  const int plane = q & 3;
+  uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t cj = __shfl(chunk[j], (lane & ~7) | p, 64);
+      c = (plane == j) ? cj : c;
+    }
+    const int bit = 24 * p;
+    w[bit >> 5] |= c << (bit & 31);
+    if ((bit & 31) > 8) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+  }
+  if (!store) return;
+  if (q < 4) {
+    *reinterpret_cast<uint4*>(lo_blk + plane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint2*>(hi_blk + plane * 8) = make_uint2(w[4], w[5]);
+  } else if (q == 4) {
+    *sc_byte = (uint8_t)sbyte;
+  }
+}
+
+// One whole 32-element block quantised by ONE lane, element i read from LDS at src[i * STRIDE]
+// (read twice: once for the block max, then in two halves for the digits, to keep the register
+// footprint small): its four plane records -- plane j's 6 dwords, element i at bits 6i -- written
+// as lo (16 B per plane, 64 B) and hi (dwords 4-5 of planes 0..3, 32 B), and the plane-0 scale
+// byte.  No cross-lane traffic.
+template <int STRIDE>
+__device__ __forceinline__ void q6_block_store_lds(const float* src, bool store, uint8_t* lo_blk, uint8_t* hi_blk,
+                                                   uint8_t* sc_byte) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < QB; ++i) amax = absmax_nan(amax, src[i * STRIDE]);
+  int shift;
+  const int sbyte = block_scale(amax, &shift);
+  uint32_t w[4][6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w[j][k] = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float v[QB / 2];
+#pragma unroll
+    for (int i = 0; i < QB / 2; ++i) v[i] = src[(16 * h + i) * STRIDE];
+#pragma unroll
+    for (int i = 0; i < QB / 2; ++i) {
+      int d[4];
+      digits4(v[i], shift, d);
+      const int bit = 6 * (16 * h + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t c = e2m3_code(d[j]);
+        w[j][bit >> 5] |= c << (bit & 31);
+        if ((bit & 31) > 26) w[j][(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+      }
+    }
+  }
+  if (!store) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<uint4*>(lo_blk + 16 * j) = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+  *reinterpret_cast<uint4*>(hi_blk) = make_uint4(w[0][4], w[0][5], w[1][4], w[1][5]);
+  *reinterpret_cast<uint4*>(hi_blk + 16) = make_uint4(w[2][4], w[2][5], w[3][4], w[3][5]);
+  *sc_byte = (uint8_t)sbyte;
+}
+
+// Rows of the E8M0 scale slab [K/64][rows_pad][2] a quantised operand of `rows` rows needs: the
+// GEMM's scale piece is one 1-KiB LDS-DMA of 512 rows from the tile's first row.
+inline int64_t q6_scale_rows(int64_t rows) { return (rows + 255) / 256 * 256 + 512; }
+
+}  // namespace bnn

@@ -30,48 +30,10 @@
 #include <algorithm>
 #include <cmath>
 
-#include "bnn_common.h"
+#include "bnn_fp6.h"
 
 namespace bnn {
 namespace {
-
-constexpr int QB = 32;        // elements per scale block
-constexpr int SCALE_BIAS = 111;  // E8M0 byte of plane 0 = e + 111 (= e - 19 + 3 + 127)
-
-// e2m3 code of the integer digit d in [-16, 16] read as d/8
-__device__ __forceinline__ uint32_t e2m3_code(int d) {
-  const uint32_t s = d < 0 ? 0x20u : 0u;
-  const uint32_t m = (uint32_t)(d < 0 ? -d : d);
-  return s | (m < 8 ? m : (m < 16 ? (0x8u | (m - 8)) : 0x10u));
-}
-
-// Block exponent from the block's |max|: e with amax in [2^(e-1), 2^e); returns the plane-0 E8M0
-// byte (255 = NaN for a non-finite block: its outputs become NaN, as the fp32 GEMM's would).
-__device__ __forceinline__ int block_scale(float amax, int* shift) {
-  if (!(amax == amax) || amax == __builtin_inff()) {
-    *shift = 0;
-    return 255;
-  }
-  int e = -111;
-  if (amax > 0.f) {
-    frexpf(amax, &e);
-    e = e < -111 ? -111 : e;     // blocks below 2^-112 quantise to ~0 (error < 2^-130)
-  }
-  *shift = 19 - e;
-  return e + SCALE_BIAS;
-}
-
-// 4 balanced base-32 digits of rint(x * 2^shift)
-__device__ __forceinline__ void digits4(float x, int shift, int (&d)[4]) {
-  int v = __float2int_rn(ldexpf(x, shift));
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int dj = ((v + 16) & 31) - 16;
-    d[j] = dj;
-    v = (v - dj) >> 5;
-  }
-  d[3] = v;
-}
 
 // ------------------------------------------------------------------------------------------
 // Row quantiser: x [M][K] (row stride ldx) -> lo, hi, scales; blocks beyond K are zero digits.
@@ -95,48 +57,8 @@ __global__ __launch_bounds__(256) void quant6_rows_k(const float* __restrict__ x
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = (k0 + j < K) ? xr[k0 + j] : 0.f;
   }
-  float amax = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float a = fabsf(v[j]);
-    amax = (a == a) ? fmaxf(amax, a) : __builtin_inff();
-  }
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-  int shift;
-  const int sbyte = block_scale(amax, &shift);
-  // this lane's 4 elements -> a 24-bit chunk per plane (element 4q+i at bits 6i of the chunk)
-  uint32_t chunk[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int d[4];
-    digits4(v[i], shift, d);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) chunk[j] |= e2m3_code(d[j]) << (6 * i);
-  }
-  // lane j of the group assembles plane j: chunk of lane p sits at bits 24p..24p+23
-  const int plane = q & 3;
-  uint32_t w[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t cj = __shfl(chunk[j], (lane & ~7) | p, 64);
-      c = (plane == j) ? cj : c;
-    }
-    const int bit = 24 * p;
-    w[bit >> 5] |= c << (bit & 31);
-    if ((bit & 31) > 8) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
-  }
-  if (q < 4) {
-    uint8_t* lo_p = lo + (row * nblk + blk) * 64 + plane * 16;
-    *reinterpret_cast<uint4*>(lo_p) = make_uint4(w[0], w[1], w[2], w[3]);
-    uint8_t* hi_p = hi + (row * nblk + blk) * 32 + plane * 8;
-    *reinterpret_cast<uint2*>(hi_p) = make_uint2(w[4], w[5]);
-  } else if (q == 4) {
-    sc[(blk >> 1) * sc_rows * 2 + row * 2 + (blk & 1)] = (uint8_t)sbyte;
-  }
+  q6_block_store(v, lane, true, lo + (row * nblk + blk) * 64, hi + (row * nblk + blk) * 32,
+                 sc + (blk >> 1) * sc_rows * 2 + row * 2 + (blk & 1));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -673,7 +595,7 @@ using namespace bnn;
 
 // scale-array row pitch: rows rounded up to 256, plus 512 rows of padding so the GEMM's per-stage
 // 1-KiB scale piece (512 rows from the tile's first row) never reads past the slab
-BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return round_up(rows, 256) + 512; }
+BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return q6_scale_rows(rows); }
 
 BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
                             uint8_t* sc, void* stream) {

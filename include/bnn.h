@@ -281,6 +281,19 @@ int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
                        const float* beta, const float* save_mean, const float* save_invstd,
                        const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
                        float* dgamma, float* dbeta, void* work, bnn_stream_t stream);
+
+/* The BatchNorm(+Dropout) backward whose dz is the upstream gradient of an FP6-backward
+ * BinarizeLinear (mnist-dist2.py:66-71 fc -> [drop ->] bn -> htanh -> fc): bnn_bn_bwd /
+ * bnn_bn_dropout_bwd (p = 0: no dropout) that also writes both FP6 digit forms of dz -- rows
+ * (lo/hi/sc as bnn_quant6_rows with Kp = C) and the transpose (as bnn_quant6_cols_t with
+ * Mp = round_up(M, 64)) -- and colsum[n] = sum_m dz[m][n] (nullable), in the same pass, so dz is
+ * never re-read; dx (the fp32 dz) is optional.  C % 64 == 0; training statistics only.  Digits
+ * are bit-identical to the standalone quantisers on the same dz. */
+int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                  const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
+                  float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
+                  uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                  bnn_stream_t stream);
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
 
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
