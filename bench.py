@@ -46,6 +46,7 @@ MI355X_FP4_DENSE_TOPS = 256 * 4 * 4096 * 2.4e9 / 1e12    # 32x32x64 f8f6f4 MFMA 
 MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
 MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
 MI355X_HBM_GBS = 8000.0
+PUBLISHED_SMALL_SPS = 60000 / 8.248   # MNIST_EPOCH_TIME(PersonalCom).csv:2-6 mean epoch, BASELINE.md §1
 
 CONFIGS = {
     # name: (model key, default per-GPU batch, description)
@@ -97,6 +98,8 @@ def parse():
     ap.add_argument("--backend", default="fp4", choices=["fp4", "mfma", "xnor"])
     ap.add_argument("--exchange", action="store_true",
                     help="run the gradient-exchange bucket path at N=1 too (flat buckets, hooks)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the training step as a HIP graph and time replays (1 GPU; bnn_amd.graph)")
     ap.add_argument("--fp32-input", action="store_true",
                     help="feed fp32 images (u/255) instead of the u8 pixels the MLPs' fc1 consumes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -222,6 +225,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_exchange = world > 1 or args.exchange
+    if args.graph and use_exchange:
+        raise SystemExit("--graph times one GPU without the gradient exchange")
     if use_exchange:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
@@ -237,7 +242,8 @@ def main():
     torch.manual_seed(0)
     model = build(args.config, args.backend).to(dev).train()
     exchange = GradExchange(model, bucket_mb=args.bucket_mb) if use_exchange else None
-    opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model))
+    dstep = BF.DeviceStep(dev).activate() if args.graph else None
+    opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model), device_step=dstep)
     as_u8 = args.config != "cnn" and not args.fp32_input
     x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev, as_u8=as_u8)
     crit = torch.nn.CrossEntropyLoss()
@@ -255,15 +261,20 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    run = step
+    if args.graph:
+        from bnn_amd.graph import GraphedStep
+        run = GraphedStep(step, opt, dstep, warmup=max(1, args.warmup))   # eager warm-up + capture
+    else:
+        for _ in range(args.warmup):
+            step()
     if use_exchange:
         dist.barrier()
     torch.cuda.synchronize()
 
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if use_exchange:
         dist.barrier()
@@ -296,7 +307,10 @@ def main():
         "ms_per_step": round(ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        # the reference's only published figure is this config's CSV epoch time
+        # (mnist-dist3.py, 784-192x3-10, batch 64, one GPU: 60000 / 8.248 s = 7,274 samples/s)
+        "vs_baseline": (round(samples / elapsed / PUBLISHED_SMALL_SPS, 2)
+                        if args.config == "small" and batch == 64 and world == 1 else None),
         "dtype": "fp4/fp6/int8 MFMA (ternary operands as FP4 e2m1, fp32 operands as 4 FP6 e2m3 digit planes "
                  "with E8M0 block scales (backward) or 3 int8 digit planes (first layer); fp32 accumulate, fp32 I/O)",
         "data": ("synthetic MNIST-shaped (80.7% zero pixels), resident in HBM as "
@@ -304,7 +318,8 @@ def main():
                  + ", random-init weights"),
         "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
-                   "backend": args.backend, "exchange": bool(use_exchange), "loss_last_step": round(final_loss, 5)},
+                   "backend": args.backend, "exchange": bool(use_exchange), "hip_graph": bool(args.graph),
+                   "loss_last_step": round(final_loss, 5)},
     }
     if ksum:
         # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (2*M*N*K) and the

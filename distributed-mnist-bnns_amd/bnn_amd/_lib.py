@@ -64,6 +64,12 @@ SIGNATURES = {
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,
                                   P]),
+    "bnn_adam_schedule": (I32, [F32, F32, F32, I64, I64, P]),
+    "bnn_adam_clamp_sched": (I32, [P, P, P, P, I64, F32, F32, F32, P, P, F32, I32, P]),
+    "bnn_adam_clamp_pack_sched": (I32, [P, P, P, P, I64, I64, F32, F32, F32, P, P, F32, I32, I32, P, I64, P, I64,
+                                        I32, P]),
+    "bnn_counter_add": (I32, [P, I64, P]),
+    "bnn_set_seed_counter": (I32, [P]),
     "bnn_quant6_scale_rows": (I64, [I64]),
     "bnn_quant6_rows": (I32, [P, I64, I64, I64, I64, P, P, P, P]),
     "bnn_quant6_cols_workspace": (I64, [I64, I64]),

@@ -243,8 +243,57 @@ def packed_weight(weight, fmt, want_q, want_qt, cache=True, qt_fmt="i8"):
     return q, qt
 
 
+_DEVICE_STEP = None
+
+
+class DeviceStep:
+    """A device-resident training-step counter, for steps captured in a HIP graph (a replay keeps
+    every kernel argument of the capture): while active, dropout masks are drawn from
+    seed + ctr * golden (bnn_set_seed_counter) and Adam reads its bias corrections from a host-built
+    table at index ctr (bnn_adam_schedule / *_sched); the optimizer advances ctr by one at the end
+    of each step, on the device."""
+
+    def __init__(self, device="cuda"):
+        self.ctr = torch.zeros((1,), dtype=torch.int64, device=device)
+        self.active = False
+        self.steps = 0          # host shadow of ctr: advance() in eager steps, note_replays() for graphs
+
+    def activate(self):
+        """Make this the process's device step: dropout then uses one base seed (drawn here from
+        torch's CPU generator) + the device counter, in eager and captured steps alike."""
+        global _DEVICE_STEP
+        self.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        L.call("bnn_set_seed_counter", L.ptr(self.ctr))
+        self.active = True
+        _DEVICE_STEP = self
+        return self
+
+    def deactivate(self):
+        global _DEVICE_STEP
+        L.call("bnn_set_seed_counter", None)
+        self.active = False
+        if _DEVICE_STEP is self:
+            _DEVICE_STEP = None
+
+    def advance(self):
+        L.call("bnn_counter_add", L.ptr(self.ctr), 1, L.stream())
+        self.steps += 1
+
+    def note_replays(self, n):
+        """A captured step that contains one advance() was replayed n times."""
+        self.steps += int(n)
+
+
+def adam_schedule(lr, beta1, beta2, step0, n, device):
+    """[n, 2] fp32 (step_size, sqrt(bias_correction2)) for Adam steps step0 .. step0+n-1, computed
+    by libbnn's host code exactly as the per-launch form does, copied to ``device``."""
+    host = torch.empty((n, 2), dtype=torch.float32)
+    L.call("bnn_adam_schedule", float(lr), float(beta1), float(beta2), int(step0), int(n), L.ptr(host))
+    return host.to(device)
+
+
 def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
-                     grad_scale=1.0, clamp=True):
+                     grad_scale=1.0, clamp=True, sched=None, ctr=None):
     """bnn_adam_clamp on a 2-D latent weight that also rewrites its cached packed operands (see
     packed_weight).  Returns False (nothing done) when ``p`` has no valid cache."""
     ent = getattr(p, "_bnn_pack", None)
@@ -257,11 +306,17 @@ def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.
     N, K = p.shape
     q, qt = ent["q"], ent["qt"]
     nbytes = 28 * N * K + (q.numel() if q is not None else 0) + (qt.numel() if qt is not None else 0)
+    tail = (1 if ent["fmt"] == "fp4" else 0, L.ptr(q), q.shape[1] if q is not None else 0,
+            L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if ent["qt_fmt"] == "fp4" else 0, L.stream())
     with _timed("sign_pack_tile_k<adam>", 0, nbytes):
-        L.call("bnn_adam_clamp_pack", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
-               float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale), int(bool(clamp)),
-               1 if ent["fmt"] == "fp4" else 0, L.ptr(q), q.shape[1] if q is not None else 0,
-               L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if ent["qt_fmt"] == "fp4" else 0, L.stream())
+        if sched is not None:
+            L.call("bnn_adam_clamp_pack_sched", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
+                   float(beta1), float(beta2), float(eps), L.ptr(sched), L.ptr(ctr), float(grad_scale),
+                   int(bool(clamp)), *tail)
+        else:
+            L.call("bnn_adam_clamp_pack", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
+                   float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale),
+                   int(bool(clamp)), *tail)
     ent["key"] = _pack_key(p)
     return True
 
@@ -711,13 +766,18 @@ def hardtanh_backward(x, g):
 
 
 def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
-                grad_scale=1.0, clamp=True):
+                grad_scale=1.0, clamp=True, sched=None, ctr=None):
     """In-place fused Adam (torch formula) + clamp to [-1, 1] on a latent weight."""
     _check(p, grad, exp_avg, exp_avg_sq)
     invalidate_packed(p)        # a raw in-place write: cached packed operands would go stale
     for t in (p, grad, exp_avg, exp_avg_sq):
         if not t.is_contiguous():
             raise ValueError("adam_clamp_: tensors must be contiguous")
+    if sched is not None:
+        L.call("bnn_adam_clamp_sched", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), p.numel(),
+               float(beta1), float(beta2), float(eps), L.ptr(sched), L.ptr(ctr), float(grad_scale),
+               int(bool(clamp)), L.stream())
+        return
     L.call("bnn_adam_clamp", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), p.numel(),
            float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale),
            int(bool(clamp)), L.stream())
@@ -897,7 +957,8 @@ def dropout_batch_norm_hardtanh(x, p, bn, seed=None):
     """nn.Dropout(p) -> nn.BatchNorm1d module (training mode) -> Hardtanh through libbnn.  The seed
     is drawn from torch's CPU generator (so torch.manual_seed makes runs repeatable) unless given."""
     if seed is None:
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        # device-step mode: a fixed base seed, the kernels add the device step counter
+        seed = _DEVICE_STEP.base_seed if _DEVICE_STEP is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
     rm, rv, bn_training, factor = _bn_module_args(bn)
     if not bn_training:
         raise ValueError("dropout_batch_norm_hardtanh is the training-mode fusion")

@@ -1,0 +1,56 @@
+"""One training step captured as a HIP graph (torch.cuda.CUDAGraph on ROCm) and replayed.
+
+The reference's loop (mnist-dist2.py:118-137) launches every op of every step from Python; at
+the published configuration (mnist-dist3.py: 784-192x3-10, batch 64) the GPU work per step is a
+few hundred microseconds, so launch overhead is most of the step.  ``GraphedStep`` captures the
+whole step -- forward, loss, backward, the fused latent update -- once and replays it:
+
+* inputs are static tensors (copy the next batch into them before each replay);
+* the quantities the host would pass per step by value -- Adam's bias corrections and the dropout
+  seed -- come from a ``functional.DeviceStep`` counter that the captured optimizer advances on
+  the device (bnn_adam_*_sched, bnn_set_seed_counter), so every replay is a distinct step and
+  the sequence equals the same number of eager device-step steps bit for bit;
+* one process, one GPU: the gradient exchange is not captured (data-parallel runs use the eager
+  path, whose collectives overlap backward).
+"""
+import torch
+
+
+class GraphedStep:
+    def __init__(self, step_fn, optimizer, device_step, warmup=2):
+        if device_step is None or not device_step.active:
+            raise ValueError("GraphedStep: needs an active functional.DeviceStep")
+        if getattr(optimizer, "device_step", None) is not device_step:
+            raise ValueError("GraphedStep: the optimizer must run on the same DeviceStep")
+        self.opt, self.ds = optimizer, device_step
+        # eager warm-up on a side stream (torch's capture recipe): builds the packed-weight caches,
+        # constant vectors and the Adam schedule outside the capture
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                step_fn()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = step_fn()
+        # the capture ran the host side of one step without executing it on the device
+        self._shadow(-1)
+
+    def _shadow(self, n):
+        self.ds.note_replays(n)
+        for group in self.opt.param_groups:
+            for p in group["params"]:
+                st = self.opt.state.get(p)
+                if st and "step" in st:
+                    st["step"] += n
+
+    def __call__(self, n=1):
+        """Replay the captured step n times; returns the step function's (static) output."""
+        for _ in range(n):
+            self.graph.replay()
+        self._shadow(n)
+        return self.out
+
+
+__all__ = ["GraphedStep"]

@@ -15,6 +15,10 @@ of the parameters the reference clamps, with an optional gradient scale (1/world
 gradient exchange summed instead of averaged).  For a binarized layer's weight the same kernel
 also rewrites the next forward's packed ternary operands (bnn_adam_clamp_pack), replacing the
 per-forward sign-pack of the weight.
+
+With ``device_step`` (a ``functional.DeviceStep``) the step is graph-capturable: the bias
+corrections come from a device table indexed by the device step counter (bit-identical to the
+per-launch values), and the counter is advanced on the device after the last update.
 """
 import torch
 
@@ -36,18 +40,44 @@ def org_protocol_step(model, optimizer):
 class LatentAdam(torch.optim.Optimizer):
     """Adam (torch defaults) fused with clamp(-1, 1) for the parameters in ``clamp_params``."""
 
+    SCHEDULE_STEPS = 1 << 20      # device-step table length (8 MiB per parameter group)
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, clamp_params=(),
-                 grad_scale=1.0):
+                 grad_scale=1.0, device_step=None):
         defaults = dict(lr=lr, betas=betas, eps=eps)
         super().__init__(params, defaults)
         self._clamp = {id(p) for p in clamp_params}
         self.grad_scale = grad_scale
+        self.device_step = device_step
+        self._sched = {}              # group index -> (table, lr, betas, first step, device ctr base)
+
+    def _schedule(self, gi, group, step, device):
+        """Device table for this group covering the device counter's steps: entry i holds the bias
+        corrections of Adam step (step at table build) + i - (counter at build)."""
+        ds = self.device_step
+        key = (group["lr"], tuple(group["betas"]))
+        ent = self._sched.get(gi)
+        if ent is None or ent[1] != key:
+            # entry c = Adam step first + c for device counter value c (build it before capturing)
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("LatentAdam: run one eager step with device_step before capturing")
+            first = step - ds.steps
+            if first < 1:
+                raise RuntimeError("LatentAdam: device step counter ahead of the optimizer's steps")
+            tab = BF.adam_schedule(group["lr"], *group["betas"], first, ds.steps + self.SCHEDULE_STEPS, device)
+            ent = (tab, key)
+            self._sched[gi] = ent
+        if ds.steps >= ent[0].shape[0]:
+            raise RuntimeError("LatentAdam: device-step schedule exhausted")
+        return ent[0]
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        for group in self.param_groups:
+        ds = self.device_step
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
+            sched = None
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -60,8 +90,15 @@ class LatentAdam(torch.optim.Optimizer):
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 args = (g, st["exp_avg"], st["exp_avg_sq"], st["step"], group["lr"], b1, b2, group["eps"],
                         self.grad_scale, id(p) in self._clamp)
+                kw = {}
+                if ds is not None:
+                    if sched is None:
+                        sched = self._schedule(gi, group, st["step"], p.device)
+                    kw = dict(sched=sched, ctr=ds.ctr)
                 # a binarized layer's weight also gets its next-forward ternary operands rewritten in
                 # the same pass (bnn_adam_clamp_pack); anything else: plain fused Adam + clamp
-                if not BF.adam_clamp_pack_(p, *args):
-                    BF.adam_clamp_(p, *args)
+                if not BF.adam_clamp_pack_(p, *args, **kw):
+                    BF.adam_clamp_(p, *args, **kw)
+        if ds is not None:
+            ds.advance()
         return loss

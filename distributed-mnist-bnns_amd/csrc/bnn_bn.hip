@@ -24,9 +24,23 @@
 namespace bnn {
 namespace {
 
-constexpr int BN_ROWS = 256;  // rows per partial-statistics chunk
+constexpr int BN_ROWS = 256;  // most rows per partial-statistics chunk
 
-inline int64_t bn_chunks(int64_t M) { return std::max<int64_t>(1, (M + BN_ROWS - 1) / BN_ROWS); }
+// Rows per chunk of the column reductions: 256, halved while the reduction (one thread per 4
+// columns and chunk) would have fewer than 2^17 threads -- a [4096, 3072] batch gets 16-row
+// chunks (196 K threads) instead of 48 workgroups, a [65536, 8192] one keeps 256.
+inline int64_t bn_chunk_rows(int64_t M, int64_t C) {
+  int64_t rows = BN_ROWS;
+  while (rows > 1 && (C / 4) * ((M + rows - 1) / rows) < (1 << 17)) rows >>= 1;
+  return rows;
+}
+inline int64_t bn_chunks(int64_t M, int64_t C) {
+  const int64_t rows = bn_chunk_rows(M, C);
+  return std::max<int64_t>(1, (M + rows - 1) / rows);
+}
+inline dim3 reduce_grid(int64_t M, int64_t C) {
+  return dim3((unsigned)(((C / 4) * bn_chunks(M, C) + 255) / 256));
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
@@ -39,7 +53,18 @@ struct Drop {
   uint32_t thresh;  // keep iff hash < thresh
   int on;
   float scale;      // 1 / (1 - p)
+  const int64_t* ctr = nullptr;   // device step counter folded into the seed (bnn_set_seed_counter)
 };
+
+// Process-wide device step counter for graph-captured training steps: dropout launches made
+// while it is set draw their mask from seed + ctr[0] * golden, so one captured graph replays with
+// a fresh mask per step (forward and backward of a step read the same counter value).
+const int64_t* g_seed_ctr = nullptr;
+
+__device__ __forceinline__ Drop drop_resolve(Drop d) {
+  if (d.on && d.ctr != nullptr) d.seed += (uint64_t)d.ctr[0] * 0xD1B54A32D192ED03ull;
+  return d;
+}
 
 __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
   uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;   // splitmix64 finaliser
@@ -57,7 +82,7 @@ __device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4])
 }
 
 inline Drop make_drop(float p, uint64_t seed) {
-  Drop d{seed, 0u, 0, 1.f};
+  Drop d{seed, 0u, 0, 1.f, g_seed_ctr};
   if (p > 0.f && p < 1.f) {
     const double t = (1.0 - (double)p) * 4294967296.0;
     d.thresh = t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
@@ -79,11 +104,16 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
                                                    const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, int hardtanh,
                                                    double* __restrict__ p0, double* __restrict__ p1,
-                                                   Drop dp = Drop{0, 0, 0, 1.f}) {
-  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (c >= C) return;
-  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  const int64_t r1 = (M < r0 + BN_ROWS) ? M : r0 + BN_ROWS;
+                                                   int64_t chunk_rows, Drop dp0 = Drop{0, 0, 0, 1.f}) {
+  const Drop dp = drop_resolve(dp0);
+  // thread -> (4-column group, chunk): consecutive threads read consecutive columns of a row
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t C4 = C / 4;
+  const int64_t chunk = id / C4;
+  const int64_t c = (id - chunk * C4) * 4;
+  const int64_t r0 = chunk * chunk_rows;
+  if (r0 >= M) return;
+  const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
   float mu[4], lo[4] = {0, 0, 0, 0}, is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
   if (MODE == 0) {
@@ -137,7 +167,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
       b[j] += (double)fb[j];
     }
   }
-  const int64_t o = blockIdx.y * C + c;
+  const int64_t o = chunk * C + c;
   if (MODE == 0) {
     const double n = (double)(r1 - r0);
 #pragma unroll
@@ -158,7 +188,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
 // Final merges: a workgroup owns 64 columns; its 4 waves each merge every 4th chunk (r = wave,
 // wave+4, ...) and wave 0 folds the 4 group results in order -- 4x the parallelism of one thread
 // per column walking all R chunks, still a fixed (deterministic) order.
-constexpr int FIN_COLS = 64, FIN_GROUPS = 4;
+constexpr int FIN_COLS = 16, FIN_GROUPS = 16;
 
 inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + FIN_COLS - 1) / FIN_COLS)); }
 
@@ -195,7 +225,7 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
   __syncthreads();
   if (grp != 0 || c >= C) return;
   n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
-  for (int gI = 0; gI < FIN_GROUPS; ++gI) {
+  for (int gI = 0; gI < FIN_GROUPS; ++gI) {   // fixed order
     const double nb = sn[gI][lc];
     if (nb == 0.0) continue;
     const double nt = n + nb, delta = sm[gI][lc] - mean;
@@ -234,10 +264,18 @@ __device__ __forceinline__ float4 ld4_or(const float* p, int64_t c, float dflt) 
 // blockIdx.y = APPLY_ROWS-row chunk.  Each thread keeps its 4 columns' parameters in registers and
 // walks the rows (per row the workgroup touches one contiguous 4 KiB segment): no per-element
 // index modulo and no per-element reloads of the column vectors.
+// Rows per workgroup: 64, halved (down to 4) while the grid has fewer than 2048 workgroups.
 constexpr int APPLY_ROWS = 64;
 
+__host__ __device__ inline int64_t apply_rows(int64_t M, int64_t C) {
+  int64_t rows = APPLY_ROWS;
+  while (rows > 4 && ((C / 4 + 255) / 256) * ((M + rows - 1) / rows) < 2048) rows >>= 1;
+  return rows;
+}
+
 inline dim3 apply_grid(int64_t M, int64_t C) {
-  return dim3((unsigned)((C / 4 + 255) / 256), (unsigned)((M + APPLY_ROWS - 1) / APPLY_ROWS));
+  const int64_t rows = apply_rows(M, C);
+  return dim3((unsigned)((C / 4 + 255) / 256), (unsigned)((M + rows - 1) / rows));
 }
 
 __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, int64_t M, int64_t C,
@@ -246,10 +284,12 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
                                                   const float* __restrict__ invstd,
                                                   const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, int hardtanh,
-                                                  float* __restrict__ y, Drop dp = Drop{0, 0, 0, 1.f}) {
+                                                  float* __restrict__ y, Drop dp0 = Drop{0, 0, 0, 1.f}) {
+  const Drop dp = drop_resolve(dp0);
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
-  const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
+  const int64_t ar = apply_rows(M, C);
+  const int64_t r0 = (int64_t)blockIdx.y * ar, r1 = (r0 + ar < M) ? r0 + ar : M;
   const float4 mv = ld4(mean + c), iv = ld4(invstd + c), lv = ld4_or(mean_lo, c, 0.f);
   const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
   const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -286,8 +326,11 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
   sb[grp][lc] = s2;
   __syncthreads();
   if (grp != 0 || c >= C) return;
-  s = sa[0][lc] + sa[1][lc] + sa[2][lc] + sa[3][lc];
-  s2 = sb[0][lc] + sb[1][lc] + sb[2][lc] + sb[3][lc];
+  s = 0.0, s2 = 0.0;
+  for (int gI = 0; gI < FIN_GROUPS; ++gI) {   // fixed order
+    s += sa[gI][lc];
+    s2 += sb[gI][lc];
+  }
   if (dbeta) dbeta[c] = (float)s;
   if (dgamma) dgamma[c] = (float)s2;
   k0[c] = (float)s;
@@ -302,12 +345,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
                                                       const float* __restrict__ beta, int hardtanh,
                                                       const float* __restrict__ sg,
                                                       const float* __restrict__ sgx, float inv_n,
-                                                      float* __restrict__ dx, Drop dp = Drop{0, 0, 0, 1.f}) {
+                                                      float* __restrict__ dx, Drop dp0 = Drop{0, 0, 0, 1.f}) {
+  const Drop dp = drop_resolve(dp0);
   // inv_n = 1/M with batch statistics (train); 0 in eval mode, where mean/invstd are the running
   // statistics (constants): dx = gamma*invstd*g
   const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (c >= C) return;
-  const int64_t r0 = (int64_t)blockIdx.y * APPLY_ROWS, r1 = (r0 + APPLY_ROWS < M) ? r0 + APPLY_ROWS : M;
+  const int64_t ar = apply_rows(M, C);
+  const int64_t r0 = (int64_t)blockIdx.y * ar, r1 = (r0 + ar < M) ? r0 + ar : M;
   const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
   const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f), lv = ld4_or(mean_lo, c, 0.f);
   const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -363,7 +408,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
                                                          const float* __restrict__ beta, int hardtanh,
                                                          const float* __restrict__ sg,
                                                          const float* __restrict__ sgx, float inv_n, Q6Out o,
-                                                         Drop dp) {
+                                                         Drop dp0) {
+  const Drop dp = drop_resolve(dp0);
   __shared__ __attribute__((aligned(16))) float tile[Q6T_SUB * Q6T_LD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * Q6T_COLS;
@@ -451,8 +497,8 @@ inline int grid_for(int64_t n) {
 }
 
 bool bn_args_ok(const float* x, int64_t M, int64_t C) {
-  return x && M > 0 && C > 0 && C % 4 == 0 && aligned16(x) && bn_chunks(M) <= 65535 &&
-         (M + APPLY_ROWS - 1) / APPLY_ROWS <= 65535;
+  return x && M > 0 && C > 0 && C % 4 == 0 && aligned16(x) && (C / 4) * bn_chunks(M, C) < (1LL << 31) &&
+         (M + apply_rows(M, C) - 1) / apply_rows(M, C) <= 65535;
 }
 
 bool vec_ok(const float* p) { return p == nullptr || aligned16(p); }
@@ -737,7 +783,7 @@ using namespace bnn;
 
 BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
   // two double partial arrays [R][C] + two float vectors [C]
-  return 2 * bn_chunks(M) * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
+  return 2 * bn_chunks(M, C) * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
 }
 
 static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -752,15 +798,15 @@ static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* 
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t R = bn_chunks(M);
+  const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   // without a caller buffer the lo part of the mean lives in the workspace (the bwd's k0 slot)
   float* lo = save_mean_lo ? save_mean_lo : reinterpret_cast<float*>(p1 + R * C);
-  hipLaunchKernelGGL(bn_reduce_k<0>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x,
-                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, dp);
+  hipLaunchKernelGGL(bn_reduce_k<0>, reduce_grid(M, C), dim3(256), 0, s, x,
+                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
-                     running_var, save_mean, save_invstd, lo, (int64_t)BN_ROWS, (int64_t)1);
+                     running_var, save_mean, save_invstd, lo, bn_chunk_rows(M, C), (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
     hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, lo, save_invstd,
                        gamma, beta, hardtanh, y, dp);
@@ -815,13 +861,13 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t R = bn_chunks(M);
+  const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
-                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
+  hipLaunchKernelGGL(bn_reduce_k<1>, reduce_grid(M, C), dim3(256), 0, s, x, dy,
+                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
@@ -874,13 +920,13 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const Drop dp = make_drop(p, seed);
-  const int64_t R = bn_chunks(M);
+  const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL(bn_reduce_k<1>, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy,
-                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, dp);
+  hipLaunchKernelGGL(bn_reduce_k<1>, reduce_grid(M, C), dim3(256), 0, s, x, dy,
+                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
@@ -893,7 +939,13 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
   return check_launch("bnn_bn_bwd_q6");
 }
 
-__global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d, float* __restrict__ out) {
+BNN_API int bnn_set_seed_counter(const int64_t* ctr) {
+  g_seed_ctr = ctr;
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d0, float* __restrict__ out) {
+  const Drop d = drop_resolve(d0);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     out[i] = (!d.on || drop_keep(d, (uint64_t)i)) ? d.scale : 0.f;   // p == 0: the fused passes never mask

@@ -91,7 +91,21 @@ struct AdamArgs {
   float* v;
   float b1, b2, eps, step_size, bc2_sqrt, gscale;
   int clamp;
+  // device-step form (graph-captured steps): (step_size, bc2_sqrt) = sched[2 * ctr[0] + {0, 1}],
+  // a host-built table of the same bias corrections (bnn_adam_schedule)
+  const float* sched = nullptr;
+  const int64_t* ctr = nullptr;
 };
+
+// step_size / bc2_sqrt of this launch (from the arguments, or the device-step table)
+__device__ __forceinline__ AdamArgs adam_resolve(AdamArgs a) {
+  if (a.sched != nullptr) {
+    const int64_t i = a.ctr[0];
+    a.step_size = a.sched[2 * i];
+    a.bc2_sqrt = a.sched[2 * i + 1];
+  }
+  return a;
+}
 
 void adam_bias_correction(float lr, float beta1, float beta2, int64_t step, float* step_size, float* bc2_sqrt);
 

@@ -60,7 +60,8 @@ struct ColAffine {
 // sign_pack_tile_k: the fused latent update of mnist-dist2.py:131-137 that also writes the next
 // forward's ternary operands).  p, g, m, v share the row-major [M][K] layout (ldx = K).
 __device__ __forceinline__ void adam16(float* __restrict__ prow, int64_t off, int64_t k, int64_t K, bool vec,
-                                       const AdamArgs& a, float (&v)[16]) {
+                                       const AdamArgs& a0, float (&v)[16]) {
+  const AdamArgs a = adam_resolve(a0);
   float g[16], mm[16], vv[16];
   load16(prow, k, K, vec, v);
   load16(a.g + off, k, K, vec, g);
@@ -303,16 +304,29 @@ __global__ __launch_bounds__(256) void quant_rows_k(const float* __restrict__ x,
   }
 }
 
-constexpr int COL_ROWS = 256;  // rows per column-statistics chunk
+constexpr int COL_ROWS = 256;  // most rows per column-statistics chunk
+
+// 256 rows per chunk, halved while the statistics pass would have fewer than 2^17 threads (as
+// bnn_bn.hip's reductions): small batches get enough workgroups to fill the chip.
+inline int64_t col_chunk_rows(int64_t M, int64_t N) {
+  int64_t rows = COL_ROWS;
+  while (rows > 1 && ((N + 3) / 4) * ((M + rows - 1) / rows) < (1 << 17) && (M + rows / 2 - 1) / (rows / 2) <= 65535)
+    rows >>= 1;
+  return rows;
+}
+inline int64_t col_chunks(int64_t M, int64_t N) {
+  const int64_t rows = col_chunk_rows(M, N);
+  return std::max<int64_t>(1, (M + rows - 1) / rows);
+}
 
 // Pass 1: per (row chunk, column) absolute max and double sum.
 __global__ __launch_bounds__(256) void colstats_k(const float* __restrict__ x, int64_t M, int64_t N,
                                                   int64_t ldx, float* __restrict__ pmax,
-                                                  double* __restrict__ psum) {
+                                                  double* __restrict__ psum, int64_t crows) {
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.y * COL_ROWS;
+  const int64_t r0 = (int64_t)blockIdx.y * crows;
   if (n >= N) return;
-  const int64_t r1 = (M < r0 + COL_ROWS) ? M : r0 + COL_ROWS;
+  const int64_t r1 = (M < r0 + crows) ? M : r0 + crows;
   float amax = 0.f;
   double sum = 0.0;
   for (int64_t r = r0; r < r1; ++r) {
@@ -329,11 +343,11 @@ __global__ __launch_bounds__(256) void colstats_k(const float* __restrict__ x, i
 // double accumulation (bit-identical results), a quarter of the load instructions.
 __global__ __launch_bounds__(256) void colstats4_k(const float* __restrict__ x, int64_t M, int64_t N,
                                                    int64_t ldx, float* __restrict__ pmax,
-                                                   double* __restrict__ psum) {
+                                                   double* __restrict__ psum, int64_t crows) {
   const int64_t n = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  const int64_t r0 = (int64_t)blockIdx.y * COL_ROWS;
+  const int64_t r0 = (int64_t)blockIdx.y * crows;
   if (n >= N) return;
-  const int64_t r1 = (M < r0 + COL_ROWS) ? M : r0 + COL_ROWS;
+  const int64_t r1 = (M < r0 + crows) ? M : r0 + crows;
   float amax[4] = {0.f, 0.f, 0.f, 0.f};
   double sum[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t r = r0; r < r1; ++r) {
@@ -535,12 +549,12 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
   return check_launch("bnn_sign_pack_fp4");
 }
 
-BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
-                                int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
-                                float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
-                                int64_t ldqt, int32_t qt_fmt, void* stream) {
-  if (!p || !grad || !exp_avg || !exp_avg_sq || N <= 0 || K <= 0 || step < 1 || (fmt != 0 && fmt != 1) ||
-      (!q && !qt)) {
+static int adam_clamp_pack_impl(float* p, const AdamArgs& a, int64_t N, int64_t K, int32_t fmt, void* q,
+                                int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
+  const float* grad = a.g;
+  const float* exp_avg = a.m;
+  const float* exp_avg_sq = a.v;
+  if (!p || !grad || !exp_avg || !exp_avg_sq || N <= 0 || K <= 0 || (fmt != 0 && fmt != 1) || (!q && !qt)) {
     set_error("bnn_adam_clamp_pack: bad arguments (N=%lld K=%lld fmt=%d)", (long long)N, (long long)K, fmt);
     return kErrInval;
   }
@@ -562,9 +576,6 @@ BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, flo
     set_error("bnn_adam_clamp_pack: N too large for one launch (%lld)", (long long)N);
     return kErrInval;
   }
-  float step_size, bc2_sqrt;
-  adam_bias_correction(lr, beta1, beta2, step, &step_size, &bc2_sqrt);
-  const AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bc2_sqrt, grad_scale, clamp};
   const int vec = aligned16(p) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq) && (K % 4 == 0);
   if (fmt == 0)
     hipLaunchKernelGGL((sign_pack_tile_k<0, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
@@ -573,6 +584,34 @@ BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, flo
     hipLaunchKernelGGL((sign_pack_tile_k<1, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
                        K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a, qt_fmt);
   return check_launch("bnn_adam_clamp_pack");
+}
+
+BNN_API int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
+                                int64_t K, float lr, float beta1, float beta2, float eps, int64_t step,
+                                float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
+                                int64_t ldqt, int32_t qt_fmt, void* stream) {
+  if (step < 1) {
+    set_error("bnn_adam_clamp_pack: step must be >= 1");
+    return kErrInval;
+  }
+  float step_size, bc2_sqrt;
+  adam_bias_correction(lr, beta1, beta2, step, &step_size, &bc2_sqrt);
+  const AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bc2_sqrt, grad_scale, clamp};
+  return adam_clamp_pack_impl(p, a, N, K, fmt, q, ldq, qt, ldqt, qt_fmt, stream);
+}
+
+BNN_API int bnn_adam_clamp_pack_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N,
+                                      int64_t K, float beta1, float beta2, float eps, const float* sched,
+                                      const int64_t* ctr, float grad_scale, int32_t clamp, int32_t fmt, void* q,
+                                      int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
+  if (!sched || !ctr) {
+    set_error("bnn_adam_clamp_pack_sched: null schedule / counter");
+    return kErrInval;
+  }
+  AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, 0.f, 1.f, grad_scale, clamp};
+  a.sched = sched;
+  a.ctr = ctr;
+  return adam_clamp_pack_impl(p, a, N, K, fmt, q, ldq, qt, ldqt, qt_fmt, stream);
 }
 
 BNN_API int bnn_sign_f32(const float* x, float* y, int64_t n, void* stream) {
@@ -616,7 +655,7 @@ BNN_API int bnn_quant_rows(const float* x, int64_t M, int64_t K, int64_t ldx, in
 }
 
 BNN_API int64_t bnn_quant_cols_workspace(int64_t M, int64_t N) {
-  const int64_t R = std::max<int64_t>(1, (M + COL_ROWS - 1) / COL_ROWS);
+  const int64_t R = col_chunks(M, N);
   return round_up(R * N * (int64_t)sizeof(float), 256) + R * N * (int64_t)sizeof(double);
 }
 
@@ -630,7 +669,7 @@ BNN_API int bnn_quant_cols_t_dsum(const float* x, int64_t M, int64_t N, int64_t 
     return kErrInval;
   }
   if (N == 0) return 0;
-  const int64_t R = std::max<int64_t>(1, (M + COL_ROWS - 1) / COL_ROWS);
+  const int64_t R = col_chunks(M, N);
   if (R > 65535 || ldqt / TILE > 65535) {
     set_error("bnn_quant_cols_t: M too large for one launch (%lld)", (long long)M);
     return kErrInval;
@@ -641,10 +680,10 @@ BNN_API int bnn_quant_cols_t_dsum(const float* x, int64_t M, int64_t N, int64_t 
   const unsigned gn = (unsigned)((N + 255) / 256);
   if (M > 0 && aligned16(x) && ldx % 4 == 0 && N % 4 == 0) {
     hipLaunchKernelGGL(colstats4_k, dim3((unsigned)((N / 4 + 255) / 256), (unsigned)R), dim3(256), 0, S(stream), x,
-                       M, N, ldx, pmax, psum);
+                       M, N, ldx, pmax, psum, col_chunk_rows(M, N));
   } else if (M > 0) {
     hipLaunchKernelGGL(colstats_k, dim3(gn, (unsigned)R), dim3(256), 0, S(stream), x, M, N, ldx, pmax,
-                       psum);
+                       psum, col_chunk_rows(M, N));
   } else {
     (void)hipMemsetAsync(pmax, 0, R * N * sizeof(float), S(stream));
     (void)hipMemsetAsync(psum, 0, R * N * sizeof(double), S(stream));

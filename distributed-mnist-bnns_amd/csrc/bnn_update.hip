@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256) void hardtanh_bwd_k(const float* __restrict__ 
 }
 
 // Adam + clamp over a flat tensor (math: adam_elem in bnn_common.h).
-__global__ __launch_bounds__(256) void adam_clamp_k(float* __restrict__ p, int64_t n, AdamArgs a) {
+__global__ __launch_bounds__(256) void adam_clamp_k(float* __restrict__ p, int64_t n, AdamArgs a0) {
+  const AdamArgs a = adam_resolve(a0);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float mi = a.m[i], vi = a.v[i];
@@ -89,4 +90,45 @@ BNN_API int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* e
   const AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, step_size, bc2_sqrt, grad_scale, clamp};
   hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, n, a);
   return check_launch("bnn_adam_clamp");
+}
+
+BNN_API int bnn_adam_clamp_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                 float beta1, float beta2, float eps, const float* sched, const int64_t* ctr,
+                                 float grad_scale, int32_t clamp, void* stream) {
+  if (!p || !grad || !exp_avg || !exp_avg_sq || n < 0 || !sched || !ctr) {
+    set_error("bnn_adam_clamp_sched: bad arguments");
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  AdamArgs a{grad, exp_avg, exp_avg_sq, beta1, beta2, eps, 0.f, 1.f, grad_scale, clamp};
+  a.sched = sched;
+  a.ctr = ctr;
+  hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, n, a);
+  return check_launch("bnn_adam_clamp_sched");
+}
+
+BNN_API int bnn_adam_schedule(float lr, float beta1, float beta2, int64_t step0, int64_t n, float* out) {
+  if (!out || n < 0 || step0 < 1) {
+    set_error("bnn_adam_schedule: bad arguments");
+    return kErrInval;
+  }
+  for (int64_t i = 0; i < n; ++i) adam_bias_correction(lr, beta1, beta2, step0 + i, &out[2 * i], &out[2 * i + 1]);
+  return 0;
+}
+
+namespace bnn {
+namespace {
+__global__ void counter_add_k(int64_t* ctr, int64_t v) {
+  if (threadIdx.x == 0) ctr[0] += v;
+}
+}  // namespace
+}  // namespace bnn
+
+BNN_API int bnn_counter_add(int64_t* ctr, int64_t v, void* stream) {
+  if (!ctr) {
+    set_error("bnn_counter_add: null counter");
+    return kErrInval;
+  }
+  hipLaunchKernelGGL(counter_add_k, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), ctr, v);
+  return check_launch("bnn_counter_add");
 }

@@ -332,6 +332,28 @@ int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_
                         float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
                         int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
 
+/* ---------------------------------------------------------------- device-step form (HIP graphs)
+ * A captured training step replays with frozen kernel arguments, so the per-step quantities the
+ * host passes by value (Adam's bias corrections, the dropout seed) are read from device memory:
+ * ctr[0] = the step index since the counter was created, advanced by bnn_counter_add at the end
+ * of each optimizer step (inside the graph).
+ * bnn_adam_schedule: host-only; out[2i], out[2i+1] = the (step_size, sqrt(1 - beta2^s)) that
+ * bnn_adam_clamp computes for step s = step0 + i (same double arithmetic, bit-identical).
+ * bnn_adam_clamp_sched / bnn_adam_clamp_pack_sched: bnn_adam_clamp / bnn_adam_clamp_pack with
+ * those two values taken from sched[2 * ctr[0]] on the device.
+ * bnn_set_seed_counter: process-wide; while non-NULL every dropout launch (bnn_bn_dropout_*,
+ * bnn_bn_bwd_q6, bnn_dropout_mask) draws its mask from seed + ctr[0] * 0xD1B54A32D192ED03. */
+int bnn_adam_schedule(float lr, float beta1, float beta2, int64_t step0, int64_t n, float* out);
+int bnn_adam_clamp_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                         float beta2, float eps, const float* sched, const int64_t* ctr, float grad_scale,
+                         int32_t clamp, bnn_stream_t stream);
+int bnn_adam_clamp_pack_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t N, int64_t K,
+                              float beta1, float beta2, float eps, const float* sched, const int64_t* ctr,
+                              float grad_scale, int32_t clamp, int32_t fmt, void* q, int64_t ldq, int8_t* qt,
+                              int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
+int bnn_counter_add(int64_t* ctr, int64_t v, bnn_stream_t stream);
+int bnn_set_seed_counter(const int64_t* ctr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,137 @@
+"""HIP-graph training steps (bnn_amd.graph.GraphedStep + functional.DeviceStep).
+
+* Adam with its bias corrections read from the device table (bnn_adam_*_sched) equals the
+  per-launch form bit for bit (the table is the same host arithmetic);
+* a captured step replayed n times equals n eager device-step steps bit for bit -- parameters,
+  Adam moments, BatchNorm running statistics and the loss -- dropout included (the device counter
+  gives every replay its own mask, the same one the eager step draws);
+* distinct replays are distinct steps (the weights move, dropout masks differ).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def F():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import functional
+    return functional
+
+
+def _model(seed, widths=(256, 128, 64), p_drop=0.3):
+    from bnn_amd import nets
+    torch.manual_seed(seed)
+    return nets.MLP(*widths, p_drop=p_drop, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+
+
+def _batch(M=256, seed=3):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    u = torch.randint(0, 256, (M, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    y = torch.randint(0, 10, (M,), generator=g, device="cuda")
+    return u, y
+
+
+def _state(m, opt):
+    out = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+    for i, p in enumerate(m.parameters()):
+        st = opt.state.get(p, {})
+        for k in ("exp_avg", "exp_avg_sq"):
+            if k in st:
+                out[f"opt{i}.{k}"] = st[k].cpu().numpy().copy()
+    return out
+
+
+def _step_fn(m, opt, u, y):
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        for p in m.parameters():
+            p.grad = None
+        loss = crit(m(u), y)
+        loss.backward()
+        opt.step()
+        return loss
+    return step
+
+
+def test_device_step_adam_equals_per_launch(F):
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch()
+    states = []
+    for dev_step in (False, True):
+        m = _model(11, p_drop=0.0)
+        ds = F.DeviceStep().activate() if dev_step else None
+        try:
+            opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+            step = _step_fn(m, opt, u, y)
+            for _ in range(4):
+                step()
+            torch.cuda.synchronize()
+            states.append(_state(m, opt))
+        finally:
+            if ds is not None:
+                ds.deactivate()
+    a, b = states
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("widths,M", [((256, 128, 64), 256), ((192, 192, 192), 64)])
+def test_graph_replays_equal_eager_device_steps(F, widths, M):
+    from bnn_amd.graph import GraphedStep
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch(M)
+    runs = []
+    for graphed in (False, True):
+        m = _model(5, widths)
+        torch.manual_seed(99)                       # the DeviceStep's base dropout seed
+        ds = F.DeviceStep().activate()
+        try:
+            opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+            step = _step_fn(m, opt, u, y)
+            losses = []
+            if graphed:
+                g = GraphedStep(step, opt, ds, warmup=2)       # 2 eager steps + capture
+                for _ in range(3):
+                    losses.append(float(g().item()))
+            else:
+                for i in range(5):
+                    loss = step()
+                    if i >= 2:
+                        losses.append(float(loss.item()))
+            torch.cuda.synchronize()
+            assert ds.steps == 5 and int(ds.ctr.item()) == 5
+            runs.append((_state(m, opt), losses))
+        finally:
+            ds.deactivate()
+    (a, la), (b, lb) = runs
+    assert la == lb
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_replays_are_distinct_steps(F):
+    from bnn_amd.graph import GraphedStep
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch()
+    m = _model(7)
+    ds = F.DeviceStep().activate()
+    try:
+        opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+        g = GraphedStep(_step_fn(m, opt, u, y), opt, ds, warmup=1)
+        w0 = m.fc2.weight.detach().clone()
+        l1 = float(g().item())
+        w1 = m.fc2.weight.detach().clone()
+        l2 = float(g().item())
+        assert not torch.equal(w0, w1) and not torch.equal(w1, m.fc2.weight)
+        assert l1 != l2
+        assert int(m.bn1.num_batches_tracked.item()) == 3       # warm-up + 2 replays
+    finally:
+        ds.deactivate()
