@@ -24,8 +24,10 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from . import functional as BF
 from . import nets
 from .checkpoint import load_checkpoint, save_checkpoint
+from .graph import GraphedStep
 from .data import load_idx_dataset, shard_indices, synthetic_mnist
 from .optim import LatentAdam
 from .parallel import GradExchange
@@ -59,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--dataset-size", type=int, default=60000, help="synthetic training set size")
     ap.add_argument("--idx-images", default=None)
     ap.add_argument("--idx-labels", default=None)
+    ap.add_argument("--graph", action="store_true", help="replay each full batch's step from a HIP graph "
+                    "(one process; bnn_amd.graph)")
     ap.add_argument("--fp32-input", action="store_true", help="keep the dataset as fp32 images (u/255) "
                     "instead of u8 pixels")
     ap.add_argument("--max-steps", type=int, default=0, help="stop each epoch after this many steps")
@@ -99,7 +103,10 @@ def train(gpu, args):
     model = nets.MODELS[args.model](org_protocol=False, mutate_input=False,
                                     fused_bn=True).to(device)
     exchange = GradExchange(model) if world > 1 else None
-    opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=nets.binary_params(model))
+    if args.graph and world > 1:
+        raise SystemExit("--graph runs one process (the gradient exchange is not captured)")
+    dstep = BF.DeviceStep(device).activate() if args.graph else None
+    opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=nets.binary_params(model), device_step=dstep)
     crit = torch.nn.CrossEntropyLoss()
     first_epoch = 1
     if args.resume:
@@ -108,6 +115,16 @@ def train(gpu, args):
     idx = torch.tensor(shard_indices(len(data), world, rank), device=device)
     nb = (len(idx) + args.batch_size - 1) // args.batch_size
     T, E = [], []
+    graphed = static_x = static_y = None
+
+    def _step(xb, yb):
+        for p in model.parameters():
+            p.grad = None
+        lo = crit(model(xb), yb)
+        lo.backward()
+        opt.step()
+        return lo
+
     starts = datetime.now()
     for epoch in range(first_epoch, args.epochs + 1):
         T.append(["epoch", epoch])
@@ -120,17 +137,31 @@ def train(gpu, args):
                 break
             sel = idx[batch_idx * args.batch_size:(batch_idx + 1) * args.batch_size]
             x, y = data.index_select(0, sel), targets.index_select(0, sel)
-            if exchange is not None:
-                exchange.zero_grad()
+            quirk = epoch % 40 == 0 and not args.no_lr_quirk
+            if args.graph and len(sel) == args.batch_size and not quirk:
+                # full batches replay one captured step on static buffers (the last, short batch
+                # and lr-quirk epochs run eagerly)
+                if graphed is None:
+                    static_x, static_y = x.clone(), y.clone()
+                    graphed = GraphedStep(lambda: _step(static_x, static_y), opt, dstep, warmup=1)
+                else:
+                    static_x.copy_(x)
+                    static_y.copy_(y)
+                    graphed()
+                loss = graphed.out
             else:
-                opt.zero_grad(set_to_none=True)
-            loss = crit(model(x), y)
-            if epoch % 40 == 0 and not args.no_lr_quirk:
-                opt.param_groups[0]["lr"] *= 0.1
-            loss.backward()
-            if exchange is not None:
-                exchange.finish()
-            opt.step()
+                if exchange is not None:
+                    exchange.zero_grad()
+                else:
+                    opt.zero_grad(set_to_none=True)
+                loss = crit(model(x), y)
+                if quirk:
+                    opt.param_groups[0]["lr"] *= 0.1
+                    graphed = None          # the captured step holds the old lr's Adam schedule
+                loss.backward()
+                if exchange is not None:
+                    exchange.finish()
+                opt.step()
             meter.update(time.time() - end)     # host time per batch, as utils.AverageMeter use
             end = time.time()
             if batch_idx % args.log_interval == 0:
@@ -153,6 +184,8 @@ def train(gpu, args):
             import pandas as pd
             pd.DataFrame(T).to_csv(f"{args.csv_prefix}_BATCH_TIME.csv")
             pd.DataFrame(E).to_csv(f"{args.csv_prefix}_EPOCH_TIME.csv")
+    if dstep is not None:
+        dstep.deactivate()
     if world > 1:
         dist.destroy_process_group()
     return model

@@ -135,3 +135,17 @@ def test_replays_are_distinct_steps(F):
         assert int(m.bn1.num_batches_tracked.item()) == 3       # warm-up + 2 replays
     finally:
         ds.deactivate()
+
+
+def test_trainer_graph_mode(F):
+    """bnn_amd.trainer --graph: full batches replay one captured step, the short last batch runs
+    eagerly; every batch is one optimizer step and the device counter tracks them."""
+    from bnn_amd import trainer
+    args = trainer.parse(["--model", "small", "--epochs", "2", "--dataset-size", "600", "--batch-size", "128",
+                          "--log-interval", "2", "--graph"])
+    m = trainer.train(0, args)
+    assert F._DEVICE_STEP is None                       # the trainer releases the seed counter
+    nb = -(-600 // 128)
+    for p in m.parameters():
+        assert torch.isfinite(p).all()
+    assert int(m.bn1.num_batches_tracked.item()) == 2 * nb
