@@ -45,6 +45,9 @@ MI355X_INT8_DENSE_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12   # 32x32x32 i8 MFMA: 204
 MI355X_FP4_DENSE_TOPS = 256 * 4 * 4096 * 2.4e9 / 1e12    # 32x32x64 f8f6f4 MFMA (FP4/FP6): 4096 ops/clk/SIMD
 MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
 MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
+# ternary XNOR-popcount on the VALU: 5 ops (and, xor, and, 2 x v_bcnt_u32 accumulate) per 32 MACs,
+# 4 SIMDs x 16 lanes per CU per clock (tools/xnor_probe.py)
+MI355X_XNOR_TOPS = 64 * 256 * 2.4e9 * (2 * 32 / 5) / 1e12
 MI355X_HBM_GBS = 8000.0
 PUBLISHED_SMALL_SPS = 60000 / 8.248   # MNIST_EPOCH_TIME(PersonalCom).csv:2-6 mean epoch, BASELINE.md §1
 
@@ -81,8 +84,8 @@ def op_peak(kernel):
         return "mfma", MI355X_FP4_DENSE_TOPS, "ternary GEMM ops 2*M*N*K on the FP4 MFMA"
     if kernel.startswith("gemm_fp6"):   # same f8f6f4 MFMA, FP6 x FP4 issues at the FP4 rate
         return "mfma", MI355X_FP4_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the FP6 x FP4 MFMA (4 digit planes)"
-    if kernel.startswith("gemm_xnor"):   # SURVEY §8(d): VALU popcount bound with the nonzero-mask plane
-        return "valu", 840.0, "ternary popcount ops 2*M*N*K"
+    if kernel.startswith("gemm_xnor"):   # VALU popcount bound with the nonzero-mask plane
+        return "valu", MI355X_XNOR_TOPS, "ternary popcount ops 2*M*N*K"
     return "mfma", MI355X_INT8_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the int8 MFMA"
 
 
