@@ -483,12 +483,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
   }
 }
 
+// colsum[n] = sum_r part[r][n]: FIN_COLS columns x FIN_GROUPS chunk groups per workgroup, the
+// groups folded in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void q6_colsum_final_k(const double* __restrict__ part, int64_t R, int64_t N,
                                                          float* __restrict__ out) {
-  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  __shared__ double sa[FIN_GROUPS][FIN_COLS];
+  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
+  const int64_t n = (int64_t)blockIdx.x * FIN_COLS + lc;
   double s = 0.0;
-  for (int64_t r = 0; r < R; ++r) s += part[r * N + n];
+  if (n < N)
+    for (int64_t r = grp; r < R; r += FIN_GROUPS) s += part[r * N + n];
+  sa[grp][lc] = s;
+  __syncthreads();
+  if (grp != 0 || n >= N) return;
+  s = 0.0;
+  for (int gI = 0; gI < FIN_GROUPS; ++gI) s += sa[gI][lc];
   out[n] = (float)s;
 }
 
@@ -935,7 +944,8 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
                      dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, k0,
                      k1, 1.f / (float)M, o, dp);
   if (colsum)
-    hipLaunchKernelGGL(q6_colsum_final_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, p0, R, C, colsum);
+    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + Q6T_ROWS - 1) / Q6T_ROWS, C,
+                       colsum);
   return check_launch("bnn_bn_bwd_q6");
 }
 

@@ -150,6 +150,7 @@ struct Gemm6Params {
   int64_t ldc;
   int M, N, K;
   int gm, gn;
+  int group;   // raster group rows (tile6_of)
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -180,11 +181,13 @@ __device__ __forceinline__ void barrier6() {
 }
 
 // Bijective XCD remap + grouped raster (as bnn_gemm.hip's tile_of).
-__device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int& tm, int& tn) {
+// G = tile rows per raster group: an XCD's ~32 co-resident workgroups then cover about G rows x
+// 32/G columns, re-reading each A panel (3.1 B/element) once per 32/G columns and each B panel
+// (0.5 B/element) once per G rows; 4 suits dX (K = 8192), 8 the long-K dW (tools/gpu_fp6_group.sh).
+__device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int G, int& tm, int& tn) {
   const int nwg = gm * gn;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  constexpr int G = 8;
   const int per_group = G * gn;
   const int g = L / per_group, first = g * G;
   const int gs = min(gm - first, G);
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   int tm, tn;
-  tile6_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  tile6_of(blockIdx.x, p.gm, p.gn, p.group, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int64_t nblk = p.K / QB;
   const int nk = p.K / 64;
@@ -647,7 +650,7 @@ BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
     return kErrInval;
   }
   if (M == 0 || N == 0) return 0;
-  Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0};
+  Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4};
   return pick6(M, N)->fn(p, S6(stream));
 }
 
