@@ -589,6 +589,287 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
   }
 }
 
+// ------------------------------------------------------------------ backward data on the bf16 MFMA (x3)
+// dX[ci][pix] = sum_k Wb[ci][k] * dY[k](pix) with k = (tap, co), co innermost: every fp32 dY value is
+// split EXACTLY into three bf16 terms (d1 = trunc_bf16(y), d2 = trunc_bf16(y - d1), d3 = y - d1 - d2,
+// 24 mantissa bits = 3 x 8), the ternary weights are exact in bf16, so the three
+// v_mfma_f32_16x16x32_bf16 passes multiply exactly and accumulate in fp32 (the fp32 reference's
+// numerics class) at 3 bf16 passes = 1.6x the fp32-MFMA rate per pass... and 8x the K per
+// instruction: K = 32 (8 channels of one tap per lane: one ds_read_b128 from a channels-innermost
+// halo image [OHp][OWp][Cop] per plane), where the f32 MFMA takes 4.
+//   16x16x32 bf16 lane map: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], D[4(l>>4)+r][l&15].
+typedef short bf8 __attribute__((ext_vector_type(8)));
+
+constexpr int B3_W = 8, B3_T = 64 * B3_W;   // 8 waves: two per SIMD, so LDS / MFMA latency overlaps
+
+struct B3Data {
+  int C, H, W, Co, Cop, KH, KW, OH, OW, pad, OHp, OWp, taps, Kp, ntile_pix;
+  int ps;    // halo pixel stride in bf16 elements: Cop + 8 (16-B aligned; 16 consecutive pixels'
+             // 16-B chunks land on 16 distinct 4-bank groups -- conflict-free ds_*_b128)
+  int ws;    // weight row stride: Kp + 8 (same reason for the A reads)
+};
+
+__device__ __forceinline__ void bf16x3_split(float y, unsigned short& d1, unsigned short& d2, unsigned short& d3) {
+  const uint32_t u = __float_as_uint(y);
+  const uint32_t h1 = u & 0xFFFF0000u;                 // truncation: y - d1 is exact in fp32
+  const float r1 = y - __uint_as_float(h1);
+  const uint32_t h2 = __float_as_uint(r1) & 0xFFFF0000u;
+  const float r2 = r1 - __uint_as_float(h2);           // <= 8 significant bits left: exact in bf16
+  d1 = (unsigned short)(h1 >> 16);
+  d2 = (unsigned short)(h2 >> 16);
+  d3 = (unsigned short)(__float_as_uint(r2) >> 16);
+}
+
+template <int NT, int MT>
+__global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restrict__ dy, const float* __restrict__ w,
+                                                            float* __restrict__ dx, int64_t N, B3Data g) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  unsigned short* wsb = reinterpret_cast<unsigned short*>(ldsf);          // [16 NT][ws] ternary bf16
+  unsigned short* img = wsb + 16 * NT * g.ws;                              // 3 x [OHp * OWp][ps]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int KK = g.KH * g.KW;
+  const int plane = g.OHp * g.OWp * g.ps;
+  const float inv_ws = 1.f / (float)g.ws, inv_cop = 1.f / (float)g.Cop, inv_kw = 1.f / (float)g.KW;
+  for (int i = t; i < 16 * NT * g.ws; i += B3_T) {
+    const int ci = fdivi(i, inv_ws), k = i - ci * g.ws;
+    const int tap = fdivi(k, inv_cop), co = k - tap * g.Cop;
+    int v = 0;
+    if (ci < g.C && k < g.Kp && tap < g.taps && co < g.Co) v = tsign(w[(co * g.C + ci) * KK + tap]);
+    wsb[i] = v > 0 ? 0x3F80 : (v < 0 ? 0xBF80 : 0);
+  }
+  for (int i = t; i < 3 * plane; i += B3_T) img[i] = 0;   // zero halo (interior rewritten per sample)
+  const int hT = g.KH - 1 - g.pad, wT = g.KW - 1 - g.pad;
+  const int HW = g.H * g.W, ohw = g.OH * g.OW;
+  int hb[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    int pix = (wv + B3_W * m) * 16 + (lane & 15);
+    if (pix >= HW) pix = 0;   // padded column: computed, never stored
+    const int ih = pix / g.W, iw = pix - ih * g.W;
+    hb[m] = ih * g.OWp + iw;
+  }
+  const int my_tiles = (g.ntile_pix - wv + B3_W - 1) / B3_W;
+  const int chunk = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  const float inv_ohw = 1.f / (float)ohw, inv_ow = 1.f / (float)g.OW;
+  const int nunit = (g.Cop / 8) * ohw;    // staging unit = 8 channels of one pixel
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();
+    const float* dn = dy + n * (int64_t)g.Co * ohw;
+    for (int u = t; u < nunit; u += B3_T) {
+      // lanes walk consecutive pixels of one 8-channel group: each of the 8 loads is coalesced,
+      // each plane's 16-B chunk one ds_write_b128
+      const int c8 = fdivi(u, inv_ohw), r = u - c8 * ohw;
+      const int oh = fdivi(r, inv_ow), ow = r - oh * g.OW;
+      bf8 v1, v2, v3;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int co = 8 * c8 + j;
+        const float y = co < g.Co ? dn[(int64_t)co * ohw + r] : 0.f;
+        unsigned short d1, d2, d3;
+        bf16x3_split(y, d1, d2, d3);
+        v1[j] = (short)d1;
+        v2[j] = (short)d2;
+        v3[j] = (short)d3;
+      }
+      const int o = ((oh + hT) * g.OWp + ow + wT) * g.ps + 8 * c8;
+      *reinterpret_cast<bf8*>(img + o) = v1;
+      *reinterpret_cast<bf8*>(img + plane + o) = v2;
+      *reinterpret_cast<bf8*>(img + 2 * plane + o) = v3;
+    }
+    __syncthreads();
+    mf4 acc[NT][MT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+      const int k = k0 + 8 * chunk;
+      const int tq = fdivi(k, inv_cop), co0 = k - tq * g.Cop;
+      const int tap = min(tq, g.taps - 1);                 // padded k: zero weights
+      const int kh = fdivi(tap, inv_kw), kw = tap - kh * g.KW;
+      const int hoff = (g.KH - 1 - kh) * g.OWp + (g.KW - 1 - kw);
+      bf8 av[NT];
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+        av[a] = *reinterpret_cast<const bf8*>(wsb + (a * 16 + (lane & 15)) * g.ws + k);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        bf8 bv[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          bv[m] = *reinterpret_cast<const bf8*>(img + j * plane + (hb[m] + hoff) * g.ps + co0);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int a = 0; a < NT; ++a)
+            acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[m], acc[a][m], 0, 0, 0);
+      }
+    }
+    float* xn = dx + n * (int64_t)g.C * HW;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m >= my_tiles) continue;
+      const int pix = (wv + B3_W * m) * 16 + (lane & 15);
+      if (pix >= HW) continue;
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ci = a * 16 + 4 * chunk + r;
+          if (ci < g.C) xn[(int64_t)ci * HW + pix] = acc[a][m][r];
+        }
+    }
+  }
+}
+
+// Backward filter on the bf16 MFMA (x3): dW[co][combo] = sum_{n,p} dY[n][co][p] * Xb[n][combo](p),
+// combo = (ci, kh, kw).  A = dY (the three exact bf16 terms, rows co, K = pixels), B = the ternary
+// input (exact in bf16; binarised, or any input that is exact in bf16 -- see b3_filt_geom).  K runs
+// over output pixels in rows padded to OWq = round_up(OW, 8), so a lane's 8 consecutive k are 8
+// pixels of one row: one ds_read_b128 from dY's plane, and one from the kw-shifted copy of the
+// input row (KW copies, so every tap's 8-pixel window starts 16-B aligned).  Each wave owns a set
+// of combo tiles for all co tiles (the A fragments are loaded once per k-step and reused).
+struct B3Filt {
+  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, OWq, Kp, Kd, xrow, Co16, NA, ncombo, ntn, WT, KS;
+};
+
+template <int NA, int MT>
+__global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __restrict__ dy,
+                                                              const float* __restrict__ x, int binarize,
+                                                              float* __restrict__ part, int64_t N, B3Filt g,
+                                                              int with_bias) {
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+  unsigned short* dyp = reinterpret_cast<unsigned short*>(ldsf);       // 3 x [Co16][Kd]
+  const int PL = g.Co16 * g.Kd;
+  unsigned short* xs = dyp + 3 * PL;                                    // KW x [C][Hp][xrow]
+  const int XL = g.C * g.Hp * g.xrow;
+  float* bpart = reinterpret_cast<float*>(xs + g.KW * XL);             // [Co16][Kp / 8]
+  __shared__ float sbias[64];
+  const float inv_kk = 1.f / (float)(g.KH * g.KW), inv_kw = 1.f / (float)g.KW, inv_owq = 1.f / (float)g.OWq;
+  const float inv_dq = 1.f / (float)(g.OH * (g.OWq / 8)), inv_nq = 1.f / (float)(g.OWq / 8);
+  const float inv_xq = 1.f / (float)(g.C * g.Hp * (g.OWq / 8)), inv_hq = 1.f / (float)(g.Hp * (g.OWq / 8));
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int grp = wv % g.WT, ks = wv / g.WT;
+  const int KK = g.KH * g.KW;
+  const int nq = g.OWq / 8, kq = g.Kp / 8;
+  if (t < 64) sbias[t] = 0.f;
+  for (int i = t; i < 3 * PL; i += B3_T) dyp[i] = 0;     // zero tails: co >= Co, k >= OH*OWq
+  for (int i = t; i < g.Co16 * kq; i += B3_T) bpart[i] = 0.f;
+  int boff[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int nt = min(grp + g.WT * m, g.ntn - 1);
+    int combo = nt * 16 + (lane & 15);
+    if (combo >= g.ncombo) combo = 0;   // padded column: computed, never stored
+    const int ci = fdivi(combo, inv_kk), kk = combo - ci * KK, kh = fdivi(kk, inv_kw), kw = kk - kh * g.KW;
+    boff[m] = ((kw * g.C + ci) * g.Hp + kh) * g.xrow;
+  }
+  const int my_tiles = (g.ntn - grp + g.WT - 1) / g.WT;
+  mf4 acc[NA][MT];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
+  const int kslice = g.Kp / g.KS, k_lo = ks * kslice, k_hi = k_lo + kslice;
+  const int chunk = lane >> 4;
+  const int ohw = g.OH * g.OW, hw = g.H * g.W;
+  const int ndu = g.Co16 * g.OH * nq;                    // dY staging units (8 pixels of a row)
+  const int nxu = g.KW * g.C * g.Hp * nq;                 // input staging units (8 of a shifted row)
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  for (int64_t n = n0; n < n1; ++n) {
+    __syncthreads();   // previous sample's fragment reads are done
+    const float* dn = dy + n * (int64_t)g.Co * ohw;
+    for (int u = t; u < ndu; u += B3_T) {
+      const int co = fdivi(u, inv_dq), r = u - co * (g.OH * nq), oh = fdivi(r, inv_nq), q = r - oh * nq;
+      bf8 v1, v2, v3;
+      float bsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ow = 8 * q + j;
+        const float y = (co < g.Co && ow < g.OW) ? dn[(int64_t)co * ohw + oh * g.OW + ow] : 0.f;
+        bsum += y;
+        unsigned short d1, d2, d3;
+        bf16x3_split(y, d1, d2, d3);
+        v1[j] = (short)d1;
+        v2[j] = (short)d2;
+        v3[j] = (short)d3;
+      }
+      const int o = co * g.Kd + oh * g.OWq + 8 * q;
+      *reinterpret_cast<bf8*>(dyp + o) = v1;
+      *reinterpret_cast<bf8*>(dyp + PL + o) = v2;
+      *reinterpret_cast<bf8*>(dyp + 2 * PL + o) = v3;
+      bpart[co * kq + oh * nq + q] = bsum;
+    }
+    const float* xn = x + n * (int64_t)g.C * hw;
+    for (int u = t; u < nxu; u += B3_T) {
+      const int kw = fdivi(u, inv_xq), r0 = u - kw * (g.C * g.Hp * nq);
+      const int c = fdivi(r0, inv_hq), r1 = r0 - c * (g.Hp * nq), ihh = fdivi(r1, inv_nq), q = r1 - ihh * nq;
+      const int ih = ihh - g.pad;
+      bf8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int iw = 8 * q + j + kw - g.pad;
+        float xv = 0.f;
+        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) xv = xn[(int64_t)c * hw + ih * g.W + iw];
+        if (binarize) xv = (float)tsign(xv);
+        v[j] = (short)(__float_as_uint(xv) >> 16);     // exact: +-1 / 0 (or a bf16-exact input)
+      }
+      *reinterpret_cast<bf8*>(xs + kw * XL + (c * g.Hp + ihh) * g.xrow + 8 * q) = v;
+    }
+    __syncthreads();
+    if (with_bias) {   // dB: wave w folds channels w, w+4, ... (fixed order: deterministic)
+      for (int co = wv; co < g.Co; co += B3_W) {
+        float sb = 0.f;
+        for (int i = lane; i < kq; i += 64) sb += bpart[co * kq + i];
+        const double tot = wave_sum((double)sb);
+        if (lane == 0) sbias[co] += (float)tot;
+      }
+    }
+    for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
+      const int kk = k0 + 8 * chunk;
+      const int ohq = fdivi(kk, inv_owq), ow0 = kk - ohq * g.OWq;
+      const int oh = min(ohq, g.OH - 1);                   // k tail: zero dY, any valid input row
+      bf8 av[NA][3];
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          av[a][j] = *reinterpret_cast<const bf8*>(dyp + j * PL + (16 * a + (lane & 15)) * g.Kd + kk);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const bf8 bv = *reinterpret_cast<const bf8*>(xs + boff[m] + oh * g.xrow + ow0);
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a][j], bv, acc[a][m], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t nelem = (int64_t)g.Co * g.ncombo + g.Co;
+  float* row = part + ((int64_t)blockIdx.x * g.KS + ks) * nelem;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m >= my_tiles) continue;
+    const int combo = (grp + g.WT * m) * 16 + (lane & 15);
+    if (combo >= g.ncombo) continue;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * a + 4 * chunk + r;
+        if (co < g.Co) row[(int64_t)co * g.ncombo + combo] = acc[a][m][r];
+      }
+  }
+  if (t < g.Co) {   // bias partial in k-slice 0's row, zero in the others
+    part[((int64_t)blockIdx.x * g.KS) * nelem + (int64_t)g.Co * g.ncombo + t] = with_bias ? sbias[t] : 0.f;
+    for (int q2 = 1; q2 < g.KS; ++q2)
+      part[((int64_t)blockIdx.x * g.KS + q2) * nelem + (int64_t)g.Co * g.ncombo + t] = 0.f;
+  }
+}
+
 // Backward filter: dW[co][combo] = sum_{n,p} dY[n][co][p] * Xs[n][combo][p], combo = (ci, kh, kw).
 // Tiles (co16, combo16) are dealt to WT wave groups; the remaining 4/WT factor splits the pixel
 // range (K), each (block, k-slice) writing one partial row for conv_filter_tile_reduce{1,2}_k.
@@ -843,6 +1124,54 @@ inline bool mf_data_geom(const ConvShape& s, MfData* g, int64_t* lds) {
   return *lds <= kMaxTileLds;
 }
 
+inline bool b3_data_geom(const ConvShape& s, B3Data* g, int64_t* lds) {
+  if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.pad <= s.KH - 1 && s.pad <= s.KW - 1 && s.C <= 32))
+    return false;
+  B3Data d;
+  d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
+  d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
+  d.Cop = (int)round_up(d.Co, 8);
+  d.OHp = d.OH + 2 * (d.KH - 1 - d.pad);
+  d.OWp = d.OW + 2 * (d.KW - 1 - d.pad);
+  d.taps = d.KH * d.KW;
+  d.Kp = (int)round_up((int64_t)d.taps * d.Cop, 32);
+  d.ntile_pix = (d.H * d.W + 15) / 16;
+  d.ps = d.Cop + 8;
+  d.ws = d.Kp + 8;
+  if ((d.ntile_pix + B3_W - 1) / B3_W > 16 || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
+  const int nt = d.C <= 16 ? 1 : 2;
+  *lds = (int64_t)16 * nt * d.ws * 2 + (int64_t)3 * d.OHp * d.OWp * d.ps * 2;
+  *g = d;
+  return *lds <= kMaxTileLds;
+}
+
+// bf16x3 filter kernel: the input must be exact in bf16 -- binarised (the BinCNN's layers both are)
+inline bool b3_filt_geom(const ConvShape& s, int binarize, B3Filt* g, int64_t* lds) {
+  if (!(binarize && s.groups == 1 && s.stride == 1 && s.dil == 1 && s.Co <= 64 && s.pad <= s.KH - 1 &&
+        s.pad <= s.KW - 1))
+    return false;
+  B3Filt d;
+  d.C = (int)s.C; d.H = (int)s.H; d.W = (int)s.W; d.Co = (int)s.Co; d.KH = (int)s.KH; d.KW = (int)s.KW;
+  d.OH = (int)s.OH; d.OW = (int)s.OW; d.pad = s.pad;
+  d.Hp = d.H + 2 * d.pad;
+  d.OWq = (int)round_up(d.OW, 8);
+  d.Co16 = (int)round_up(d.Co, 16);
+  d.NA = d.Co16 / 16;
+  d.ncombo = d.C * d.KH * d.KW;
+  d.ntn = (d.ncombo + 15) / 16;
+  d.WT = d.ntn >= 8 ? 8 : (d.ntn >= 4 ? 4 : (d.ntn >= 2 ? 2 : 1));
+  d.KS = B3_W / d.WT;
+  d.Kp = (int)round_up((int64_t)d.OH * d.OWq, 32 * d.KS);
+  d.Kd = d.Kp + 8;
+  d.xrow = d.OWq;
+  if ((d.ntn + d.WT - 1) / d.WT > 8) return false;
+  if ((int64_t)d.C * d.H * d.W >= (1 << 20) || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
+  // rows read: oh + kh < OH + KH - 1 <= Hp (stride 1, pad <= K-1)
+  *lds = (int64_t)3 * d.Co16 * d.Kd * 2 + (int64_t)d.KW * d.C * d.Hp * d.xrow * 2 + (int64_t)d.Co16 * (d.Kp / 8) * 4;
+  *g = d;
+  return *lds <= kMaxTileLds;
+}
+
 inline bool mf_filt_geom(const ConvShape& s, MfFilt* g, int64_t* lds) {
   if (!(s.groups == 1 && s.stride == 1 && s.dil == 1 && s.Co <= 64)) return false;
   MfFilt d;
@@ -882,12 +1211,13 @@ int64_t tile_filter_parts(const ConvShape& s) {
 
 using namespace bnn;
 
-// 1 (default): backward convolutions on the f32-MFMA implicit-GEMM kernels where the shape allows;
-// 0: the VALU LDS-tiled / generic kernels (kept as the cross-check in the parity tests).
+// 1 (default): backward data on the bf16x3 MFMA kernel, backward filter / forward on the f32-MFMA
+// and int8-MFMA implicit-GEMM kernels, where the shape allows; 2: the f32-MFMA backward data
+// kernel instead of bf16x3; 0: the VALU LDS-tiled / generic kernels (the parity tests' cross-checks).
 static int g_conv_mfma = 1;
 
-BNN_API int bnn_conv_set_mfma(int32_t on) {
-  g_conv_mfma = on != 0;
+BNN_API int bnn_conv_set_mfma(int32_t mode) {
+  g_conv_mfma = mode < 0 ? 1 : (mode > 2 ? 1 : mode);
   return 0;
 }
 
@@ -950,6 +1280,23 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   const int64_t total = N * C * H * W;
   if (total == 0) return 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  B3Data bd;
+  int64_t blds = 0;
+  if (g_conv_mfma == 1 && b3_data_geom(s, &bd, &blds)) {
+    const size_t lds = (size_t)blds;
+    const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
+    const int per_wave = (bd.ntile_pix + B3_W - 1) / B3_W;
+#define BNN_B3D(NT_, MT_) BNN_TILE_LAUNCH((conv_bwd_data_bf3_k<NT_, MT_>), grid, dim3(B3_T), lds, st, dy, w_latent, dx, N, bd)
+    if (bd.C <= 16) {
+      if (per_wave <= 1) BNN_B3D(1, 1); else if (per_wave <= 2) BNN_B3D(1, 2); else if (per_wave <= 4) BNN_B3D(1, 4);
+      else if (per_wave <= 8) BNN_B3D(1, 8); else BNN_B3D(1, 16);
+    } else {
+      if (per_wave <= 1) BNN_B3D(2, 1); else if (per_wave <= 2) BNN_B3D(2, 2); else if (per_wave <= 4) BNN_B3D(2, 4);
+      else if (per_wave <= 8) BNN_B3D(2, 8); else BNN_B3D(2, 16);
+    }
+#undef BNN_B3D
+    return check_launch("bnn_conv2d_bwd_data");
+  }
   MfData md;
   int64_t mlds = 0;
   if (g_conv_mfma && mf_data_geom(s, &md, &mlds)) {
@@ -996,7 +1343,7 @@ BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co
   const int64_t tnel = (int64_t)CO * ncombo + CO;
   const int64_t tiled = round_up(parts * tnel * (int64_t)sizeof(float), 256) +
                         filter_slices(parts) * tnel * (int64_t)sizeof(double);
-  const int64_t mparts = ((std::max<int64_t>(N, 1) + MF_IPB - 1) / MF_IPB) * 4;
+  const int64_t mparts = ((std::max<int64_t>(N, 1) + MF_IPB - 1) / MF_IPB) * B3_W;   // k-slices <= 8
   const int64_t mnel = Co * ncombo + Co;
   const int64_t mfma = round_up(mparts * mnel * (int64_t)sizeof(float), 256) +
                        filter_slices(mparts) * mnel * (int64_t)sizeof(double);
@@ -1016,6 +1363,31 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   const int64_t nw = Co * (C / groups) * KH * KW;
   const int64_t nelem = nw + Co;
   const int64_t nchunks = filter_chunks(std::max<int64_t>(N, 1), nelem);
+  B3Filt bf;
+  int64_t blds = 0;
+  if (N > 0 && g_conv_mfma == 1 && b3_filt_geom(s, binarize_input, &bf, &blds)) {
+    const int64_t nblk = (N + MF_IPB - 1) / MF_IPB;
+    const int64_t parts = nblk * bf.KS;
+    const int64_t nel = (int64_t)Co * bf.ncombo + Co;
+    float* part = reinterpret_cast<float*>(work);
+    const size_t lds = (size_t)blds;
+    const int per_wave = (bf.ntn + bf.WT - 1) / bf.WT;
+#define BNN_B3F(NA_, MT_) BNN_TILE_LAUNCH((conv_bwd_filter_bf3_k<NA_, MT_>), dim3((unsigned)nblk), dim3(B3_T), lds, st, dy, x, binarize_input, part, N, bf, db != nullptr)
+#define BNN_B3F_MT(NA_) \
+    if (per_wave <= 1) BNN_B3F(NA_, 1); else if (per_wave <= 2) BNN_B3F(NA_, 2); else if (per_wave <= 4) BNN_B3F(NA_, 4); \
+    else BNN_B3F(NA_, 8);
+    if (bf.NA == 1) { BNN_B3F_MT(1) } else if (bf.NA == 2) { BNN_B3F_MT(2) } else if (bf.NA == 3) { BNN_B3F_MT(3) } else { BNN_B3F_MT(4) }
+#undef BNN_B3F_MT
+#undef BNN_B3F
+    const int64_t nsl = filter_slices(parts);
+    double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                              round_up(parts * nel * (int64_t)sizeof(float), 256));
+    hipLaunchKernelGGL(conv_filter_tile_reduce1_k, dim3((unsigned)((nel + 255) / 256), (unsigned)nsl), dim3(256), 0,
+                       st, part, parts, nel, nsl, slice);
+    hipLaunchKernelGGL(conv_filter_tile_reduce2_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, slice,
+                       nsl, (int)Co, bf.ncombo, (int)Co, dw, db);
+    return check_launch("bnn_conv2d_bwd_filter");
+  }
   MfFilt mf;
   int64_t mlds = 0;
   if (N > 0 && g_conv_mfma && mf_filt_geom(s, &mf, &mlds)) {

@@ -203,10 +203,12 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
                           int32_t dil, int32_t groups, bnn_stream_t stream);
 
 /* Convolution engine switch: 1 (default) = MFMA implicit-GEMM kernels for stride-1 ungrouped
- * shapes -- backward on v_mfma_f32_16x16x4_f32 (exact f32 products), forward with a binarised
- * input and C % 16 == 0 on v_mfma_i32_16x16x64_i8 (exact integer sums); 0 = the VALU LDS-tiled /
- * generic kernels.  Process-global; for cross-checks and the kernel sweep. */
-int bnn_conv_set_mfma(int32_t on);
+ * shapes -- backward data on v_mfma_f32_16x16x32_bf16 with dY split exactly into three bf16
+ * terms (exact products, fp32 accumulation), backward filter on v_mfma_f32_16x16x4_f32 (exact f32
+ * products), forward with a binarised input and C % 16 == 0 on v_mfma_i32_16x16x64_i8 (exact
+ * integer sums); 2 = as 1 but backward data on the f32 MFMA; 0 = the VALU LDS-tiled / generic
+ * kernels.  Process-global; for cross-checks and the kernel sweep. */
+int bnn_conv_set_mfma(int32_t mode);
 
 /* ---------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
  * The layers between the binarized GEMMs in the reference Net (mnist-dist2.py:52-74):

@@ -255,8 +255,9 @@ def test_conv_tiled_and_generic_shapes_vs_oracle(F, shape):
     (2, 32, 6, 6, 64, 1, 0, True),
 ])
 def test_conv_backward_mfma_matches_valu(F, shape):
-    """The MFMA implicit-GEMM conv kernels (int8 forward, f32 backward) against the float64 oracle
-    and against the VALU kernels (bnn_conv_set_mfma(0)) on the same inputs."""
+    """The MFMA implicit-GEMM conv kernels (int8 forward; backward data on bf16x3 (mode 1) or f32
+    (mode 2), backward filter on f32) against the float64 oracle and against the VALU kernels
+    (bnn_conv_set_mfma(0)) on the same inputs."""
     from bnn_amd import _lib as L
     N, C, H, W, Co, K, pad, binarize = shape
     rng = np.random.default_rng(N + C + Co)
@@ -265,7 +266,7 @@ def test_conv_backward_mfma_matches_valu(F, shape):
     b = rng.standard_normal(Co).astype(np.float32)
     grads = []
     try:
-        for on in (1, 0):
+        for on in (1, 2, 0):
             L.call("bnn_conv_set_mfma", on)
             xt, wt, bt = dev(x).requires_grad_(True), dev(w).requires_grad_(True), dev(b).requires_grad_(True)
             y = F.binary_conv2d(xt, wt, bt, binarize, 1, pad, 1, 1)
@@ -276,7 +277,7 @@ def test_conv_backward_mfma_matches_valu(F, shape):
         L.call("bnn_conv_set_mfma", 1)
     _, xu = O.conv2d_forward(x, w, b, 1, pad, 1, 1)
     dx64, dw64, db64 = O.conv2d_backward(xu, w, dy, 1, pad, 1, 1)
-    assert np.array_equal(grads[0][3], grads[1][3])      # forward: int8-MFMA conv == VALU conv, bitwise
+    assert np.array_equal(grads[0][3], grads[2][3])      # forward: int8-MFMA conv == VALU conv, bitwise
     for g in grads:
         assert rel_err(g[0], dx64) < GRAD_TOL
         assert rel_err(g[1], dw64) < GRAD_TOL
