@@ -59,6 +59,10 @@ SIGNATURES = {
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
                             P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
+    "bnn_bn_head_workspace": (I64, [I64, I64, I32]),
+    "bnn_bn_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
+    "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P,
+                                 P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),

@@ -946,6 +946,87 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
                 None, None, None, None, None, None)
 
 
+HEAD_NOUT = 10
+
+
+class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
+    """fc4(hardtanh(bn3(drop(z)))) in training mode, fused (mnist-dist2.py:69-76): the BatchNorm
+    statistics pass, then ONE pass that forms h3 tile by tile and multiplies it into the head
+    (bnn_bn_head_fwd) -- h3 [M, C] is never written.  Backward (bnn_bn_head_bwd_q6): dh3 = dY4 . W4
+    is formed per element inside the BatchNorm passes, dW4 = dY4^T . h3 accumulated there, and dz
+    comes out with its FP6 digits for the upstream linear (the _Q6_ATTR hand-off)."""
+
+    @staticmethod
+    def forward(ctx, z, weight, bias, running_mean, running_var, momentum, eps, p, seed, w4, b4):
+        _check(z, weight, bias, running_mean, running_var, w4, b4)
+        ctx.q6 = _q6_wanted(z, z.shape[-1])
+        z = _c2d(z)
+        M, C = z.shape
+        gw = weight.detach() if weight is not None else None
+        gb = bias.detach() if bias is not None else None
+        ws = _bn_ws(M, C, z.device)
+        mean, invstd, mlo = _bn_stat_buffers(C, z.device)
+        with _timed("bn_dropout_fwd_stats", 0, 4 * M * C):
+            L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
+                   L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p), int(seed), L.ptr(ws), L.stream())
+        w4c = w4.detach().contiguous()
+        y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
+        with _timed("bn_head_fwd", 2.0 * M * C * HEAD_NOUT, 4 * M * C + 4 * M * HEAD_NOUT):
+            L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
+                   float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4.detach() if b4 is not None else None),
+                   L.ptr(y4), L.stream())
+        ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, w4c)
+        ctx.p, ctx.seed = p, seed
+        ctx.has_b4 = b4 is not None
+        return y4
+
+    @staticmethod
+    def backward(ctx, dy4):
+        z, gw, gb, mean, invstd, mlo, w4c = ctx.saved_tensors
+        dy4 = _c2d(dy4)
+        M, C = z.shape
+        dev = z.device
+        dx = torch.empty_like(z)
+        dgw = torch.empty((C,), dtype=torch.float32, device=dev) if gw is not None else None
+        dgb = torch.empty((C,), dtype=torch.float32, device=dev) if gb is not None else None
+        dw4 = torch.empty((HEAD_NOUT, C), dtype=torch.float32, device=dev)
+        rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
+        Mp = round_up(M)
+        cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
+        cs = torch.empty((C,), dtype=torch.float32, device=dev)
+        ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, HEAD_NOUT),), dtype=torch.uint8, device=dev)
+        with _timed("bn_head_bwd_q6", 2.0 * 2 * M * C * HEAD_NOUT, 16 * M * C + 4 * M * C + 6 * M * C):
+            L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw), L.ptr(gb),
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dgw),
+                   L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo),
+                   L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
+        if ctx.q6:
+            setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
+        db4 = dy4.sum(0) if ctx.has_b4 and ctx.needs_input_grad[10] else None
+        return (dx, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, dw4 if ctx.needs_input_grad[9] else None, db4)
+
+
+def head_fusable(x, bn, fc):
+    """drop -> bn -> htanh -> fc as one libbnn head (DropoutBNHardtanhLinearFunction): training-mode
+    BatchNorm1d with batch statistics, a Linear(C, 10), C % 256 == 0."""
+    return (x.is_cuda and x.dim() == 2 and x.shape[1] % 256 == 0 and x.shape[0] > 0 and bn.training
+            and bn.track_running_stats and isinstance(fc, torch.nn.Linear) and fc.out_features == HEAD_NOUT
+            and fc.in_features == x.shape[1] and bn.momentum is not None)
+
+
+def dropout_bn_hardtanh_linear(x, p, bn, fc, seed=None):
+    """fc(hardtanh(bn(nn.Dropout(p)(x)))) through libbnn (training mode; see head_fusable)."""
+    if seed is None:
+        seed = _DEVICE_STEP.base_seed if _DEVICE_STEP is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+    rm, rv, bn_training, factor = _bn_module_args(bn)
+    if not bn_training:
+        raise ValueError("dropout_bn_hardtanh_linear is the training-mode fusion")
+    return DropoutBNHardtanhLinearFunction.apply(x, bn.weight, bn.bias, rm, rv, factor, bn.eps, float(p), seed,
+                                                 fc.weight, fc.bias)
+
+
 def dropout_mask(n, p, seed, device="cuda"):
     """The keep mask (scaled: 1/(1-p) or 0) the fused dropout passes use for elements 0..n-1."""
     out = torch.empty((n,), dtype=torch.float32, device=device)

@@ -37,6 +37,7 @@ class MLP(nn.Module):
         # fused_bn: bn_i -> htanh_i run as one libbnn BatchNorm+Hardtanh pass (same parameters,
         # buffers and math; replaces torch's BatchNorm1d kernels)
         self.fused_bn = fused_bn
+        self.fused_head = True     # with fused_bn: drop -> bn3 -> htanh3 -> fc4 as one libbnn op
         self.fc1 = BinarizeLinear(784, h1)
         self.htanh1 = nn.Hardtanh()
         self.bn1 = nn.BatchNorm1d(h1)
@@ -70,6 +71,10 @@ class MLP(nn.Module):
         x = x.view(-1, 28 * 28)
         x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, self.fc1(x))
         x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x)
+        if (self.fused_bn and self.fused_head and self.training and self.bn3.training
+                and BF.head_fusable(x, self.bn3, self.fc4)):
+            # drop -> bn3 -> htanh3 -> fc4 as one libbnn head: h3 is never written
+            return self.logsoftmax(BF.dropout_bn_hardtanh_linear(x, self.drop.p, self.bn3, self.fc4))
         if (self.fused_bn and self.training and self.drop.p > 0 and self.bn3.training and x.is_cuda
                 and x.dim() == 2 and x.shape[1] % 4 == 0):
             # drop -> bn3 -> htanh3 as one libbnn op (mask regenerated in every pass, never stored)

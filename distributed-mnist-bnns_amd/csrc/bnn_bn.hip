@@ -66,19 +66,41 @@ __device__ __forceinline__ Drop drop_resolve(Drop d) {
   return d;
 }
 
+// 32-bit arithmetic only (two murmur3 fmix32 rounds keyed by the 64-bit seed): the element index
+// is taken mod 2^32, the mask of every pass over the same tensor is the same function of it.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
 __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
-  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;   // splitmix64 finaliser
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
+  const uint32_t h = fmix32((uint32_t)i * 0x9E3779B1u ^ (uint32_t)seed);
+  return fmix32(h ^ (uint32_t)(seed >> 32));
 }
 
 __device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
 
-__device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4]) {
+// keep bits of elements i0 .. i0+3 (bit j), evaluated once and applied to both the input and the
+// gradient where a pass needs both
+__device__ __forceinline__ uint32_t drop_bits4(const Drop& d, uint64_t i0) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m |= (uint32_t)drop_keep(d, i0 + j) << j;
+  return m;
+}
+
+__device__ __forceinline__ void drop4m(const Drop& d, uint32_t m, float (&v)[4]) {
   if (!d.on) return;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = drop_keep(d, i0 + j) ? v[j] * d.scale : 0.f;
+  for (int j = 0; j < 4; ++j) v[j] = ((m >> j) & 1u) ? v[j] * d.scale : 0.f;
+}
+
+__device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4]) {
+  if (!d.on) return;
+  drop4m(d, drop_bits4(d, i0), v);
 }
 
 inline Drop make_drop(float p, uint64_t seed) {
@@ -364,7 +386,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
     const float4 xv = ld4(x + r * C + c), gv = ld4(dy + r * C + c);
     float xs[4] = {xv.x, xv.y, xv.z, xv.w};
     const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
-    drop4(dp, (uint64_t)(r * C + c), xs);
+    const uint32_t km = dp.on ? drop_bits4(dp, (uint64_t)(r * C + c)) : 0u;
+    drop4m(dp, km, xs);
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -373,7 +396,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
       const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
       o[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
     }
-    drop4(dp, (uint64_t)(r * C + c), o);   // dropout backward: grad * mask * scale
+    drop4m(dp, km, o);   // dropout backward: grad * mask * scale
     *reinterpret_cast<float4*>(dx + r * C + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
@@ -391,6 +414,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
 constexpr int Q6T_ROWS = 256, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
 
+// The fused head's upstream gradient for 4 columns: g[j] = sum_q dY4[q] * W4[q][c + j] (fp32, q in
+// order -- the same rounding in the statistics pass and the apply pass).
+template <int NOUT>
+__device__ __forceinline__ void head_grad4(const float* __restrict__ d4, const float (&wc)[NOUT > 0 ? NOUT : 1][4],
+                                           float (&g)[4]) {
+  float dq[NOUT];
+#pragma unroll
+  for (int q = 0; q < NOUT; ++q) dq[q] = d4[q];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NOUT; ++q) s = fmaf(dq[q], wc[q][j], s);
+    g[j] = s;
+  }
+}
+
 struct Q6Out {
   float* dx;                       // [M][C] or null
   uint8_t *rlo, *rhi, *rsc;        // rows of dz: [M][C/32][64], [M][C/32][32], [C/64][rsc_rows][2]
@@ -400,6 +440,9 @@ struct Q6Out {
   double* part;                    // [M/256 chunks][C] partial column sums, or null
 };
 
+// NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
+// and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
+template <int NOUT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
@@ -408,7 +451,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
                                                          const float* __restrict__ beta, int hardtanh,
                                                          const float* __restrict__ sg,
                                                          const float* __restrict__ sgx, float inv_n, Q6Out o,
-                                                         Drop dp0) {
+                                                         Drop dp0, const float* __restrict__ w4 = nullptr) {
   const Drop dp = drop_resolve(dp0);
   __shared__ __attribute__((aligned(16))) float tile[Q6T_SUB * Q6T_LD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -425,21 +468,60 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
   const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
   const float a0[4] = {s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n};
   const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
+  float wc[NOUT > 0 ? NOUT : 1][4];       // the head's weight columns c..c+3
+  if constexpr (NOUT > 0) {
+#pragma unroll
+    for (int q = 0; q < NOUT; ++q) {
+      const float4 f = ld4(w4 + q * C + c);
+      wc[q][0] = f.x, wc[q][1] = f.y, wc[q][2] = f.z, wc[q][3] = f.w;
+    }
+  }
   double csum = 0.0;                      // waves 2-3: column lane, rows of block wave-2 of each sub-tile
   const int64_t mp = o.nblk_m * QB;
+  constexpr int D4LD = NOUT > 0 ? (NOUT + 3) / 4 * 4 : 4;
+  __shared__ __attribute__((aligned(16))) float d4s[NOUT > 0 ? Q6T_SUB * D4LD : 4];
+  // software pipeline: sub-tile s+1's x (and dY) rows are loaded into registers before sub-tile s
+  // is quantised, so their HBM latency hides behind the quantiser's VALU work
+  constexpr int NI = Q6T_SUB / 16;
+  float4 xr[NI], gr[NOUT > 0 ? 1 : NI];
+  auto load_sub = [&](int64_t m0n) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int64_t r = m0n + (t >> 4) + 16 * i;
+      if (m0n < mp && r < M) {
+        xr[i] = ld4(x + r * C + c);
+        if constexpr (NOUT == 0) gr[i] = ld4(dy + r * C + c);
+      }
+    }
+  };
+  load_sub(mbase);
   for (int sub = 0; sub < Q6T_ROWS / Q6T_SUB; ++sub) {
     const int64_t m0 = mbase + sub * Q6T_SUB;
     if (m0 >= mp) break;                       // block-uniform
+    if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows
+      for (int i = t; i < Q6T_SUB * D4LD; i += 256) {
+        const int rr = i / D4LD, q = i - rr * D4LD;
+        d4s[i] = (m0 + rr < M && q < NOUT) ? dy[(m0 + rr) * NOUT + q] : 0.f;
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int i = 0; i < Q6T_SUB / 16; ++i) {
       const int rr = (t >> 4) + 16 * i;
       const int64_t r = m0 + rr;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
-        const float4 xv = ld4(x + r * C + c), gv = ld4(dy + r * C + c);
+        const float4 xv = xr[i];
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-        const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
-        drop4(dp, (uint64_t)(r * C + c), xs);
+        float gs[4];
+        if constexpr (NOUT > 0) {
+          head_grad4<NOUT>(d4s + rr * D4LD, wc, gs);
+        } else {
+          const float4 gv = gr[i];
+          gs[0] = gv.x, gs[1] = gv.y, gs[2] = gv.z, gs[3] = gv.w;
+        }
+        const uint32_t km = dp.on ? drop_bits4(dp, (uint64_t)(r * C + c)) : 0u;
+        drop4m(dp, km, xs);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float xh = ((xs[j] - ms[j]) - lo[j]) * is[j];
@@ -447,12 +529,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
           const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
           v[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
         }
-        drop4(dp, (uint64_t)(r * C + c), v);
+        drop4m(dp, km, v);
         if (o.dx) *reinterpret_cast<float4*>(o.dx + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
       }
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
     }
     __syncthreads();
+    load_sub(m0 + Q6T_SUB);
     if (wave < 2) {
       // row block (row m0 + lane, columns c0 + 32 wave ..)
       const int rr = lane, b = wave;
@@ -485,6 +568,169 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
 
 // colsum[n] = sum_r part[r][n]: FIN_COLS columns x FIN_GROUPS chunk groups per workgroup, the
 // groups folded in a fixed order (deterministic)
+// ------------------------------------------------------------------ fused head: [drop ->] bn -> htanh -> Linear
+// mnist-dist2.py:69-76: fc3 -> drop -> bn3 -> htanh3 -> fc4 (nn.Linear(C, 10)).  The fp32 hardtanh
+// output h3 [M][C] is never written: the forward forms h3 tile by tile from z and multiplies it
+// into the head on the f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation,
+// the numerics class of the reference's F.linear); the backward forms dh3 = dY4 . W4 per element
+// inside the BatchNorm passes and accumulates dW4 = dY4^T . h3 there (h3 recomputed from z).
+constexpr int HD_ROWS = 64, HD_COLS = 64, HD_LD = HD_COLS + 4;
+
+typedef float hf4 __attribute__((ext_vector_type(4)));
+
+template <int NOUT>
+__global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x, int64_t M, int64_t C,
+                                                     const float* __restrict__ mean, const float* __restrict__ mean_lo,
+                                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, const float* __restrict__ w4,
+                                                     const float* __restrict__ b4, float* __restrict__ y4, Drop dp0) {
+  static_assert(NOUT <= 16, "one 16-column MFMA tile");
+  __shared__ __attribute__((aligned(16))) float ht[HD_ROWS * HD_LD];
+  __shared__ float ws[16 * HD_COLS];
+  const Drop dp = drop_resolve(dp0);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * HD_ROWS;
+  const int cq = 4 * (t & 15);
+  hf4 acc = hf4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t c0 = 0; c0 < C; c0 += HD_COLS) {
+    const int64_t c = c0 + cq;
+    const float4 mv = ld4(mean + c), iv = ld4(invstd + c), lv = ld4_or(mean_lo, c, 0.f);
+    const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
+    const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+    const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+    const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
+    __syncthreads();   // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < HD_ROWS / 16; ++i) {
+      const int rr = (t >> 4) + 16 * i;
+      const int64_t r = r0 + rr;
+      float h[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < M) {
+        const float4 xv = ld4(x + r * C + c);
+        float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        drop4(dp, (uint64_t)(r * C + c), xs);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          h[j] = fminf(fmaxf(fmaf(((xs[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]), -1.f), 1.f);
+      }
+      *reinterpret_cast<float4*>(ht + rr * HD_LD + cq) = make_float4(h[0], h[1], h[2], h[3]);
+    }
+    for (int i = t; i < 16 * HD_COLS; i += 256) {
+      const int q = i / HD_COLS, k = i - q * HD_COLS;
+      ws[i] = q < NOUT ? w4[q * C + c0 + k] : 0.f;
+    }
+    __syncthreads();
+    // wave wv: rows 16 wv .. +15 of the tile; A = h3 rows, B = W4^T (16 x 16 of which NOUT real)
+#pragma unroll
+    for (int k0 = 0; k0 < HD_COLS; k0 += 4) {
+      const float a = ht[(16 * wv + (lane & 15)) * HD_LD + k0 + (lane >> 4)];
+      const float b = ws[(lane & 15) * HD_COLS + k0 + (lane >> 4)];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+  }
+  const int col = lane & 15;
+  if (col < NOUT) {
+    const float bias = b4 ? b4[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t r = r0 + 16 * wv + 4 * (lane >> 4) + i;
+      if (r < M) y4[r * NOUT + col] = acc[i] + bias;
+    }
+  }
+}
+
+// Statistics pass of the head's BatchNorm backward (bn_reduce_k MODE 1 with g = dY4 . W4 formed per
+// element) plus the head's weight gradient partials dW4[q][c] over the chunk's rows (fp32 per chunk).
+template <int NOUT>
+__global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict__ x, const float* __restrict__ d4,
+                                                        const float* __restrict__ w4, int64_t M, int64_t C,
+                                                        const float* __restrict__ mean, const float* __restrict__ mean_lo,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        double* __restrict__ p0, double* __restrict__ p1,
+                                                        float* __restrict__ pw, int64_t chunk_rows, Drop dp0) {
+  const Drop dp = drop_resolve(dp0);
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t C4 = C / 4;
+  const int64_t chunk = id / C4;
+  const int64_t c = (id - chunk * C4) * 4;
+  const int64_t r0 = chunk * chunk_rows;
+  if (r0 >= M) return;
+  const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
+  float mu[4], lo[4], is[4], ga[4], be[4];
+  float wc[NOUT][4], aw[NOUT][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mu[j] = mean[c + j];
+    lo[j] = mean_lo ? mean_lo[c + j] : 0.f;
+    is[j] = invstd[c + j];
+    ga[j] = gamma ? gamma[c + j] : 1.f;
+    be[j] = beta ? beta[c + j] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NOUT; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wc[q][j] = w4[q * C + c + j];
+      aw[q][j] = 0.f;
+    }
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; r += 16) {
+    float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
+    const int64_t re = (r + 16 < r1) ? r + 16 : r1;
+    for (int64_t rr = r; rr < re; ++rr) {
+      const float4 xv = ld4(x + rr * C + c);
+      float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      drop4(dp, (uint64_t)(rr * C + c), xs);
+      // C % 256 == 0 (host check): a wave's 64 column groups share the chunk, so the row is
+      // wave-uniform and dY4's row comes in through scalar loads
+      const int64_t ru = (int64_t)__builtin_amdgcn_readfirstlane((int)rr);
+      float dq[NOUT];
+#pragma unroll
+      for (int q = 0; q < NOUT; ++q) dq[q] = d4[ru * NOUT + q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float gsum = 0.f;
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) gsum = fmaf(dq[q], wc[q][j], gsum);   // head_grad4's order
+        const float xh = ((xs[j] - mu[j]) - lo[j]) * is[j];
+        const float y = fmaf(xh, ga[j], be[j]);
+        const bool in = y > -1.f && y < 1.f;
+        const float g = in ? gsum : 0.f;
+        fa[j] += g;
+        fb[j] = fmaf(g, xh, fb[j]);
+        const float h = fminf(fmaxf(y, -1.f), 1.f);     // the forward's h3
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) aw[q][j] = fmaf(dq[q], h, aw[q][j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] += (double)fa[j];
+      b[j] += (double)fb[j];
+    }
+  }
+  const int64_t o = chunk * C + c;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p0[o + j] = a[j];
+    p1[o + j] = b[j];
+  }
+#pragma unroll
+  for (int q = 0; q < NOUT; ++q)
+    *reinterpret_cast<float4*>(pw + (chunk * NOUT + q) * C + c) = make_float4(aw[q][0], aw[q][1], aw[q][2], aw[q][3]);
+}
+
+// dW4[q][c] = sum over chunks of the partials, in chunk order (double)
+__global__ __launch_bounds__(256) void head_dw_final_k(const float* __restrict__ pw, int64_t R, int64_t nq, int64_t C,
+                                                       float* __restrict__ dw4) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nq * C) return;
+  double s = 0.0;
+  for (int64_t r = 0; r < R; ++r) s += (double)pw[r * nq * C + e];
+  dw4[e] = (float)s;
+}
+
 __global__ __launch_bounds__(256) void q6_colsum_final_k(const double* __restrict__ part, int64_t R, int64_t N,
                                                          float* __restrict__ out) {
   __shared__ double sa[FIN_GROUPS][FIN_COLS];
@@ -940,13 +1186,73 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
-  hipLaunchKernelGGL(bn_bwd_apply_q6_k, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
+  hipLaunchKernelGGL(bn_bwd_apply_q6_k<0>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
                      dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, k0,
                      k1, 1.f / (float)M, o, dp);
   if (colsum)
     hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + Q6T_ROWS - 1) / Q6T_ROWS, C,
                        colsum);
   return check_launch("bnn_bn_bwd_q6");
+}
+
+constexpr int HEAD_NOUT = 10;   // the reference head: nn.Linear(C, 10) (mnist-dist2.py:73)
+
+BNN_API int64_t bnn_bn_head_workspace(int64_t M, int64_t C, int32_t nout) {
+  return bnn_bn_workspace(M, C) + round_up(bn_chunks(M, C) * (int64_t)nout * C * (int64_t)sizeof(float), 256);
+}
+
+BNN_API int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+                            const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
+                            const float* w4, int32_t nout, const float* b4, float* y4, void* stream) {
+  if (!bn_args_ok(x, M, C) || C % HD_COLS != 0 || !mean || !invstd || !w4 || !y4 || nout != HEAD_NOUT ||
+      !aligned16(mean) || !aligned16(invstd) || !vec_ok(mean_lo) || !vec_ok(gamma) || !vec_ok(beta) ||
+      !(p >= 0.f && p < 1.f)) {
+    set_error("bnn_bn_head_fwd: bad arguments (M=%lld C=%lld nout=%d; C %% 64 == 0, nout == 10)", (long long)M,
+              (long long)C, nout);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL(bn_head_fwd_k<HEAD_NOUT>, dim3((unsigned)((M + HD_ROWS - 1) / HD_ROWS)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, M, C, mean, mean_lo, invstd, gamma, beta, w4, b4, y4,
+                     make_drop(p, seed));
+  return check_launch("bnn_bn_head_fwd");
+}
+
+BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
+                               const float* gamma, const float* beta, const float* save_mean,
+                               const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
+                               float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
+                               uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                               void* stream) {
+  if (!bn_args_ok(x, M, C) || C % 256 != 0 || !dy4 || !w4 || !dw4 || nout != HEAD_NOUT || !save_mean ||
+      !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
+      !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !aligned16(w4) || !rlo || !rhi || !rsc || !clo ||
+      !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) ||
+      !(p >= 0.f && p < 1.f) || (M + Q6T_ROWS - 1) / Q6T_ROWS > 65535) {
+    set_error("bnn_bn_head_bwd_q6: bad arguments (M=%lld C=%lld nout=%d)", (long long)M, (long long)C, nout);
+    return kErrInval;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Drop dp = make_drop(p, seed);
+  const int64_t R = bn_chunks(M, C);
+  double* p0 = reinterpret_cast<double*>(work);
+  double* p1 = p0 + R * C;
+  float* k0 = reinterpret_cast<float*>(p1 + R * C);
+  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
+  float* pw = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + bnn_bn_workspace(M, C));
+  hipLaunchKernelGGL(bn_head_reduce_k<HEAD_NOUT>, reduce_grid(M, C), dim3(256), 0, s, x, dy4, w4, M, C, save_mean,
+                     save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + 255) / 256)), dim3(256), 0, s, pw, R,
+                     (int64_t)nout, C, dw4);
+  const int64_t mp = round_up(M, 64);
+  Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
+  hipLaunchKernelGGL(bn_bwd_apply_q6_k<HEAD_NOUT>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
+                     dim3(256), 0, s, x, dy4, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, 1, k0, k1,
+                     1.f / (float)M, o, dp, w4);
+  if (colsum)
+    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + Q6T_ROWS - 1) / Q6T_ROWS, C,
+                       colsum);
+  return check_launch("bnn_bn_head_bwd_q6");
 }
 
 BNN_API int bnn_set_seed_counter(const int64_t* ctr) {

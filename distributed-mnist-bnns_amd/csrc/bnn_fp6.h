@@ -44,6 +44,21 @@ __device__ __forceinline__ void digits4(float x, int shift, int (&d)[4]) {
   d[3] = v;
 }
 
+// The four plane codes of rint(x * 2^shift) (|.| <= 2^19) without the digit arithmetic: with
+// w = v + 16 * (1 + 32 + 1024 + 32768) >= 0, the balanced digits are d_j = e_j - 16 for the plain
+// base-32 digits e_j of w (e_3 = w >> 15 unmasked, <= 32), and the e2m3 code of d = e - 16 is
+// e - 16 for e >= 16, else 32 | (16 - e) = 48 - e.  Bit-identical to digits4 + e2m3_code.
+constexpr int DIGIT_BIAS = 16 * (1 + 32 + 1024 + 32768);
+
+__device__ __forceinline__ void codes4(float x, int shift, uint32_t (&c)[4]) {
+  const uint32_t w = (uint32_t)(__float2int_rn(ldexpf(x, shift)) + DIGIT_BIAS);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t e = j < 3 ? __builtin_amdgcn_ubfe(w, 5 * j, 5) : (w >> 15);
+    c[j] = e >= 16u ? e - 16u : 48u - e;
+  }
+}
+
 __device__ __forceinline__ float absmax_nan(float amax, float x) {
   const float a = fabsf(x);
   return (a == a) ? fmaxf(amax, a) : __builtin_inff();
@@ -67,10 +82,10 @@ __device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bo
   uint32_t chunk[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    int d[4];
-    digits4(v[i], shift, d);
+    uint32_t cd[4];
+    codes4(v[i], shift, cd);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) chunk[j] |= e2m3_code(d[j]) << (6 * i);
+    for (int j = 0; j < 4; ++j) chunk[j] |= cd[j] << (6 * i);
   }
   // lane j of the group assembles plane j: chunk of lane p sits at bits 24p..24p+23
   const int plane = q & 3;
@@ -121,12 +136,12 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
     for (int i = 0; i < QB / 2; ++i) v[i] = src[(16 * h + i) * STRIDE];
 #pragma unroll
     for (int i = 0; i < QB / 2; ++i) {
-      int d[4];
-      digits4(v[i], shift, d);
+      uint32_t cd[4];
+      codes4(v[i], shift, cd);
       const int bit = 6 * (16 * h + i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t c = e2m3_code(d[j]);
+        const uint32_t c = cd[j];
         w[j][bit >> 5] |= c << (bit & 31);
         if ((bit & 31) > 26) w[j][(bit >> 5) + 1] |= c >> (32 - (bit & 31));
       }

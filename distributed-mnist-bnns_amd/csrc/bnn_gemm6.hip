@@ -100,12 +100,12 @@ __global__ __launch_bounds__(512) void quant6_cols_t_k(const float* __restrict__
       for (int i = 0; i < 6; ++i) w[j][i] = 0;
 #pragma unroll
     for (int i = 0; i < QB; ++i) {
-      int d[4];
-      digits4(v[i], shift, d);
+      uint32_t cd[4];
+      codes4(v[i], shift, cd);
       const int bit = 6 * i;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t c = e2m3_code(d[j]);
+        const uint32_t c = cd[j];
         w[j][bit >> 5] |= c << (bit & 31);
         if ((bit & 31) > 26) w[j][(bit >> 5) + 1] |= c >> (32 - (bit & 31));
       }

@@ -298,6 +298,26 @@ int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const f
                   bnn_stream_t stream);
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
 
+/* The network's head fused with its BatchNorm (mnist-dist2.py:69-76: fc3 -> drop -> bn3 -> htanh3
+ * -> fc4 = nn.Linear(C, nout)), training mode, nout == 10, C % 256 == 0: the fp32 hardtanh
+ * output h3 is never written.
+ * bnn_bn_head_fwd: y4[m][q] = sum_c h3[m][c] W4[q][c] + b4[q] with h3 = clamp(BN(drop(x)), -1, 1)
+ *   formed from x with the statistics of bnn_bn_dropout_fwd_train (y = NULL: statistics only);
+ *   products exact in f32, f32 accumulation (v_mfma_f32_16x16x4_f32).
+ * bnn_bn_head_bwd_q6: given dY4 [M][nout], the BatchNorm(+dropout) backward with the incoming
+ *   gradient dh3 = dY4 . W4 formed per element, as bnn_bn_bwd_q6 (dx optional, both FP6 digit
+ *   forms of dx, colsum of dx), plus dW4 = dY4^T . h3 [nout][C] (h3 recomputed from x).
+ *   work: bnn_bn_head_workspace(M, C, nout) bytes.  The head's bias gradient is sum_m dY4. */
+int64_t bnn_bn_head_workspace(int64_t M, int64_t C, int32_t nout);
+int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+                    const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
+                    const float* w4, int32_t nout, const float* b4, float* y4, bnn_stream_t stream);
+int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
+                       const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                       const float* save_mean_lo, float p, uint64_t seed, float* dx, float* dgamma, float* dbeta,
+                       float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi,
+                       uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
+
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
  * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = ((x-mean)-mean_lo)*invstd*gamma+beta exactly as
  * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0
