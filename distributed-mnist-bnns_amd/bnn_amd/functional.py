@@ -972,7 +972,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
                    L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p), int(seed), L.ptr(ws), L.stream())
         w4c = w4.detach().contiguous()
         y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
-        with _timed("bn_head_fwd", 2.0 * M * C * HEAD_NOUT, 4 * M * C + 4 * M * HEAD_NOUT):
+        with _timed("bn_head_fwd", 0, 4 * M * C + 4 * M * HEAD_NOUT):
             L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
                    float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4.detach() if b4 is not None else None),
                    L.ptr(y4), L.stream())
@@ -996,7 +996,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
         cs = torch.empty((C,), dtype=torch.float32, device=dev)
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, HEAD_NOUT),), dtype=torch.uint8, device=dev)
-        with _timed("bn_head_bwd_q6", 2.0 * 2 * M * C * HEAD_NOUT, 16 * M * C + 4 * M * C + 6 * M * C):
+        with _timed("bn_head_bwd_q6", 0, 16 * M * C + 4 * M * C + 6 * M * C):
             L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw), L.ptr(gb),
                    L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dgw),
                    L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo),

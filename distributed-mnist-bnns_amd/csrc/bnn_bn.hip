@@ -414,6 +414,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
 constexpr int Q6T_ROWS = 256, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
 
+// Rows per workgroup of the fused apply: 256, or 64 when that leaves fewer than 1024 workgroups
+// (small batches); never fewer rows than a statistics chunk (the column-sum partials reuse the
+// statistics workspace, one row per workgroup row).
+inline int64_t q6_rows(int64_t M, int64_t C) {
+  if ((C / Q6T_COLS) * ((M + Q6T_ROWS - 1) / Q6T_ROWS) >= 1024) return Q6T_ROWS;
+  return bn_chunk_rows(M, C) <= Q6T_SUB ? Q6T_SUB : Q6T_ROWS;
+}
+
 // The fused head's upstream gradient for 4 columns: g[j] = sum_q dY4[q] * W4[q][c + j] (fp32, q in
 // order -- the same rounding in the statistics pass and the apply pass).
 template <int NOUT>
@@ -451,12 +459,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
                                                          const float* __restrict__ beta, int hardtanh,
                                                          const float* __restrict__ sg,
                                                          const float* __restrict__ sgx, float inv_n, Q6Out o,
-                                                         Drop dp0, const float* __restrict__ w4 = nullptr) {
+                                                         Drop dp0, const float* __restrict__ w4, int rows_wg) {
   const Drop dp = drop_resolve(dp0);
   __shared__ __attribute__((aligned(16))) float tile[Q6T_SUB * Q6T_LD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * Q6T_COLS;
-  const int64_t mbase = (int64_t)blockIdx.y * Q6T_ROWS;
+  const int64_t mbase = (int64_t)blockIdx.y * rows_wg;
   const int64_t nblk_c = C / QB;
   // elementwise mapping: float4 f = t + 256 i of a 64 x 64 sub-tile: row f / 16, columns 4 (f % 16)
   const int cq = 4 * (t & 15);
@@ -495,7 +503,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
     }
   };
   load_sub(mbase);
-  for (int sub = 0; sub < Q6T_ROWS / Q6T_SUB; ++sub) {
+  for (int sub = 0; sub < rows_wg / Q6T_SUB; ++sub) {
     const int64_t m0 = mbase + sub * Q6T_SUB;
     if (m0 >= mp) break;                       // block-uniform
     if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows
@@ -721,13 +729,21 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict_
     *reinterpret_cast<float4*>(pw + (chunk * NOUT + q) * C + c) = make_float4(aw[q][0], aw[q][1], aw[q][2], aw[q][3]);
 }
 
-// dW4[q][c] = sum over chunks of the partials, in chunk order (double)
+// dW4[q][c] = sum over chunks of the partials: FIN_COLS elements x FIN_GROUPS chunk groups per
+// workgroup, groups folded in a fixed order (double, deterministic)
 __global__ __launch_bounds__(256) void head_dw_final_k(const float* __restrict__ pw, int64_t R, int64_t nq, int64_t C,
                                                        float* __restrict__ dw4) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nq * C) return;
+  __shared__ double sa[FIN_GROUPS][FIN_COLS];
+  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
+  const int64_t e = (int64_t)blockIdx.x * FIN_COLS + lc, ne = nq * C;
   double s = 0.0;
-  for (int64_t r = 0; r < R; ++r) s += (double)pw[r * nq * C + e];
+  if (e < ne)
+    for (int64_t r = grp; r < R; r += FIN_GROUPS) s += (double)pw[r * ne + e];
+  sa[grp][lc] = s;
+  __syncthreads();
+  if (grp != 0 || e >= ne) return;
+  s = 0.0;
+  for (int gI = 0; gI < FIN_GROUPS; ++gI) s += sa[gI][lc];
   dw4[e] = (float)s;
 }
 
@@ -1168,7 +1184,7 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
       (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
       !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !rlo || !rhi || !rsc || !clo || !chi || !csc ||
       !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) || !(p >= 0.f && p < 1.f) ||
-      (M + Q6T_ROWS - 1) / Q6T_ROWS > 65535) {
+      (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_bwd_q6: bad arguments (M=%lld C=%lld; C must be a multiple of 64, 0 <= p < 1)", (long long)M,
               (long long)C);
     return kErrInval;
@@ -1186,12 +1202,12 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
-  hipLaunchKernelGGL(bn_bwd_apply_q6_k<0>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
+  const int64_t qr = q6_rows(M, C);
+  hipLaunchKernelGGL(bn_bwd_apply_q6_k<0>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr)),
                      dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, k0,
-                     k1, 1.f / (float)M, o, dp);
+                     k1, 1.f / (float)M, o, dp, nullptr, (int)qr);
   if (colsum)
-    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + Q6T_ROWS - 1) / Q6T_ROWS, C,
-                       colsum);
+    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_bwd_q6");
 }
 
@@ -1227,7 +1243,7 @@ BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4
       !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
       !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !aligned16(w4) || !rlo || !rhi || !rsc || !clo ||
       !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) ||
-      !(p >= 0.f && p < 1.f) || (M + Q6T_ROWS - 1) / Q6T_ROWS > 65535) {
+      !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_head_bwd_q6: bad arguments (M=%lld C=%lld nout=%d)", (long long)M, (long long)C, nout);
     return kErrInval;
   }
@@ -1242,16 +1258,16 @@ BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4
   hipLaunchKernelGGL(bn_head_reduce_k<HEAD_NOUT>, reduce_grid(M, C), dim3(256), 0, s, x, dy4, w4, M, C, save_mean,
                      save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
-  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + 255) / 256)), dim3(256), 0, s, pw, R,
+  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, s, pw, R,
                      (int64_t)nout, C, dw4);
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
-  hipLaunchKernelGGL(bn_bwd_apply_q6_k<HEAD_NOUT>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + Q6T_ROWS - 1) / Q6T_ROWS)),
+  const int64_t qr = q6_rows(M, C);
+  hipLaunchKernelGGL(bn_bwd_apply_q6_k<HEAD_NOUT>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr)),
                      dim3(256), 0, s, x, dy4, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, 1, k0, k1,
-                     1.f / (float)M, o, dp, w4);
+                     1.f / (float)M, o, dp, w4, (int)qr);
   if (colsum)
-    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + Q6T_ROWS - 1) / Q6T_ROWS, C,
-                       colsum);
+    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_head_bwd_q6");
 }
 
