@@ -66,8 +66,11 @@ __device__ __forceinline__ Drop drop_resolve(Drop d) {
   return d;
 }
 
-// 32-bit arithmetic only (two murmur3 fmix32 rounds keyed by the 64-bit seed): the element index
-// is taken mod 2^32, the mask of every pass over the same tensor is the same function of it.
+// 32-bit arithmetic only: one murmur3 fmix32 round of (element index * golden) XOR a 32-bit key
+// folded from the 64-bit seed (the key is loop-invariant: the compiler hoists it, so an element
+// costs one multiply-xor and the round).  The element index is taken mod 2^32; the mask of every
+// pass over the same tensor is the same function of it.  XOR keying (not a Weyl offset) so two
+// seeds never give shifted copies of one mask.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -76,9 +79,12 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h ^ (h >> 16);
 }
 
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+  return (uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x5BD1E995u);
+}
+
 __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
-  const uint32_t h = fmix32((uint32_t)i * 0x9E3779B1u ^ (uint32_t)seed);
-  return fmix32(h ^ (uint32_t)(seed >> 32));
+  return fmix32((uint32_t)i * 0x9E3779B1u ^ drop_key(seed));
 }
 
 __device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
@@ -155,11 +161,25 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
       be[j] = beta ? beta[c + j] : 0.f;
     }
   }
+  // rows in batches of RB whose loads are all issued before any is used (several KiB in flight
+  // per wave: the pass is latency-bound otherwise); the arithmetic order is unchanged
+  constexpr int RB = 8;
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
-    for (int64_t rr = r; rr < re; ++rr) {
-      const float4 xv = ld4(x + rr * C + c);
+    for (int64_t rb = r; rb < re; rb += RB) {
+    float4 xb[RB], gb[MODE == 1 ? RB : 1];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t rr = rb + u < re ? rb + u : re - 1;
+      xb[u] = ld4(x + rr * C + c);
+      if constexpr (MODE == 1) gb[u] = ld4(dy + rr * C + c);
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t rr = rb + u;
+      if (rr >= re) break;
+      const float4 xv = xb[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
       if (MODE == 0) {
@@ -171,7 +191,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
           sx[j] += (double)xs[j];      // exact batch sum (see file header)
         }
       } else {
-        const float4 gv = ld4(dy + rr * C + c);
+        const float4 gv = gb[MODE == 1 ? u : 0];
         const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -182,6 +202,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
           fb[j] = fmaf(g, xh, fb[j]);
         }
       }
+    }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -582,7 +603,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
 // into the head on the f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation,
 // the numerics class of the reference's F.linear); the backward forms dh3 = dY4 . W4 per element
 // inside the BatchNorm passes and accumulates dW4 = dY4^T . h3 there (h3 recomputed from z).
-constexpr int HD_ROWS = 64, HD_COLS = 64, HD_LD = HD_COLS + 4;
+constexpr int HD_ROWS = 64, HD_COLS = 128, HD_LD = HD_COLS + 4;
+// elementwise map of a 64 x 128 chunk: thread -> 4 columns 4 (t % 32), rows t / 32 + 8 i
+constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
 
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
@@ -598,23 +621,47 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x
   const Drop dp = drop_resolve(dp0);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * HD_ROWS;
-  const int cq = 4 * (t & 15);
+  const int cq = 4 * (t % HD_CG);
   hf4 acc = hf4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t c0 = 0; c0 < C; c0 += HD_COLS) {
+  // software pipeline: chunk c0 + 64's x rows, W4 columns and BatchNorm parameters are fetched into
+  // registers before chunk c0 is normalised and multiplied (the pass is latency-bound otherwise)
+  struct Fetch {
+    float4 x[HD_NI];
+    float w[16 * HD_COLS / 256];
+    float4 mv, iv, lv, gv, bv;
+  };
+  auto fetch = [&](int64_t c0, Fetch& f) __attribute__((always_inline)) {
     const int64_t c = c0 + cq;
-    const float4 mv = ld4(mean + c), iv = ld4(invstd + c), lv = ld4_or(mean_lo, c, 0.f);
-    const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
-    const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
-    const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
-    const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+    for (int i = 0; i < HD_NI; ++i) {
+      const int64_t r = r0 + t / HD_CG + HD_RS * i;
+      if (r < M) f.x[i] = ld4(x + r * C + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 16 * HD_COLS / 256; ++u) {
+      const int i = t + 256 * u, q = i / HD_COLS, k = i - q * HD_COLS;
+      f.w[u] = q < NOUT ? w4[q * C + c0 + k] : 0.f;
+    }
+    f.mv = ld4(mean + c), f.iv = ld4(invstd + c), f.lv = ld4_or(mean_lo, c, 0.f);
+    f.gv = ld4_or(gamma, c, 1.f), f.bv = ld4_or(beta, c, 0.f);
+  };
+  Fetch nx;
+  fetch(0, nx);
+  for (int64_t c0 = 0; c0 < C; c0 += HD_COLS) {
+    const Fetch cur = nx;
+    if (c0 + HD_COLS < C) fetch(c0 + HD_COLS, nx);
+    const int64_t c = c0 + cq;
+    const float mu[4] = {cur.mv.x, cur.mv.y, cur.mv.z, cur.mv.w}, is[4] = {cur.iv.x, cur.iv.y, cur.iv.z, cur.iv.w};
+    const float lo[4] = {cur.lv.x, cur.lv.y, cur.lv.z, cur.lv.w};
+    const float ga[4] = {cur.gv.x, cur.gv.y, cur.gv.z, cur.gv.w}, be[4] = {cur.bv.x, cur.bv.y, cur.bv.z, cur.bv.w};
     __syncthreads();   // the previous chunk's fragment reads are done
 #pragma unroll
-    for (int i = 0; i < HD_ROWS / 16; ++i) {
-      const int rr = (t >> 4) + 16 * i;
+    for (int i = 0; i < HD_NI; ++i) {
+      const int rr = t / HD_CG + HD_RS * i;
       const int64_t r = r0 + rr;
       float h[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
-        const float4 xv = ld4(x + r * C + c);
+        const float4 xv = cur.x[i];
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         drop4(dp, (uint64_t)(r * C + c), xs);
 #pragma unroll
@@ -623,10 +670,8 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x
       }
       *reinterpret_cast<float4*>(ht + rr * HD_LD + cq) = make_float4(h[0], h[1], h[2], h[3]);
     }
-    for (int i = t; i < 16 * HD_COLS; i += 256) {
-      const int q = i / HD_COLS, k = i - q * HD_COLS;
-      ws[i] = q < NOUT ? w4[q * C + c0 + k] : 0.f;
-    }
+#pragma unroll
+    for (int u = 0; u < 16 * HD_COLS / 256; ++u) ws[t + 256 * u] = cur.w[u];
     __syncthreads();
     // wave wv: rows 16 wv .. +15 of the tile; A = h3 rows, B = W4^T (16 x 16 of which NOUT real)
 #pragma unroll
@@ -686,8 +731,16 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict_
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
-    for (int64_t rr = r; rr < re; ++rr) {
-      const float4 xv = ld4(x + rr * C + c);
+    constexpr int RB = 8;   // rows whose x loads are issued together (as bn_reduce_k)
+    for (int64_t rb = r; rb < re; rb += RB) {
+    float4 xb[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) xb[u] = ld4(x + (rb + u < re ? rb + u : re - 1) * C + c);
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t rr = rb + u;
+      if (rr >= re) break;
+      const float4 xv = xb[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
       // C % 256 == 0 (host check): a wave's 64 column groups share the chunk, so the row is
@@ -711,6 +764,7 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict_
 #pragma unroll
         for (int q = 0; q < NOUT; ++q) aw[q][j] = fmaf(dq[q], h, aw[q][j]);
       }
+    }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -565,6 +565,10 @@ const Variant6 kVariants6[] = {
     // pipelined form 2: 128 x 512 tile, every wave 32 rows x 256 columns (4 x 2 waves)
     {12, "gemm_fp6_k<4, 2, 1, 8, 3, 0, 2, 2>", launch6<4, 2, 1, 8, 3, 0, 2, 2>, 128},
     {13, "gemm_fp6_k<4, 1, 1, 8, 3, 0, 2, 2>", launch6<4, 1, 1, 8, 3, 0, 2, 2>, 128},
+    // 4-wave workgroups small enough in LDS for two per CU: one workgroup's barrier wait or
+    // epilogue overlaps the other's MFMAs
+    {14, "gemm_fp6_k<1, 4, 2, 4, 2>", launch6<1, 4, 2, 4, 2>, 64},
+    {15, "gemm_fp6_k<2, 2, 2, 4, 2>", launch6<2, 2, 2, 4, 2>, 128},
     // timing-only diagnostics of variant 5 (wrong results; never picked by default)
     {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128},
     {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128},

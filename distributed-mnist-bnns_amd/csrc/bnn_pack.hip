@@ -211,6 +211,90 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
   }
 }
 
+// The benched form of bnn_bn_apply_pack (FP4 rows + FP4 transpose, C % 256 == 0) on 256 x 256
+// tiles: sign_pack_tile_k's 64 x 64 tiles give each lane 16 consecutive floats (64-B strided
+// loads) and write 32-B fragments of 128-B lines; here every load instruction is one 1-KiB run of
+// a row, the FP4 rows leave as one 128-B run per wave instruction, and the transpose leaves as
+// whole 128-B lines (256 rows = 128 B of a transposed row).
+// Phase 1: wave w walks rows w, w+4, ..; lane l owns columns 4l..4l+3: y = BN(x) (bit-identical to
+// sign_pack_tile_k<., 1>), its 4 FP4 codes (16 bits) go to q and into an LDS nibble image
+// [256 rows][33 dwords] (dword slot XOR-swizzled by row bits 6-7).
+// Phase 2: thread = (8-column block kb, 32-row group mg): 4 x (8 dwords = an 8 x 8 nibble block,
+// transposed in registers by three block-swap stages) -> 8 transposed rows x 16 B.
+// LDS reads are conflict-free: bank = 32 (mg & 1) + 33 b + (kb ^ ((mg >> 1) << 3)) mod 64.
+constexpr int AP_T = 256, AP_LD = 33;
+
+__device__ __forceinline__ void nib_swap(uint32_t& a, uint32_t& b, int s, uint32_t mask) {
+  const uint32_t t = ((a >> s) ^ b) & mask;
+  b ^= t;
+  a ^= t << s;
+}
+
+// 8 x 8 nibble transpose: x[i] = row i (nibble c at bits 4c) -> x[c] = column c (nibble i at 4i)
+__device__ __forceinline__ void nib_transpose8(uint32_t (&x)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) nib_swap(x[i], x[i + 4], 16, 0x0000FFFFu);
+#pragma unroll
+  for (int i = 0; i < 8; i += 4) {
+    nib_swap(x[i], x[i + 2], 8, 0x00FF00FFu);
+    nib_swap(x[i + 1], x[i + 3], 8, 0x00FF00FFu);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) nib_swap(x[i], x[i + 1], 4, 0x0F0F0F0Fu);
+}
+
+__global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(const float* __restrict__ x, int64_t M, int64_t C,
+                                                           ColAffine af, uint8_t* __restrict__ q, int64_t ldq,
+                                                           uint8_t* __restrict__ qt, int64_t ldqt) {
+  __shared__ uint32_t img[AP_T * AP_LD];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t k0 = (int64_t)blockIdx.x * AP_T, m0 = (int64_t)blockIdx.y * AP_T;
+  const int64_t cb = k0 + 4 * lane;
+  const float4 mv = *reinterpret_cast<const float4*>(af.mean + cb);
+  const float4 iv = *reinterpret_cast<const float4*>(af.invstd + cb);
+  const float4 gv = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb) : make_float4(1, 1, 1, 1);
+  const float4 bv = af.beta ? *reinterpret_cast<const float4*>(af.beta + cb) : make_float4(0, 0, 0, 0);
+  const float4 lv = af.mean_lo ? *reinterpret_cast<const float4*>(af.mean_lo + cb) : make_float4(0, 0, 0, 0);
+  const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+  const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
+  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+  uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
+#pragma unroll 4
+  for (int i = 0; i < AP_T / 4; ++i) {
+    const int r = wave + 4 * i;
+    const int64_t m = m0 + r;
+    uint32_t code = 0;
+    if (m < M) {
+      const float4 f = *reinterpret_cast<const float4*>(x + m * C + cb);
+      const float v[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) code |= fp4_code(tsign(fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]))) << (4 * j);
+      *reinterpret_cast<uint16_t*>(q + m * ldq + k0 / 2 + 2 * lane) = (uint16_t)code;
+    }
+    const int slot = (lane >> 1) ^ (((r >> 6) & 3) << 3);
+    img16[(r * AP_LD + slot) * 2 + (lane & 1)] = (uint16_t)code;
+  }
+  __syncthreads();
+  const int mg = t & 7, kb = t >> 3;
+  uint32_t out[8][4];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 32 * mg + 8 * qq + i;
+      w[i] = img[r * AP_LD + (kb ^ ((mg >> 1) << 3))];
+    }
+    nib_transpose8(w);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) out[c][qq] = w[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    *reinterpret_cast<uint4*>(qt + (k0 + 8 * kb + c) * ldqt + m0 / 2 + 16 * mg) =
+        make_uint4(out[c][0], out[c][1], out[c][2], out[c][3]);
+}
+
 __global__ __launch_bounds__(256) void sign_f32_k(const float* __restrict__ x, float* __restrict__ y,
                                                   int64_t n, int vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -724,6 +808,12 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   const ColAffine af{mean, mean_lo, invstd, gamma, beta,
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
+  if (fmt == 1 && q && qt && qt_fmt == 1 && C % AP_T == 0 && af.vec && vec && (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024) {
+    hipLaunchKernelGGL(bn_apply_pack_fp4_k, dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)), dim3(256),
+                       0, S(stream), x, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
+                       reinterpret_cast<uint8_t*>(qt), ldqt);
+    return check_launch("bnn_bn_apply_pack");
+  }
   // 4 row tiles per workgroup when that still leaves >= 8K workgroups (amortised parameter loads)
   const int rt = (gx * ((gy + 3) / 4) >= 8192) ? 4 : 1;
   const unsigned gyr = (unsigned)((gy + rt - 1) / rt);

@@ -81,6 +81,16 @@ def bn_stats(F, z, C):
 @pytest.mark.parametrize("with_qt", [None, 0, 1])
 def test_bn_apply_pack_bit_exact(F, M, C, fmt, with_qt):
     """with_qt: no transpose, an int8 transpose (0) or an FP4 transpose (1, the FP6 GEMMs' B)."""
+    _apply_pack_case(F, M, C, fmt, with_qt)
+
+
+def test_bn_apply_pack_wide_tiles_bit_exact(F):
+    """The 256 x 256-tile kernel bnn_bn_apply_pack takes for FP4 rows + FP4 transpose at wide-MLP
+    sizes (>= 1024 tiles; ragged last row tile), against the same float64 restatement."""
+    _apply_pack_case(F, 8200, 8192, 1, 1)
+
+
+def _apply_pack_case(F, M, C, fmt, with_qt):
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M * 7 + C + fmt)
     # integer-valued pre-activations + a per-column bias (what a binarized GEMM produces): ties

@@ -565,3 +565,26 @@ def test_dropout_batchnorm_hardtanh_vs_explicit_mask(F, M, C, p):
     assert rel_err(host(bn_a.bias.grad), host(bn_b.bias.grad)) < GRAD_TOL
     assert close(host(bn_a.running_mean), host(bn_b.running_mean), 1e-5, 1e-6)
     assert close(host(bn_a.running_var), host(bn_b.running_var), 1e-5, 1e-6)
+
+
+def test_dropout_mask_statistics(F):
+    """The fused passes' keep mask (bnn_dropout_mask regenerates it): keep fraction within 5 sigma
+    of 1 - p on 2^24 elements, and no correlation (|r| < 5/sqrt(n)) between neighbouring elements,
+    elements one wide-MLP row apart, or the masks of consecutive seeds / device-step seeds."""
+    n, p = 1 << 24, 0.3
+    seed = 987654321
+    a = (F.dropout_mask(n, p, seed) > 0).double()
+    keep = a.mean().item()
+    assert abs(keep - (1 - p)) < 5 * (p * (1 - p) / n) ** 0.5
+
+    def corr(u, v):
+        u = u - u.mean()
+        v = v - v.mean()
+        return (u * v).mean().item() / (u.std().item() * v.std().item())
+
+    lim = 5 / n ** 0.5
+    assert abs(corr(a[:-1], a[1:])) < lim
+    assert abs(corr(a[:-8192], a[8192:])) < lim
+    for s2 in (seed + 1, seed + 0xD1B54A32D192ED03 % (1 << 64), seed ^ (1 << 40)):
+        b = (F.dropout_mask(n, p, s2 % (1 << 64)) > 0).double()
+        assert abs(corr(a, b)) < lim, s2
