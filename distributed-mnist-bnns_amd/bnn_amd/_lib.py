@@ -35,6 +35,7 @@ SIGNATURES = {
     "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_fp4_i16": (I32, [P, I64, P, I64, P, I64, I64, I64, I64, P]),
     "bnn_gemm_set_variant": (I32, [I32]),
     "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64, I64]),
     "bnn_gemm_xnor": (I32, [P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
@@ -64,6 +65,13 @@ SIGNATURES = {
     "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P,
                                  P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
+    "bnn_bn_fwd_train_i16": (I32, [P, P, I64, I64, P, P, P, P, F32, F32, P, P, P, F32, U64, P, P]),
+    "bnn_bn_apply_pack_i16": (I32, [P, P, I64, I64, P, P, P, P, P, P, I64, P, I64, P]),
+    "bnn_bn_bwd_q6_i16": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
+                                P, P]),
+    "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
+    "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P,
+                                     P, P, P, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,

@@ -107,6 +107,8 @@ def _check(*ts, dtype=torch.float32):
 
 def _c2d(x):
     """Contiguous fp32 2-D view."""
+    if getattr(x, "_bnn_z16", None) is not None:
+        raise RuntimeError("a z16 pre-activation placeholder reached an op that reads fp32 values")
     return x if x.is_contiguous() else x.contiguous()
 
 
@@ -387,6 +389,53 @@ def gemm_fp4(A4, B4, M, N, bias=None, k_true=None):
     with _timed(name, 2.0 * M * N * k_true, (M + N) * Kb + 4 * M * N):
         L.call("bnn_gemm_fp4", L.ptr(A4), Kb, L.ptr(B4), Kb, L.ptr(bias), L.ptr(C), N, M, N, Kb, L.stream())
     return C
+
+
+def gemm_fp4_i16(A4, B4, M, N, k_true=None):
+    """gemm_fp4 without bias, the exact dot products as int16 [M, N] (bnn_gemm_fp4_i16)."""
+    Kb = A4.shape[-1]
+    assert B4.shape[-1] == Kb and Kb % ALIGN == 0 and 2 * Kb <= 32767 and N % 4 == 0
+    C = torch.empty((M, N), dtype=torch.int16, device=A4.device)
+    if M == 0 or N == 0:
+        return C
+    k_true = 2 * Kb if k_true is None else k_true
+    name = (gemm_kernel_name(0, 0, M, N, Kb) + " [i16]") if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * k_true, (M + N) * Kb + 2 * M * N):
+        L.call("bnn_gemm_fp4_i16", L.ptr(A4), Kb, L.ptr(B4), Kb, L.ptr(C), N, M, N, Kb, L.stream())
+    return C
+
+
+# Compact pre-activations (z16): the output z = F.linear(sign(h), W_b) + bias of a hidden
+# BinarizeLinear (binarized_modules.py:80-83) is an integer plus a per-column bias, so when its only
+# consumer is a libbnn BatchNorm pass it travels as int16 dot products + the bias
+# (bnn_gemm_fp4_i16; the *_i16 BatchNorm entries form fl(I + bias), bit-identical to the fp32 z)
+# at half the bytes of every pass over it.  Autograd sees a stride-0 float placeholder of z's
+# shape carrying (int16, bias) in _Z16_ATTR; only the z16-aware functions below read it, and its
+# gradient is an ordinary fp32 tensor.
+Z16 = True
+_Z16_ATTR = "_bnn_z16"
+
+
+def z16_ok(M, N, K):
+    """Whether a hidden BinarizeLinear [K -> N] over M rows may hand its output on as z16."""
+    return (Z16 and Q6_HANDOFF and DIGIT_GEMM == "fp6" and N % 256 == 0 and round_up(K, 256) <= 32767
+            and (N // 256) * ((M + 255) // 256) >= 512)
+
+
+Z16_HANDOFFS = 0          # z16 placeholders produced (tests check the hand-off actually ran)
+
+
+def _z16_carrier(y16, bias):
+    global Z16_HANDOFFS
+    Z16_HANDOFFS += 1
+    ph = torch.zeros((1,), dtype=torch.float32, device=y16.device).as_strided(tuple(y16.shape), (0, 0))
+    setattr(ph, _Z16_ATTR, (y16, bias))
+    return ph
+
+
+def _z16_of(x):
+    """(int16 [M, C], bias [C] or None) carried by a z16 placeholder, or None."""
+    return getattr(x, _Z16_ATTR, None)
 
 
 def gemm_xnor(a_bits, b_bits, M, N, bias=None):
@@ -834,19 +883,27 @@ def _q6_take(dy):
     return ent[1:] if ent[0] == _q6_key(dy) else None
 
 
-def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name):
-    """BatchNorm(+Dropout) backward that also quantises dz (returned, with the digits attached)."""
-    dev = x.device
-    dx = torch.empty_like(x)
+def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name, z16=None):
+    """BatchNorm(+Dropout) backward that also quantises dz (returned, with the digits attached).
+    z16 = (int16, bias): the input in its compact form (x unused)."""
+    dev = dy.device
+    dx = torch.empty((M, C), dtype=torch.float32, device=dev)
     rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
     Mp = round_up(M)
     cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
-    with _timed(name, 0, 16 * M * C + 4 * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
-        L.call("bnn_bn_bwd_q6", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
-               L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
-               L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws),
-               L.stream())
+    xb = 8 if z16 is None else 4       # bytes per element read by the two passes over x
+    with _timed(name, 0, xb * M * C + 8 * M * C + 4 * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
+        if z16 is None:
+            L.call("bnn_bn_bwd_q6", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+                   L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
+                   L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
+                   L.ptr(ws), L.stream())
+        else:
+            L.call("bnn_bn_bwd_q6_i16", L.ptr(z16[0]), L.ptr(z16[1]), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw),
+                   L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi),
+                   L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
     setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
     return dx
 
@@ -960,34 +1017,52 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
     def forward(ctx, z, weight, bias, running_mean, running_var, momentum, eps, p, seed, w4, b4):
         _check(z, weight, bias, running_mean, running_var, w4, b4)
         ctx.q6 = _q6_wanted(z, z.shape[-1])
-        z = _c2d(z)
+        zz = _z16_of(z)                       # (int16, bias): the compact pre-activation
+        if zz is None:
+            z = _c2d(z)
         M, C = z.shape
         gw = weight.detach() if weight is not None else None
         gb = bias.detach() if bias is not None else None
         ws = _bn_ws(M, C, z.device)
         mean, invstd, mlo = _bn_stat_buffers(C, z.device)
-        with _timed("bn_dropout_fwd_stats", 0, 4 * M * C):
-            L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
-                   L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
-                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p), int(seed), L.ptr(ws), L.stream())
+        mom = float(momentum if momentum is not None else -1.0)
+        with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
+            if zz is None:
+                L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
+                       L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p),
+                       int(seed), L.ptr(ws), L.stream())
+            else:
+                L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
+                       L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
+                       L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
         w4c = w4.detach().contiguous()
         y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
-        with _timed("bn_head_fwd", 0, 4 * M * C + 4 * M * HEAD_NOUT):
-            L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
-                   float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4.detach() if b4 is not None else None),
-                   L.ptr(y4), L.stream())
-        ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, w4c)
+        b4d = b4.detach() if b4 is not None else None
+        with _timed("bn_head_fwd", 0, (4 if zz is None else 2) * M * C + 4 * M * HEAD_NOUT):
+            if zz is None:
+                L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
+                       L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d), L.ptr(y4), L.stream())
+            else:
+                L.call("bnn_bn_head_fwd_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
+                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d),
+                       L.ptr(y4), L.stream())
+        if zz is None:
+            ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, w4c, None)
+        else:
+            ctx.save_for_backward(zz[0], gw, gb, mean, invstd, mlo, w4c, zz[1])
+        ctx.z16 = zz is not None
+        ctx.dims = (M, C)
         ctx.p, ctx.seed = p, seed
         ctx.has_b4 = b4 is not None
         return y4
 
     @staticmethod
     def backward(ctx, dy4):
-        z, gw, gb, mean, invstd, mlo, w4c = ctx.saved_tensors
+        z, gw, gb, mean, invstd, mlo, w4c, zb = ctx.saved_tensors
         dy4 = _c2d(dy4)
-        M, C = z.shape
+        M, C = ctx.dims
         dev = z.device
-        dx = torch.empty_like(z)
+        dx = torch.empty((M, C), dtype=torch.float32, device=dev)
         dgw = torch.empty((C,), dtype=torch.float32, device=dev) if gw is not None else None
         dgb = torch.empty((C,), dtype=torch.float32, device=dev) if gb is not None else None
         dw4 = torch.empty((HEAD_NOUT, C), dtype=torch.float32, device=dev)
@@ -996,11 +1071,18 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
         cs = torch.empty((C,), dtype=torch.float32, device=dev)
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, HEAD_NOUT),), dtype=torch.uint8, device=dev)
-        with _timed("bn_head_bwd_q6", 0, 16 * M * C + 4 * M * C + 6 * M * C):
-            L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw), L.ptr(gb),
-                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dgw),
-                   L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo),
-                   L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
+        with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + 4 * M * C + 6 * M * C):
+            if not ctx.z16:
+                L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw),
+                       L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx),
+                       L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
+                       L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
+            else:
+                L.call("bnn_bn_head_bwd_q6_i16", L.ptr(z), L.ptr(zb), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C,
+                       L.ptr(gw), L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed),
+                       L.ptr(dx), L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
+                       L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws),
+                       L.stream())
         if ctx.q6:
             setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
         db4 = dy4.sum(0) if ctx.has_b4 and ctx.needs_input_grad[10] else None
@@ -1146,43 +1228,65 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
     dW = dY^T.sign(h) on the digit GEMM, then the fused BatchNorm+Hardtanh backward."""
 
     @staticmethod
-    def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend):
+    def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend, emit_z16=False):
         _check(z, bn_w, bn_b, rm, rv, weight, bias)
         ctx.q6 = _q6_wanted(z, z.shape[-1], training)
-        z = _c2d(z)
+        zz = _z16_of(z)                       # (int16, bias): z in its compact form
+        if zz is None:
+            z = _c2d(z)
         M, C = z.shape
         N = weight.shape[0]
+        fp4 = backend == "fp4"
+        ctx.fp6 = fp4 and DIGIT_GEMM == "fp6"
+        if zz is not None and not (training and ctx.fp6 and ctx.q6 and C % 256 == 0):
+            raise RuntimeError("a z16 pre-activation needs the training-mode FP4/FP6 consumer (z16_ok)")
         gw = bn_w.detach() if bn_w is not None else None
         gb = bn_b.detach() if bn_b is not None else None
         if training:
             mean, invstd, mlo = _bn_stat_buffers(C, z.device)
             ws = _bn_ws(M, C, z.device)
-            with _timed("bn_fwd_stats", 0, 4 * M * C):
-                L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv),
-                       float(momentum if momentum is not None else -1.0), float(eps), L.ptr(mean),
-                       L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
+            mom = float(momentum if momentum is not None else -1.0)
+            with _timed("bn_fwd_stats", 0, (4 if zz is None else 2) * M * C):
+                if zz is None:
+                    L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv), mom,
+                           float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
+                else:
+                    L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm),
+                           L.ptr(rv), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 0.0, 0, L.ptr(ws),
+                           L.stream())
         else:
             mean, mlo = rm.contiguous(), None
             invstd = (rv + eps).rsqrt()
         need_dh = any(ctx.needs_input_grad[:3])
-        need_dw = ctx.needs_input_grad[8]
-        fp4 = backend == "fp4"
-        ctx.fp6 = fp4 and DIGIT_GEMM == "fp6"
+        need_dw = ctx.needs_input_grad[8] or zz is not None
         qf = "fp4" if ctx.fp6 else "i8"
         q = torch.empty((M, round_up(C, 256) // 2) if fp4 else (M, round_up(C)),
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
         qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
-        with _timed("bn_apply_pack", 0, 4 * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
-            L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb),
-                   1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
-                   1 if qf == "fp4" else 0, L.stream())
+        nx = 4 if zz is None else 2
+        with _timed("bn_apply_pack", 0, nx * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
+            if zz is None:
+                L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
+                       L.ptr(gb), 1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
+                       1 if qf == "fp4" else 0, L.stream())
+            else:
+                L.call("bnn_bn_apply_pack_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
+                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], L.stream())
         b = bias.detach() if bias is not None else None
         wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True, qt_fmt=qf)
-        if fp4:
+        if emit_z16 and fp4 and training:
+            # the next BatchNorm reads z = fl(I + bias) from int16 I: a snapshot of the bias (the
+            # optimizer updates the Parameter in place after this step's backward)
+            y = _z16_carrier(gemm_fp4_i16(q, wq, M, N, k_true=C), b.clone() if b is not None else None)
+        elif fp4:
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
             y = gemm_i8(q, 1, wq, 1, M, N, bias=b, k_true=C)
-        ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, qt, wqt)
+        if zz is None:
+            ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, qt, wqt, None)
+        else:
+            ctx.save_for_backward(zz[0], gw, gb, mean, invstd, mlo, qt, wqt, zz[1])
+        ctx.z16 = zz is not None
         ctx.training = training
         ctx.dims = (M, C, N)
         ctx.has_bias = bias is not None
@@ -1192,7 +1296,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        z, gw, gb, mean, invstd, mlo, qt, wqt = ctx.saved_tensors
+        z, gw, gb, mean, invstd, mlo, qt, wqt, zb = ctx.saved_tensors
         M, C, N = ctx.dims
         dy = _c2d(dy)
         dz = dgw = dgb = dw = db = None
@@ -1223,18 +1327,21 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             dgb = torch.empty((C,), dtype=torch.float32, device=z.device) if gb is not None else None
             ws = _bn_ws(M, C, z.device)
             if ctx.q6:
-                dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6")
+                dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6",
+                                z16=(z, zb) if ctx.z16 else None)
             else:
                 dz = torch.empty_like(z)
                 with _timed("bn_bwd", 0, 16 * M * C):
                     _bn_bwd_call(ctx.training, z, dh, M, C, gw, gb, mean, invstd, mlo, True, dz, dgw, dgb, ws)
         return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, dw, db, None)
+                None, None, None, None, None, dw, db, None, None)
 
 
-def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4"):
+def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4", emit_z16=False):
     """fc(hardtanh(bn(z))) through BNHardtanhBinaryLinearFunction (bn: nn.BatchNorm1d, fc: a
-    BinarizeLinear holding its latent weight, i.e. ``org_protocol = False``)."""
+    BinarizeLinear holding its latent weight, i.e. ``org_protocol = False``).  emit_z16: return
+    fc's output as a z16 placeholder (its consumer must be a z16-aware libbnn BatchNorm pass:
+    bn_hardtanh_binary_linear or dropout_bn_hardtanh_linear in training mode; see z16_ok)."""
     rm, rv, bn_training, factor = _bn_module_args(bn)
     return BNHardtanhBinaryLinearFunction.apply(z, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
-                                                fc.weight, fc.bias, backend)
+                                                fc.weight, fc.bias, backend, bool(emit_z16))

@@ -59,18 +59,40 @@ class MLP(nn.Module):
             return BF.batch_norm_hardtanh(x, bn)
         return ht(bn(x))
 
-    def _bnh_fc(self, bn, ht, fc, z):
+    def _fusable(self, fc, z):
+        return (self.fused_bn and z.is_cuda and z.dim() == 2 and z.shape[1] % 4 == 0 and not fc.org_protocol
+                and fc.backend in ("fp4", "mfma"))
+
+    def _bnh_fc(self, bn, ht, fc, z, emit_z16=False):
         """fc(ht(bn(z))); fused into one libbnn op (no fp32 hardtanh output) when the fc keeps
         its latent weight in the Parameter and runs an MFMA backend."""
-        if (self.fused_bn and z.is_cuda and z.dim() == 2 and z.shape[1] % 4 == 0 and not fc.org_protocol
-                and fc.backend in ("fp4", "mfma")):
-            return BF.bn_hardtanh_binary_linear(z, bn, fc, fc.backend)
+        if self._fusable(fc, z):
+            return BF.bn_hardtanh_binary_linear(z, bn, fc, fc.backend, emit_z16=emit_z16)
         return fc(self._bnh(bn, ht, z))
+
+    def _z16(self, fc, M, consumer):
+        """fc's output may travel as int16 dot products + bias (functional.z16_ok): it is produced by
+        the fused FP4 path and its consumer is a z16-aware libbnn BatchNorm pass."""
+        return (consumer and self.training and fc.backend == "fp4" and not fc.org_protocol
+                and BF.z16_ok(M, fc.out_features, fc.in_features))
+
+    def _head_fused(self, x_width):
+        return (self.fused_bn and self.fused_head and self.training and self.bn3.training
+                and x_width % 256 == 0 and self.fc4.out_features == BF.HEAD_NOUT and self.bn3.track_running_stats
+                and self.bn3.momentum is not None)
 
     def forward(self, x):
         x = x.view(-1, 28 * 28)
-        x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, self.fc1(x))
-        x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x)
+        z1 = self.fc1(x)
+        M = z1.shape[0]
+        fuse2 = self._fusable(self.fc2, z1)
+        # fc2's output feeds the fused bn2 -> fc3 op; fc3's the fused head
+        z16_2 = fuse2 and self._z16(self.fc2, M, self._fusable(self.fc3, z1) and self.fc3.backend == "fp4"
+                                    and self.bn2.training)
+        x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, z1, emit_z16=z16_2)
+        z16_3 = (self._fusable(self.fc3, x) and self._z16(self.fc3, M, self._head_fused(self.fc3.out_features))
+                 and x.is_cuda)
+        x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x, emit_z16=z16_3)
         if (self.fused_bn and self.fused_head and self.training and self.bn3.training
                 and BF.head_fusable(x, self.bn3, self.fc4)):
             # drop -> bn3 -> htanh3 -> fc4 as one libbnn head: h3 is never written

@@ -124,8 +124,8 @@ inline Drop make_drop(float p, uint64_t seed) {
 //         float partials see deviations rather than raw magnitudes; merged with Chan's formula.
 // MODE 1: per-chunk (sum g, sum g*xhat) with g = dy*mask(y).
 // One thread = 4 adjacent columns (float4), rows walked in 16-row float partials folded to double.
-template <int MODE>
-__global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, const float* __restrict__ dy,
+template <int MODE, bool Z16 = false>
+__global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restrict__ dy,
                                                    int64_t M, int64_t C, const float* __restrict__ mean,
                                                    const float* __restrict__ mean_lo,
                                                    const float* __restrict__ invstd,
@@ -144,8 +144,9 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
   const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
   float mu[4], lo[4] = {0, 0, 0, 0}, is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
+  const float4 xb = xin_bias4<Z16>(xin, c);
   if (MODE == 0) {
-    const float4 sv = ld4(x + r0 * C + c);
+    const float4 sv = xin_load4<Z16>(xin, r0 * C + c, xb);
     mu[0] = sv.x;
     mu[1] = sv.y;
     mu[2] = sv.z;
@@ -168,18 +169,18 @@ __global__ __launch_bounds__(256) void bn_reduce_k(const float* __restrict__ x, 
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
     for (int64_t rb = r; rb < re; rb += RB) {
-    float4 xb[RB], gb[MODE == 1 ? RB : 1];
+    float4 xv8[RB], gb[MODE == 1 ? RB : 1];
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u < re ? rb + u : re - 1;
-      xb[u] = ld4(x + rr * C + c);
+      xv8[u] = xin_load4<Z16>(xin, rr * C + c, xb);
       if constexpr (MODE == 1) gb[u] = ld4(dy + rr * C + c);
     }
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u;
       if (rr >= re) break;
-      const float4 xv = xb[u];
+      const float4 xv = xv8[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
       if (MODE == 0) {
@@ -471,8 +472,8 @@ struct Q6Out {
 
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
-template <int NOUT>
-__global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict__ x, const float* __restrict__ dy,
+template <int NOUT, bool Z16 = false>
+__global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
                                                          const float* __restrict__ invstd,
@@ -492,6 +493,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
   const int64_t c = c0 + cq;
   const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
   const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f), lv = ld4_or(mean_lo, c, 0.f);
+  const float4 xb = xin_bias4<Z16>(xin, c);
   const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
   const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
   const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
@@ -512,13 +514,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
   // software pipeline: sub-tile s+1's x (and dY) rows are loaded into registers before sub-tile s
   // is quantised, so their HBM latency hides behind the quantiser's VALU work
   constexpr int NI = Q6T_SUB / 16;
-  float4 xr[NI], gr[NOUT > 0 ? 1 : NI];
+  XRaw<Z16> xr[NI];
+  float4 gr[NOUT > 0 ? 1 : NI];
   auto load_sub = [&](int64_t m0n) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int64_t r = m0n + (t >> 4) + 16 * i;
       if (m0n < mp && r < M) {
-        xr[i] = ld4(x + r * C + c);
+        xr[i] = xin_raw4<Z16>(xin, r * C + c);
         if constexpr (NOUT == 0) gr[i] = ld4(dy + r * C + c);
       }
     }
@@ -540,7 +543,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(const float* __restrict
       const int64_t r = m0 + rr;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
-        const float4 xv = xr[i];
+        const float4 xv = xin_cvt4<Z16>(xr[i], xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         float gs[4];
         if constexpr (NOUT > 0) {
@@ -609,8 +612,8 @@ constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
 
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
-template <int NOUT>
-__global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x, int64_t M, int64_t C,
+template <int NOUT, bool Z16 = false>
+__global__ __launch_bounds__(256) void bn_head_fwd_k(XIn xin, int64_t M, int64_t C,
                                                      const float* __restrict__ mean, const float* __restrict__ mean_lo,
                                                      const float* __restrict__ invstd, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, const float* __restrict__ w4,
@@ -626,16 +629,18 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x
   // software pipeline: chunk c0 + 64's x rows, W4 columns and BatchNorm parameters are fetched into
   // registers before chunk c0 is normalised and multiplied (the pass is latency-bound otherwise)
   struct Fetch {
-    float4 x[HD_NI];
+    XRaw<Z16> x[HD_NI];
+    float4 xb;
     float w[16 * HD_COLS / 256];
     float4 mv, iv, lv, gv, bv;
   };
   auto fetch = [&](int64_t c0, Fetch& f) __attribute__((always_inline)) {
     const int64_t c = c0 + cq;
+    f.xb = xin_bias4<Z16>(xin, c);
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) {
       const int64_t r = r0 + t / HD_CG + HD_RS * i;
-      if (r < M) f.x[i] = ld4(x + r * C + c);
+      if (r < M) f.x[i] = xin_raw4<Z16>(xin, r * C + c);
     }
 #pragma unroll
     for (int u = 0; u < 16 * HD_COLS / 256; ++u) {
@@ -661,7 +666,7 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x
       const int64_t r = r0 + rr;
       float h[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
-        const float4 xv = cur.x[i];
+        const float4 xv = xin_cvt4<Z16>(cur.x[i], cur.xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         drop4(dp, (uint64_t)(r * C + c), xs);
 #pragma unroll
@@ -694,8 +699,8 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(const float* __restrict__ x
 
 // Statistics pass of the head's BatchNorm backward (bn_reduce_k MODE 1 with g = dY4 . W4 formed per
 // element) plus the head's weight gradient partials dW4[q][c] over the chunk's rows (fp32 per chunk).
-template <int NOUT>
-__global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict__ x, const float* __restrict__ d4,
+template <int NOUT, bool Z16 = false>
+__global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __restrict__ d4,
                                                         const float* __restrict__ w4, int64_t M, int64_t C,
                                                         const float* __restrict__ mean, const float* __restrict__ mean_lo,
                                                         const float* __restrict__ invstd,
@@ -728,19 +733,20 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(const float* __restrict_
       aw[q][j] = 0.f;
     }
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  const float4 xbias = xin_bias4<Z16>(xin, c);
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
     constexpr int RB = 8;   // rows whose x loads are issued together (as bn_reduce_k)
     for (int64_t rb = r; rb < re; rb += RB) {
-    float4 xb[RB];
+    float4 xv8[RB];
 #pragma unroll
-    for (int u = 0; u < RB; ++u) xb[u] = ld4(x + (rb + u < re ? rb + u : re - 1) * C + c);
+    for (int u = 0; u < RB; ++u) xv8[u] = xin_load4<Z16>(xin, (rb + u < re ? rb + u : re - 1) * C + c, xbias);
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u;
       if (rr >= re) break;
-      const float4 xv = xb[u];
+      const float4 xv = xv8[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
       // C % 256 == 0 (host check): a wave's 64 column groups share the chunk, so the row is
@@ -827,6 +833,12 @@ bool bn_args_ok(const float* x, int64_t M, int64_t C) {
 }
 
 bool vec_ok(const float* p) { return p == nullptr || aligned16(p); }
+
+// the int16 form (XIn z16): 8-B aligned values (4 per 8-B load), 16-B aligned bias or none
+bool bn_args_ok16(const XIn& in, int64_t M, int64_t C) {
+  return in.p && (reinterpret_cast<uintptr_t>(in.p) & 7) == 0 && vec_ok(in.bias) && M > 0 && C > 0 && C % 4 == 0 &&
+         (C / 4) * bn_chunks(M, C) < (1LL << 31) && (M + apply_rows(M, C) - 1) / apply_rows(M, C) <= 65535;
+}
 
 
 // ------------------------------------------------------------------ BatchNorm2d (+ Hardtanh, + MaxPool2d(2))
@@ -1111,13 +1123,14 @@ BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
   return 2 * bn_chunks(M, C) * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
 }
 
-static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
+static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* save_mean_lo, float* y,
                              int32_t hardtanh, void* work, void* stream, Drop dp) {
-  if (!bn_args_ok(x, M, C) || !save_mean || !save_invstd || !work || !vec_ok(y) || !vec_ok(save_mean_lo) ||
-      (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) || !vec_ok(beta) ||
-      !aligned16(save_mean) || !aligned16(save_invstd)) {
+  const float* x = reinterpret_cast<const float*>(xin.p);
+  if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || !save_mean || !save_invstd || !work || !vec_ok(y) ||
+      !vec_ok(save_mean_lo) || (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) ||
+      !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || (z16 && y != nullptr)) {
     set_error("bnn_bn_fwd_train: bad arguments (M=%lld C=%lld; C must be a multiple of 4, M > 0)",
               (long long)M, (long long)C);
     return kErrInval;
@@ -1128,8 +1141,12 @@ static int bn_fwd_train_impl(const float* x, int64_t M, int64_t C, const float* 
   double* p1 = p0 + R * C;
   // without a caller buffer the lo part of the mean lives in the workspace (the bwd's k0 slot)
   float* lo = save_mean_lo ? save_mean_lo : reinterpret_cast<float*>(p1 + R * C);
-  hipLaunchKernelGGL(bn_reduce_k<0>, reduce_grid(M, C), dim3(256), 0, s, x,
-                     nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
+  if (z16)
+    hipLaunchKernelGGL((bn_reduce_k<0, true>), reduce_grid(M, C), dim3(256), 0, s, xin,
+                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
+  else
+    hipLaunchKernelGGL((bn_reduce_k<0, false>), reduce_grid(M, C), dim3(256), 0, s, xin,
+                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
                      running_var, save_mean, save_invstd, lo, bn_chunk_rows(M, C), (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
@@ -1142,8 +1159,8 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
                              void* work, void* stream) {
-  return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
-                           save_mean_lo, y, hardtanh, work, stream, make_drop(0.f, 0));
+  return bn_fwd_train_impl(XIn{x, nullptr}, false, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(0.f, 0));
 }
 
 BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -1154,8 +1171,20 @@ BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const
     set_error("bnn_bn_dropout_fwd_train: p must be in [0, 1) (got %g)", (double)p);
     return kErrInval;
   }
-  return bn_fwd_train_impl(x, M, C, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd,
-                           save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed));
+  return bn_fwd_train_impl(XIn{x, nullptr}, false, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed));
+}
+
+BNN_API int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                                 float* save_mean, float* save_invstd, float* save_mean_lo, float p, uint64_t seed,
+                                 void* work, void* stream) {
+  if (!(p >= 0.f && p < 1.f)) {
+    set_error("bnn_bn_fwd_train_i16: p must be in [0, 1) (got %g)", (double)p);
+    return kErrInval;
+  }
+  return bn_fwd_train_impl(XIn{x16, xbias}, true, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                           save_mean, save_invstd, save_mean_lo, nullptr, 0, work, stream, make_drop(p, seed));
 }
 
 BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -1191,7 +1220,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL(bn_reduce_k<1>, reduce_grid(M, C), dim3(256), 0, s, x, dy,
+  hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy,
                      M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
@@ -1229,16 +1258,17 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
                      work, stream, make_drop(p, seed), true);
 }
 
-BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,
                           const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
                           float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
                           uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
-  if (!bn_args_ok(x, M, C) || C % Q6T_COLS != 0 || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work ||
-      (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
-      !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !rlo || !rhi || !rsc || !clo || !chi || !csc ||
-      !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) || !(p >= 0.f && p < 1.f) ||
-      (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
+  const float* x = reinterpret_cast<const float*>(xin.p);
+  if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % Q6T_COLS != 0 || !dy || !aligned16(dy) ||
+      !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) ||
+      !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !rlo || !rhi || !rsc || !clo ||
+      !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) ||
+      !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_bwd_q6: bad arguments (M=%lld C=%lld; C must be a multiple of 64, 0 <= p < 1)", (long long)M,
               (long long)C);
     return kErrInval;
@@ -1250,19 +1280,45 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL(bn_reduce_k<1>, reduce_grid(M, C), dim3(256), 0, s, x, dy,
-                     M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
+  if (z16)
+    hipLaunchKernelGGL((bn_reduce_k<1, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+                       save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
+  else
+    hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+                       save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
   const int64_t qr = q6_rows(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_q6_k<0>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr)),
-                     dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, k0,
-                     k1, 1.f / (float)M, o, dp, nullptr, (int)qr);
+  const dim3 g((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr));
+  if (z16)
+    hipLaunchKernelGGL((bn_bwd_apply_q6_k<0, true>), g, dim3(256), 0, s, xin, dy, M, C, save_mean, save_mean_lo,
+                       save_invstd, gamma, beta, hardtanh, k0, k1, 1.f / (float)M, o, dp, nullptr, (int)qr);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_q6_k<0, false>), g, dim3(256), 0, s, xin, dy, M, C, save_mean, save_mean_lo,
+                       save_invstd, gamma, beta, hardtanh, k0, k1, 1.f / (float)M, o, dp, nullptr, (int)qr);
   if (colsum)
     hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_bwd_q6");
+}
+
+BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                          const float* beta, const float* save_mean, const float* save_invstd,
+                          const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
+  return bn_bwd_q6_impl(XIn{x, nullptr}, false, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream);
+}
+
+BNN_API int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
+                              const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                              const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                              uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
+  return bn_bwd_q6_impl(XIn{x16, xbias}, true, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream);
 }
 
 constexpr int HEAD_NOUT = 10;   // the reference head: nn.Linear(C, 10) (mnist-dist2.py:73)
@@ -1271,33 +1327,55 @@ BNN_API int64_t bnn_bn_head_workspace(int64_t M, int64_t C, int32_t nout) {
   return bnn_bn_workspace(M, C) + round_up(bn_chunks(M, C) * (int64_t)nout * C * (int64_t)sizeof(float), 256);
 }
 
-BNN_API int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+static int bn_head_fwd_impl(XIn xin, bool z16, int64_t M, int64_t C, const float* mean, const float* invstd,
                             const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
                             const float* w4, int32_t nout, const float* b4, float* y4, void* stream) {
-  if (!bn_args_ok(x, M, C) || C % HD_COLS != 0 || !mean || !invstd || !w4 || !y4 || nout != HEAD_NOUT ||
-      !aligned16(mean) || !aligned16(invstd) || !vec_ok(mean_lo) || !vec_ok(gamma) || !vec_ok(beta) ||
-      !(p >= 0.f && p < 1.f)) {
-    set_error("bnn_bn_head_fwd: bad arguments (M=%lld C=%lld nout=%d; C %% 64 == 0, nout == 10)", (long long)M,
+  const float* x = reinterpret_cast<const float*>(xin.p);
+  if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % HD_COLS != 0 || !mean || !invstd || !w4 || !y4 ||
+      nout != HEAD_NOUT || !aligned16(mean) || !aligned16(invstd) || !vec_ok(mean_lo) || !vec_ok(gamma) ||
+      !vec_ok(beta) || !(p >= 0.f && p < 1.f)) {
+    set_error("bnn_bn_head_fwd: bad arguments (M=%lld C=%lld nout=%d; C %% 128 == 0, nout == 10)", (long long)M,
               (long long)C, nout);
     return kErrInval;
   }
-  hipLaunchKernelGGL(bn_head_fwd_k<HEAD_NOUT>, dim3((unsigned)((M + HD_ROWS - 1) / HD_ROWS)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), x, M, C, mean, mean_lo, invstd, gamma, beta, w4, b4, y4,
-                     make_drop(p, seed));
+  const dim3 g((unsigned)((M + HD_ROWS - 1) / HD_ROWS));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (z16)
+    hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, true>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
+                       beta, w4, b4, y4, make_drop(p, seed));
+  else
+    hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
+                       beta, w4, b4, y4, make_drop(p, seed));
   return check_launch("bnn_bn_head_fwd");
 }
 
-BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
-                               const float* gamma, const float* beta, const float* save_mean,
+BNN_API int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
+                            const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
+                            const float* w4, int32_t nout, const float* b4, float* y4, void* stream) {
+  return bn_head_fwd_impl(XIn{x, nullptr}, false, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, w4, nout, b4, y4,
+                          stream);
+}
+
+BNN_API int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
+                                const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
+                                float p, uint64_t seed, const float* w4, int32_t nout, const float* b4, float* y4,
+                                void* stream) {
+  return bn_head_fwd_impl(XIn{x16, xbias}, true, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, w4, nout, b4, y4,
+                          stream);
+}
+
+static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float* w4, int32_t nout, int64_t M,
+                               int64_t C, const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
                                float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
                                uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                                void* stream) {
-  if (!bn_args_ok(x, M, C) || C % 256 != 0 || !dy4 || !w4 || !dw4 || nout != HEAD_NOUT || !save_mean ||
-      !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) ||
-      !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !aligned16(w4) || !rlo || !rhi || !rsc || !clo ||
-      !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) ||
-      !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
+  const float* x = reinterpret_cast<const float*>(xin.p);
+  if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % 256 != 0 || !dy4 || !w4 || !dw4 ||
+      nout != HEAD_NOUT || !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) ||
+      !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !aligned16(w4) ||
+      !rlo || !rhi || !rsc || !clo || !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) ||
+      !aligned16(chi) || !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_head_bwd_q6: bad arguments (M=%lld C=%lld nout=%d)", (long long)M, (long long)C, nout);
     return kErrInval;
   }
@@ -1309,20 +1387,50 @@ BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   float* pw = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + bnn_bn_workspace(M, C));
-  hipLaunchKernelGGL(bn_head_reduce_k<HEAD_NOUT>, reduce_grid(M, C), dim3(256), 0, s, x, dy4, w4, M, C, save_mean,
-                     save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
+  if (z16)
+    hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
+  else
+    hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, s, pw, R,
                      (int64_t)nout, C, dw4);
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
   const int64_t qr = q6_rows(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_q6_k<HEAD_NOUT>, dim3((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr)),
-                     dim3(256), 0, s, x, dy4, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, 1, k0, k1,
-                     1.f / (float)M, o, dp, w4, (int)qr);
+  const dim3 g((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr));
+  if (z16)
+    hipLaunchKernelGGL((bn_bwd_apply_q6_k<HEAD_NOUT, true>), g, dim3(256), 0, s, xin, dy4, M, C, save_mean,
+                       save_mean_lo, save_invstd, gamma, beta, 1, k0, k1, 1.f / (float)M, o, dp, w4, (int)qr);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_q6_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, dy4, M, C, save_mean,
+                       save_mean_lo, save_invstd, gamma, beta, 1, k0, k1, 1.f / (float)M, o, dp, w4, (int)qr);
   if (colsum)
     hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_head_bwd_q6");
+}
+
+BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
+                               const float* gamma, const float* beta, const float* save_mean,
+                               const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
+                               float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
+                               uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                               void* stream) {
+  return bn_head_bwd_q6_impl(XIn{x, nullptr}, false, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
+                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, clo, chi, csc, colsum,
+                             work, stream);
+}
+
+BNN_API int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy4, const float* w4,
+                                   int32_t nout, int64_t M, int64_t C, const float* gamma, const float* beta,
+                                   const float* save_mean, const float* save_invstd, const float* save_mean_lo,
+                                   float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, float* dw4,
+                                   uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc,
+                                   float* colsum, void* work, void* stream) {
+  return bn_head_bwd_q6_impl(XIn{x16, xbias}, true, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
+                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, clo, chi, csc, colsum,
+                             work, stream);
 }
 
 BNN_API int bnn_set_seed_counter(const int64_t* ctr) {

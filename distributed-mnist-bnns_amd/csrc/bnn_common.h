@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #define BNN_API extern "C" __attribute__((visibility("default")))
 
@@ -29,6 +30,52 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // Ternary sign as used by the reference (models/binarized_modules.py:13, Tensor.sign()):
 // +1 for x>0, -1 for x<0, 0 for x==0 (NaN maps to 0 here; the reference would propagate NaN).
 __device__ __forceinline__ int tsign(float x) { return (x > 0.f) - (x < 0.f); }
+
+// The input of a BatchNorm pass: fp32 x [M][C], or (z16) the int16 exact dot products I of the
+// ternary BinarizeLinear that produced it (bnn_gemm_fp4_i16) plus that layer's fp32 bias, read as
+// x = fl(I + bias) -- bit-identical to the fp32 value the GEMM epilogue would have stored (it
+// computes the same one rounding), at half the bytes.  bias may be null (a bias-free Linear).
+struct XIn {
+  const void* p;
+  const float* bias;
+};
+
+template <bool Z16>
+__device__ __forceinline__ float4 xin_bias4(const XIn& in, int64_t c) {
+  if constexpr (Z16) {
+    if (in.bias != nullptr) return *reinterpret_cast<const float4*>(in.bias + c);
+  }
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// 4 consecutive elements from flat index idx (a multiple of 4) in two steps -- the raw load
+// (uint2 of 4 int16, or float4) and the conversion with b = xin_bias4 of their columns -- so a
+// software-pipelined pass can issue the load early and convert at use (converting at issue would
+// make the load's first use, and its wait, immediate).
+template <bool Z16>
+using XRaw = typename std::conditional<Z16, uint2, float4>::type;
+
+template <bool Z16>
+__device__ __forceinline__ XRaw<Z16> xin_raw4(const XIn& in, int64_t idx) {
+  if constexpr (Z16)
+    return *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(in.p) + idx);
+  else
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in.p) + idx);
+}
+
+template <bool Z16>
+__device__ __forceinline__ float4 xin_cvt4(const XRaw<Z16>& u, const float4& b) {
+  if constexpr (Z16)
+    return make_float4((float)(int16_t)(u.x & 0xFFFFu) + b.x, (float)(int16_t)(u.x >> 16) + b.y,
+                       (float)(int16_t)(u.y & 0xFFFFu) + b.z, (float)(int16_t)(u.y >> 16) + b.w);
+  else
+    return u;
+}
+
+template <bool Z16>
+__device__ __forceinline__ float4 xin_load4(const XIn& in, int64_t idx, const float4& b) {
+  return xin_cvt4<Z16>(xin_raw4<Z16>(in, idx), b);
+}
 
 // Block-uniform wave index (provably uniform for the compiler -> SGPR).
 __device__ __forceinline__ int wave_id() {

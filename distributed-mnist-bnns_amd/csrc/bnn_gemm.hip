@@ -40,6 +40,9 @@ struct GemmParams {
   const int64_t* row_off;
   const int64_t* col_off;
   double off_mul;
+  // int16 output (ternary x ternary forms without scales, offsets or bias): the exact dot products
+  // |sum| <= K < 2^15 as int16 [M][ldc] instead of fp32 C (bnn_gemm_fp4_i16)
+  int16_t* C16 = nullptr;
 };
 
 __device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
@@ -632,6 +635,20 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
         const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
         if (row >= p.M) continue;
+        if (p.C16 != nullptr) {   // ldc % 4 == 0 (host check): one 8-B store of 4 exact sums
+          int16_t* d16 = p.C16 + (int64_t)row * p.ldc + c0;
+          if (c0 + 3 < p.N) {
+            const uint32_t lo = (uint32_t)(uint16_t)(int16_t)v.x | ((uint32_t)(uint16_t)(int16_t)v.y << 16);
+            const uint32_t hi = (uint32_t)(uint16_t)(int16_t)v.z | ((uint32_t)(uint16_t)(int16_t)v.w << 16);
+            *reinterpret_cast<uint2*>(d16) = make_uint2(lo, hi);
+          } else {
+            const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (c0 + j < p.N) d16[j] = (int16_t)vs[j];
+          }
+          continue;
+        }
         float* dst = p.C + (int64_t)row * p.ldc + c0;
         if (vec_ok && c0 + 3 < p.N) {
           *reinterpret_cast<float4*>(dst) = v;
@@ -832,6 +849,27 @@ BNN_API int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_
   if (M == 0 || N == 0) return 0;
   GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
                nullptr, nullptr, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, nullptr, nullptr, 0.0};
+  return pick_kernel(0, 0, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+BNN_API int bnn_gemm_fp4_i16(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, int16_t* C16,
+                             int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+  // K bytes = 2K ternary products per output: |sum| <= 2K must fit int16
+  if (!C16 || ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(C16) & 7) != 0 || 2 * K > 32767) {
+    set_error("bnn_gemm_fp4_i16: bad arguments (ldc=%lld, K=%lld bytes; ldc %% 4 == 0, 8-B aligned output, "
+              "2K <= 32767)", (long long)ldc, (long long)K);
+    return kErrInval;
+  }
+  if (!A || !B || M < 0 || N < 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K || lda % 16 != 0 ||
+      ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) || M > 0x7fffffff || N > 0x7fffffff ||
+      lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31)) {
+    set_error("bnn_gemm_fp4_i16: bad arguments (M=%lld N=%lld K=%lld bytes)", (long long)M, (long long)N,
+              (long long)K);
+    return kErrInval;
+  }
+  if (M == 0 || N == 0) return 0;
+  GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
+               nullptr, nullptr, nullptr, nullptr, ldc, (int)M, (int)N, (int)K, 0, 0, nullptr, nullptr, 0.0, C16};
   return pick_kernel(0, 0, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 

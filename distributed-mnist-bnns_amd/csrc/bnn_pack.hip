@@ -243,7 +243,8 @@ __device__ __forceinline__ void nib_transpose8(uint32_t (&x)[8]) {
   for (int i = 0; i < 8; i += 2) nib_swap(x[i], x[i + 1], 4, 0x0F0F0F0Fu);
 }
 
-__global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(const float* __restrict__ x, int64_t M, int64_t C,
+template <bool Z16>
+__global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, int64_t C,
                                                            ColAffine af, uint8_t* __restrict__ q, int64_t ldq,
                                                            uint8_t* __restrict__ qt, int64_t ldqt) {
   __shared__ uint32_t img[AP_T * AP_LD];
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(const float* __restri
   const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
   const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
   const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+  const float4 xb = xin_bias4<Z16>(xin, cb);
   uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
 #pragma unroll 4
   for (int i = 0; i < AP_T / 4; ++i) {
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(const float* __restri
     const int64_t m = m0 + r;
     uint32_t code = 0;
     if (m < M) {
-      const float4 f = *reinterpret_cast<const float4*>(x + m * C + cb);
+      const float4 f = xin_load4<Z16>(xin, m * C + cb, xb);
       const float v[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) code |= fp4_code(tsign(fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]))) << (4 * j);
@@ -809,8 +811,8 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
   if (fmt == 1 && q && qt && qt_fmt == 1 && C % AP_T == 0 && af.vec && vec && (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024) {
-    hipLaunchKernelGGL(bn_apply_pack_fp4_k, dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)), dim3(256),
-                       0, S(stream), x, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
+    hipLaunchKernelGGL((bn_apply_pack_fp4_k<false>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+                       dim3(256), 0, S(stream), XIn{x, nullptr}, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
                        reinterpret_cast<uint8_t*>(qt), ldqt);
     return check_launch("bnn_bn_apply_pack");
   }
@@ -824,4 +826,24 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
     hipLaunchKernelGGL((sign_pack_tile_k<0, 1>), dim3((unsigned)gx, gyr), dim3(256), 0, S(stream), x, M,
                        C, C, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, af, rt, gy, AdamArgs{}, qt_fmt);
   return check_launch("bnn_bn_apply_pack");
+}
+
+// bnn_bn_apply_pack for the int16 form of the BatchNorm input (XIn z16: x = fl(I + xbias), the
+// output of bnn_gemm_fp4_i16): FP4 rows + FP4 transpose only, C % 256 == 0, any M.
+BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
+                                  const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
+                                  uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, void* stream) {
+  const ColAffine af{mean, mean_lo, invstd, gamma, beta,
+                     aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
+                         (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
+  if (!x16 || (reinterpret_cast<uintptr_t>(x16) & 7) != 0 || (xbias && !aligned16(xbias)) || !mean || !invstd ||
+      !af.vec || M <= 0 || C <= 0 || C % AP_T != 0 || !q || !qt || ldq < C / 2 || !aligned16(q) ||
+      !qt_ok(reinterpret_cast<const int8_t*>(qt), M, ldqt, 1) || (M + AP_T - 1) / AP_T > 65535) {
+    set_error("bnn_bn_apply_pack_i16: bad arguments (M=%lld C=%lld ldq=%lld ldqt=%lld; C %% 256 == 0)", (long long)M,
+              (long long)C, (long long)ldq, (long long)ldqt);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL((bn_apply_pack_fp4_k<true>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+                     dim3(256), 0, S(stream), XIn{x16, xbias}, M, C, af, q, ldq, qt, ldqt);
+  return check_launch("bnn_bn_apply_pack_i16");
 }

@@ -136,6 +136,13 @@ int bnn_row_sums(const int8_t* q, int64_t N, int64_t K, int64_t ldq, int64_t* ou
 int bnn_gemm_fp4(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
                  float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
 
+/* bnn_gemm_fp4 without bias, writing the exact dot products as int16 C16 [M][ldc] (ldc % 4 == 0,
+ * 8-B aligned; 2K <= 32767 so |sum| fits): the compact pre-activation of a hidden BinarizeLinear
+ * (its z = fl(C16 + bias) is formed by the BatchNorm passes that read it, the *_i16 entries
+ * below), half the bytes of the fp32 output on every pass over it. */
+int bnn_gemm_fp4_i16(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, int16_t* C16, int64_t ldc,
+                     int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
+
 /* Tuning hook (not part of the stable contract): select the bnn_gemm_i8 kernel variant for all
  * later calls in this process; -1 restores the built-in default table (tools/gemm_sweep.py). */
 int bnn_gemm_set_variant(int32_t variant);
@@ -299,7 +306,7 @@ int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const f
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
 
 /* The network's head fused with its BatchNorm (mnist-dist2.py:69-76: fc3 -> drop -> bn3 -> htanh3
- * -> fc4 = nn.Linear(C, nout)), training mode, nout == 10, C % 256 == 0: the fp32 hardtanh
+ * -> fc4 = nn.Linear(C, nout)), training mode, nout == 10, C % 256 == 0 (the forward: C % 128): the fp32 hardtanh
  * output h3 is never written.
  * bnn_bn_head_fwd: y4[m][q] = sum_c h3[m][c] W4[q][c] + b4[q] with h3 = clamp(BN(drop(x)), -1, 1)
  *   formed from x with the statistics of bnn_bn_dropout_fwd_train (y = NULL: statistics only);
@@ -327,6 +334,40 @@ int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_
 int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                       const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
                       int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
+
+/* The int16 form of the BatchNorm input (z16): x16 [M][C] the int16 dot products of
+ * bnn_gemm_fp4_i16 (8-B aligned), xbias [C] that layer's bias (16-B aligned, nullable), read as
+ * x = fl(x16 + xbias) -- the value the fp32 GEMM epilogue stores, so every result is bit-identical
+ * to the fp32 entry on that x.  Training-mode statistics passes only:
+ *   bnn_bn_fwd_train_i16     = bnn_bn_dropout_fwd_train with y = NULL (p = 0: no dropout)
+ *   bnn_bn_apply_pack_i16    = bnn_bn_apply_pack, fmt 1 rows + qt_fmt 1 transpose, C % 256 == 0
+ *   bnn_bn_bwd_q6_i16        = bnn_bn_bwd_q6
+ *   bnn_bn_head_fwd_i16      = bnn_bn_head_fwd
+ *   bnn_bn_head_bwd_q6_i16   = bnn_bn_head_bwd_q6
+ * replaces: the fp32 z = F.linear(sign(h), W_b) + bias (binarized_modules.py:80-83) that the
+ * reference materialises between a hidden BinarizeLinear and its BatchNorm (mnist-dist2.py:66-70). */
+int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                         float* save_mean, float* save_invstd, float* save_mean_lo, float p, uint64_t seed,
+                         void* work, bnn_stream_t stream);
+int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
+                          const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
+                          uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, bnn_stream_t stream);
+int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
+                      const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                      const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx, float* dgamma,
+                      float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi,
+                      uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
+int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
+                        const float* invstd, const float* mean_lo, const float* gamma, const float* beta, float p,
+                        uint64_t seed, const float* w4, int32_t nout, const float* b4, float* y4,
+                        bnn_stream_t stream);
+int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy4, const float* w4, int32_t nout,
+                           int64_t M, int64_t C, const float* gamma, const float* beta, const float* save_mean,
+                           const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed, float* dx,
+                           float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc,
+                           uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                           bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */
