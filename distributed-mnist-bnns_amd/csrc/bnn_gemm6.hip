@@ -216,6 +216,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   static_assert(PP != 1 || (WM == 2 && STAGES == 3 && DIAG == 0), "pipelined form 1: 2 tile rows, 3 stages");
   static_assert(PP != 2 || (WM == 1 && WN % 2 == 0 && STAGES == 3 && DIAG == 0),
                 "pipelined form 2: 1 tile row, an even number of tile columns, 3 stages");
+  static_assert(PP != 3 || (WAVES_M == 2 && WM == 2 && STAGES == 3 && DIAG == 0),
+                "ping-pong form: 2 wave rows (the two groups), 2 tile rows, 3 stages");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_ST = BM * 2, B_ST = BN * 32;
@@ -362,7 +364,72 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
     }
   };
 
-  if constexpr (PP == 2) {
+  if constexpr (PP == 3) {
+    // Ping-pong (cdna_hip_programming.md §5, the 8-phase template's stagger): wave row g = wm is a
+    // group of 4 waves, one per SIMD; group 1 runs one barrier behind group 0, so between two
+    // barriers one group issues its 16 MFMAs while the other issues its fragment reads (and LDS-DMA
+    // pieces) -- every SIMD's matrix pipe is fed by one wave while its partner reads.  Per k-step a
+    // wave runs two phases (A tile 0 with the B fragments, then A tile 1), each {reads, wait for
+    // them, barrier X, MFMAs, barrier Y}.  Reads are waited for BEFORE X, so a slot is free for
+    // the DMA one barrier later; stage kt+2 is issued at k-step kt's phase 0 into the slot of
+    // stage kt-1 (read by both groups two or more barriers earlier); every wave's stage kt+1
+    // pieces are waited for before its phase-1 X barrier, which precedes all reads of stage kt+1.
+    // wave w runs on SIMD w % 4 (grouping by wave parity instead put both of a SIMD's waves in one
+    // group and ran 28% slower): the wave rows are the groups
+    const int grp = wm;
+    auto bar = [&]() __attribute__((always_inline)) { barrier6(); };
+    auto mma_tile_pl = [&](const AFrag& f, const v4i (&bf)[WN], v16f (&ac)[WN]) __attribute__((always_inline)) {
+      const int sb = f.sb;
+      const v8i av[4] = {f.a0, f.a1, f.a2, f.a3};
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        const int sj = sb == 255 ? 255 : sb + 5 * j;
+#pragma unroll
+        for (int u = 0; u < WN; ++u) {
+          const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+          ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av[j], bb, ac[u], 2, 4, 0, sj, 0, 127);
+        }
+      }
+    };
+    auto buf_of = [&](int kt) __attribute__((always_inline)) { return smem + (kt % STAGES) * ST; };
+    if (0 < nk) stage(0, 0);
+    if (1 < nk) stage(1, 1);
+    if (nk >= 2) {
+      if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();
+    } else {
+      wait_vmcnt6<0>();
+    }
+    bar();
+    if (grp == 1) bar();    // the stagger
+    v4i bf[WN];
+    AFrag fa;
+    for (int kt = 0; kt < nk; ++kt) {
+      // phase 0: A tile 0 + B
+      if (kt + 2 < nk) stage(kt + 2, (kt + 2) % STAGES);
+      read_b(buf_of(kt), bf);
+      read_a(buf_of(kt), 0, fa);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+      mma_tile_pl(fa, bf, acc[0]);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // phase 1: A tile 1 (same B)
+      read_a(buf_of(kt), 1, fa);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (kt + 2 < nk) {     // stage kt+1 landed; stage kt+2 may still be in flight
+        if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();
+      } else {
+        wait_vmcnt6<0>();
+      }
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+      mma_tile_pl(fa, bf, acc[1]);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+    if (grp == 0) bar();    // equal barrier counts: group 1 ran one extra at the start
+  } else if constexpr (PP == 2) {
     // form 2: one A fragment per k-step; its MFMAs against B columns [0, WN/2) run while the
     // columns [WN/2, WN) are read, then the barrier retires the next stage and its A fragment and
     // first-half B columns are read while the second-half MFMAs run
@@ -569,6 +636,10 @@ const Variant6 kVariants6[] = {
     // epilogue overlaps the other's MFMAs
     {14, "gemm_fp6_k<1, 4, 2, 4, 2>", launch6<1, 4, 2, 4, 2>, 64},
     {15, "gemm_fp6_k<2, 2, 2, 4, 2>", launch6<2, 2, 2, 4, 2>, 128},
+    // ping-pong: the two wave rows run a phase apart, one group's MFMAs beside the other's reads
+    // (equal to variant 7 within 1% on the wide shapes: the MFMA-busy fraction stays ~0.6 --
+    // profiles/r02_fp6_pingpong.txt)
+    {16, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 3>", launch6<2, 4, 2, 4, 3, 0, 2, 3>, 128},
     // timing-only diagnostics of variant 5 (wrong results; never picked by default)
     {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128},
     {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128},
