@@ -883,25 +883,41 @@ def _q6_take(dy):
     return ent[1:] if ent[0] == _q6_key(dy) else None
 
 
+def _dz_placeholder(M, C, device):
+    """The gradient of a z16 pre-activation: its only reader is the producing linear's backward,
+    which takes the FP6 digits handed to it, so dz itself is never written (a stride-0 tensor of
+    the right shape carries the hand-off)."""
+    return torch.zeros((1,), dtype=torch.float32, device=device).as_strided((M, C), (0, 0))
+
+
+def _q6_take_required(dy):
+    pre = _q6_take(dy)
+    if pre is None and dy.dim() == 2 and dy.stride() == (0, 0):
+        raise RuntimeError("a z16 gradient placeholder lost its FP6 hand-off (was the pre-activation consumed twice?)")
+    return pre
+
+
 def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name, z16=None):
     """BatchNorm(+Dropout) backward that also quantises dz (returned, with the digits attached).
-    z16 = (int16, bias): the input in its compact form (x unused)."""
+    z16 = (int16, bias): the input in its compact form (x unused); dz is then not written (the
+    returned gradient is a placeholder carrying only the digits, _dz_placeholder)."""
     dev = dy.device
-    dx = torch.empty((M, C), dtype=torch.float32, device=dev)
+    dx = torch.empty((M, C), dtype=torch.float32, device=dev) if z16 is None else _dz_placeholder(M, C, dev)
+    dx_ptr = L.ptr(dx) if z16 is None else None
     rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
     Mp = round_up(M)
     cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
-    xb = 8 if z16 is None else 4       # bytes per element read by the two passes over x
-    with _timed(name, 0, xb * M * C + 8 * M * C + 4 * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
+    xb, dzb = (8, 4) if z16 is None else (4, 0)   # bytes per element: two passes over x, the dz write
+    with _timed(name, 0, xb * M * C + 8 * M * C + dzb * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
         if z16 is None:
             L.call("bnn_bn_bwd_q6", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
-                   L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
+                   L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
                    L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
                    L.ptr(ws), L.stream())
         else:
             L.call("bnn_bn_bwd_q6_i16", L.ptr(z16[0]), L.ptr(z16[1]), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
-                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), int(hardtanh), float(p), int(seed), L.ptr(dx), L.ptr(dw),
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw),
                    L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi),
                    L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
     setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
@@ -1062,7 +1078,8 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         dy4 = _c2d(dy4)
         M, C = ctx.dims
         dev = z.device
-        dx = torch.empty((M, C), dtype=torch.float32, device=dev)
+        # z16 input: its producer's backward takes the digits; dz itself is never written
+        dx = _dz_placeholder(M, C, dev) if ctx.z16 else torch.empty((M, C), dtype=torch.float32, device=dev)
         dgw = torch.empty((C,), dtype=torch.float32, device=dev) if gw is not None else None
         dgb = torch.empty((C,), dtype=torch.float32, device=dev) if gb is not None else None
         dw4 = torch.empty((HEAD_NOUT, C), dtype=torch.float32, device=dev)
@@ -1071,7 +1088,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
         cs = torch.empty((C,), dtype=torch.float32, device=dev)
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, HEAD_NOUT),), dtype=torch.uint8, device=dev)
-        with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + 4 * M * C + 6 * M * C):
+        with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + (0 if ctx.z16 else 4) * M * C + 6 * M * C):
             if not ctx.z16:
                 L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw),
                        L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx),
@@ -1080,10 +1097,10 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
             else:
                 L.call("bnn_bn_head_bwd_q6_i16", L.ptr(z), L.ptr(zb), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C,
                        L.ptr(gw), L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed),
-                       L.ptr(dx), L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
+                       None, L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
                        L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws),
                        L.stream())
-        if ctx.q6:
+        if ctx.q6 or ctx.z16:
             setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
         db4 = dy4.sum(0) if ctx.has_b4 and ctx.needs_input_grad[10] else None
         return (dx, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
@@ -1298,10 +1315,11 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
     def backward(ctx, dy):
         z, gw, gb, mean, invstd, mlo, qt, wqt, zb = ctx.saved_tensors
         M, C, N = ctx.dims
-        dy = _c2d(dy)
+        pre = _q6_take_required(dy) if ctx.fp6 else None       # digits of dy from the BatchNorm backward
+        if pre is None:
+            dy = _c2d(dy)
         dz = dgw = dgb = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[9]
-        pre = _q6_take(dy) if ctx.fp6 else None       # digits of dy from the BatchNorm backward
         if ctx.needs_input_grad[8] or need_db:
             if pre is not None:
                 dt, cs = pre[1], (pre[2] if need_db else None)
