@@ -72,6 +72,8 @@ SIGNATURES = {
     "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
     "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P,
                                      P, P, P, P]),
+    "bnn_bn_bwd_i8cols_workspace": (I64, [I64, I64]),
+    "bnn_bn_bwd_i8cols": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,

@@ -438,6 +438,16 @@ def _z16_of(x):
     return getattr(x, _Z16_ATTR, None)
 
 
+def _grad_sink(w):
+    """(view, exchange) when a GradExchange lets this weight's gradient be written straight into
+    its bucket view (parallel.GradExchange direct_write), else (None, None)."""
+    ex = getattr(w, "_bnn_grad_sink", None)
+    if ex is None:
+        return None, None
+    v = ex.grad_sink(w)
+    return (v, ex) if v is not None and v.is_contiguous() and v.shape == w.shape else (None, None)
+
+
 def gemm_xnor(a_bits, b_bits, M, N, bias=None):
     """XNOR-popcount GEMM on (sign, nonzero) bit-plane pairs; same result as the (1,1) int8 form."""
     (As, An), (Bs, Bn) = a_bits, b_bits
@@ -697,6 +707,8 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
                            bias=bias.detach() if bias is not None else None, col_off=R, off_mul=s0, k_true=K,
                            label="pixels")
         ctx.save_for_backward(qt)
+        if I8C_HANDOFF and need_dw:
+            setattr(y, _I8C_WANT, True)
         return y
 
     @staticmethod
@@ -709,9 +721,14 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
         if M == 0:
             return (None, torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
                     torch.zeros((N,), dtype=torch.float32, device=dev) if need_db else None, None, None, None)
-        dy = _c2d(dy)
+        pre = _i8c_take(dy)          # the digits straight from the BatchNorm backward, if it made them
+        if pre is None:
+            dy = _c2d(dy)
         if ctx.needs_input_grad[1] or need_db:
-            dt, sc, cs, ds = quant_cols_t(dy, want_colsum=need_db, want_dsum=True)   # dY^T digits, T[n]
+            if pre is not None:
+                dt, sc, cs, ds = pre
+            else:
+                dt, sc, cs, ds = quant_cols_t(dy, want_colsum=need_db, want_dsum=True)   # dY^T digits, T[n]
             if ctx.needs_input_grad[1]:
                 dw = gemm_i8_affine(dt, 3, qt, 1, N, K, a_scale=sc, b_scale=_const_vec(ctx.a, K, dev),
                                     row_off=ds, off_mul=ctx.s0, k_true=M, label="pixels")
@@ -922,6 +939,43 @@ def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, 
                    L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
     setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
     return dx
+
+
+# int8 column digits of dz handed from the BatchNorm backward to the input layer's weight gradient
+# (bnn_bn_bwd_i8cols -> BinaryLinearPixelsFunction.backward): the pixel layer needs dz only as the
+# digit planes of dz^T (with scales, column sums and exact digit sums), so dz is never written.
+_I8C_ATTR = "_bnn_i8c"
+_I8C_WANT = "_bnn_i8c_consumer"
+I8C_HANDOFF = True
+
+
+def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db):
+    dev = x.device
+    ldqt = round_up(M)
+    dg = torch.empty((3, C, ldqt), dtype=torch.int8, device=dev)
+    sc = torch.empty((C,), dtype=torch.float32, device=dev)
+    cs = torch.empty((C,), dtype=torch.float32, device=dev)
+    ds = torch.empty((C,), dtype=torch.int64, device=dev)
+    ws = torch.empty((L.lib().bnn_bn_bwd_i8cols_workspace(M, C),), dtype=torch.uint8, device=dev)
+    with _timed("bn_bwd_i8cols", 0, 24 * M * C + dg.numel()):
+        L.call("bnn_bn_bwd_i8cols", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+               L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc), L.ptr(cs), L.ptr(ds),
+               L.ptr(ws), L.stream())
+    dz = _dz_placeholder(M, C, dev)
+    setattr(dz, _I8C_ATTR, (_q6_key(dz), dg, sc, cs, ds))
+    return dz
+
+
+def _i8c_take(dy):
+    ent = getattr(dy, _I8C_ATTR, None)
+    if ent is None:
+        if dy.dim() == 2 and dy.stride() == (0, 0):
+            raise RuntimeError("a gradient placeholder lost its int8 column-digit hand-off")
+        return None
+    delattr(dy, _I8C_ATTR)
+    if ent[0] != _q6_key(dy):
+        raise RuntimeError("stale int8 column-digit hand-off")
+    return ent[1:]
 
 
 class BatchNormHardtanhFunction(torch.autograd.Function):
@@ -1248,6 +1302,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
     def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend, emit_z16=False):
         _check(z, bn_w, bn_b, rm, rv, weight, bias)
         ctx.q6 = _q6_wanted(z, z.shape[-1], training)
+        ctx.i8c = (I8C_HANDOFF and bool(getattr(z, _I8C_WANT, False)) and training and not ctx.q6
+                   and z.dim() == 2 and z.shape[-1] % 4 == 0)
         zz = _z16_of(z)                       # (int16, bias): z in its compact form
         if zz is None:
             z = _c2d(z)
@@ -1304,6 +1360,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         else:
             ctx.save_for_backward(zz[0], gw, gb, mean, invstd, mlo, qt, wqt, zz[1])
         ctx.z16 = zz is not None
+        ctx.weight_ref = weight
         ctx.training = training
         ctx.dims = (M, C, N)
         ctx.has_bias = bias is not None
@@ -1320,15 +1377,16 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             dy = _c2d(dy)
         dz = dgw = dgb = dw = db = None
         need_db = ctx.has_bias and ctx.needs_input_grad[9]
+        sink, ex = _grad_sink(ctx.weight_ref) if ctx.needs_input_grad[8] and ctx.fp6 else (None, None)
         if ctx.needs_input_grad[8] or need_db:
-            if pre is not None:
-                dt, cs = pre[1], (pre[2] if need_db else None)
+            if ctx.fp6:
+                dt, cs = (pre[1], (pre[2] if need_db else None)) if pre is not None else \
+                    quant6_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[8]:
-                    dw = gemm_fp6(dt, qt, C, k_true=M)
-            elif ctx.fp6:
-                dt, cs = quant6_cols_t(dy, want_colsum=need_db)
-                if ctx.needs_input_grad[8]:
-                    dw = gemm_fp6(dt, qt, C, k_true=M)                         # dY^T . sign(h)
+                    dw = gemm_fp6(dt, qt, C, k_true=M, out=sink)               # dY^T . sign(h)
+                    if sink is not None:        # written into the bucket view: nothing to accumulate
+                        ex.grad_written(ctx.weight_ref)
+                        dw = None
             else:
                 dt, sc, cs = quant_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[8]:
@@ -1347,6 +1405,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             if ctx.q6:
                 dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6",
                                 z16=(z, zb) if ctx.z16 else None)
+            elif ctx.i8c:
+                dz = _bn_bwd_i8c(z, dh, M, C, gw, gb, mean, invstd, mlo, dgw, dgb)
             else:
                 dz = torch.empty_like(z)
                 with _timed("bn_bwd", 0, 16 * M * C):

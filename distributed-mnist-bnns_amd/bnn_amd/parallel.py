@@ -24,7 +24,13 @@ MI355X design:
   every rank; ``finish()`` joins them before the optimizer.  With RCCL the reduction is
   ``ReduceOp.AVG``; gloo (CPU tests) has no AVG, so it sums and divides;
 * DDP's per-forward buffer broadcast is ONE collective per device over a flat byte staging
-  buffer (not one per running_mean / running_var / num_batches_tracked).
+  buffer (not one per running_mean / running_var / num_batches_tracked);
+* direct write (``direct_write=True``): a libbnn layer whose weight gradient is one GEMM writes it
+  straight into the weight's bucket view (functional._grad_sink) and reports it
+  (``grad_written``), instead of returning a fresh tensor that autograd's AccumulateGrad then adds
+  into the zeroed view -- one read-modify-write pass over the 563 MB of wide-MLP gradients fewer
+  per step.  Valid while each weight gets one gradient per backward (no accumulation across
+  micro-batches); the sink is armed by ``zero_grad`` and disarmed once the weight is written.
 """
 import math
 
@@ -53,7 +59,7 @@ class _Bucket:
 
 class GradExchange:
     def __init__(self, module, process_group=None, bucket_mb=64, broadcast_buffers=True,
-                 init_broadcast=True):
+                 init_broadcast=True, direct_write=True):
         if not dist.is_available() or not dist.is_initialized():
             raise RuntimeError("GradExchange needs an initialised torch.distributed process group")
         self.module = module
@@ -72,8 +78,13 @@ class GradExchange:
         self.buckets, self._param_buckets, self._flats = self._build_buckets(list(reversed(params)))
         self._next = 0
         self._handles = []
+        self._armed = set()        # weights whose zeroed bucket view a layer may overwrite
+        self.direct_write = direct_write
+        self.direct_writes = 0     # gradients written straight into their views (tests, logs)
         for p in params:
             self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(self._param_buckets[p])))
+            if direct_write:
+                p._bnn_grad_sink = self
         if broadcast_buffers:
             self._handles.append(module.register_forward_pre_hook(lambda m, inp: self.sync_buffers()))
 
@@ -181,6 +192,23 @@ class GradExchange:
             b.pending = b.nparams
             b.work = None
         self._next = 0
+        if self.direct_write:
+            self._armed = {id(p) for _, plist, _ in self._flats for p in plist}
+
+    def grad_sink(self, p):
+        """The zeroed bucket view a layer's backward may write p's whole gradient into, or None
+        (not armed: outside zero_grad .. backward, or already written this step)."""
+        if id(p) not in self._armed:
+            return None
+        return p.grad
+
+    def grad_written(self, p):
+        """p's gradient was written into its view by the layer (what the accumulate hook reports)."""
+        self._armed.discard(id(p))
+        self.direct_writes += 1
+        for bi in self._param_buckets[p]:
+            self.buckets[bi].pending -= 1
+        self._launch_ready()
 
     @staticmethod
     def _is_view(p, flat):
@@ -193,6 +221,7 @@ class GradExchange:
 
     def _make_hook(self, bucket_ids):
         def hook(p):
+            self._armed.discard(id(p))
             for bi in bucket_ids:
                 self.buckets[bi].pending -= 1
             self._launch_ready()
@@ -208,6 +237,7 @@ class GradExchange:
 
     def finish(self):
         """Join all bucket reductions (launching any a hook did not reach, e.g. unused params)."""
+        self._armed = set()
         for b in self.buckets:
             b.pending = 0
         self._launch_ready()
@@ -222,3 +252,8 @@ class GradExchange:
         for h in self._handles:
             h.remove()
         self._handles = []
+        self._armed = set()
+        for _, plist, _ in self._flats:
+            for p in plist:
+                if getattr(p, "_bnn_grad_sink", None) is self:
+                    del p._bnn_grad_sink

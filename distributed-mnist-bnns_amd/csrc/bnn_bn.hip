@@ -412,12 +412,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
     drop4m(dp, km, xs);
     float o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float xh = ((xs[j] - ms[j]) - lo[j]) * is[j];
-      const float yv = fmaf(xh, ga[j], be[j]);
-      const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
-      o[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
-    }
+    for (int j = 0; j < 4; ++j) o[j] = bn_dz1(xs[j], gs[j], ms[j], lo[j], is[j], ga[j], be[j], a0[j], a1[j], hardtanh);
     drop4m(dp, km, o);   // dropout backward: grad * mask * scale
     *reinterpret_cast<float4*>(dx + r * C + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
@@ -555,12 +550,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q6_k(XIn xin, const float* _
         const uint32_t km = dp.on ? drop_bits4(dp, (uint64_t)(r * C + c)) : 0u;
         drop4m(dp, km, xs);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xh = ((xs[j] - ms[j]) - lo[j]) * is[j];
-          const float yv = fmaf(xh, ga[j], be[j]);
-          const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? gs[j] : 0.f;
-          v[j] = ga[j] * is[j] * (g - a0[j] - xh * a1[j]);
-        }
+        for (int j = 0; j < 4; ++j)
+          v[j] = bn_dz1(xs[j], gs[j], ms[j], lo[j], is[j], ga[j], be[j], a0[j], a1[j], hardtanh);
         drop4m(dp, km, v);
         if (o.dx) *reinterpret_cast<float4*>(o.dx + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
       }
@@ -1230,6 +1221,34 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
   }
   return check_launch("bnn_bn_bwd");
 }
+
+namespace bnn {
+int64_t bn_workspace_bytes(int64_t M, int64_t C) { return bnn_bn_workspace(M, C); }
+
+// The statistics half of the training-mode backward (bnn_bn_bwd without its apply pass): k0 =
+// sum g, k1 = sum g*xhat per column (and dgamma / dbeta) in `work` (bnn_bn_workspace bytes).
+// For passes in other files that form dz themselves (bnn_bn_bwd_i8cols, bnn_pack.hip).
+int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
+                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out) {
+  if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work || !vec_ok(gamma) ||
+      !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo)) {
+    set_error("bn_bwd_sums: bad arguments");
+    return kErrInval;
+  }
+  const int64_t R = bn_chunks(M, C);
+  double* p0 = reinterpret_cast<double*>(work);
+  double* p1 = p0 + R * C;
+  float* k0 = reinterpret_cast<float*>(p1 + R * C);
+  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
+  hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C, save_mean,
+                     save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), make_drop(0.f, 0));
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  *k0_out = k0;
+  *k1_out = k1;
+  return check_launch("bn_bwd_sums");
+}
+}  // namespace bnn
 
 BNN_API int bnn_bn_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd,

@@ -77,6 +77,21 @@ __device__ __forceinline__ float4 xin_load4(const XIn& in, int64_t idx, const fl
   return xin_cvt4<Z16>(xin_raw4<Z16>(in, idx), b);
 }
 
+// The training-mode BatchNorm(+Hardtanh) backward for one element (mnist-dist2.py:66-74): with
+// xh = ((x - mean) - mean_lo) * invstd, y = xh*gamma + beta, g = dy masked by -1 < y < 1,
+// dz = gamma*invstd*(g - a0 - xh*a1), a0 = sum(g)/M, a1 = sum(g*xh)/M.  One definition for every
+// pass that forms dz (bn_bwd_apply_k, the fused FP6 and int8 quantising passes), so they agree
+// bit for bit.
+__device__ __forceinline__ float bn_dz1(float x, float g, float m, float lo, float is, float ga, float be, float a0,
+                                        float a1, int hardtanh) {
+  // no mul+add contraction: the rounding must not depend on the kernel this is inlined into
+#pragma clang fp contract(off)
+  const float xh = ((x - m) - lo) * is;
+  const float yv = fmaf(xh, ga, be);
+  const float gg = (!hardtanh || (yv > -1.f && yv < 1.f)) ? g : 0.f;
+  return ga * is * (gg - a0 - xh * a1);
+}
+
 // Block-uniform wave index (provably uniform for the compiler -> SGPR).
 __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -483,6 +483,47 @@ __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax
   if (dsum != nullptr) dsum[n] = 0;   // quant_cols_t_k accumulates the digit sums into it
 }
 
+// quant_cols_t_k's second half, shared with bn_dz_quant_cols_t_k: the 64 x 64 tile of packed
+// digits (row m, column n) written transposed as 3 int8 planes dt[d][n][m], plus the exact digit
+// column sums.  Call after the tile is complete (__syncthreads).
+__device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int t, int64_t n0, int64_t m0, int64_t N,
+                                          int64_t ldqt, int64_t plane, int8_t* __restrict__ dt,
+                                          int64_t* __restrict__ dsum) {
+  const int nn = t >> 2, mc = (t & 3) * 16;
+  const int64_t n = n0 + nn;
+  if (n < N && m0 + mc < ldqt) {
+    int g[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][nn];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int sh8 = 8 * d;
+      v4i w;
+      w.x = pack4(g[0] >> sh8, g[1] >> sh8, g[2] >> sh8, g[3] >> sh8);
+      w.y = pack4(g[4] >> sh8, g[5] >> sh8, g[6] >> sh8, g[7] >> sh8);
+      w.z = pack4(g[8] >> sh8, g[9] >> sh8, g[10] >> sh8, g[11] >> sh8);
+      w.w = pack4(g[12] >> sh8, g[13] >> sh8, g[14] >> sh8, g[15] >> sh8);
+      *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc) = w;
+    }
+  }
+  if (dsum != nullptr) {
+    // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22
+    // each, so 64 of them fit an int); the 4 lanes sharing n are adjacent
+    int part = 0;
+    if (n < N && m0 + mc < ldqt) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int g = tile[mc + j][nn];
+        part += (int)(int8_t)(g & 255) + 256 * (int)(int8_t)((g >> 8) & 255) + 65536 * (int)(int8_t)((g >> 16) & 255);
+      }
+    }
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    if ((t & 3) == 0 && n < N && part != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n), (unsigned long long)(long long)part);
+  }
+}
+
 __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ x, int64_t M,
                                                       int64_t N, int64_t ldx,
                                                       const float* __restrict__ scale,
@@ -517,39 +558,123 @@ __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ 
     tile[r][c + j] = packed;
   }
   __syncthreads();
-  const int nn = t >> 2, mc = (t & 3) * 16;
-  const int64_t n = n0 + nn;
-  if (n < N && m0 + mc < ldqt) {
-    int g[16];
+  qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum);
+}
+
+// ------------------------------------------------------------------ BatchNorm backward -> dz^T int8 digits
+// The input layer's weight gradient dW1 = dz^T . x (the first BinarizeLinear, fed by u8 pixels:
+// bnn_gemm_i8_affine) needs dz only as the int8 digit planes of its columns.  These two passes form
+// dz from (x, dy) with bn_dz1 -- the exact value bnn_bn_bwd writes -- and never store it: pass 1
+// is colstats4_k on dz (per-chunk column absmax and double sums), pass 2 quant_cols_t_k on dz.
+// Bit-identical to bnn_quant_cols_t_dsum(bnn_bn_bwd(...)).
+struct BnCols {
+  const float *mean, *mean_lo, *invstd, *gamma, *beta, *k0, *k1;
+  float inv_n;
+  int hardtanh;
+};
+
+struct Bn4 {
+  float m[4], lo[4], is[4], ga[4], be[4], a0[4], a1[4];
+};
+
+__device__ __forceinline__ void bn4_load(const BnCols& b, int64_t c, Bn4& o) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][nn];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const int sh8 = 8 * d;
-      v4i w;
-      w.x = pack4(g[0] >> sh8, g[1] >> sh8, g[2] >> sh8, g[3] >> sh8);
-      w.y = pack4(g[4] >> sh8, g[5] >> sh8, g[6] >> sh8, g[7] >> sh8);
-      w.z = pack4(g[8] >> sh8, g[9] >> sh8, g[10] >> sh8, g[11] >> sh8);
-      w.w = pack4(g[12] >> sh8, g[13] >> sh8, g[14] >> sh8, g[15] >> sh8);
-      *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc) = w;
-    }
+  for (int j = 0; j < 4; ++j) {
+    o.m[j] = b.mean[c + j];
+    o.lo[j] = b.mean_lo ? b.mean_lo[c + j] : 0.f;
+    o.is[j] = b.invstd[c + j];
+    o.ga[j] = b.gamma ? b.gamma[c + j] : 1.f;
+    o.be[j] = b.beta ? b.beta[c + j] : 0.f;
+    o.a0[j] = b.k0[c + j] * b.inv_n;
+    o.a1[j] = b.k1[c + j] * b.inv_n;
   }
-  if (dsum != nullptr) {
-    // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22
-    // each, so 64 of them fit an int); the 4 lanes sharing n are adjacent
-    int part = 0;
-    if (n < N && m0 + mc < ldqt) {
+}
+
+__global__ __launch_bounds__(256) void bn_dz_colstats4_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int64_t M, int64_t N, BnCols bc, float* __restrict__ pmax,
+                                                         double* __restrict__ psum, int64_t crows) {
+  const int64_t n = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * crows;
+  if (n >= N) return;
+  const int64_t r1 = (M < r0 + crows) ? M : r0 + crows;
+  Bn4 b;
+  bn4_load(bc, n, b);
+  float amax[4] = {0.f, 0.f, 0.f, 0.f};
+  double sum[4] = {0.0, 0.0, 0.0, 0.0};
+  constexpr int RB = 8;   // rows whose loads are issued together
+  for (int64_t rb = r0; rb < r1; rb += RB) {
+    float4 xv[RB], gv[RB];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int g = tile[mc + j][nn];
-        part += (int)(int8_t)(g & 255) + 256 * (int)(int8_t)((g >> 8) & 255) + 65536 * (int)(int8_t)((g >> 16) & 255);
+    for (int u = 0; u < RB; ++u) {
+      const int64_t r = rb + u < r1 ? rb + u : r1 - 1;
+      xv[u] = *reinterpret_cast<const float4*>(x + r * N + n);
+      gv[u] = *reinterpret_cast<const float4*>(dy + r * N + n);
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      if (rb + u >= r1) break;
+      const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w}, gs[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
+        amax[j] = absmax_acc(amax[j], v);
+        sum[j] += (double)v;
       }
     }
-    part += __shfl_xor(part, 1, 64);
-    part += __shfl_xor(part, 2, 64);
-    if ((t & 3) == 0 && n < N && part != 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n), (unsigned long long)(long long)part);
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pmax[blockIdx.y * N + n + j] = amax[j];
+    psum[blockIdx.y * N + n + j] = sum[j];
+  }
+}
+
+// 64 x 64 tile; stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread needs the
+// BatchNorm parameters of 4 columns only; stage 2: qct_store
+__global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                            int64_t M, int64_t N, BnCols bc,
+                                                            const float* __restrict__ scale, int8_t* __restrict__ dt,
+                                                            int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum) {
+  __shared__ int tile[TILE][TILE + 1];
+  const int64_t n0 = (int64_t)blockIdx.x * TILE, m0 = (int64_t)blockIdx.y * TILE;
+  const int t = threadIdx.x, cg = t & 15, rg = t >> 4;
+  const int64_t c = n0 + 4 * cg;
+  Bn4 b;
+  int sft[4];
+  if (c < N) {
+    bn4_load(bc, c, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float s = scale[c + j];
+      sft[j] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;   // INT32_MIN -> digits 0
+    }
+  }
+  float4 xv[4], gv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + 4 * rg + i;
+    if (c < N && m < M) {
+      xv[i] = *reinterpret_cast<const float4*>(x + m * N + c);
+      gv[i] = *reinterpret_cast<const float4*>(dy + m * N + c);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + 4 * rg + i;
+    const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int packed = 0;
+      if (c < N && m < M && sft[j] != INT32_MIN) {
+        const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
+        const Digits d = to_digits(v, sft[j]);
+        packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
+      }
+      tile[4 * rg + i][4 * cg + j] = packed;
+    }
+  }
+  __syncthreads();
+  qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum);
 }
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -846,4 +971,46 @@ BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_
   hipLaunchKernelGGL((bn_apply_pack_fp4_k<true>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                      dim3(256), 0, S(stream), XIn{x16, xbias}, M, C, af, q, ldq, qt, ldqt);
   return check_launch("bnn_bn_apply_pack_i16");
+}
+
+namespace bnn {
+int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
+                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out);
+int64_t bn_workspace_bytes(int64_t M, int64_t C);
+}  // namespace bnn
+
+BNN_API int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C) {
+  return round_up(bn_workspace_bytes(M, C), 256) + bnn_quant_cols_workspace(M, C);
+}
+
+BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                              const float* beta, const float* save_mean, const float* save_invstd,
+                              const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
+                              int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
+                              int64_t* dsum, void* work, void* stream) {
+  if (!x || !dy || !digits_t || !scale || !work || M <= 0 || C <= 0 || C % 4 != 0 || !aligned16(x) ||
+      !aligned16(dy) || ldqt % TILE != 0 || ldqt < round_up(M, TILE) || plane < C * ldqt || plane % 16 != 0 ||
+      !aligned16(digits_t) || col_chunks(M, C) > 65535 || ldqt / TILE > 65535) {
+    set_error("bnn_bn_bwd_i8cols: bad arguments (M=%lld C=%lld ldqt=%lld plane=%lld)", (long long)M, (long long)C,
+              (long long)ldqt, (long long)plane);
+    return kErrInval;
+  }
+  hipStream_t s = S(stream);
+  const float *k0, *k1;
+  int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta, work, s,
+                       &k0, &k1);
+  if (rc) return rc;
+  char* qw = reinterpret_cast<char*>(work) + round_up(bn_workspace_bytes(M, C), 256);
+  const int64_t R = col_chunks(M, C);
+  float* pmax = reinterpret_cast<float*>(qw);
+  double* psum = reinterpret_cast<double*>(qw + round_up(R * C * (int64_t)sizeof(float), 256));
+  const BnCols bc{save_mean, save_mean_lo, save_invstd, gamma, beta, k0, k1, 1.f / (float)M, hardtanh};
+  hipLaunchKernelGGL(bn_dz_colstats4_k, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy, M,
+                     C, bc, pmax, psum, col_chunk_rows(M, C));
+  hipLaunchKernelGGL(colfinal_k, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, s, pmax, psum, C, R, scale, colsum,
+                     dsum);
+  hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)(ldqt / TILE)), dim3(256),
+                     0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum);
+  return check_launch("bnn_bn_bwd_i8cols");
 }

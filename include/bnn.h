@@ -369,6 +369,19 @@ int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* 
                            uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                            bnn_stream_t stream);
 
+/* The BatchNorm(+Hardtanh) backward feeding the first BinarizeLinear's weight gradient on u8
+ * pixels (mnist-dist2.py:52-54 fc1 -> bn1 -> htanh1; dW1 = dz^T . x on bnn_gemm_i8_affine): dz is
+ * formed from (x, dy) exactly as bnn_bn_bwd writes it, but only delivered as what that GEMM reads --
+ * bnn_quant_cols_t_dsum's outputs (3 int8 digit planes of dz^T, per-column scale, colsum = the
+ * bias gradient, dsum = exact digit sums) -- bit-identical to bnn_bn_bwd + bnn_quant_cols_t_dsum,
+ * without writing or re-reading dz.  Training statistics, no dropout; dgamma/dbeta as bnn_bn_bwd.
+ * work: bnn_bn_bwd_i8cols_workspace(M, C) bytes. */
+int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C);
+int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                      const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
+                      float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale,
+                      float* colsum, int64_t* dsum, void* work, bnn_stream_t stream);
+
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */
 int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_stream_t stream);

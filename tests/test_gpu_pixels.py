@@ -175,3 +175,58 @@ def test_net_on_pixels_drop_in(F, t10k):
     dead = ~t10k[:512].any(0)
     w1 = host(m.fc1.weight)
     assert np.array_equal(w1[:, dead], w0[:, dead]) and not np.array_equal(w1, w0)
+
+
+@pytest.mark.parametrize("M,C", [(1000, 512), (4096, 768), (77, 64)])
+def test_bn_bwd_i8cols_bit_identical(F, M, C):
+    """bnn_bn_bwd_i8cols (dz formed from x, dy twice, never stored) equals bnn_bn_bwd followed by
+    bnn_quant_cols_t_dsum on the written dz: digit planes, scales, column sums (dB), exact digit
+    sums (T) and dgamma / dbeta -- bit for bit."""
+    from bnn_amd import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(M + C)
+    x = (torch.randint(-40, 41, (M, C), generator=g, device="cuda").float() + 0.37)
+    dy = torch.randn(M, C, generator=g, device="cuda")
+    dy[:, 3] = 0.0                                    # an all-zero gradient column: scale 0
+    gam = torch.rand(C, generator=g, device="cuda") + 0.5
+    bet = torch.rand(C, generator=g, device="cuda") - 0.5
+    mean, invstd, lo = (torch.empty(C, device="cuda") for _ in range(3))
+    ws = torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device="cuda")
+    L.call("bnn_bn_fwd_train", L.ptr(x), M, C, L.ptr(gam), L.ptr(bet), None, None, -1.0, 1e-5, L.ptr(mean),
+           L.ptr(invstd), L.ptr(lo), None, 1, L.ptr(ws), L.stream())
+    dz = torch.empty(M, C, device="cuda")
+    dg_a, db_a = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    L.call("bnn_bn_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(lo), 1,
+           L.ptr(dz), L.ptr(dg_a), L.ptr(db_a), L.ptr(ws), L.stream())
+    ref = F.quant_cols_t(dz, want_colsum=True, want_dsum=True)
+    dg_b, db_b = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    out = F._bn_bwd_i8c(x, dy, M, C, gam, bet, mean, invstd, lo, dg_b, db_b)
+    got = F._i8c_take(out)
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert torch.equal(dg_a, dg_b) and torch.equal(db_a, db_b)
+
+
+def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
+    """A fused MLP training step on u8 pixels with the fc1 weight gradient fed by the int8
+    column-digit hand-off equals the step with the hand-off off (dz written, re-read, quantised)."""
+    from bnn_amd import nets
+    g = torch.Generator(device="cuda").manual_seed(7)
+    u = torch.randint(0, 256, (2048, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    u[:, :, :3] = 0                                   # dead pixels: exact-zero weight gradients
+    y = torch.randint(0, 10, (2048,), generator=g, device="cuda")
+    grads = []
+    for on in (True, False):
+        F.I8C_HANDOFF = on
+        try:
+            torch.manual_seed(0)
+            m = nets.MLP(1024, 512, 256, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+            torch.manual_seed(1)
+            torch.nn.CrossEntropyLoss()(m(u), y).backward()
+            grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
+        finally:
+            F.I8C_HANDOFF = True
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+    dead = grads[0]["fc1.weight"].view(1024, 28, 28)[:, :3]
+    assert not dead.any()
