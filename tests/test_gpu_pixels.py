@@ -222,7 +222,9 @@ def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
             torch.manual_seed(0)
             m = nets.MLP(1024, 512, 256, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
             torch.manual_seed(1)
+            n0 = F.I8C_HANDOFFS
             torch.nn.CrossEntropyLoss()(m(u), y).backward()
+            assert F.I8C_HANDOFFS - n0 == (1 if on else 0)
             grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
         finally:
             F.I8C_HANDOFF = True
