@@ -47,7 +47,8 @@ __device__ __forceinline__ void digits4(float x, int shift, int (&d)[4]) {
 // The four plane codes of rint(x * 2^shift) (|.| <= 2^19) without the digit arithmetic: with
 // w = v + 16 * (1 + 32 + 1024 + 32768) >= 0, the balanced digits are d_j = e_j - 16 for the plain
 // base-32 digits e_j of w (e_3 = w >> 15 unmasked, <= 32), and the e2m3 code of d = e - 16 is
-// e - 16 for e >= 16, else 32 | (16 - e) = 48 - e.  Bit-identical to digits4 + e2m3_code.
+// e - 16 for e >= 16, else 32 | (16 - e) = 48 - e, i.e. min(e - 16, 48 - e) in unsigned arithmetic.
+// Bit-identical to digits4 + e2m3_code.
 constexpr int DIGIT_BIAS = 16 * (1 + 32 + 1024 + 32768);
 
 __device__ __forceinline__ void codes4(float x, int shift, uint32_t (&c)[4]) {
@@ -55,7 +56,8 @@ __device__ __forceinline__ void codes4(float x, int shift, uint32_t (&c)[4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t e = j < 3 ? __builtin_amdgcn_ubfe(w, 5 * j, 5) : (w >> 15);
-    c[j] = e >= 16u ? e - 16u : 48u - e;
+    // e >= 16: e - 16 (<= 16) < 48 - e; e < 16: e - 16 wraps above 48 - e -- one unsigned min
+    c[j] = min(e - 16u, 48u - e);
   }
 }
 

@@ -577,16 +577,24 @@ struct Bn4 {
   float m[4], lo[4], is[4], ga[4], be[4], a0[4], a1[4];
 };
 
+__device__ __forceinline__ void ld4a(const float* p, int64_t c, float dflt, float (&o)[4]) {
+  const float4 v = p ? *reinterpret_cast<const float4*>(p + c) : make_float4(dflt, dflt, dflt, dflt);
+  o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
+}
+
+// the 4 columns' parameters with 16-B loads (C % 4 == 0, vectors 16-B aligned: host check)
 __device__ __forceinline__ void bn4_load(const BnCols& b, int64_t c, Bn4& o) {
+  ld4a(b.mean, c, 0.f, o.m);
+  ld4a(b.mean_lo, c, 0.f, o.lo);
+  ld4a(b.invstd, c, 0.f, o.is);
+  ld4a(b.gamma, c, 1.f, o.ga);
+  ld4a(b.beta, c, 0.f, o.be);
+  ld4a(b.k0, c, 0.f, o.a0);
+  ld4a(b.k1, c, 0.f, o.a1);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    o.m[j] = b.mean[c + j];
-    o.lo[j] = b.mean_lo ? b.mean_lo[c + j] : 0.f;
-    o.is[j] = b.invstd[c + j];
-    o.ga[j] = b.gamma ? b.gamma[c + j] : 1.f;
-    o.be[j] = b.beta ? b.beta[c + j] : 0.f;
-    o.a0[j] = b.k0[c + j] * b.inv_n;
-    o.a1[j] = b.k1[c + j] * b.inv_n;
+    o.a0[j] *= b.inv_n;
+    o.a1[j] *= b.inv_n;
   }
 }
 
@@ -629,14 +637,17 @@ __global__ __launch_bounds__(256) void bn_dz_colstats4_k(const float* __restrict
   }
 }
 
-// 64 x 64 tile; stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread needs the
-// BatchNorm parameters of 4 columns only; stage 2: qct_store
+// 64-column strip x QC_RT 64-row tiles per workgroup (the column parameters are loaded once per
+// strip); per tile, stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread needs
+// the BatchNorm parameters of 4 columns only; stage 2: qct_store
+constexpr int QC_RT = 8;
+
 __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                             int64_t M, int64_t N, BnCols bc,
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
                                                             int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum) {
   __shared__ int tile[TILE][TILE + 1];
-  const int64_t n0 = (int64_t)blockIdx.x * TILE, m0 = (int64_t)blockIdx.y * TILE;
+  const int64_t n0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, cg = t & 15, rg = t >> 4;
   const int64_t c = n0 + 4 * cg;
   Bn4 b;
@@ -649,6 +660,10 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
       sft[j] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;   // INT32_MIN -> digits 0
     }
   }
+  for (int it = 0; it < QC_RT; ++it) {
+  const int64_t m0 = ((int64_t)blockIdx.y * QC_RT + it) * TILE;
+  if (m0 >= ldqt) break;                      // uniform per workgroup
+  if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
   float4 xv[4], gv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -675,6 +690,7 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
   }
   __syncthreads();
   qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum);
+  }
 }
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -991,7 +1007,9 @@ BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_
                               int64_t* dsum, void* work, void* stream) {
   if (!x || !dy || !digits_t || !scale || !work || M <= 0 || C <= 0 || C % 4 != 0 || !aligned16(x) ||
       !aligned16(dy) || ldqt % TILE != 0 || ldqt < round_up(M, TILE) || plane < C * ldqt || plane % 16 != 0 ||
-      !aligned16(digits_t) || col_chunks(M, C) > 65535 || ldqt / TILE > 65535) {
+      !aligned16(digits_t) || col_chunks(M, C) > 65535 || ldqt / TILE > 65535 || !aligned16(save_mean) ||
+      !aligned16(save_invstd) || (save_mean_lo && !aligned16(save_mean_lo)) || (gamma && !aligned16(gamma)) ||
+      (beta && !aligned16(beta))) {
     set_error("bnn_bn_bwd_i8cols: bad arguments (M=%lld C=%lld ldqt=%lld plane=%lld)", (long long)M, (long long)C,
               (long long)ldqt, (long long)plane);
     return kErrInval;
@@ -1010,7 +1028,7 @@ BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_
                      C, bc, pmax, psum, col_chunk_rows(M, C));
   hipLaunchKernelGGL(colfinal_k, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, s, pmax, psum, C, R, scale, colsum,
                      dsum);
-  hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)(ldqt / TILE)), dim3(256),
-                     0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum);
+  hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT)),
+                     dim3(256), 0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum);
   return check_launch("bnn_bn_bwd_i8cols");
 }
