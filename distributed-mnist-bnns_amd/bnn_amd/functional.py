@@ -960,7 +960,7 @@ def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db):
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
     ds = torch.empty((C,), dtype=torch.int64, device=dev)
     ws = torch.empty((L.lib().bnn_bn_bwd_i8cols_workspace(M, C),), dtype=torch.uint8, device=dev)
-    with _timed("bn_bwd_i8cols", 0, 24 * M * C + dg.numel()):
+    with _timed("bn_bwd_i8cols", 0, 16 * M * C + dg.numel()):
         L.call("bnn_bn_bwd_i8cols", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc), L.ptr(cs), L.ptr(ds),
                L.ptr(ws), L.stream())

@@ -123,6 +123,9 @@ inline Drop make_drop(float p, uint64_t seed) {
 // MODE 0: per-chunk (mean, M2), accumulated as deviations from the chunk's first row so the
 //         float partials see deviations rather than raw magnitudes; merged with Chan's formula.
 // MODE 1: per-chunk (sum g, sum g*xhat) with g = dy*mask(y).
+// MODE 2: MODE 1 (the same sums, bit for bit) + per-chunk max|g| and max|xhat| into pmx
+//         ([chunks][C] each, max|xhat| R*C floats after max|g|): the a-priori bound on |dz| that
+//         bnn_bn_bwd_i8cols scales its int8 column digits by (no column-max pass over dz).
 // One thread = 4 adjacent columns (float4), rows walked in 16-row float partials folded to double.
 template <int MODE, bool Z16 = false>
 __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restrict__ dy,
@@ -132,7 +135,9 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
                                                    const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, int hardtanh,
                                                    double* __restrict__ p0, double* __restrict__ p1,
-                                                   int64_t chunk_rows, Drop dp0 = Drop{0, 0, 0, 1.f}) {
+                                                   int64_t chunk_rows, Drop dp0 = Drop{0, 0, 0, 1.f},
+                                                   float* __restrict__ pmx = nullptr) {
+  constexpr bool BWD = MODE >= 1;
   const Drop dp = drop_resolve(dp0);
   // thread -> (4-column group, chunk): consecutive threads read consecutive columns of a row
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -144,6 +149,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
   const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
   float mu[4], lo[4] = {0, 0, 0, 0}, is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
+  float gmx[4] = {0, 0, 0, 0}, xmx[4] = {0, 0, 0, 0};   // MODE 2
   const float4 xb = xin_bias4<Z16>(xin, c);
   if (MODE == 0) {
     const float4 sv = xin_load4<Z16>(xin, r0 * C + c, xb);
@@ -169,12 +175,12 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
     for (int64_t rb = r; rb < re; rb += RB) {
-    float4 xv8[RB], gb[MODE == 1 ? RB : 1];
+    float4 xv8[RB], gb[BWD ? RB : 1];
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u < re ? rb + u : re - 1;
       xv8[u] = xin_load4<Z16>(xin, rr * C + c, xb);
-      if constexpr (MODE == 1) gb[u] = ld4(dy + rr * C + c);
+      if constexpr (BWD) gb[u] = ld4(dy + rr * C + c);
     }
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
           sx[j] += (double)xs[j];      // exact batch sum (see file header)
         }
       } else {
-        const float4 gv = gb[MODE == 1 ? u : 0];
+        const float4 gv = gb[BWD ? u : 0];
         const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -201,6 +207,11 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
           const float g = (!hardtanh || (y > -1.f && y < 1.f)) ? gs[j] : 0.f;
           fa[j] += g;
           fb[j] = fmaf(g, xh, fb[j]);
+          if constexpr (MODE == 2) {   // NaN -> inf: the bound (and the scale) become non-finite
+            const float ag = fabsf(g), ax = fabsf(xh);
+            gmx[j] = (ag == ag) ? fmaxf(gmx[j], ag) : __builtin_inff();
+            xmx[j] = (ax == ax) ? fmaxf(xmx[j], ax) : __builtin_inff();
+          }
         }
       }
     }
@@ -226,13 +237,18 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
       p0[o + j] = a[j];
       p1[o + j] = b[j];
     }
+    if constexpr (MODE == 2) {
+      const int64_t RC = ((M + chunk_rows - 1) / chunk_rows) * C;
+      *reinterpret_cast<float4*>(pmx + o) = make_float4(gmx[0], gmx[1], gmx[2], gmx[3]);
+      *reinterpret_cast<float4*>(pmx + RC + o) = make_float4(xmx[0], xmx[1], xmx[2], xmx[3]);
+    }
   }
 }
 
 // Final merges: a workgroup owns 64 columns; its 4 waves each merge every 4th chunk (r = wave,
 // wave+4, ...) and wave 0 folds the 4 group results in order -- 4x the parallelism of one thread
 // per column walking all R chunks, still a fixed (deterministic) order.
-constexpr int FIN_COLS = 16, FIN_GROUPS = 16;
+constexpr int FIN_COLS = 16, FIN_GROUPS = 16, FIN_B = 8;
 
 inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + FIN_COLS - 1) / FIN_COLS)); }
 
@@ -251,15 +267,29 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
   const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
   double n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
   if (c < C) {
-    for (int64_t r = grp; r < R; r += FIN_GROUPS) {  // Chan et al. merge, fixed order
-      const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
-      const double nb = (double)((hi - r * chunk_rows) * hw);
-      const double mb = p0[r * C + c] / nb, m2b = p1[r * C + c];
-      const double nt = n + nb, delta = mb - mean;
-      mean += delta * nb / nt;
-      m2 += m2b + delta * delta * n * nb / nt;
-      n = nt;
-      sum += p0[r * C + c];
+    // Chan et al. merge, fixed order; the partials of FIN_B chunks are loaded before any is
+    // merged (a serial load -> merge chain is latency-bound at ~1 us per chunk)
+    for (int64_t rb = grp; rb < R; rb += FIN_B * FIN_GROUPS) {
+      double q0[FIN_B], q1[FIN_B];
+#pragma unroll
+      for (int u = 0; u < FIN_B; ++u) {
+        const int64_t r = rb + u * FIN_GROUPS;
+        q0[u] = r < R ? p0[r * C + c] : 0.0;
+        q1[u] = r < R ? p1[r * C + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < FIN_B; ++u) {
+        const int64_t r = rb + u * FIN_GROUPS;
+        if (r >= R) break;
+        const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
+        const double nb = (double)((hi - r * chunk_rows) * hw);
+        const double mb = q0[u] / nb, m2b = q1[u];
+        const double nt = n + nb, delta = mb - mean;
+        mean += delta * nb / nt;
+        m2 += m2b + delta * delta * n * nb / nt;
+        n = nt;
+        sum += q0[u];
+      }
     }
   }
   sn[grp][lc] = n;
@@ -353,32 +383,79 @@ __global__ __launch_bounds__(256) void bn_apply_k(const float* __restrict__ x, i
   }
 }
 
+// I8C (optional, bnn_bn_bwd_i8cols): also folds bn_reduce_k MODE 2's per-chunk max|g| / max|xhat|
+// (pmx) and writes the int8 column-digit scale from the bound on |dz| (see bnn_pack.hip,
+// bn_dz_quant_cols_t_k) plus zeroed digit sums.
+struct I8cBound {
+  const float* pmx;       // [R][C] max|g|, then [R][C] max|xhat|; null = off
+  const float* invstd;
+  const float* gamma;
+  float inv_n;
+  float* scale;
+  int64_t* dsum;
+};
+
 __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__ p0,
                                                       const double* __restrict__ p1, int64_t C, int64_t R,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                      float* __restrict__ k0, float* __restrict__ k1) {
+                                                      float* __restrict__ k0, float* __restrict__ k1,
+                                                      I8cBound ib = I8cBound{nullptr, nullptr, nullptr, 0.f, nullptr, nullptr}) {
   __shared__ double sa[FIN_GROUPS][FIN_COLS], sb[FIN_GROUPS][FIN_COLS];
+  __shared__ float sg[FIN_GROUPS][FIN_COLS], sx[FIN_GROUPS][FIN_COLS];
   const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
   const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
   double s = 0.0, s2 = 0.0;
+  float gm = 0.f, xm = 0.f;
   if (c < C)
-    for (int64_t r = grp; r < R; r += FIN_GROUPS) {
-      s += p0[r * C + c];
-      s2 += p1[r * C + c];
+    for (int64_t rb = grp; rb < R; rb += FIN_B * FIN_GROUPS) {   // batched loads, fixed order
+      double q0[FIN_B], q1[FIN_B];
+      float qg[FIN_B], qx[FIN_B];
+#pragma unroll
+      for (int u = 0; u < FIN_B; ++u) {
+        const int64_t r = rb + u * FIN_GROUPS;
+        q0[u] = r < R ? p0[r * C + c] : 0.0;
+        q1[u] = r < R ? p1[r * C + c] : 0.0;
+        qg[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[r * C + c] : 0.f;
+        qx[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[(R + r) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < FIN_B; ++u) {
+        if (rb + u * FIN_GROUPS >= R) break;
+        s += q0[u];
+        s2 += q1[u];
+        gm = fmaxf(gm, qg[u]);
+        xm = fmaxf(xm, qx[u]);
+      }
     }
   sa[grp][lc] = s;
   sb[grp][lc] = s2;
+  sg[grp][lc] = gm;
+  sx[grp][lc] = xm;
   __syncthreads();
   if (grp != 0 || c >= C) return;
   s = 0.0, s2 = 0.0;
   for (int gI = 0; gI < FIN_GROUPS; ++gI) {   // fixed order
     s += sa[gI][lc];
     s2 += sb[gI][lc];
+    gm = fmaxf(gm, sg[gI][lc]);
+    xm = fmaxf(xm, sx[gI][lc]);
   }
   if (dbeta) dbeta[c] = (float)s;
   if (dgamma) dgamma[c] = (float)s2;
   k0[c] = (float)s;
   k1[c] = (float)s2;
+  if (ib.pmx != nullptr) {
+    // |dz| = |gamma*invstd| |g - a0 - xhat*a1| <= |gamma*invstd| (max|g| + |a0| + max|xhat| |a1|), with
+    // a0, a1 formed as the passes that compute dz form them; 1 + 2^-16 covers bn_dz1's roundings
+    const float is = ib.invstd[c], ga = ib.gamma ? ib.gamma[c] : 1.f;
+    const float a0 = (float)s * ib.inv_n, a1 = (float)s2 * ib.inv_n;
+    const float bound = fabsf(ga * is) * ((gm + fabsf(a0)) + xm * fabsf(a1)) * (1.f + 0x1p-16f);
+    int shift;
+    float sc;
+    digit_scale(bound, &shift, &sc);
+    ib.scale[c] = sc;
+    if (ib.dsum != nullptr) ib.dsum[c] = 0;
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ x, const float* __restrict__ dy,
@@ -789,6 +866,7 @@ __global__ __launch_bounds__(256) void head_dw_final_k(const float* __restrict__
   const int64_t e = (int64_t)blockIdx.x * FIN_COLS + lc, ne = nq * C;
   double s = 0.0;
   if (e < ne)
+#pragma unroll 8
     for (int64_t r = grp; r < R; r += FIN_GROUPS) s += (double)pw[r * ne + e];
   sa[grp][lc] = s;
   __syncthreads();
@@ -805,6 +883,7 @@ __global__ __launch_bounds__(256) void q6_colsum_final_k(const double* __restric
   const int64_t n = (int64_t)blockIdx.x * FIN_COLS + lc;
   double s = 0.0;
   if (n < N)
+#pragma unroll 8
     for (int64_t r = grp; r < R; r += FIN_GROUPS) s += part[r * N + n];
   sa[grp][lc] = s;
   __syncthreads();
@@ -1224,13 +1303,15 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
 
 namespace bnn {
 int64_t bn_workspace_bytes(int64_t M, int64_t C) { return bnn_bn_workspace(M, C); }
+int64_t bn_reduce_chunks(int64_t M, int64_t C) { return bn_chunks(M, C); }
 
 // The statistics half of the training-mode backward (bnn_bn_bwd without its apply pass): k0 =
 // sum g, k1 = sum g*xhat per column (and dgamma / dbeta) in `work` (bnn_bn_workspace bytes).
 // For passes in other files that form dz themselves (bnn_bn_bwd_i8cols, bnn_pack.hip).
 int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                 const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
-                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out) {
+                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out,
+                float* pmx, float* scale, int64_t* dsum) {
   if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work || !vec_ok(gamma) ||
       !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo)) {
     set_error("bn_bwd_sums: bad arguments");
@@ -1241,9 +1322,20 @@ int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const flo
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C, save_mean,
-                     save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), make_drop(0.f, 0));
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  if (pmx && !scale) {
+    set_error("bn_bwd_sums: the bound pass needs the scale output");
+    return kErrInval;
+  }
+  if (pmx)
+    hipLaunchKernelGGL((bn_reduce_k<2, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
+                       make_drop(0.f, 0), pmx);
+  else
+    hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
+                       make_drop(0.f, 0));
+  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1,
+                     I8cBound{pmx, save_invstd, gamma, 1.f / (float)M, scale, dsum});
   *k0_out = k0;
   *k1_out = k1;
   return check_launch("bn_bwd_sums");

@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void colsum_final_k(const double* __restrict__
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
   double s = 0.0;
+#pragma unroll 8
   for (int64_t r = 0; r < R; ++r) s += part[r * N + n];
   out[n] = (float)s;
 }

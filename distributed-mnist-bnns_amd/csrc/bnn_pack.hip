@@ -331,7 +331,9 @@ __global__ __launch_bounds__(256) void sign_pack_bits_k(const float* __restrict_
     const int64_t k = ch * 64 + lane;
     const float v = (k < K) ? x[m * ldx + k] : 0.f;
     const unsigned long long s = __ballot(v < 0.f);
-    const unsigned long long z = __ballot(v != 0.f);
+    // nonzero and not NaN (sign 0, as tsign()), as an integer test: the backend lowers a ballot of
+    // the ordered fcmp one (and of fabs(v) > 0) to v_cmp_neq_f32, which is true for NaN
+    const unsigned long long z = __ballot((__float_as_uint(v) & 0x7fffffffu) - 1u < 0x7f800000u);
     const int64_t w = ch * 2 + (lane & 1);
     if (lane < 2 && w < ldw) {
       sb[m * ldw + w] = (uint32_t)(lane ? (s >> 32) : s);
@@ -486,9 +488,12 @@ __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax
 // quant_cols_t_k's second half, shared with bn_dz_quant_cols_t_k: the 64 x 64 tile of packed
 // digits (row m, column n) written transposed as 3 int8 planes dt[d][n][m], plus the exact digit
 // column sums.  Call after the tile is complete (__syncthreads).
+// With acc != null the 4-lane part of column n0 + t/4 is added to *acc (every lane of the 4)
+// instead of atomically to dsum[n]: a caller walking several tiles of the same columns issues one
+// atomic per column at the end.
 __device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int t, int64_t n0, int64_t m0, int64_t N,
                                           int64_t ldqt, int64_t plane, int8_t* __restrict__ dt,
-                                          int64_t* __restrict__ dsum) {
+                                          int64_t* __restrict__ dsum, long long* acc = nullptr) {
   const int nn = t >> 2, mc = (t & 3) * 16;
   const int64_t n = n0 + nn;
   if (n < N && m0 + mc < ldqt) {
@@ -519,7 +524,9 @@ __device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int
     }
     part += __shfl_xor(part, 1, 64);
     part += __shfl_xor(part, 2, 64);
-    if ((t & 3) == 0 && n < N && part != 0)
+    if (acc != nullptr)
+      *acc += part;
+    else if ((t & 3) == 0 && n < N && part != 0)
       atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n), (unsigned long long)(long long)part);
   }
 }
@@ -563,10 +570,16 @@ __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ 
 
 // ------------------------------------------------------------------ BatchNorm backward -> dz^T int8 digits
 // The input layer's weight gradient dW1 = dz^T . x (the first BinarizeLinear, fed by u8 pixels:
-// bnn_gemm_i8_affine) needs dz only as the int8 digit planes of its columns.  These two passes form
-// dz from (x, dy) with bn_dz1 -- the exact value bnn_bn_bwd writes -- and never store it: pass 1
-// is colstats4_k on dz (per-chunk column absmax and double sums), pass 2 quant_cols_t_k on dz.
-// Bit-identical to bnn_quant_cols_t_dsum(bnn_bn_bwd(...)).
+// bnn_gemm_i8_affine) needs dz only as the int8 digit planes of its columns.  dz is formed from
+// (x, dy) with bn_dz1 -- the exact value bnn_bn_bwd writes -- in ONE pass after the statistics
+// pass, and never stored.  The column scale comes from an a-priori bound instead of a column-max
+// pass over dz: the statistics pass (bn_reduce_k MODE 2) also records max|g| and max|xhat| per
+// column, and |dz| = |gamma*invstd| |g - a0 - xhat*a1| <= |gamma*invstd| (max|g| + |a0| + max|xhat| |a1|)
+// =: B (times 1 + 2^-16 for bn_dz1's few fp32 roundings).  Digits keep 23 bits below B, i.e.
+// |dz - scale*v| <= scale/2 = 2^-23 * 2^ceil(log2 B): log2(B / max|dz|) bits fewer than scaling by
+// the true column max (B <= (2 + max|xhat|) |gamma*invstd| max|g| since |a0| <= max|g| and
+// |a1| <= max|g| mean|xhat| <= max|g|).  The bias gradient (column sums of dz, double) is
+// accumulated by the same pass.
 struct BnCols {
   const float *mean, *mean_lo, *invstd, *gamma, *beta, *k0, *k1;
   float inv_n;
@@ -598,55 +611,32 @@ __device__ __forceinline__ void bn4_load(const BnCols& b, int64_t c, Bn4& o) {
   }
 }
 
-__global__ __launch_bounds__(256) void bn_dz_colstats4_k(const float* __restrict__ x, const float* __restrict__ dy,
-                                                         int64_t M, int64_t N, BnCols bc, float* __restrict__ pmax,
-                                                         double* __restrict__ psum, int64_t crows) {
-  const int64_t n = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  const int64_t r0 = (int64_t)blockIdx.y * crows;
+// colsum[n] = the fixed-order double sum of the quantiser's per-workgroup-row partials
+__global__ __launch_bounds__(256) void bn_dz_colsum_k(const double* __restrict__ part, int64_t R, int64_t N,
+                                                      float* __restrict__ colsum) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
-  const int64_t r1 = (M < r0 + crows) ? M : r0 + crows;
-  Bn4 b;
-  bn4_load(bc, n, b);
-  float amax[4] = {0.f, 0.f, 0.f, 0.f};
-  double sum[4] = {0.0, 0.0, 0.0, 0.0};
-  constexpr int RB = 8;   // rows whose loads are issued together
-  for (int64_t rb = r0; rb < r1; rb += RB) {
-    float4 xv[RB], gv[RB];
-#pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const int64_t r = rb + u < r1 ? rb + u : r1 - 1;
-      xv[u] = *reinterpret_cast<const float4*>(x + r * N + n);
-      gv[u] = *reinterpret_cast<const float4*>(dy + r * N + n);
-    }
-#pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      if (rb + u >= r1) break;
-      const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w}, gs[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
-        amax[j] = absmax_acc(amax[j], v);
-        sum[j] += (double)v;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    pmax[blockIdx.y * N + n + j] = amax[j];
-    psum[blockIdx.y * N + n + j] = sum[j];
-  }
+  double s = 0.0;
+#pragma unroll 8
+  for (int64_t r = 0; r < R; ++r) s += part[r * N + n];
+  colsum[n] = (float)s;
 }
 
 // 64-column strip x QC_RT 64-row tiles per workgroup (the column parameters are loaded once per
 // strip); per tile, stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread needs
-// the BatchNorm parameters of 4 columns only; stage 2: qct_store
+// the BatchNorm parameters of 4 columns only; stage 2: qct_store.  With part != null the strip's
+// column sums of dz (double; rows in a fixed order) go to part[blockIdx.y][N].
 constexpr int QC_RT = 8;
+
+__host__ __device__ inline int64_t qc_strips(int64_t M) { return (M + TILE * QC_RT - 1) / (TILE * QC_RT); }
 
 __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                             int64_t M, int64_t N, BnCols bc,
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
-                                                            int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum) {
-  __shared__ int tile[TILE][TILE + 1];
+                                                            int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum,
+                                                            double* __restrict__ part = nullptr) {
+  __shared__ __attribute__((aligned(16))) int tile[TILE][TILE + 1];
+  double csum[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t n0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, cg = t & 15, rg = t >> 4;
   const int64_t c = n0 + 4 * cg;
@@ -660,36 +650,62 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
       sft[j] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;   // INT32_MIN -> digits 0
     }
   }
-  for (int it = 0; it < QC_RT; ++it) {
-  const int64_t m0 = ((int64_t)blockIdx.y * QC_RT + it) * TILE;
-  if (m0 >= ldqt) break;                      // uniform per workgroup
-  if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
+  // software pipeline: tile it+1's x / dy rows are loaded before tile it's transposed store
   float4 xv[4], gv[4];
+  auto load = [&](int64_t m0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + 4 * rg + i;
-    if (c < N && m < M) {
-      xv[i] = *reinterpret_cast<const float4*>(x + m * N + c);
-      gv[i] = *reinterpret_cast<const float4*>(dy + m * N + c);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + 4 * rg + i;
-    const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int packed = 0;
-      if (c < N && m < M && sft[j] != INT32_MIN) {
-        const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
-        const Digits d = to_digits(v, sft[j]);
-        packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = m0 + 4 * rg + i;
+      if (c < N && m < M) {
+        xv[i] = *reinterpret_cast<const float4*>(x + m * N + c);
+        gv[i] = *reinterpret_cast<const float4*>(dy + m * N + c);
       }
-      tile[4 * rg + i][4 * cg + j] = packed;
     }
+  };
+  const int64_t mb = (int64_t)blockIdx.y * QC_RT * TILE;
+  long long dacc = 0;   // this thread's column (n0 + t/4) digit sum over the strip
+  load(mb);
+  for (int it = 0; it < QC_RT; ++it) {
+    const int64_t m0 = mb + (int64_t)it * TILE;
+    if (m0 >= ldqt) break;                      // uniform per workgroup
+    if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = m0 + 4 * rg + i;
+      const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int packed = 0;
+        if (c < N && m < M) {
+          const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
+          csum[j] += (double)v;
+          if (sft[j] != INT32_MIN) {
+            const Digits d = to_digits(v, sft[j]);
+            packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
+          }
+        }
+        tile[4 * rg + i][4 * cg + j] = packed;
+      }
+    }
+    if (it + 1 < QC_RT && m0 + TILE < ldqt) load(m0 + TILE);
+    __syncthreads();
+    qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum, &dacc);
   }
-  __syncthreads();
-  qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum);
+  if (dsum != nullptr && (t & 3) == 0 && n0 + (t >> 2) < N && dacc != 0)
+    atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n0 + (t >> 2)), (unsigned long long)dacc);
+  if (part != nullptr && blockIdx.y < qc_strips(M)) {
+    // fixed-order fold of the 16 row groups' sums (the tile is free: every qct_store read is done)
+    __syncthreads();
+    double* ps = reinterpret_cast<double*>(&tile[0][0]);   // [16][64] doubles = 8 KiB <= 16.6 KiB
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ps[rg * TILE + 4 * cg + j] = csum[j];
+    __syncthreads();
+    if (t < TILE && n0 + t < N) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += ps[r * TILE + t];
+      part[(int64_t)blockIdx.y * N + n0 + t] = s;
+    }
   }
 }
 
@@ -992,12 +1008,20 @@ BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_
 namespace bnn {
 int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                 const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
-                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out);
+                float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out,
+                float* pmx = nullptr, float* scale = nullptr, int64_t* dsum = nullptr);
 int64_t bn_workspace_bytes(int64_t M, int64_t C);
+int64_t bn_reduce_chunks(int64_t M, int64_t C);
 }  // namespace bnn
 
+// workspace: the statistics pass's | its per-chunk maxima (2 x chunks x C floats) | the
+// quantiser's per-strip column sums (strips x C doubles)
+static int64_t i8c_pmx_bytes(int64_t M, int64_t C) {
+  return round_up(2 * bn_reduce_chunks(M, C) * C * (int64_t)sizeof(float), 256);
+}
+
 BNN_API int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C) {
-  return round_up(bn_workspace_bytes(M, C), 256) + bnn_quant_cols_workspace(M, C);
+  return round_up(bn_workspace_bytes(M, C), 256) + i8c_pmx_bytes(M, C) + qc_strips(M) * C * (int64_t)sizeof(double);
 }
 
 BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
@@ -1016,19 +1040,17 @@ BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_
   }
   hipStream_t s = S(stream);
   const float *k0, *k1;
-  int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta, work, s,
-                       &k0, &k1);
-  if (rc) return rc;
   char* qw = reinterpret_cast<char*>(work) + round_up(bn_workspace_bytes(M, C), 256);
-  const int64_t R = col_chunks(M, C);
-  float* pmax = reinterpret_cast<float*>(qw);
-  double* psum = reinterpret_cast<double*>(qw + round_up(R * C * (int64_t)sizeof(float), 256));
+  float* pmx = reinterpret_cast<float*>(qw);
+  double* part = reinterpret_cast<double*>(qw + i8c_pmx_bytes(M, C));
+  // statistics pass + its final merge, which also writes scale (from the bound) and zeroes dsum
+  int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta, work, s,
+                       &k0, &k1, pmx, scale, dsum);
+  if (rc) return rc;
   const BnCols bc{save_mean, save_mean_lo, save_invstd, gamma, beta, k0, k1, 1.f / (float)M, hardtanh};
-  hipLaunchKernelGGL(bn_dz_colstats4_k, dim3((unsigned)((C / 4 + 255) / 256), (unsigned)R), dim3(256), 0, s, x, dy, M,
-                     C, bc, pmax, psum, col_chunk_rows(M, C));
-  hipLaunchKernelGGL(colfinal_k, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, s, pmax, psum, C, R, scale, colsum,
-                     dsum);
   hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT)),
-                     dim3(256), 0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum);
+                     dim3(256), 0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum, colsum ? part : nullptr);
+  if (colsum)
+    hipLaunchKernelGGL(bn_dz_colsum_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, qc_strips(M), C, colsum);
   return check_launch("bnn_bn_bwd_i8cols");
 }

@@ -148,6 +148,28 @@ def test_sign_pack_layouts(F):
     assert not sb[:, 5:].any() and not nz[:, 5:].any()
 
 
+def test_sign_of_nan_is_zero(F):
+    """Documented deviation: the ternary kernels map sign(NaN) to 0 where the
+    reference's Tensor.sign() (binarized_modules.py:13) would propagate NaN.  Pinned for every
+    packed form and through a binarised forward: a NaN latent weight acts as a zero weight."""
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((67, 300)).astype(np.float32)
+    x[::4, ::7] = np.nan
+    z = np.where(np.isnan(x), np.float32(0), x)
+    for want_qt in (False, True):
+        a, b = F.sign_pack(dev(x), True, want_qt), F.sign_pack(dev(z), True, want_qt)
+        assert all(torch.equal(p, q) for p, q in zip(a, b) if p is not None)
+    a, b = F.sign_pack_fp4(dev(x), want_qt=True), F.sign_pack_fp4(dev(z), want_qt=True)
+    assert all(torch.equal(p, q) for p, q in zip(a, b) if p is not None)
+    a, b = F.sign_pack_bits(dev(x)), F.sign_pack_bits(dev(z))
+    assert all(torch.equal(p, q) for p, q in zip(a, b))
+    h = np.sign(rng.standard_normal((33, 300))).astype(np.float32)
+    bias = rng.standard_normal(67).astype(np.float32)
+    y_nan, *_ = run_linear(F, h, x, bias, np.zeros((33, 67), np.float32), True, backend="fp4")
+    y_zero, *_ = run_linear(F, h, z, bias, np.zeros((33, 67), np.float32), True, backend="fp4")
+    assert np.array_equal(y_nan, y_zero) and np.isfinite(y_nan).all()
+
+
 def _recon(d, s):
     d = d.astype(np.float64)
     return (d[2] * 65536 + d[1] * 256 + d[0]) * s

@@ -178,15 +178,19 @@ def test_net_on_pixels_drop_in(F, t10k):
 
 
 @pytest.mark.parametrize("M,C", [(1000, 512), (4096, 768), (77, 64)])
-def test_bn_bwd_i8cols_bit_identical(F, M, C):
-    """bnn_bn_bwd_i8cols (dz formed from x, dy twice, never stored) equals bnn_bn_bwd followed by
-    bnn_quant_cols_t_dsum on the written dz: digit planes, scales, column sums (dB), exact digit
-    sums (T) and dgamma / dbeta -- bit for bit."""
+def test_bn_bwd_i8cols_vs_written_dz(F, M, C):
+    """bnn_bn_bwd_i8cols (dz formed from x, dy after the statistics pass, never stored; column
+    scale from the a-priori bound of bn_reduce_k MODE 2) against bnn_bn_bwd's written dz:
+    dgamma / dbeta bit for bit; every digit decodes to dz within half its scale; the scale lies
+    between the true-max scale and a few bits above it; the digit sums (T) are exact; the column
+    sums (dB) match float64."""
     from bnn_amd import _lib as L
     g = torch.Generator(device="cuda").manual_seed(M + C)
     x = (torch.randint(-40, 41, (M, C), generator=g, device="cuda").float() + 0.37)
+    x[M // 3, 5] = 900.0                              # an outlier row: max|xhat| far above typical
     dy = torch.randn(M, C, generator=g, device="cuda")
     dy[:, 3] = 0.0                                    # an all-zero gradient column: scale 0
+    dy[:, 7] *= torch.exp(4 * torch.randn(M, generator=g, device="cuda"))   # heavy-tailed column
     gam = torch.rand(C, generator=g, device="cuda") + 0.5
     bet = torch.rand(C, generator=g, device="cuda") - 0.5
     mean, invstd, lo = (torch.empty(C, device="cuda") for _ in range(3))
@@ -197,19 +201,28 @@ def test_bn_bwd_i8cols_bit_identical(F, M, C):
     dg_a, db_a = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     L.call("bnn_bn_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(lo), 1,
            L.ptr(dz), L.ptr(dg_a), L.ptr(db_a), L.ptr(ws), L.stream())
-    ref = F.quant_cols_t(dz, want_colsum=True, want_dsum=True)
+    _, sc_ref, _ = F.quant_cols_t(dz, want_colsum=False)
     dg_b, db_b = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     out = F._bn_bwd_i8c(x, dy, M, C, gam, bet, mean, invstd, lo, dg_b, db_b)
-    got = F._i8c_take(out)
-    torch.cuda.synchronize()
-    for a, b in zip(ref, got):
-        assert torch.equal(a, b)
+    dt, sc, cs, ds = (host(t) for t in F._i8c_take(out))
     assert torch.equal(dg_a, dg_b) and torch.equal(db_a, db_b)
+    z64, sc_ref = host(dz).astype(np.float64), host(sc_ref)
+    assert sc[3] == 0 and sc_ref[3] == 0 and not dt[:, 3].any()
+    live = sc_ref > 0
+    assert np.all(sc[live] >= sc_ref[live]) and np.all(sc[live] <= 64 * sc_ref[live])
+    d = dt[:, :, :M].astype(np.int64)
+    v = d[2] * 65536 + d[1] * 256 + d[0]                        # [C][M]
+    assert np.all(np.abs(v * sc[:, None].astype(np.float64) - z64.T) <= sc[:, None] / 2 * (1 + 1e-6))
+    assert not dt[:, :, M:].any()
+    assert np.array_equal(ds, v.sum(1))
+    assert rel_err(cs, z64.sum(0)) < 1e-6
 
 
 def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
     """A fused MLP training step on u8 pixels with the fc1 weight gradient fed by the int8
-    column-digit hand-off equals the step with the hand-off off (dz written, re-read, quantised)."""
+    column-digit hand-off equals the step with the hand-off off (dz written, re-read, quantised):
+    every other gradient bit for bit; fc1's weight and bias gradients (digits scaled by the
+    a-priori bound, column sums in another order) within 1e-6 norm-wise; dead pixels exact zeros."""
     from bnn_amd import nets
     g = torch.Generator(device="cuda").manual_seed(7)
     u = torch.randint(0, 256, (2048, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
@@ -229,6 +242,9 @@ def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
         finally:
             F.I8C_HANDOFF = True
     for k in grads[0]:
-        assert torch.equal(grads[0][k], grads[1][k]), k
+        if k in ("fc1.weight", "fc1.bias"):
+            assert rel_err(host(grads[0][k]), host(grads[1][k]).astype(np.float64)) < 1e-6, k
+        else:
+            assert torch.equal(grads[0][k], grads[1][k]), k
     dead = grads[0]["fc1.weight"].view(1024, 28, 28)[:, :3]
     assert not dead.any()
