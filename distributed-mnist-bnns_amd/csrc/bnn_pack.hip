@@ -491,34 +491,55 @@ __global__ __launch_bounds__(256) void colfinal_k(const float* __restrict__ pmax
 // With acc != null the 4-lane part of column n0 + t/4 is added to *acc (every lane of the 4)
 // instead of atomically to dsum[n]: a caller walking several tiles of the same columns issues one
 // atomic per column at the end.
-__device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int t, int64_t n0, int64_t m0, int64_t N,
-                                          int64_t ldqt, int64_t plane, int8_t* __restrict__ dt,
-                                          int64_t* __restrict__ dsum, long long* acc = nullptr) {
-  const int nn = t >> 2, mc = (t & 3) * 16;
+// Tile element (row, col) at tile[row * LD + col], or with SWZ (LD = 64) at the 16-B chunk
+// (col / 4) ^ (4 * ((row / RPL) % 4)): conflict-free both for 16-B row writes and for the
+// column reads of qct_store_t (the 4 lanes of a column read rows RPL apart).
+template <int LD, bool SWZ, int RPL>
+__device__ __forceinline__ int qct_at(const int* tile, int row, int col) {
+  if constexpr (SWZ) {
+    constexpr int SH = RPL == 32 ? 5 : 4;
+    return tile[row * LD + ((((col >> 2) ^ (((row >> SH) & 3) << 2))) << 2) + (col & 3)];
+  } else {
+    return tile[row * LD + col];
+  }
+}
+
+// RPL = rows per lane: a tile of 4 * RPL rows, each column written as 4 * RPL contiguous bytes
+// per plane (RPL = 32: whole 128-B lines).
+template <int LD, bool SWZ, int RPL = 16>
+__device__ __forceinline__ void qct_store_t(const int* tile, int t, int64_t n0, int64_t m0, int64_t N,
+                                            int64_t ldqt, int64_t plane, int8_t* __restrict__ dt,
+                                            int64_t* __restrict__ dsum, long long* acc = nullptr) {
+  const int nn = t >> 2, mc = (t & 3) * RPL;
   const int64_t n = n0 + nn;
   if (n < N && m0 + mc < ldqt) {
-    int g[16];
+    int g[RPL];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) g[j] = tile[mc + j][nn];
+    for (int j = 0; j < RPL; ++j) g[j] = qct_at<LD, SWZ, RPL>(tile, mc + j, nn);
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       const int sh8 = 8 * d;
-      v4i w;
-      w.x = pack4(g[0] >> sh8, g[1] >> sh8, g[2] >> sh8, g[3] >> sh8);
-      w.y = pack4(g[4] >> sh8, g[5] >> sh8, g[6] >> sh8, g[7] >> sh8);
-      w.z = pack4(g[8] >> sh8, g[9] >> sh8, g[10] >> sh8, g[11] >> sh8);
-      w.w = pack4(g[12] >> sh8, g[13] >> sh8, g[14] >> sh8, g[15] >> sh8);
-      *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc) = w;
+#pragma unroll
+      for (int q = 0; q < RPL / 16; ++q) {
+        if (m0 + mc + 16 * q >= ldqt) break;
+        v4i w;
+        w.x = pack4(g[16 * q + 0] >> sh8, g[16 * q + 1] >> sh8, g[16 * q + 2] >> sh8, g[16 * q + 3] >> sh8);
+        w.y = pack4(g[16 * q + 4] >> sh8, g[16 * q + 5] >> sh8, g[16 * q + 6] >> sh8, g[16 * q + 7] >> sh8);
+        w.z = pack4(g[16 * q + 8] >> sh8, g[16 * q + 9] >> sh8, g[16 * q + 10] >> sh8, g[16 * q + 11] >> sh8);
+        w.w = pack4(g[16 * q + 12] >> sh8, g[16 * q + 13] >> sh8, g[16 * q + 14] >> sh8, g[16 * q + 15] >> sh8);
+        *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc + 16 * q) = w;
+      }
     }
   }
   if (dsum != nullptr) {
     // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22
-    // each, so 64 of them fit an int); the 4 lanes sharing n are adjacent
+    // each, so 4 * RPL of them fit an int); the 4 lanes sharing n are adjacent.  Rows beyond
+    // ldqt hold zeros.
     int part = 0;
     if (n < N && m0 + mc < ldqt) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int g = tile[mc + j][nn];
+      for (int j = 0; j < RPL; ++j) {
+        const int g = qct_at<LD, SWZ, RPL>(tile, mc + j, nn);
         part += (int)(int8_t)(g & 255) + 256 * (int)(int8_t)((g >> 8) & 255) + 65536 * (int)(int8_t)((g >> 16) & 255);
       }
     }
@@ -529,6 +550,12 @@ __device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int
     else if ((t & 3) == 0 && n < N && part != 0)
       atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n), (unsigned long long)(long long)part);
   }
+}
+
+__device__ __forceinline__ void qct_store(const int (&tile)[TILE][TILE + 1], int t, int64_t n0, int64_t m0, int64_t N,
+                                          int64_t ldqt, int64_t plane, int8_t* __restrict__ dt,
+                                          int64_t* __restrict__ dsum) {
+  qct_store_t<TILE + 1, false>(&tile[0][0], t, n0, m0, N, ldqt, plane, dt, dsum);
 }
 
 __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ x, int64_t M,
@@ -623,9 +650,12 @@ __global__ __launch_bounds__(256) void bn_dz_colsum_k(const double* __restrict__
 }
 
 // 64-column strip x QC_RT 64-row tiles per workgroup (the column parameters are loaded once per
-// strip); per tile, stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread needs
-// the BatchNorm parameters of 4 columns only; stage 2: qct_store.  With part != null the strip's
-// column sums of dz (double; rows in a fixed order) go to part[blockIdx.y][N].
+// strip); per 64-row tile, stage 1: thread = 4 columns (t % 16) x 4 rows (t / 16), so each thread
+// needs the BatchNorm parameters of 4 columns only, into a swizzled 128-row LDS tile; every second
+// tile, stage 2 (qct_store_t, 32 rows per lane) writes the 128 rows: 128-B lines per column and
+// plane.  Software-pipelined: tile it+1's x / dy rows are loaded before tile it is stored.  With
+// part != null the strip's column sums of dz (double; rows in a fixed order) go to
+// part[blockIdx.y][N].
 constexpr int QC_RT = 8;
 
 __host__ __device__ inline int64_t qc_strips(int64_t M) { return (M + TILE * QC_RT - 1) / (TILE * QC_RT); }
@@ -635,7 +665,8 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
                                                             int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum,
                                                             double* __restrict__ part = nullptr) {
-  __shared__ __attribute__((aligned(16))) int tile[TILE][TILE + 1];
+  constexpr int TM = 2 * TILE;                                       // rows per store tile
+  __shared__ __attribute__((aligned(16))) int tile[TM * TILE];       // swizzled (qct_at<TILE, true, 32>)
   double csum[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t n0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, cg = t & 15, rg = t >> 4;
@@ -650,7 +681,6 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
       sft[j] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;   // INT32_MIN -> digits 0
     }
   }
-  // software pipeline: tile it+1's x / dy rows are loaded before tile it's transposed store
   float4 xv[4], gv[4];
   auto load = [&](int64_t m0) __attribute__((always_inline)) {
 #pragma unroll
@@ -668,35 +698,47 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
   for (int it = 0; it < QC_RT; ++it) {
     const int64_t m0 = mb + (int64_t)it * TILE;
     if (m0 >= ldqt) break;                      // uniform per workgroup
-    if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
+    if (it > 0 && (it & 1) == 0) __syncthreads();   // the previous store tile's reads are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t m = m0 + 4 * rg + i;
       const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+      int packed[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        int packed = 0;
         if (c < N && m < M) {
           const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
           csum[j] += (double)v;
           if (sft[j] != INT32_MIN) {
             const Digits d = to_digits(v, sft[j]);
-            packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
+            packed[j] = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
           }
         }
-        tile[4 * rg + i][4 * cg + j] = packed;
       }
+      const int row = (it & 1) * TILE + 4 * rg + i;
+      *reinterpret_cast<int4*>(tile + row * TILE + ((cg ^ (((row >> 5) & 3) << 2)) << 2)) =
+          make_int4(packed[0], packed[1], packed[2], packed[3]);
     }
-    if (it + 1 < QC_RT && m0 + TILE < ldqt) load(m0 + TILE);
-    __syncthreads();
-    qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum, &dacc);
+    const bool last = it + 1 == QC_RT || m0 + TILE >= ldqt;
+    if (!last) load(m0 + TILE);
+    if ((it & 1) == 1 || last) {
+      if ((it & 1) == 0) {   // an odd tile count: the second half of the store tile is zeros
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = TILE + 4 * rg + i;
+          *reinterpret_cast<int4*>(tile + row * TILE + ((cg ^ (((row >> 5) & 3) << 2)) << 2)) = make_int4(0, 0, 0, 0);
+        }
+      }
+      __syncthreads();
+      qct_store_t<TILE, true, 32>(tile, t, n0, m0 - (it & 1) * TILE, N, ldqt, plane, dt, dsum, &dacc);
+    }
   }
   if (dsum != nullptr && (t & 3) == 0 && n0 + (t >> 2) < N && dacc != 0)
     atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n0 + (t >> 2)), (unsigned long long)dacc);
   if (part != nullptr && blockIdx.y < qc_strips(M)) {
     // fixed-order fold of the 16 row groups' sums (the tile is free: every qct_store read is done)
     __syncthreads();
-    double* ps = reinterpret_cast<double*>(&tile[0][0]);   // [16][64] doubles = 8 KiB <= 16.6 KiB
+    double* ps = reinterpret_cast<double*>(tile);   // [16][64] doubles = 8 KiB <= 32 KiB
 #pragma unroll
     for (int j = 0; j < 4; ++j) ps[rg * TILE + 4 * cg + j] = csum[j];
     __syncthreads();
