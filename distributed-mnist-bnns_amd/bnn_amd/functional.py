@@ -529,9 +529,11 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None):
         return C
     k_true = K if k_true is None else k_true
     name = L.lib().bnn_gemm_fp6_kernel(M, N).decode() if _TIMER is not None else ""
+    wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)    # split-K partials (small grids), else 0
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=B4.device) if wsb > 0 else None
     with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):
-        L.call("bnn_gemm_fp6", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
-               L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.stream())
+        L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
+               L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
     return C
 
 

@@ -152,6 +152,11 @@ struct Gemm6Params {
   int M, N, K;
   int gm, gn;
   int group;   // raster group rows (tile6_of)
+  // split-K (grids too small to fill the chip): workgroup bid computes k-steps
+  // [split * kps, min((split + 1) * kps, K / 64)) of tile bid / ksplit, split = bid % ksplit, and
+  // writes its fp32 partial (no bias) to part[split][M][N]; gemm6_splitk_sum_k folds the splits
+  int ksplit, kps;
+  float* part;
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -231,10 +236,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   int tm, tn;
-  tile6_of(blockIdx.x, p.gm, p.gn, p.group, tm, tn);
+  const int split = p.ksplit > 1 ? (int)(blockIdx.x % p.ksplit) : 0;
+  tile6_of(p.ksplit > 1 ? (int)(blockIdx.x / p.ksplit) : (int)blockIdx.x, p.gm, p.gn, p.group, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int64_t nblk = p.K / QB;
-  const int nk = p.K / 64;
+  const int ks0 = split * p.kps;                          // this workgroup's first k-step
+  const int nk = min(p.K / 64 - ks0, p.kps);
 
   // One stage = I_LO + I_HI + I_SC + I_B LDS-DMA pieces of 1 KiB (64 lanes x 16 B): lo 8 rows per
   // piece, hi 16 rows, scales 512 rows of 2-B entries (only this tile's BM rows are loaded), B 32
@@ -263,10 +270,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
     const int lrow = i * 32 + (lane >> 1), c = lane & 1;
     off_b[ii] = (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
   }
-  const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64;
-  const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32;
-  const uint8_t* sc_base = p.asc + (int64_t)m0 * 2;
-  const uint8_t* b_base = p.b + (int64_t)n0 * p.ldb;
+  const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64 + (int64_t)ks0 * 128;
+  const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32 + (int64_t)ks0 * 64;
+  const uint8_t* sc_base = p.asc + (int64_t)m0 * 2 + (int64_t)ks0 * p.asc_rows * 2;
+  const uint8_t* b_base = p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
   auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
     if constexpr (DIAG == 1) return;
     char* base = smem + buf * ST;
@@ -559,7 +566,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   wait_vmcnt6<0>();
   barrier6();
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
-  const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
+  // split-K: this split's partial, row pitch N, no bias (added once by the fold)
+  float* const Cout = p.ksplit > 1 ? p.part + (int64_t)split * p.M * p.N : p.C;
+  const int64_t ldo = p.ksplit > 1 ? p.N : p.ldc;
+  const float* const bias = p.ksplit > 1 ? nullptr : p.bias;
+  const bool vec_ok = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0);
 #pragma unroll
   for (int t = 0; t < WM; ++t) {
     const int trow0 = m0 + wm * WM * 32 + t * 32;
@@ -567,12 +578,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
     for (int u = 0; u < WN; ++u) {
       const int tcol0 = n0 + wn * WN * 32 + u * 32;
       const int col = tcol0 + r;
-      const float bb = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+      const float bb = (bias && col < p.N) ? bias[col] : 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
         float f = acc[t][u][i];
-        if (p.bias) f += bb;
+        if (bias) f += bb;
         patch[lr * 32 + ((((r >> 2) ^ (lr & 7)) << 2) | (r & 3))] = f;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -582,7 +593,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
         const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
         const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
         if (row >= p.M) continue;
-        float* dst = p.C + (int64_t)row * p.ldc + c0;
+        float* dst = Cout + (int64_t)row * ldo + c0;
         if (vec_ok && c0 + 3 < p.N) {
           *reinterpret_cast<float4*>(dst) = v;
         } else {
@@ -597,13 +608,49 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   }
 }
 
+// C = bias + sum over splits of the partials, in split order (deterministic); float4 per thread
+__global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restrict__ part, int S, int64_t M, int64_t N,
+                                                          const float* __restrict__ bias, float* __restrict__ C,
+                                                          int64_t ldc) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= M * N) return;
+  const int64_t m = i / N, n = i - m * N;       // N % 4 == 0 (host check): 4 elements of one row
+  float4 a = *reinterpret_cast<const float4*>(part + i);
+  for (int sp = 1; sp < S; ++sp) {
+    const float4 b = *reinterpret_cast<const float4*>(part + sp * M * N + i);
+    a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
+  }
+  if (bias) a.x += bias[n], a.y += bias[n + 1], a.z += bias[n + 2], a.w += bias[n + 3];
+  float* dst = C + m * ldc + n;
+  if (((reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    *reinterpret_cast<float4*>(dst) = a;
+  } else {   // e.g. a gradient-bucket view at an odd offset: same sums, scalar stores
+    dst[0] = a.x, dst[1] = a.y, dst[2] = a.z, dst[3] = a.w;
+  }
+}
+
+// Split count for a grid of `tiles` workgroups over nk k-steps: none while the grid fills the chip
+// twice over; otherwise enough splits for ~3 workgroups per CU, each split >= 8 k-steps.
+inline int ksplit_for(int64_t tiles, int nk, int64_t N) {
+  if (tiles >= 512 || N % 4 != 0) return 1;
+  const int64_t want = (768 + tiles - 1) / tiles;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, nk / 8));
+}
+
 template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0>
 int launch6(Gemm6Params p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
   p.gn = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES, DIAG, OCC, PP>), dim3((unsigned)((int64_t)p.gm * p.gn)),
-                     dim3(64 * WAVES_M * WAVES_N), 0, s, p);
+  if (p.part == nullptr) p.ksplit = 1;
+  const int nk = p.K / 64;
+  p.kps = (nk + p.ksplit - 1) / p.ksplit;
+  p.ksplit = (nk + p.kps - 1) / p.kps;          // no empty split
+  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES, DIAG, OCC, PP>),
+                     dim3((unsigned)((int64_t)p.gm * p.gn * p.ksplit)), dim3(64 * WAVES_M * WAVES_N), 0, s, p);
+  if (p.ksplit > 1)
+    hipLaunchKernelGGL(gemm6_splitk_sum_k, dim3((unsigned)(((int64_t)p.M * p.N / 4 + 255) / 256)), dim3(256), 0, s,
+                       p.part, p.ksplit, (int64_t)p.M, (int64_t)p.N, p.bias, p.C, p.ldc);
   return check_launch("bnn_gemm_fp6");
 }
 
@@ -612,38 +659,39 @@ struct Variant6 {
   const char* name;
   int (*fn)(Gemm6Params, hipStream_t);
   int bm;   // rows per tile (the scale array must hold round_up(M, bm) rows... see bnn_gemm_fp6)
+  int bn;   // columns per tile
 };
 
 const Variant6 kVariants6[] = {
-    {0, "gemm_fp6_k<2, 4, 4, 2, 2>", launch6<2, 4, 4, 2, 2>, 256},
-    {1, "gemm_fp6_k<2, 4, 2, 2, 3>", launch6<2, 4, 2, 2, 3>, 128},
-    {2, "gemm_fp6_k<2, 2, 2, 2, 3>", launch6<2, 2, 2, 2, 3>, 128},
-    {3, "gemm_fp6_k<4, 2, 2, 4, 2>", launch6<4, 2, 2, 4, 2>, 256},
-    {4, "gemm_fp6_k<2, 4, 2, 2, 4>", launch6<2, 4, 2, 2, 4>, 128},
+    {0, "gemm_fp6_k<2, 4, 4, 2, 2>", launch6<2, 4, 4, 2, 2>, 256, 256},
+    {1, "gemm_fp6_k<2, 4, 2, 2, 3>", launch6<2, 4, 2, 2, 3>, 128, 256},
+    {2, "gemm_fp6_k<2, 2, 2, 2, 3>", launch6<2, 2, 2, 2, 3>, 128, 128},
+    {3, "gemm_fp6_k<4, 2, 2, 4, 2>", launch6<4, 2, 2, 4, 2>, 256, 256},
+    {4, "gemm_fp6_k<2, 4, 2, 2, 4>", launch6<2, 4, 2, 2, 4>, 128, 256},
     // tall-N tiles: the FP6 operand costs 3 B/element against 0.5 for FP4, so BM x BN = 128 x 512
     // moves 29% fewer bytes per MAC than 256 x 256 and leaves room for a third stage
-    {5, "gemm_fp6_k<2, 4, 2, 4, 3>", launch6<2, 4, 2, 4, 3>, 128},
-    {6, "gemm_fp6_k<1, 8, 4, 2, 3>", launch6<1, 8, 4, 2, 3>, 128},
-    {7, "gemm_fp6_k<2, 4, 2, 4, 2>", launch6<2, 4, 2, 4, 2>, 128},
+    {5, "gemm_fp6_k<2, 4, 2, 4, 3>", launch6<2, 4, 2, 4, 3>, 128, 512},
+    {6, "gemm_fp6_k<1, 8, 4, 2, 3>", launch6<1, 8, 4, 2, 3>, 128, 512},
+    {7, "gemm_fp6_k<2, 4, 2, 4, 2>", launch6<2, 4, 2, 4, 2>, 128, 512},
     // two workgroups per CU (OCC 4: <= 128 registers per lane)
-    {8, "gemm_fp6_k<2, 4, 2, 2, 2, 0, 4>", launch6<2, 4, 2, 2, 2, 0, 4>, 128},
+    {8, "gemm_fp6_k<2, 4, 2, 2, 2, 0, 4>", launch6<2, 4, 2, 2, 2, 0, 4>, 128, 256},
     // software-pipelined k loop (PP): 128 x 512 and 128 x 256 tiles
-    {10, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 1>", launch6<2, 4, 2, 4, 3, 0, 2, 1>, 128},
-    {11, "gemm_fp6_k<2, 4, 2, 2, 3, 0, 2, 1>", launch6<2, 4, 2, 2, 3, 0, 2, 1>, 128},
+    {10, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 1>", launch6<2, 4, 2, 4, 3, 0, 2, 1>, 128, 512},
+    {11, "gemm_fp6_k<2, 4, 2, 2, 3, 0, 2, 1>", launch6<2, 4, 2, 2, 3, 0, 2, 1>, 128, 256},
     // pipelined form 2: 128 x 512 tile, every wave 32 rows x 256 columns (4 x 2 waves)
-    {12, "gemm_fp6_k<4, 2, 1, 8, 3, 0, 2, 2>", launch6<4, 2, 1, 8, 3, 0, 2, 2>, 128},
-    {13, "gemm_fp6_k<4, 1, 1, 8, 3, 0, 2, 2>", launch6<4, 1, 1, 8, 3, 0, 2, 2>, 128},
+    {12, "gemm_fp6_k<4, 2, 1, 8, 3, 0, 2, 2>", launch6<4, 2, 1, 8, 3, 0, 2, 2>, 128, 512},
+    {13, "gemm_fp6_k<4, 1, 1, 8, 3, 0, 2, 2>", launch6<4, 1, 1, 8, 3, 0, 2, 2>, 128, 256},
     // 4-wave workgroups small enough in LDS for two per CU: one workgroup's barrier wait or
     // epilogue overlaps the other's MFMAs
-    {14, "gemm_fp6_k<1, 4, 2, 4, 2>", launch6<1, 4, 2, 4, 2>, 64},
-    {15, "gemm_fp6_k<2, 2, 2, 4, 2>", launch6<2, 2, 2, 4, 2>, 128},
+    {14, "gemm_fp6_k<1, 4, 2, 4, 2>", launch6<1, 4, 2, 4, 2>, 64, 512},
+    {15, "gemm_fp6_k<2, 2, 2, 4, 2>", launch6<2, 2, 2, 4, 2>, 128, 256},
     // ping-pong: the two wave rows run a phase apart, one group's MFMAs beside the other's reads
     // (equal to variant 7 within 1% on the wide shapes: the MFMA-busy fraction stays ~0.6 --
     // profiles/r02_fp6_pingpong.txt)
-    {16, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 3>", launch6<2, 4, 2, 4, 3, 0, 2, 3>, 128},
+    {16, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 3>", launch6<2, 4, 2, 4, 3, 0, 2, 3>, 128, 512},
     // timing-only diagnostics of variant 5 (wrong results; never picked by default)
-    {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128},
-    {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128},
+    {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128, 512},
+    {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128, 512},
 };
 
 int g_variant6 = -1;
@@ -714,9 +762,38 @@ BNN_API int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx,
   return check_launch("bnn_quant6_cols_t");
 }
 
+// split-K count of the default variant for this shape (1 = no split; see ksplit_for)
+static int fp6_ksplit(int64_t M, int64_t N, int64_t K) {
+  const Variant6* v = pick6(M, N);
+  const int64_t tiles = ((M + v->bm - 1) / v->bm) * ((N + v->bn - 1) / v->bn);
+  return ksplit_for(tiles, (int)(K / 64), N);
+}
+
+BNN_API int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 != 0) return 0;
+  const int S = fp6_ksplit(M, N, K);
+  return S > 1 ? (int64_t)S * M * N * (int64_t)sizeof(float) : 0;
+}
+
+static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
+                         int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream);
+
 BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
                          const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
                          int64_t N, int64_t K, void* stream) {
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, b, ldb, bias, C, ldc, M, N, K, nullptr, 0, stream);
+}
+
+BNN_API int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                            const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
+                            int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, b, ldb, bias, C, ldc, M, N, K, work, work_bytes, stream);
+}
+
+static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
+                         int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
   if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || ldb < K / 2 || ldb % 16 != 0 ||
       ldc < N || asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
       !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
@@ -726,7 +803,13 @@ BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
     return kErrInval;
   }
   if (M == 0 || N == 0) return 0;
-  Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4};
+  // split-K only with a workspace of bnn_gemm_fp6_workspace bytes (and with the default variant)
+  const int S = (work != nullptr && g_variant6 < 0) ? fp6_ksplit(M, N, K) : 1;
+  // (the result depends on the shape only -- never on C's alignment or pitch: a gradient written
+  // straight into a bucket view must equal the one AccumulateGrad would add)
+  const bool split = S > 1 && work_bytes >= (int64_t)S * M * N * (int64_t)sizeof(float) && aligned16(work);
+  Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
+                split ? S : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr};
   return pick6(M, N)->fn(p, S6(stream));
 }
 
