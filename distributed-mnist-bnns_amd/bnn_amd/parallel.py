@@ -123,17 +123,21 @@ class GradExchange:
         buckets, param_buckets, flats = [], {}, []
         for (dtype, device), plist in groups.items():
             es = torch.empty((), dtype=dtype).element_size()
+            # every gradient view starts on a 256-B boundary: the kernels that read or write them
+            # (the fused latent update, the GEMMs writing into a view) take their vector paths
+            # (a 10-float fc4 bias first misaligned every view after it); the gaps stay zero
+            align = max(1, _ALIGN_BYTES // es)
             offsets, total = {}, 0
             for p in plist:
                 offsets[p] = total
-                total += p.numel()
+                total += -(-p.numel() // align) * align
             flat = torch.zeros(total, dtype=dtype, device=device)
             flats.append((flat, plist, offsets))
             cap = max(1, self.cap_bytes // es)
-            cur, cur_start, cur_n = [], 0, 0
+            cur, cur_start, cur_n = [], 0, 0      # cur_n: the bucket's span, gaps included
             for p in plist:
                 n, off = p.numel(), offsets[p]
-                if cur and (n > cap or cur_n + n > cap):
+                if cur and (n > cap or off + n - cur_start > cap):
                     self._close(buckets, param_buckets, flat, cur, cur_start, cur_n)
                     cur, cur_n = [], 0
                 if n > cap:                                 # split into equal slices <= cap
@@ -147,7 +151,7 @@ class GradExchange:
                 if not cur:
                     cur_start = off
                 cur.append(p)
-                cur_n += n
+                cur_n = off + n - cur_start
             if cur:
                 self._close(buckets, param_buckets, flat, cur, cur_start, cur_n)
             self._bind(flat, plist, offsets)
