@@ -681,52 +681,52 @@ constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256) void bn_head_fwd_k(XIn xin, int64_t M, int64_t C,
+__global__ __launch_bounds__(256, Z16 ? 4 : 2) void bn_head_fwd_k(XIn xin, int64_t M, int64_t C,
                                                      const float* __restrict__ mean, const float* __restrict__ mean_lo,
                                                      const float* __restrict__ invstd, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, const float* __restrict__ w4,
                                                      const float* __restrict__ b4, float* __restrict__ y4, Drop dp0) {
   static_assert(NOUT <= 16, "one 16-column MFMA tile");
   __shared__ __attribute__((aligned(16))) float ht[HD_ROWS * HD_LD];
-  __shared__ float ws[16 * HD_COLS];
+  // W4's NOUT real rows only (the MFMA's B columns NOUT..15 read as zero): with <= 128 registers
+  // (4 waves per SIMD) the 1024 workgroups of a 65536-row batch are resident at once (4 per CU,
+  // 38.8 KiB of LDS each) instead of running in two rounds at 3 per CU
+  __shared__ float ws[NOUT * HD_COLS];
   const Drop dp = drop_resolve(dp0);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * HD_ROWS;
   const int cq = 4 * (t % HD_CG);
   hf4 acc = hf4{0.f, 0.f, 0.f, 0.f};
-  // software pipeline: chunk c0 + 64's x rows, W4 columns and BatchNorm parameters are fetched into
-  // registers before chunk c0 is normalised and multiplied (the pass is latency-bound otherwise)
-  struct Fetch {
-    XRaw<Z16> x[HD_NI];
-    float4 xb;
-    float w[16 * HD_COLS / 256];
-    float4 mv, iv, lv, gv, bv;
-  };
-  auto fetch = [&](int64_t c0, Fetch& f) __attribute__((always_inline)) {
-    const int64_t c = c0 + cq;
-    f.xb = xin_bias4<Z16>(xin, c);
+  // software pipeline: chunk c0 + 128's x rows are fetched into registers before chunk c0 is
+  // normalised and multiplied (the pass is latency-bound otherwise); W4's columns and the BatchNorm
+  // parameters of the chunk (L2-resident) are loaded at its top, ahead of the barrier
+  XRaw<Z16> xn[HD_NI];
+  auto fetch_x = [&](int64_t c0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) {
       const int64_t r = r0 + t / HD_CG + HD_RS * i;
-      if (r < M) f.x[i] = xin_raw4<Z16>(xin, r * C + c);
+      if (r < M) xn[i] = xin_raw4<Z16>(xin, r * C + c0 + cq);
     }
-#pragma unroll
-    for (int u = 0; u < 16 * HD_COLS / 256; ++u) {
-      const int i = t + 256 * u, q = i / HD_COLS, k = i - q * HD_COLS;
-      f.w[u] = q < NOUT ? w4[q * C + c0 + k] : 0.f;
-    }
-    f.mv = ld4(mean + c), f.iv = ld4(invstd + c), f.lv = ld4_or(mean_lo, c, 0.f);
-    f.gv = ld4_or(gamma, c, 1.f), f.bv = ld4_or(beta, c, 0.f);
   };
-  Fetch nx;
-  fetch(0, nx);
+  fetch_x(0);
   for (int64_t c0 = 0; c0 < C; c0 += HD_COLS) {
-    const Fetch cur = nx;
-    if (c0 + HD_COLS < C) fetch(c0 + HD_COLS, nx);
+    XRaw<Z16> xc[HD_NI];
+#pragma unroll
+    for (int i = 0; i < HD_NI; ++i) xc[i] = xn[i];
+    if (c0 + HD_COLS < C) fetch_x(c0 + HD_COLS);
     const int64_t c = c0 + cq;
-    const float mu[4] = {cur.mv.x, cur.mv.y, cur.mv.z, cur.mv.w}, is[4] = {cur.iv.x, cur.iv.y, cur.iv.z, cur.iv.w};
-    const float lo[4] = {cur.lv.x, cur.lv.y, cur.lv.z, cur.lv.w};
-    const float ga[4] = {cur.gv.x, cur.gv.y, cur.gv.z, cur.gv.w}, be[4] = {cur.bv.x, cur.bv.y, cur.bv.z, cur.bv.w};
+    const float4 xb = xin_bias4<Z16>(xin, c);
+    float w4c[(NOUT * HD_COLS + 255) / 256];
+#pragma unroll
+    for (int u = 0; u < (NOUT * HD_COLS + 255) / 256; ++u) {
+      const int i = t + 256 * u, q = i / HD_COLS, k = i - q * HD_COLS;
+      w4c[u] = q < NOUT ? w4[q * C + c0 + k] : 0.f;
+    }
+    const float4 mv = ld4(mean + c), iv = ld4(invstd + c), lv = ld4_or(mean_lo, c, 0.f);
+    const float4 gv = ld4_or(gamma, c, 1.f), bv = ld4_or(beta, c, 0.f);
+    const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+    const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+    const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
     __syncthreads();   // the previous chunk's fragment reads are done
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) {
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(XIn xin, int64_t M, int64_t
       const int64_t r = r0 + rr;
       float h[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
-        const float4 xv = xin_cvt4<Z16>(cur.x[i], cur.xb);
+        const float4 xv = xin_cvt4<Z16>(xc[i], xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         drop4(dp, (uint64_t)(r * C + c), xs);
 #pragma unroll
@@ -744,13 +744,14 @@ __global__ __launch_bounds__(256) void bn_head_fwd_k(XIn xin, int64_t M, int64_t
       *reinterpret_cast<float4*>(ht + rr * HD_LD + cq) = make_float4(h[0], h[1], h[2], h[3]);
     }
 #pragma unroll
-    for (int u = 0; u < 16 * HD_COLS / 256; ++u) ws[t + 256 * u] = cur.w[u];
+    for (int u = 0; u < (NOUT * HD_COLS + 255) / 256; ++u)
+      if (t + 256 * u < NOUT * HD_COLS) ws[t + 256 * u] = w4c[u];
     __syncthreads();
     // wave wv: rows 16 wv .. +15 of the tile; A = h3 rows, B = W4^T (16 x 16 of which NOUT real)
 #pragma unroll
     for (int k0 = 0; k0 < HD_COLS; k0 += 4) {
       const float a = ht[(16 * wv + (lane & 15)) * HD_LD + k0 + (lane >> 4)];
-      const float b = ws[(lane & 15) * HD_COLS + k0 + (lane >> 4)];
+      const float b = (lane & 15) < NOUT ? ws[(lane & 15) * HD_COLS + k0 + (lane >> 4)] : 0.f;
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
     }
   }
