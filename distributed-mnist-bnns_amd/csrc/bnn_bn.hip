@@ -518,6 +518,10 @@ inline int64_t q6_rows(int64_t M, int64_t C) {
 
 // The fused head's upstream gradient for 4 columns: g[j] = sum_q dY4[q] * W4[q][c + j] (fp32, q in
 // order -- the same rounding in the statistics pass and the apply pass).
+// Column pairs on the packed FMA (v_pk_fma_f32: two lanes' fmaf per instruction, the same
+// per-element rounding and order as the scalar chain).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
 template <int NOUT>
 __device__ __forceinline__ void head_grad4(const float* __restrict__ d4, const float (&wc)[NOUT > 0 ? NOUT : 1][4],
                                            float (&g)[4]) {
@@ -525,11 +529,13 @@ __device__ __forceinline__ void head_grad4(const float* __restrict__ d4, const f
 #pragma unroll
   for (int q = 0; q < NOUT; ++q) dq[q] = d4[q];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float s = 0.f;
+  for (int jp = 0; jp < 2; ++jp) {
+    pf2 s = {0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < NOUT; ++q) s = fmaf(dq[q], wc[q][j], s);
-    g[j] = s;
+    for (int q = 0; q < NOUT; ++q)
+      s = __builtin_elementwise_fma(pf2{dq[q], dq[q]}, pf2{wc[q][2 * jp], wc[q][2 * jp + 1]}, s);
+    g[2 * jp] = s.x;
+    g[2 * jp + 1] = s.y;
   }
 }
 
@@ -825,19 +831,30 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
 #pragma unroll
       for (int q = 0; q < NOUT; ++q) dq[q] = d4[ru * NOUT + q];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float gsum = 0.f;
+      for (int jp = 0; jp < 2; ++jp) {   // column pairs: the q-sums on the packed FMA
+        pf2 gs2 = {0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < NOUT; ++q) gsum = fmaf(dq[q], wc[q][j], gsum);   // head_grad4's order
-        const float xh = ((xs[j] - mu[j]) - lo[j]) * is[j];
-        const float y = fmaf(xh, ga[j], be[j]);
-        const bool in = y > -1.f && y < 1.f;
-        const float g = in ? gsum : 0.f;
-        fa[j] += g;
-        fb[j] = fmaf(g, xh, fb[j]);
-        const float h = fminf(fmaxf(y, -1.f), 1.f);     // the forward's h3
+        for (int q = 0; q < NOUT; ++q)   // head_grad4's order
+          gs2 = __builtin_elementwise_fma(pf2{dq[q], dq[q]}, pf2{wc[q][2 * jp], wc[q][2 * jp + 1]}, gs2);
+        float hh[2];
 #pragma unroll
-        for (int q = 0; q < NOUT; ++q) aw[q][j] = fmaf(dq[q], h, aw[q][j]);
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * jp + e;
+          const float xh = ((xs[j] - mu[j]) - lo[j]) * is[j];
+          const float y = fmaf(xh, ga[j], be[j]);
+          const bool in = y > -1.f && y < 1.f;
+          const float g = in ? (e ? gs2.y : gs2.x) : 0.f;
+          fa[j] += g;
+          fb[j] = fmaf(g, xh, fb[j]);
+          hh[e] = fminf(fmaxf(y, -1.f), 1.f);     // the forward's h3
+        }
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) {
+          const pf2 a2 = __builtin_elementwise_fma(pf2{dq[q], dq[q]}, pf2{hh[0], hh[1]},
+                                                   pf2{aw[q][2 * jp], aw[q][2 * jp + 1]});
+          aw[q][2 * jp] = a2.x;
+          aw[q][2 * jp + 1] = a2.y;
+        }
       }
     }
     }
