@@ -19,9 +19,9 @@ def main():
         src = os.path.join(d, "libbnn.so")          # the bundles are extracted next to the input
         subprocess.run(["cp", LIB, src], check=True)
         subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", src], cwd=d, check=True, capture_output=True)
-        co = [f for f in os.listdir(d) if f.endswith("gfx950")][0]
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", os.path.join(d, co)], check=True,
-                               capture_output=True, text=True).stdout
+        notes = "".join(subprocess.run([f"{LLVM}/llvm-readelf", "--notes", os.path.join(d, co)], check=True,
+                                       capture_output=True, text=True).stdout
+                        for co in sorted(os.listdir(d)) if co.endswith("gfx950"))   # one code object per TU
     kernels = re.split(r"\n\s+- \.", notes)
     for k in kernels:
         m = re.search(r"\.name:\s+(\S+)", k)
