@@ -220,6 +220,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BNN_BENCH_ONE_DEVICE") == "1":   # rehearsal only: every rank on device 0
+        local = 0
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     cpu_main, cpu_extra = None, []
@@ -233,7 +235,11 @@ def main():
     if use_exchange:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        backend = os.environ.get("BNN_BENCH_BACKEND", "nccl")   # rehearsal on one device: "gloo"
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     from bnn_amd import functional as BF
     from bnn_amd.data import synthetic_mnist
