@@ -79,6 +79,7 @@ SIGNATURES = {
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,
                                   P]),
     "bnn_adam_schedule": (I32, [F32, F32, F32, I64, I64, P]),
+    "bnn_adam_clamp_multi": (I32, [I32, P, P, P, P, P, P, P, F32, F32, F32, F32, P, P, F32, P]),
     "bnn_adam_clamp_sched": (I32, [P, P, P, P, I64, F32, F32, F32, P, P, F32, I32, P]),
     "bnn_adam_clamp_pack_sched": (I32, [P, P, P, P, I64, I64, F32, F32, F32, P, P, F32, I32, I32, P, I64, P, I64,
                                         I32, P]),

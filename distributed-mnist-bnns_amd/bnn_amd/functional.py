@@ -853,6 +853,31 @@ def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, 
            int(bool(clamp)), L.stream())
 
 
+ADAM_MULTI_MAX = 16     # tensors per bnn_adam_clamp_multi launch
+
+
+def adam_clamp_multi_(items, lr, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0, sched=None, ctr=None):
+    """adam_clamp_ on several tensors in one launch per ADAM_MULTI_MAX: items = [(p, grad, exp_avg,
+    exp_avg_sq, step, clamp)], bit-identical per tensor to adam_clamp_ (bnn_adam_clamp_multi)."""
+    import ctypes
+    for i in range(0, len(items), ADAM_MULTI_MAX):
+        chunk = items[i:i + ADAM_MULTI_MAX]
+        for p, g, m, v, _, _ in chunk:
+            _check(p, g, m, v)
+            invalidate_packed(p)
+            for t in (p, g, m, v):
+                if not t.is_contiguous():
+                    raise ValueError("adam_clamp_multi_: tensors must be contiguous")
+        k = len(chunk)
+        arr = [(ctypes.c_void_p * k)(*[it[j].data_ptr() for it in chunk]) for j in range(4)]
+        nn_ = (ctypes.c_int64 * k)(*[it[0].numel() for it in chunk])
+        st = (ctypes.c_int64 * k)(*[int(it[4]) for it in chunk])
+        cl = (ctypes.c_int32 * k)(*[int(bool(it[5])) for it in chunk])
+        vp = [ctypes.cast(a, ctypes.c_void_p) for a in arr + [nn_, st, cl]]
+        L.call("bnn_adam_clamp_multi", k, *vp, float(lr), float(beta1), float(beta2), float(eps), L.ptr(sched),
+               L.ptr(ctr), float(grad_scale), L.stream())
+
+
 # ----------------------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
 def _bn_ws(M, C, device):
     return torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device=device)

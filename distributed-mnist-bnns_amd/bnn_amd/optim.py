@@ -78,6 +78,7 @@ class LatentAdam(torch.optim.Optimizer):
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             sched = None
+            small = []                # plain Adam + clamp tensors: one multi-tensor launch per 16
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -98,7 +99,10 @@ class LatentAdam(torch.optim.Optimizer):
                 # a binarized layer's weight also gets its next-forward ternary operands rewritten in
                 # the same pass (bnn_adam_clamp_pack); anything else: plain fused Adam + clamp
                 if not BF.adam_clamp_pack_(p, *args, **kw):
-                    BF.adam_clamp_(p, *args, **kw)
+                    small.append((p, g, st["exp_avg"], st["exp_avg_sq"], st["step"], id(p) in self._clamp))
+            if small:
+                BF.adam_clamp_multi_(small, group["lr"], b1, b2, group["eps"], self.grad_scale,
+                                     sched=sched, ctr=ds.ctr if ds is not None else None)
         if ds is not None:
             ds.advance()
         return loss

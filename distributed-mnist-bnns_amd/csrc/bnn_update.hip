@@ -80,7 +80,7 @@ BNN_API int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t
 BNN_API int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                            float lr, float beta1, float beta2, float eps, int64_t step,
                            float grad_scale, int32_t clamp, void* stream) {
-  if (!p || !grad || !exp_avg || !exp_avg_sq || n < 0 || step < 1) {
+  if (n < 0 || (n > 0 && (!p || !grad || !exp_avg || !exp_avg_sq)) || step < 1) {   // n == 0: nothing to do
     set_error("bnn_adam_clamp: bad arguments");
     return kErrInval;
   }
@@ -95,7 +95,7 @@ BNN_API int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* e
 BNN_API int bnn_adam_clamp_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                                  float beta1, float beta2, float eps, const float* sched, const int64_t* ctr,
                                  float grad_scale, int32_t clamp, void* stream) {
-  if (!p || !grad || !exp_avg || !exp_avg_sq || n < 0 || !sched || !ctr) {
+  if (n < 0 || (n > 0 && (!p || !grad || !exp_avg || !exp_avg_sq)) || !sched || !ctr) {
     set_error("bnn_adam_clamp_sched: bad arguments");
     return kErrInval;
   }
@@ -105,6 +105,79 @@ BNN_API int bnn_adam_clamp_sched(float* p, const float* grad, float* exp_avg, fl
   a.ctr = ctr;
   hipLaunchKernelGGL(adam_clamp_k, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, n, a);
   return check_launch("bnn_adam_clamp_sched");
+}
+
+// Multi-tensor form: up to ADAM_MT tensors (the small parameters -- biases, BatchNorm affine
+// parameters, the head -- each of which would otherwise be its own launch of a few microseconds)
+// in ONE launch, blockIdx.y = tensor; per-tensor bias corrections (or the device-step table).
+namespace bnn {
+namespace {
+constexpr int ADAM_MT = 16;
+struct AdamMulti {
+  float* p[ADAM_MT];
+  const float* g[ADAM_MT];
+  float* m[ADAM_MT];
+  float* v[ADAM_MT];
+  int64_t n[ADAM_MT];
+  float step_size[ADAM_MT], bc2_sqrt[ADAM_MT];
+  int clamp[ADAM_MT];
+  float b1, b2, eps, gscale;
+  const float* sched;
+  const int64_t* ctr;
+};
+
+__global__ __launch_bounds__(256) void adam_clamp_multi_k(AdamMulti am) {
+  const int j = blockIdx.y;
+  AdamArgs a{am.g[j], am.m[j], am.v[j], am.b1, am.b2, am.eps, am.step_size[j], am.bc2_sqrt[j], am.gscale,
+             am.clamp[j]};
+  a.sched = am.sched;
+  a.ctr = am.ctr;
+  a = adam_resolve(a);
+  float* __restrict__ p = am.p[j];
+  const int64_t n = am.n[j], stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float mi = a.m[i], vi = a.v[i];
+    p[i] = adam_elem(p[i], a.g[i], mi, vi, a);
+    a.m[i] = mi;
+    a.v[i] = vi;
+  }
+}
+}  // namespace
+}  // namespace bnn
+
+BNN_API int bnn_adam_clamp_multi(int32_t count, float* const* p, const float* const* grad, float* const* exp_avg,
+                                 float* const* exp_avg_sq, const int64_t* n, const int64_t* step,
+                                 const int32_t* clamp, float lr, float beta1, float beta2, float eps,
+                                 const float* sched, const int64_t* ctr, float grad_scale, void* stream) {
+  if (count < 0 || count > ADAM_MT || (count > 0 && (!p || !grad || !exp_avg || !exp_avg_sq || !n || !step || !clamp)) ||
+      ((sched == nullptr) != (ctr == nullptr))) {
+    set_error("bnn_adam_clamp_multi: bad arguments (count %d, at most %d tensors per launch)", count, ADAM_MT);
+    return kErrInval;
+  }
+  AdamMulti am{};
+  int64_t nmax = 0;
+  int k = 0;
+  for (int j = 0; j < count; ++j) {
+    if (n[j] < 0 || (n[j] > 0 && (!p[j] || !grad[j] || !exp_avg[j] || !exp_avg_sq[j])) || (!sched && step[j] < 1)) {
+      set_error("bnn_adam_clamp_multi: bad tensor %d", j);
+      return kErrInval;
+    }
+    if (n[j] == 0) continue;
+    am.p[k] = p[j], am.g[k] = grad[j], am.m[k] = exp_avg[j], am.v[k] = exp_avg_sq[j], am.n[k] = n[j];
+    am.clamp[k] = clamp[j];
+    if (sched) {
+      am.step_size[k] = 0.f, am.bc2_sqrt[k] = 1.f;     // from the device-step table
+    } else {
+      adam_bias_correction(lr, beta1, beta2, step[j], &am.step_size[k], &am.bc2_sqrt[k]);
+    }
+    nmax = std::max(nmax, n[j]);
+    ++k;
+  }
+  if (k == 0) return 0;
+  am.b1 = beta1, am.b2 = beta2, am.eps = eps, am.gscale = grad_scale, am.sched = sched, am.ctr = ctr;
+  const unsigned gx = (unsigned)std::min<int64_t>((nmax + 255) / 256, 1024);
+  hipLaunchKernelGGL(adam_clamp_multi_k, dim3(gx, (unsigned)k), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), am);
+  return check_launch("bnn_adam_clamp_multi");
 }
 
 BNN_API int bnn_adam_schedule(float lr, float beta1, float beta2, int64_t step0, int64_t n, float* out) {

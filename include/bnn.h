@@ -428,6 +428,14 @@ int bnn_adam_clamp_pack(float* p, const float* grad, float* exp_avg, float* exp_
  * bnn_set_seed_counter: process-wide; while non-NULL every dropout launch (bnn_bn_dropout_*,
  * bnn_bn_bwd_q6, bnn_dropout_mask) draws its mask from seed + ctr[0] * 0xD1B54A32D192ED03. */
 int bnn_adam_schedule(float lr, float beta1, float beta2, int64_t step0, int64_t n, float* out);
+/* bnn_adam_clamp (or, with sched/ctr non-NULL, bnn_adam_clamp_sched) over up to 16 tensors in one
+ * launch: host arrays of `count` device pointers, element counts, Adam step counts and clamp
+ * flags.  Bit-identical per tensor to the single-tensor entries; one launch for a network's small
+ * parameters (biases, BatchNorm affine parameters, the head) instead of one each. */
+int bnn_adam_clamp_multi(int32_t count, float* const* p, const float* const* grad, float* const* exp_avg,
+                         float* const* exp_avg_sq, const int64_t* n, const int64_t* step, const int32_t* clamp,
+                         float lr, float beta1, float beta2, float eps, const float* sched, const int64_t* ctr,
+                         float grad_scale, bnn_stream_t stream);
 int bnn_adam_clamp_sched(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
                          float beta2, float eps, const float* sched, const int64_t* ctr, float grad_scale,
                          int32_t clamp, bnn_stream_t stream);

@@ -333,6 +333,27 @@ def test_adam_clamp_matches_torch(F):
     assert close(host(p), host(p_ref), 1e-6, 0.0)
 
 
+def test_adam_clamp_multi_equals_single(F):
+    """bnn_adam_clamp_multi (LatentAdam's one launch for the small parameters): p, m, v bit-identical
+    to one bnn_adam_clamp per tensor, for 19 tensors (two launches), mixed sizes (incl. empty),
+    clamp flags and step counts."""
+    torch.manual_seed(3)
+    sizes = [10, 8192, 1, 0, 3072, 257, 65536, 10, 5, 40000, 1536, 768, 100, 2, 7, 31, 512, 9, 4096]
+    single, multi = [], []
+    for i, n in enumerate(sizes):
+        p = torch.empty(n, device="cuda").uniform_(-1.3, 1.3)
+        m, v = torch.randn(n, device="cuda") * 1e-3, torch.rand(n, device="cuda") * 1e-6
+        g = torch.randn(n, device="cuda")
+        single.append([p.clone(), g, m.clone(), v.clone(), 3 + i % 4, i % 3 != 0])
+        multi.append([p.clone(), g, m.clone(), v.clone(), 3 + i % 4, i % 3 != 0])
+    for p, g, m, v, st, cl in single:
+        F.adam_clamp_(p, g, m, v, st, lr=0.01, clamp=cl)
+    F.adam_clamp_multi_([tuple(t) for t in multi], 0.01)
+    for a, b in zip(single, multi):
+        for x, y in zip(a[:4], b[:4]):
+            assert torch.equal(x, y)
+
+
 def test_large_forward_exact_vs_rocblas(F):
     """Size-independent property at wide-MLP scale: ternary products are integers < 2^24, so an
     fp32 GEMM in any order is exact; libbnn must equal it bit-for-bit (plus the same bias add)."""

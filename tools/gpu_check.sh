@@ -13,4 +13,5 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-g
 summ gpurun_out/bench_wide.log
 timeout -k 10 300 python bench.py --config mlp --steps 50 --warmup 5 --no-cpu-baseline --no-gpu-torch --no-kernel-timing > gpurun_out/bench_mlp.log 2>&1 || { echo BENCH FAIL; tail -20 gpurun_out/bench_mlp.log; exit 1; }
 tail -1 gpurun_out/bench_mlp.log | cut -c1-200
-bash tools/gpu_stats.sh mlp --config mlp | head -14 | cut -c1-160
+bash tools/gpu_stats.sh mlp --config mlp > gpurun_out/stats_mlp.txt || exit 1
+head -14 gpurun_out/stats_mlp.txt | cut -c1-160
