@@ -44,6 +44,7 @@ import torch.distributed as dist  # noqa: E402
 MI355X_INT8_DENSE_TOPS = 256 * 4 * 2048 * 2.4e9 / 1e12   # 32x32x32 i8 MFMA: 2048 ops/clk/SIMD
 MI355X_FP4_DENSE_TOPS = 256 * 4 * 4096 * 2.4e9 / 1e12    # 32x32x64 f8f6f4 MFMA (FP4/FP6): 4096 ops/clk/SIMD
 MI355X_F32_MFMA_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12     # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
+MI355X_BF16_DENSE_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # 16x16x32 / 32x32x16 bf16 MFMA: 1024 FLOP/clk/SIMD
 MI355X_DOT4_TOPS = 256 * 64 * 8 * 2.4e9 / 1e12           # v_dot4_i32_i8 on the VALU: 64 lanes x 8 ops /clk/CU
 # ternary XNOR-popcount on the VALU: 5 ops (and, xor, and, 2 x v_bcnt_u32 accumulate) per 32 MACs,
 # 4 SIMDs x 16 lanes per CU per clock (tools/xnor_probe.py)
@@ -68,6 +69,8 @@ def digit_pairs(kernel):
     an FP4 ternary operand on gemm_fp6 (4 passes)."""
     if kernel.startswith("gemm_fp6"):
         return 4
+    if kernel.startswith("conv2d_bwd"):   # dY as 3 exact bf16 terms (bf16x3) on the bf16 MFMA
+        return 3
     for tag, n in (("<3, 3,", 6), ("<3, 1,", 3)):
         if tag in kernel:
             return n
@@ -76,8 +79,8 @@ def digit_pairs(kernel):
 
 def op_peak(kernel):
     """(bound, dense peak TOPS, what is counted) of an ops-counted kernel."""
-    if kernel.startswith("conv2d_bwd"):
-        return "mfma", MI355X_F32_MFMA_TFLOPS, "f32 MFMA flops (2*N*Co*OH*OW*C*KH*KW)"
+    if kernel.startswith("conv2d_bwd"):   # the default bf16x3 kernels (bnn_conv_set_mfma(1))
+        return "mfma", MI355X_BF16_DENSE_TFLOPS, "algorithmic conv flops 2*N*Co*OH*OW*C*KH*KW on the bf16 MFMA (3 bf16 terms of dY)"
     if kernel.startswith("conv2d_fwd"):   # C=1 layer on VALU dot4; C%16==0 layers on int8 MFMA (looser bound)
         return "valu", MI355X_DOT4_TOPS, "int8 dot4 / MFMA ops (2*N*Co*OH*OW*C*KH*KW)"
     if kernel.startswith("gemm_fp4"):
