@@ -551,7 +551,7 @@ struct Q6Out {
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, 2) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
                                                          const float* __restrict__ invstd,

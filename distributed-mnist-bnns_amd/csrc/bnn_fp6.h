@@ -114,10 +114,18 @@ __device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bo
 }
 
 // One whole 32-element block quantised by ONE lane, element i read from LDS at src[i * STRIDE]
-// (read twice: once for the block max, then in two halves for the digits, to keep the register
-// footprint small): its four plane records -- plane j's 6 dwords, element i at bits 6i -- written
-// as lo (16 B per plane, 64 B) and hi (dwords 4-5 of planes 0..3, 32 B), and the plane-0 scale
-// byte.  No cross-lane traffic.
+// (read twice: once for the block max, then for the digits): its four plane records -- plane j's
+// 6 dwords, element i at bits 6i -- written as lo (16 B per plane, 64 B) and hi (dwords 4-5 of
+// planes 0..3, 32 B), and the plane-0 scale byte.  No cross-lane traffic.
+//
+// Encoding and packing on the conversion unit: w = rint(x 2^shift) + DIGIT_BIAS as in codes4,
+// plane j's 32 digits d = e_j - 16 (e_j the plain base-32 digits of w) are exact in f16, and ONE
+// v_cvt_scalef32_pk32_fp6_f16 per plane (scale 8: the e2m3 code of d/8) encodes and packs them
+// (element i at bits 6i, tools/probes/probe_cvt_fp6.hip).  Bit-identical to codes4 + the manual
+// 6-bit packing, with the per-plane min trick and the shift-or packing gone.
+typedef _Float16 q6v32h __attribute__((ext_vector_type(32)));
+typedef int q6v6i __attribute__((ext_vector_type(6)));
+
 template <int STRIDE>
 __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store, uint8_t* lo_blk, uint8_t* hi_blk,
                                                    uint8_t* sc_byte) {
@@ -126,36 +134,24 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
   for (int i = 0; i < QB; ++i) amax = absmax_nan(amax, src[i * STRIDE]);
   int shift;
   const int sbyte = block_scale(amax, &shift);
-  uint32_t w[4][6];
+  uint32_t w[QB];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int i = 0; i < QB; ++i) w[i] = (uint32_t)(__float2int_rn(ldexpf(src[i * STRIDE], shift)) + DIGIT_BIAS);
+  // one plane at a time (not unrolled: the 32 codes, one f16 vector and one record live at once)
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    q6v32h h;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) w[j][k] = 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float v[QB / 2];
-#pragma unroll
-    for (int i = 0; i < QB / 2; ++i) v[i] = src[(16 * h + i) * STRIDE];
-#pragma unroll
-    for (int i = 0; i < QB / 2; ++i) {
-      uint32_t cd[4];
-      codes4(v[i], shift, cd);
-      const int bit = 6 * (16 * h + i);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t c = cd[j];
-        w[j][bit >> 5] |= c << (bit & 31);
-        if ((bit & 31) > 26) w[j][(bit >> 5) + 1] |= c >> (32 - (bit & 31));
-      }
+    for (int i = 0; i < QB; ++i)   // e_3 = w >> 15 may be 32: 6 bits
+      h[i] = (_Float16)((int)__builtin_amdgcn_ubfe(w[i], 5 * j, j < 3 ? 5 : 6) - 16);
+    const q6v6i rec = __builtin_amdgcn_cvt_scalef32_pk32_fp6_f16(h, 8.0f);
+    if (store) {
+      *reinterpret_cast<uint4*>(lo_blk + 16 * j) =
+          make_uint4((uint32_t)rec[0], (uint32_t)rec[1], (uint32_t)rec[2], (uint32_t)rec[3]);
+      *reinterpret_cast<uint2*>(hi_blk + 8 * j) = make_uint2((uint32_t)rec[4], (uint32_t)rec[5]);
     }
   }
-  if (!store) return;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    *reinterpret_cast<uint4*>(lo_blk + 16 * j) = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
-  *reinterpret_cast<uint4*>(hi_blk) = make_uint4(w[0][4], w[0][5], w[1][4], w[1][5]);
-  *reinterpret_cast<uint4*>(hi_blk + 16) = make_uint4(w[2][4], w[2][5], w[3][4], w[3][5]);
-  *sc_byte = (uint8_t)sbyte;
+  if (store) *sc_byte = (uint8_t)sbyte;
 }
 
 // Rows of the E8M0 scale slab [K/64][rows_pad][2] a quantised operand of `rows` rows needs: the
