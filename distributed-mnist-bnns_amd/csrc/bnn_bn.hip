@@ -551,7 +551,7 @@ struct Q6Out {
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256, 2) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, NOUT > 0 ? 3 : 2) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
                                                          const float* __restrict__ invstd,
@@ -569,22 +569,37 @@ __global__ __launch_bounds__(256, 2) void bn_bwd_apply_q6_k(XIn xin, const float
   // elementwise mapping: float4 f = t + 256 i of a 64 x 64 sub-tile: row f / 16, columns 4 (f % 16)
   const int cq = 4 * (t & 15);
   const int64_t c = c0 + cq;
-  const float4 mv = ld4(mean + c), iv = ld4(invstd + c), s0 = ld4(sg + c), s1 = ld4(sgx + c);
-  const float4 gav = ld4_or(gamma, c, 1.f), bev = ld4_or(beta, c, 0.f), lv = ld4_or(mean_lo, c, 0.f);
-  const float4 xb = xin_bias4<Z16>(xin, c);
-  const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
-  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
-  const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
-  const float a0[4] = {s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n};
-  const float a1[4] = {s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n};
-  float wc[NOUT > 0 ? NOUT : 1][4];       // the head's weight columns c..c+3
-  if constexpr (NOUT > 0) {
+  // the 16 column groups' BatchNorm parameters (and the head's W4 columns) live in LDS and are read
+  // into registers for each sub-tile's dz phase only: dead during the quantisation phase, whose
+  // conversion-unit digits need the registers
+  // (the head variant only: it runs at 3 waves per SIMD; the plain variant keeps them in
+  // registers at 2 waves -- an LDS table filled per workgroup of 4 sub-tiles costs it more)
+  constexpr int NP = 7 + (NOUT > 0 ? NOUT : 0);
+  __shared__ float4 prm[NOUT > 0 ? NP : 1][16];
+  float4 rp[7];
+  if constexpr (NOUT == 0) {
+    const float4 s0 = ld4(sg + c), s1 = ld4(sgx + c);
+    rp[0] = ld4(mean + c), rp[1] = ld4(invstd + c), rp[2] = ld4_or(mean_lo, c, 0.f);
+    rp[3] = ld4_or(gamma, c, 1.f), rp[4] = ld4_or(beta, c, 0.f);
+    rp[5] = make_float4(s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n);
+    rp[6] = make_float4(s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n);
+  } else if (t < 16) {
+    const int64_t cg = c0 + 4 * t;
+    const float4 s0 = ld4(sg + cg), s1 = ld4(sgx + cg);
+    prm[0][t] = ld4(mean + cg);
+    prm[1][t] = ld4(invstd + cg);
+    prm[2][t] = ld4_or(mean_lo, cg, 0.f);
+    prm[3][t] = ld4_or(gamma, cg, 1.f);
+    prm[4][t] = ld4_or(beta, cg, 0.f);
+    prm[5][t] = make_float4(s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n);
+    prm[6][t] = make_float4(s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n);
+    if constexpr (NOUT > 0) {
 #pragma unroll
-    for (int q = 0; q < NOUT; ++q) {
-      const float4 f = ld4(w4 + q * C + c);
-      wc[q][0] = f.x, wc[q][1] = f.y, wc[q][2] = f.z, wc[q][3] = f.w;
+      for (int q = 0; q < NOUT; ++q) prm[7 + q][t] = ld4(w4 + q * C + cg);
     }
   }
+  if constexpr (NOUT > 0) __syncthreads();
+  const float4 xb = xin_bias4<Z16>(xin, c);
   double csum = 0.0;                      // waves 2-3: column lane, rows of block wave-2 of each sub-tile
   const int64_t mp = o.nblk_m * QB;
   constexpr int D4LD = NOUT > 0 ? (NOUT + 3) / 4 * 4 : 4;
@@ -614,6 +629,24 @@ __global__ __launch_bounds__(256, 2) void bn_bwd_apply_q6_k(XIn xin, const float
         d4s[i] = (m0 + rr < M && q < NOUT) ? dy[(m0 + rr) * NOUT + q] : 0.f;
       }
       __syncthreads();
+    }
+    if constexpr (NOUT > 0) asm volatile("" ::: "memory");   // the table reads stay inside the loop
+    const int pg = t & 15;
+    const float4 mv = NOUT > 0 ? prm[0][pg] : rp[0], iv = NOUT > 0 ? prm[1][pg] : rp[1];
+    const float4 lv = NOUT > 0 ? prm[2][pg] : rp[2], gav = NOUT > 0 ? prm[3][pg] : rp[3];
+    const float4 bev = NOUT > 0 ? prm[4][pg] : rp[4];
+    const float4 a0v = NOUT > 0 ? prm[5][pg] : rp[5], a1v = NOUT > 0 ? prm[6][pg] : rp[6];
+    const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
+    const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+    const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
+    const float a0[4] = {a0v.x, a0v.y, a0v.z, a0v.w}, a1[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
+    float wc[NOUT > 0 ? NOUT : 1][4];       // the head's weight columns c..c+3
+    if constexpr (NOUT > 0) {
+#pragma unroll
+      for (int q = 0; q < NOUT; ++q) {
+        const float4 f = prm[7 + q][pg];
+        wc[q][0] = f.x, wc[q][1] = f.y, wc[q][2] = f.z, wc[q][3] = f.w;
+      }
     }
 #pragma unroll
     for (int i = 0; i < Q6T_SUB / 16; ++i) {
