@@ -119,11 +119,13 @@ __device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bo
 // planes 0..3, 32 B), and the plane-0 scale byte.  No cross-lane traffic.
 //
 // Encoding and packing on the conversion unit: w = rint(x 2^shift) + DIGIT_BIAS as in codes4,
-// plane j's 32 digits d = e_j - 16 (e_j the plain base-32 digits of w) are exact in f16, and ONE
-// v_cvt_scalef32_pk32_fp6_f16 per plane (scale 8: the e2m3 code of d/8) encodes and packs them
-// (element i at bits 6i, tools/probes/probe_cvt_fp6.hip).  Bit-identical to codes4 + the manual
-// 6-bit packing, with the per-plane min trick and the shift-or packing gone.
+// plane j's 32 digits d = e_j - 16 (e_j the plain base-32 digits of w) are exact in f16 -- formed
+// two at a time with packed 16-bit/f16 arithmetic -- and ONE v_cvt_scalef32_pk32_fp6_f16 per plane
+// (scale 8: the e2m3 code of d/8) encodes and packs them (element i at bits 6i,
+// tools/probes/probe_cvt_fp6.hip).  Bit-identical to codes4 + the manual 6-bit packing.
 typedef _Float16 q6v32h __attribute__((ext_vector_type(32)));
+typedef _Float16 q6h2 __attribute__((ext_vector_type(2)));
+typedef uint32_t q6v16u __attribute__((ext_vector_type(16)));
 typedef int q6v6i __attribute__((ext_vector_type(6)));
 
 template <int STRIDE>
@@ -134,17 +136,29 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
   for (int i = 0; i < QB; ++i) amax = absmax_nan(amax, src[i * STRIDE]);
   int shift;
   const int sbyte = block_scale(amax, &shift);
-  uint32_t w[QB];
+  // element pairs (2k, 2k+1) packed in 16-bit halves: P = bits 0..15 of both w (digits 0-2 at
+  // bits 0, 5, 10 of each half), Q = their top digit (w >> 15, <= 32)
+  uint32_t P[QB / 2], Q[QB / 2];
 #pragma unroll
-  for (int i = 0; i < QB; ++i) w[i] = (uint32_t)(__float2int_rn(ldexpf(src[i * STRIDE], shift)) + DIGIT_BIAS);
-  // one plane at a time (not unrolled: the 32 codes, one f16 vector and one record live at once)
+  for (int k = 0; k < QB / 2; ++k) {
+    const uint32_t wa = (uint32_t)(__float2int_rn(ldexpf(src[(2 * k) * STRIDE], shift)) + DIGIT_BIAS);
+    const uint32_t wb = (uint32_t)(__float2int_rn(ldexpf(src[(2 * k + 1) * STRIDE], shift)) + DIGIT_BIAS);
+    P[k] = (wa & 0xFFFFu) | (wb << 16);
+    Q[k] = (wa >> 15) | ((wb >> 15) << 16);
+  }
+  // one plane at a time (not unrolled: the 16 pair words, one f16 vector and one record live at
+  // once).  A digit pair e (two 5/6-bit fields) becomes its f16 pair d = e - 16 exactly through
+  // the exponent trick: the halves of (e | 0x6400) read as f16 are 1024 + e, minus 1040.
 #pragma unroll 1
   for (int j = 0; j < 4; ++j) {
-    q6v32h h;
+    q6v16u hv;
 #pragma unroll
-    for (int i = 0; i < QB; ++i)   // e_3 = w >> 15 may be 32: 6 bits
-      h[i] = (_Float16)((int)__builtin_amdgcn_ubfe(w[i], 5 * j, j < 3 ? 5 : 6) - 16);
-    const q6v6i rec = __builtin_amdgcn_cvt_scalef32_pk32_fp6_f16(h, 8.0f);
+    for (int k = 0; k < QB / 2; ++k) {
+      const uint32_t e = j < 3 ? ((P[k] >> (5 * j)) & 0x001F001Fu) | 0x64006400u : Q[k] | 0x64006400u;
+      const q6h2 d = __builtin_bit_cast(q6h2, e) - q6h2{(_Float16)1040.f, (_Float16)1040.f};
+      hv[k] = __builtin_bit_cast(uint32_t, d);
+    }
+    const q6v6i rec = __builtin_amdgcn_cvt_scalef32_pk32_fp6_f16(__builtin_bit_cast(q6v32h, hv), 8.0f);
     if (store) {
       *reinterpret_cast<uint4*>(lo_blk + 16 * j) =
           make_uint4((uint32_t)rec[0], (uint32_t)rec[1], (uint32_t)rec[2], (uint32_t)rec[3]);
