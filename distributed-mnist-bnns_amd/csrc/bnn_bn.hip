@@ -506,9 +506,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // Workgroup: 256 rows x 64 columns, walked as 4 sub-tiles of 64 rows; C % 64 == 0.  Per sub-tile
 // all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
-constexpr int Q6T_ROWS = 256, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
+constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
 
-// Rows per workgroup of the fused apply: 256, or 64 when that leaves fewer than 1024 workgroups
+// Rows per workgroup of the fused apply: 512 (the parameter table is filled once per workgroup),
+// or 64 when that leaves fewer than 1024 workgroups
 // (small batches); never fewer rows than a statistics chunk (the column-sum partials reuse the
 // statistics workspace, one row per workgroup row).
 inline int64_t q6_rows(int64_t M, int64_t C) {
@@ -551,7 +552,7 @@ struct Q6Out {
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256, NOUT > 0 ? 3 : 2) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
                                                          const float* __restrict__ invstd,
@@ -571,19 +572,10 @@ __global__ __launch_bounds__(256, NOUT > 0 ? 3 : 2) void bn_bwd_apply_q6_k(XIn x
   const int64_t c = c0 + cq;
   // the 16 column groups' BatchNorm parameters (and the head's W4 columns) live in LDS and are read
   // into registers for each sub-tile's dz phase only: dead during the quantisation phase, whose
-  // conversion-unit digits need the registers
-  // (the head variant only: it runs at 3 waves per SIMD; the plain variant keeps them in
-  // registers at 2 waves -- an LDS table filled per workgroup of 4 sub-tiles costs it more)
+  // conversion-unit digits need the registers -- every variant fits 3 waves per SIMD unspilled
   constexpr int NP = 7 + (NOUT > 0 ? NOUT : 0);
-  __shared__ float4 prm[NOUT > 0 ? NP : 1][16];
-  float4 rp[7];
-  if constexpr (NOUT == 0) {
-    const float4 s0 = ld4(sg + c), s1 = ld4(sgx + c);
-    rp[0] = ld4(mean + c), rp[1] = ld4(invstd + c), rp[2] = ld4_or(mean_lo, c, 0.f);
-    rp[3] = ld4_or(gamma, c, 1.f), rp[4] = ld4_or(beta, c, 0.f);
-    rp[5] = make_float4(s0.x * inv_n, s0.y * inv_n, s0.z * inv_n, s0.w * inv_n);
-    rp[6] = make_float4(s1.x * inv_n, s1.y * inv_n, s1.z * inv_n, s1.w * inv_n);
-  } else if (t < 16) {
+  __shared__ float4 prm[NP][16];
+  if (t < 16) {
     const int64_t cg = c0 + 4 * t;
     const float4 s0 = ld4(sg + cg), s1 = ld4(sgx + cg);
     prm[0][t] = ld4(mean + cg);
@@ -598,7 +590,7 @@ __global__ __launch_bounds__(256, NOUT > 0 ? 3 : 2) void bn_bwd_apply_q6_k(XIn x
       for (int q = 0; q < NOUT; ++q) prm[7 + q][t] = ld4(w4 + q * C + cg);
     }
   }
-  if constexpr (NOUT > 0) __syncthreads();
+  __syncthreads();
   const float4 xb = xin_bias4<Z16>(xin, c);
   double csum = 0.0;                      // waves 2-3: column lane, rows of block wave-2 of each sub-tile
   const int64_t mp = o.nblk_m * QB;
@@ -630,12 +622,10 @@ __global__ __launch_bounds__(256, NOUT > 0 ? 3 : 2) void bn_bwd_apply_q6_k(XIn x
       }
       __syncthreads();
     }
-    if constexpr (NOUT > 0) asm volatile("" ::: "memory");   // the table reads stay inside the loop
+    asm volatile("" ::: "memory");   // the table reads stay inside the loop
     const int pg = t & 15;
-    const float4 mv = NOUT > 0 ? prm[0][pg] : rp[0], iv = NOUT > 0 ? prm[1][pg] : rp[1];
-    const float4 lv = NOUT > 0 ? prm[2][pg] : rp[2], gav = NOUT > 0 ? prm[3][pg] : rp[3];
-    const float4 bev = NOUT > 0 ? prm[4][pg] : rp[4];
-    const float4 a0v = NOUT > 0 ? prm[5][pg] : rp[5], a1v = NOUT > 0 ? prm[6][pg] : rp[6];
+    const float4 mv = prm[0][pg], iv = prm[1][pg], lv = prm[2][pg], gav = prm[3][pg], bev = prm[4][pg];
+    const float4 a0v = prm[5][pg], a1v = prm[6][pg];
     const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
     const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
     const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
