@@ -730,8 +730,27 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
 // pixels of one row: one ds_read_b128 from dY's plane, and one from the kw-shifted copy of the
 // input row (KW copies, so every tap's 8-pixel window starts 16-B aligned).  Each wave owns a set
 // of combo tiles for all co tiles (the A fragments are loaded once per k-step and reused).
+//   Staging, per sample: the thread's dY units (8 pixels of a row; B3_UD of them) and its slice of
+// the flat input (B3_PX elements, coalesced; fewer for the widest tilings) are loaded into
+// registers with clamped, unconditional loads (a guarded load is a branch, and the loads would not
+// batch), issued right after the previous sample's registers were written out, so they fly under
+// its image build and MFMA phase (barriers wait on LDS only).  The input lands once as ternary bf16 in a zero-haloed image xh;
+// the KW shifted copies are built from xh in LDS.  dB: each unit's owner thread accumulates the
+// unit's sum over the workgroup's samples in LDS; channels are folded once at the end.
+constexpr int B3_UD = 4, B3_PX = 8;
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)), not
+// for its global loads -- a __syncthreads() (workgroup release fence) would also drain vmcnt and
+// with it the loads in flight.  s_waitcnt simm16: vmcnt 63 | expcnt 7 | lgkmcnt 0.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (0 << 8) | (3 << 14));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct B3Filt {
-  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, OWq, Kp, Kd, xrow, Co16, NA, ncombo, ntn, WT, KS;
+  int C, H, W, Co, KH, KW, OH, OW, pad, Hp, OWq, Kp, Kd, xrow, Co16, NA, ncombo, ntn, WT, KS, Wh;
 };
 
 template <int NA, int MT>
@@ -744,7 +763,9 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
   const int PL = g.Co16 * g.Kd;
   unsigned short* xs = dyp + 3 * PL;                                    // KW x [C][Hp][xrow]
   const int XL = g.C * g.Hp * g.xrow;
-  float* bpart = reinterpret_cast<float*>(xs + g.KW * XL);             // [Co16][Kp / 8]
+  unsigned short* xh = xs + g.KW * XL;                                  // [C][Hp][Wh], zero halo
+  const int XH = g.C * g.Hp * g.Wh;
+  float* bpart = reinterpret_cast<float*>(xh + ((XH + 7) & ~7));      // [Co16][Kp / 8]
   __shared__ float sbias[64];
   const float inv_kk = 1.f / (float)(g.KH * g.KW), inv_kw = 1.f / (float)g.KW, inv_owq = 1.f / (float)g.OWq;
   const float inv_dq = 1.f / (float)(g.OH * (g.OWq / 8)), inv_nq = 1.f / (float)(g.OWq / 8);
@@ -753,8 +774,11 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
   const int grp = wv % g.WT, ks = wv / g.WT;
   const int KK = g.KH * g.KW;
   const int nq = g.OWq / 8, kq = g.Kp / 8;
+  const int ohw = g.OH * g.OW, hw = g.H * g.W;
+  const float inv_hw = 1.f / (float)hw, inv_w = 1.f / (float)g.W;
   if (t < 64) sbias[t] = 0.f;
   for (int i = t; i < 3 * PL; i += B3_T) dyp[i] = 0;     // zero tails: co >= Co, k >= OH*OWq
+  for (int i = t; i < XH; i += B3_T) xh[i] = 0;
   for (int i = t; i < g.Co16 * kq; i += B3_T) bpart[i] = 0.f;
   int boff[MT];
 #pragma unroll
@@ -773,59 +797,88 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
     for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
   const int kslice = g.Kp / g.KS, k_lo = ks * kslice, k_hi = k_lo + kslice;
   const int chunk = lane >> 4;
-  const int ohw = g.OH * g.OW, hw = g.H * g.W;
-  const int ndu = g.Co16 * g.OH * nq;                    // dY staging units (8 pixels of a row)
-  const int nxu = g.KW * g.C * g.Hp * nq;                 // input staging units (8 of a shifted row)
-  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
-  for (int64_t n = n0; n < n1; ++n) {
-    __syncthreads();   // previous sample's fragment reads are done
-    const float* dn = dy + n * (int64_t)g.Co * ohw;
-    for (int u = t; u < ndu; u += B3_T) {
-      const int co = fdivi(u, inv_dq), r = u - co * (g.OH * nq), oh = fdivi(r, inv_nq), q = r - oh * nq;
-      bf8 v1, v2, v3;
-      float bsum = 0.f;
+  const int ndu = g.Co16 * g.OH * nq;                    // dY units (8 pixels of a row)
+  const int nxu = g.KW * g.C * g.Hp * nq;                 // shifted-copy units (8 of a row)
+  // this thread's dY units u = t + 512 s: source offset of pixel 0 and the valid-pixel count
+  constexpr int W_ = NA * MT, UD = W_ >= 24 ? 1 : (W_ >= 12 ? B3_UD / 2 : B3_UD), PX = W_ >= 12 ? B3_PX / 2 : B3_PX;
+  int usrc[UD], uvalid[UD];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ow = 8 * q + j;
-        const float y = (co < g.Co && ow < g.OW) ? dn[(int64_t)co * ohw + oh * g.OW + ow] : 0.f;
-        bsum += y;
-        unsigned short d1, d2, d3;
-        bf16x3_split(y, d1, d2, d3);
-        v1[j] = (short)d1;
-        v2[j] = (short)d2;
-        v3[j] = (short)d3;
-      }
-      const int o = co * g.Kd + oh * g.OWq + 8 * q;
-      *reinterpret_cast<bf8*>(dyp + o) = v1;
-      *reinterpret_cast<bf8*>(dyp + PL + o) = v2;
-      *reinterpret_cast<bf8*>(dyp + 2 * PL + o) = v3;
-      bpart[co * kq + oh * nq + q] = bsum;
+  for (int s = 0; s < UD; ++s) {
+    const int u = min(t + s * B3_T, ndu - 1);
+    const int co = fdivi(u, inv_dq), r = u - co * (g.OH * nq), oh = fdivi(r, inv_nq), q = r - oh * nq;
+    const int ow0 = 8 * q;
+    uvalid[s] = (t + s * B3_T < ndu && co < g.Co) ? min(8, g.OW - ow0) : 0;
+    usrc[s] = min(co, g.Co - 1) * ohw + oh * g.OW + min(ow0, g.OW - 1);
+  }
+  const int tot_x = g.C * hw;
+  float ud[UD][8], px[PX];
+  auto fetch = [&](int64_t n) {   // clamped, unconditional: the loads batch
+    const float* dn = dy + n * (int64_t)g.Co * ohw;
+    const float* xn = x + n * (int64_t)tot_x;
+#pragma unroll
+    for (int s = 0; s < UD; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ud[s][j] = dn[usrc[s] + min(j, max(uvalid[s] - 1, 0))];
+#pragma unroll
+    for (int s = 0; s < PX; ++s) px[s] = xn[min(t + s * B3_T, tot_x - 1)];
+  };
+  auto put_unit = [&](int u, const float* v, int valid) {   // 3 bf16 planes + the unit's dB partial
+    const int co = fdivi(u, inv_dq), r = u - co * (g.OH * nq), oh = fdivi(r, inv_nq), q = r - oh * nq;
+    bf8 v1, v2, v3;
+    float bsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float y = j < valid ? v[j] : 0.f;
+      bsum += y;
+      unsigned short d1, d2, d3;
+      bf16x3_split(y, d1, d2, d3);
+      v1[j] = (short)d1;
+      v2[j] = (short)d2;
+      v3[j] = (short)d3;
     }
-    const float* xn = x + n * (int64_t)g.C * hw;
-    for (int u = t; u < nxu; u += B3_T) {
+    const int o = co * g.Kd + oh * g.OWq + 8 * q;
+    *reinterpret_cast<bf8*>(dyp + o) = v1;
+    *reinterpret_cast<bf8*>(dyp + PL + o) = v2;
+    *reinterpret_cast<bf8*>(dyp + 2 * PL + o) = v3;
+    bpart[co * kq + oh * nq + q] += bsum;   // this thread owns the unit for every sample
+  };
+  auto put_x = [&](int i, float v) {
+    const int c = fdivi(i, inv_hw), r = i - c * hw, ih = fdivi(r, inv_w), iw = r - ih * g.W;
+    const float xv = binarize ? (float)tsign(v) : v;
+    xh[(c * g.Hp + ih + g.pad) * g.Wh + iw + g.pad] = (unsigned short)(__float_as_uint(xv) >> 16);
+  };
+  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  if (n0 < n1) fetch(n0);
+  for (int64_t n = n0; n < n1; ++n) {
+    lds_barrier();   // previous sample's fragment and xh reads are done
+#pragma unroll
+    for (int s = 0; s < UD; ++s)
+      if (t + s * B3_T < ndu) put_unit(t + s * B3_T, ud[s], uvalid[s]);
+#pragma unroll
+    for (int s = 0; s < PX; ++s)
+      if (t + s * B3_T < tot_x) put_x(t + s * B3_T, px[s]);
+    for (int u = t + UD * B3_T; u < ndu; u += B3_T) {   // beyond the register slots: direct
+      const int co = fdivi(u, inv_dq), r = u - co * (g.OH * nq), oh = fdivi(r, inv_nq), q = r - oh * nq;
+      const int valid = co < g.Co ? min(8, g.OW - 8 * q) : 0;
+      const float* src = dy + n * (int64_t)g.Co * ohw + min(co, g.Co - 1) * ohw + oh * g.OW;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[min(8 * q + j, g.OW - 1)];
+      put_unit(u, v, valid);
+    }
+    for (int i = t + PX * B3_T; i < tot_x; i += B3_T) put_x(i, x[n * (int64_t)tot_x + i]);
+    if (n + 1 < n1) fetch(n + 1);   // in flight across the copy build and the MFMA phase
+    lds_barrier();
+    for (int u = t; u < nxu; u += B3_T) {   // shifted copies from xh: copy kw, column p = x col p + kw - pad
       const int kw = fdivi(u, inv_xq), r0 = u - kw * (g.C * g.Hp * nq);
       const int c = fdivi(r0, inv_hq), r1 = r0 - c * (g.Hp * nq), ihh = fdivi(r1, inv_nq), q = r1 - ihh * nq;
-      const int ih = ihh - g.pad;
+      const unsigned short* src = xh + (c * g.Hp + ihh) * g.Wh + 8 * q + kw;
       bf8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int iw = 8 * q + j + kw - g.pad;
-        float xv = 0.f;
-        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) xv = xn[(int64_t)c * hw + ih * g.W + iw];
-        if (binarize) xv = (float)tsign(xv);
-        v[j] = (short)(__float_as_uint(xv) >> 16);     // exact: +-1 / 0 (or a bf16-exact input)
-      }
+      for (int j = 0; j < 8; ++j) v[j] = (short)src[j];
       *reinterpret_cast<bf8*>(xs + kw * XL + (c * g.Hp + ihh) * g.xrow + 8 * q) = v;
     }
-    __syncthreads();
-    if (with_bias) {   // dB: wave w folds channels w, w+4, ... (fixed order: deterministic)
-      for (int co = wv; co < g.Co; co += B3_W) {
-        float sb = 0.f;
-        for (int i = lane; i < kq; i += 64) sb += bpart[co * kq + i];
-        const double tot = wave_sum((double)sb);
-        if (lane == 0) sbias[co] += (float)tot;
-      }
-    }
+    lds_barrier();
     for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
       const int kk = k0 + 8 * chunk;
       const int ohq = fdivi(kk, inv_owq), ow0 = kk - ohq * g.OWq;
@@ -845,6 +898,15 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
           for (int j = 0; j < 3; ++j)
             acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a][j], bv, acc[a][m], 0, 0, 0);
       }
+    }
+  }
+  __syncthreads();
+  if (with_bias) {   // dB: wave w folds channels w, w+8, ... (fixed order: deterministic)
+    for (int co = wv; co < g.Co; co += B3_W) {
+      float sb = 0.f;
+      for (int i = lane; i < kq; i += 64) sb += bpart[co * kq + i];
+      const double tb = wave_sum((double)sb);
+      if (lane == 0) sbias[co] = (float)tb;
     }
   }
   __syncthreads();
@@ -1164,10 +1226,12 @@ inline bool b3_filt_geom(const ConvShape& s, int binarize, B3Filt* g, int64_t* l
   d.Kp = (int)round_up((int64_t)d.OH * d.OWq, 32 * d.KS);
   d.Kd = d.Kp + 8;
   d.xrow = d.OWq;
+  d.Wh = (int)round_up((int64_t)d.OWq + d.KW - 1, 8);   // xh columns read: 8q + kw + j < OWq + KW - 1
   if ((d.ntn + d.WT - 1) / d.WT > 8) return false;
   if ((int64_t)d.C * d.H * d.W >= (1 << 20) || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
   // rows read: oh + kh < OH + KH - 1 <= Hp (stride 1, pad <= K-1)
-  *lds = (int64_t)3 * d.Co16 * d.Kd * 2 + (int64_t)d.KW * d.C * d.Hp * d.xrow * 2 + (int64_t)d.Co16 * (d.Kp / 8) * 4;
+  *lds = (int64_t)3 * d.Co16 * d.Kd * 2 + (int64_t)d.KW * d.C * d.Hp * d.xrow * 2 +
+         round_up((int64_t)d.C * d.Hp * d.Wh, 8) * 2 + (int64_t)d.Co16 * (d.Kp / 8) * 4;
   *g = d;
   return *lds <= kMaxTileLds;
 }
