@@ -600,6 +600,16 @@ __global__ __launch_bounds__(MF_T) void conv_bwd_data_mfma_k(const float* __rest
 //   16x16x32 bf16 lane map: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], D[4(l>>4)+r][l&15].
 typedef short bf8 __attribute__((ext_vector_type(8)));
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)), not
+// for its global loads -- a __syncthreads() (workgroup release fence) would also drain vmcnt and
+// with it the loads in flight.  s_waitcnt simm16: vmcnt 63 | expcnt 7 | lgkmcnt 0.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (0 << 8) | (3 << 14));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 constexpr int B3_W = 8, B3_T = 64 * B3_W;   // 8 waves: two per SIMD, so LDS / MFMA latency overlaps
 
 struct B3Data {
@@ -620,6 +630,8 @@ __device__ __forceinline__ void bf16x3_split(float y, unsigned short& d1, unsign
   d3 = (unsigned short)(__float_as_uint(r2) >> 16);
 }
 
+constexpr int B3_DU = 2;   // register-prefetched dY units per thread (backward data)
+
 template <int NT, int MT>
 __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restrict__ dy, const float* __restrict__ w,
                                                             float* __restrict__ dx, int64_t N, B3Data g) {
@@ -630,12 +642,23 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
   const int KK = g.KH * g.KW;
   const int plane = g.OHp * g.OWp * g.ps;
   const float inv_ws = 1.f / (float)g.ws, inv_cop = 1.f / (float)g.Cop, inv_kw = 1.f / (float)g.KW;
-  for (int i = t; i < 16 * NT * g.ws; i += B3_T) {
-    const int ci = fdivi(i, inv_ws), k = i - ci * g.ws;
-    const int tap = fdivi(k, inv_cop), co = k - tap * g.Cop;
-    int v = 0;
-    if (ci < g.C && k < g.Kp && tap < g.taps && co < g.Co) v = tsign(w[(co * g.C + ci) * KK + tap]);
-    wsb[i] = v > 0 ? 0x3F80 : (v < 0 ? 0xBF80 : 0);
+  for (int i0 = t; i0 < 16 * NT * g.ws; i0 += 8 * B3_T) {   // 8 loads per thread in flight
+    float v[8];
+    bool ok[8];
+#pragma unroll
+    for (int k8 = 0; k8 < 8; ++k8) {
+      const int i = i0 + k8 * B3_T;
+      const int ci = fdivi(i, inv_ws), k = i - ci * g.ws;
+      const int tap = fdivi(k, inv_cop), co = k - tap * g.Cop;
+      ok[k8] = i < 16 * NT * g.ws && ci < g.C && k < g.Kp && tap < g.taps && co < g.Co;
+      v[k8] = w[ok[k8] ? (co * g.C + ci) * KK + tap : 0];   // clamped, unconditional: loads batch
+    }
+#pragma unroll
+    for (int k8 = 0; k8 < 8; ++k8) {
+      const int i = i0 + k8 * B3_T;
+      const int sv = ok[k8] ? tsign(v[k8]) : 0;
+      if (i < 16 * NT * g.ws) wsb[i] = sv > 0 ? 0x3F80 : (sv < 0 ? 0xBF80 : 0);
+    }
   }
   for (int i = t; i < 3 * plane; i += B3_T) img[i] = 0;   // zero halo (interior rewritten per sample)
   const int hT = g.KH - 1 - g.pad, wT = g.KW - 1 - g.pad;
@@ -653,31 +676,52 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
   const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
   const float inv_ohw = 1.f / (float)ohw, inv_ow = 1.f / (float)g.OW;
   const int nunit = (g.Cop / 8) * ohw;    // staging unit = 8 channels of one pixel
-  for (int64_t n = n0; n < n1; ++n) {
-    __syncthreads();
-    const float* dn = dy + n * (int64_t)g.Co * ohw;
-    for (int u = t; u < nunit; u += B3_T) {
-      // lanes walk consecutive pixels of one 8-channel group: each of the 8 loads is coalesced,
-      // each plane's 16-B chunk one ds_write_b128
-      const int c8 = fdivi(u, inv_ohw), r = u - c8 * ohw;
-      const int oh = fdivi(r, inv_ow), ow = r - oh * g.OW;
-      bf8 v1, v2, v3;
+  // lanes walk consecutive pixels of one 8-channel group: each of the 8 loads is coalesced, each
+  // plane's 16-B chunk one ds_write_b128.  The thread's first B3_DU units of the next sample are
+  // loaded into registers (clamped, unconditional: they batch) while this one is multiplied.
+  auto put = [&](int u, const float* v) {
+    const int c8 = fdivi(u, inv_ohw), r = u - c8 * ohw;
+    const int oh = fdivi(r, inv_ow), ow = r - oh * g.OW;
+    bf8 v1, v2, v3;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int co = 8 * c8 + j;
-        const float y = co < g.Co ? dn[(int64_t)co * ohw + r] : 0.f;
-        unsigned short d1, d2, d3;
-        bf16x3_split(y, d1, d2, d3);
-        v1[j] = (short)d1;
-        v2[j] = (short)d2;
-        v3[j] = (short)d3;
-      }
-      const int o = ((oh + hT) * g.OWp + ow + wT) * g.ps + 8 * c8;
-      *reinterpret_cast<bf8*>(img + o) = v1;
-      *reinterpret_cast<bf8*>(img + plane + o) = v2;
-      *reinterpret_cast<bf8*>(img + 2 * plane + o) = v3;
+    for (int j = 0; j < 8; ++j) {
+      const float y = 8 * c8 + j < g.Co ? v[j] : 0.f;
+      unsigned short d1, d2, d3;
+      bf16x3_split(y, d1, d2, d3);
+      v1[j] = (short)d1;
+      v2[j] = (short)d2;
+      v3[j] = (short)d3;
     }
-    __syncthreads();
+    const int o = ((oh + hT) * g.OWp + ow + wT) * g.ps + 8 * c8;
+    *reinterpret_cast<bf8*>(img + o) = v1;
+    *reinterpret_cast<bf8*>(img + plane + o) = v2;
+    *reinterpret_cast<bf8*>(img + 2 * plane + o) = v3;
+  };
+  auto load_unit = [&](int64_t n, int u, float* v) {
+    const int uc = min(u, nunit - 1);
+    const int c8 = fdivi(uc, inv_ohw), r = uc - c8 * ohw;
+    const float* dn = dy + n * (int64_t)g.Co * ohw + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = dn[min(8 * c8 + j, g.Co - 1) * ohw];
+  };
+  float ud[B3_DU][8];
+  auto fetch = [&](int64_t n) {
+#pragma unroll
+    for (int s = 0; s < B3_DU; ++s) load_unit(n, t + s * B3_T, ud[s]);
+  };
+  if (n0 < n1) fetch(n0);
+  for (int64_t n = n0; n < n1; ++n) {
+    lds_barrier();   // previous sample's fragment reads are done (and the set-up above on entry)
+#pragma unroll
+    for (int s = 0; s < B3_DU; ++s)
+      if (t + s * B3_T < nunit) put(t + s * B3_T, ud[s]);
+    for (int u = t + B3_DU * B3_T; u < nunit; u += B3_T) {
+      float v[8];
+      load_unit(n, u, v);
+      put(u, v);
+    }
+    if (n + 1 < n1) fetch(n + 1);
+    lds_barrier();
     mf4 acc[NT][MT];
 #pragma unroll
     for (int a = 0; a < NT; ++a)
@@ -738,16 +782,6 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
 // the KW shifted copies are built from xh in LDS.  dB: each unit's owner thread accumulates the
 // unit's sum over the workgroup's samples in LDS; channels are folded once at the end.
 constexpr int B3_UD = 4, B3_PX = 8;
-
-// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)), not
-// for its global loads -- a __syncthreads() (workgroup release fence) would also drain vmcnt and
-// with it the loads in flight.  s_waitcnt simm16: vmcnt 63 | expcnt 7 | lgkmcnt 0.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0xF | (7 << 4) | (0 << 8) | (3 << 14));
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 struct B3Filt {
   int C, H, W, Co, KH, KW, OH, OW, pad, Hp, OWq, Kp, Kd, xrow, Co16, NA, ncombo, ntn, WT, KS, Wh;
@@ -1066,6 +1100,9 @@ struct MfFwd {
   int C, H, W, Co, KH, KW, OH, OW, pad, Hp, Wp, CB, KC, KCp, ntile_pix;
 };
 
+constexpr int FW_IPB = 8;    // samples per forward workgroup (the weight staging amortises)
+constexpr int FW_PX = 16;    // per-thread register slots of the next sample's input
+
 template <int COT>
 __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias, float* __restrict__ y,
@@ -1075,14 +1112,24 @@ __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restric
   int8_t* xs = ws + COT * 16 * g.KCp * 16;                      // [Hp][Wp][C]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int KK = g.KH * g.KW, rowb = g.KCp * 16;
-  for (int i = t; i < COT * 16 * rowb; i += MF_T) {
-    const int co = i / rowb, kb = i - co * rowb, ch = kb >> 4, ci16 = kb & 15;
-    int v = 0;
-    if (co < g.Co && ch < g.KC) {
-      const int tap = ch / g.CB, ci = (ch - tap * g.CB) * 16 + ci16;
-      v = tsign(w[(co * g.C + ci) * KK + tap]);
+  {   // ternary weights, 8 loads per thread in flight (clamped, unconditional: they batch)
+    const int nws = COT * 16 * rowb;
+    const float inv_rowb = 1.f / (float)rowb, inv_cb = 1.f / (float)g.CB;
+    for (int i0 = t; i0 < nws; i0 += 8 * MF_T) {
+      float v[8];
+      bool ok[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k * MF_T;
+        const int co = fdivi(i, inv_rowb), kb = i - co * rowb, ch = kb >> 4, ci16 = kb & 15;
+        const int tap = fdivi(ch, inv_cb), ci = (ch - tap * g.CB) * 16 + ci16;
+        ok[k] = i < nws && co < g.Co && ch < g.KC;
+        v[k] = w[ok[k] ? (co * g.C + ci) * KK + tap : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (i0 + k * MF_T < nws) ws[i0 + k * MF_T] = (int8_t)(ok[k] ? tsign(v[k]) : 0);
     }
-    ws[i] = (int8_t)v;
   }
   const int nxs = g.Hp * g.Wp * g.C;
   for (int i = t; i < nxs; i += MF_T) xs[i] = 0;
@@ -1099,15 +1146,29 @@ __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restric
   const int my_tiles = (g.ntile_pix - wv + 3) / 4;
   const int h = lane >> 4;
   const float inv_w = 1.f / (float)g.W, inv_hw = 1.f / (float)HW;
-  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  const int64_t n0 = (int64_t)blockIdx.x * FW_IPB, n1 = (n0 + FW_IPB < N) ? n0 + FW_IPB : N;
+  const int tot = g.C * HW;
+  auto put = [&](int i, float v) {
+    const int c = fdivi(i, inv_hw), r = i - c * HW, ih = fdivi(r, inv_w), iw = r - ih * g.W;
+    xs[((ih + g.pad) * g.Wp + iw + g.pad) * g.C + c] = (int8_t)tsign(v);
+  };
+  // the next sample's input: flat, clamped, unconditional loads (they batch), in flight across
+  // the MFMA phase and the output stores (the barriers wait on LDS only)
+  float px[FW_PX];
+  auto fetch = [&](int64_t n) {
+    const float* xn = x + n * (int64_t)tot;
+#pragma unroll
+    for (int s = 0; s < FW_PX; ++s) px[s] = xn[min(t + s * MF_T, tot - 1)];
+  };
+  if (n0 < n1) fetch(n0);
   for (int64_t n = n0; n < n1; ++n) {
-    __syncthreads();
-    const float* xn = x + n * g.C * HW;
-    for (int i = t; i < g.C * HW; i += MF_T) {
-      const int c = fdivi(i, inv_hw), r = i - c * HW, ih = fdivi(r, inv_w), iw = r - ih * g.W;
-      xs[((ih + g.pad) * g.Wp + iw + g.pad) * g.C + c] = (int8_t)tsign(xn[i]);
-    }
-    __syncthreads();
+    lds_barrier();   // previous sample's fragment reads are done (and the set-up above on entry)
+#pragma unroll
+    for (int s = 0; s < FW_PX; ++s)
+      if (t + s * MF_T < tot) put(t + s * MF_T, px[s]);
+    for (int i = t + FW_PX * MF_T; i < tot; i += MF_T) put(i, x[n * (int64_t)tot + i]);
+    if (n + 1 < n1) fetch(n + 1);
+    lds_barrier();
     v4i acc[COT][4];
 #pragma unroll
     for (int a = 0; a < COT; ++a)
@@ -1301,7 +1362,7 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
   int64_t mlds = 0;
   if (binarize_input && g_conv_mfma && mf_fwd_geom(s, &mf, &mlds)) {
     const size_t lds = (size_t)mlds;
-    const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
+    const dim3 grid((unsigned)((N + FW_IPB - 1) / FW_IPB));
     const int cot = (mf.Co + 15) / 16;
     if (cot == 1) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<1>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
     else if (cot == 2) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<2>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
