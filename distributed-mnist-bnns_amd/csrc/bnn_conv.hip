@@ -467,7 +467,15 @@ __global__ __launch_bounds__(256) void conv_filter_tile_reduce2_k(const double* 
   const int64_t nelem = (int64_t)CO * ncombo + CO;
   if (e >= nelem) return;
   double acc = 0.0;
-  for (int64_t q = 0; q < nslices; ++q) acc += slice[q * nelem + e];
+  int64_t q = 0;
+  for (; q + 8 <= nslices; q += 8) {   // 8 independent loads in flight; the adds stay in order
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = slice[(q + j) * nelem + e];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  for (; q < nslices; ++q) acc += slice[q * nelem + e];
   if (e < (int64_t)CO * ncombo) {
     const int64_t co = e / ncombo, combo = e % ncombo;
     if (co < Co) dw[co * ncombo + combo] = (float)acc;
