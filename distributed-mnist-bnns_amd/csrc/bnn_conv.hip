@@ -231,21 +231,33 @@ __global__ __launch_bounds__(TILE_T) void conv_fwd_bin_tile_k(const float* __res
   for (int i = t; i < nw; i += TILE_T) {
     const int co = i % CO, cg = (i / CO) % g.C4, kk = i / (CO * g.C4);
     const int kh = kk / g.KW, kw = kk % g.KW;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // clamped, unconditional loads: the four batch
+      const int ci = min(4 * cg + j, g.C - 1);
+      v[j] = w[((min(co, g.Co - 1) * g.C + ci) * g.KH + kh) * g.KW + kw];
+    }
     int word = 0;
-    if (co < g.Co)
-      for (int j = 0; j < 4; ++j) {
-        const int ci = 4 * cg + j;
-        if (ci < g.C) word |= (tsign(w[((co * g.C + ci) * g.KH + kh) * g.KW + kw]) & 255) << (8 * j);
-      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (co < g.Co && 4 * cg + j < g.C) word |= (tsign(v[j]) & 255) << (8 * j);
     ws[i] = word;
   }
   for (int i = t; i < nx; i += TILE_T) xs[i] = 0;
   __syncthreads();
   int8_t* xs8 = reinterpret_cast<int8_t*>(xs);
   const float* xn = x + (int64_t)n * g.C * g.H * g.W;
-  for (int i = t; i < g.C * g.H * g.W; i += TILE_T) {   // coalesced over the NCHW plane
-    const int iw = i % g.W, ih = (i / g.W) % g.H, c = i / (g.W * g.H);
-    xs8[((ih + g.pad) * g.Wp + (iw + g.pad)) * g.C4 * 4 + c] = (int8_t)tsign(xn[i]);
+  const int nin = g.C * g.H * g.W;
+  for (int i0 = t; i0 < nin; i0 += 4 * TILE_T) {   // coalesced over the NCHW plane, 4 loads in flight
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = xn[min(i0 + j * TILE_T, nin - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * TILE_T;
+      const int iw = i % g.W, ih = (i / g.W) % g.H, c = i / (g.W * g.H);
+      if (i < nin) xs8[((ih + g.pad) * g.Wp + (iw + g.pad)) * g.C4 * 4 + c] = (int8_t)tsign(v[j]);
+    }
   }
   __syncthreads();
   for (int p = t; p < g.OH * g.OW; p += TILE_T) {
