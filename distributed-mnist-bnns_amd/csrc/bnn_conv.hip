@@ -282,6 +282,76 @@ __global__ __launch_bounds__(TILE_T) void conv_fwd_bin_tile_k(const float* __res
   }
 }
 
+// Single-channel binary input (the BinCNN's first layer): 4 kw taps per dot4 instead of one useful
+// byte in four.  Input signs as bytes [Hp][Wq] (Wq = round_up(Wp, 4), zero halo, 16 slack bytes),
+// weights [KH][KWG][CO] words holding taps 4g..4g+3 of one row (zero beyond KW).  A pixel's
+// window of row kh starts at byte b = (oh+kh)*Wq + ow: the KWG+1 dwords from b/4 and
+// v_alignbyte give its taps in order; bytes past KW meet zero weight bytes.  Integer sums, so
+// bit-identical to conv_fwd_bin_tile_k.
+template <int CO, int KWG>
+__global__ __launch_bounds__(TILE_T) void conv_fwd_bin_c1_k(const float* __restrict__ x,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias,
+                                                            float* __restrict__ y, TileGeo g, int Wq) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  int* ws = lds;                                   // [KH][KWG][CO]
+  int* xw = lds + g.KH * KWG * CO;                 // [Hp][Wq / 4] words of sign bytes
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int nw = g.KH * KWG * CO, nxw = (g.Hp * Wq + 16) / 4;
+  for (int i = t; i < nw; i += TILE_T) {
+    const int co = i % CO, r = i / CO, kg = r % KWG, kh = r / KWG;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)   // clamped, unconditional: the loads batch
+      v[j] = w[(min(co, g.Co - 1) * g.KH + kh) * g.KW + min(4 * kg + j, g.KW - 1)];
+    int word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (co < g.Co && 4 * kg + j < g.KW) word |= (tsign(v[j]) & 255) << (8 * j);
+    ws[i] = word;
+  }
+  for (int i = t; i < nxw; i += TILE_T) xw[i] = 0;
+  __syncthreads();
+  int8_t* xb = reinterpret_cast<int8_t*>(xw);
+  const float* xn = x + (int64_t)n * g.H * g.W;
+  const int nin = g.H * g.W;
+  for (int i0 = t; i0 < nin; i0 += 4 * TILE_T) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = xn[min(i0 + j * TILE_T, nin - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * TILE_T, ih = i / g.W, iw = i - ih * g.W;
+      if (i < nin) xb[(ih + g.pad) * Wq + iw + g.pad] = (int8_t)tsign(v[j]);
+    }
+  }
+  __syncthreads();
+  for (int p = t; p < g.OH * g.OW; p += TILE_T) {
+    const int oh = p / g.OW, ow = p - oh * g.OW;
+    int acc[CO];
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[co] = 0;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int b = (oh + kh) * Wq + ow, sh = b & 3;
+      const int* src = xw + (b >> 2);
+      int d[KWG + 1];
+#pragma unroll
+      for (int k = 0; k <= KWG; ++k) d[k] = src[k];
+      const int* wr = ws + kh * KWG * CO;
+#pragma unroll
+      for (int kg = 0; kg < KWG; ++kg) {
+        const int xv = (int)__builtin_amdgcn_alignbyte((unsigned)d[kg + 1], (unsigned)d[kg], (unsigned)sh);
+#pragma unroll
+        for (int co = 0; co < CO; ++co) acc[co] = __builtin_amdgcn_sdot4(xv, wr[kg * CO + co], acc[co], false);
+      }
+    }
+    float* yp = y + (int64_t)n * g.Co * g.OH * g.OW + p;
+#pragma unroll
+    for (int co = 0; co < CO; ++co)
+      if (co < g.Co) yp[(int64_t)co * g.OH * g.OW] = (float)acc[co] + (bias ? bias[co] : 0.f);
+  }
+}
+
 template <int CO>
 __global__ __launch_bounds__(TILE_T) void conv_fwd_f32_tile_k(const float* __restrict__ x,
                                                               const float* __restrict__ w,
@@ -1387,6 +1457,24 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
     if (cot == 1) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<1>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
     else if (cot == 2) BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<2>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
     else BNN_TILE_LAUNCH(conv_fwd_i8mfma_k<4>, grid, dim3(MF_T), lds, st, x, w_latent, bias, y, N, mf);
+    return check_launch("bnn_conv2d_fwd");
+  }
+  if (binarize_input && g_conv_mfma && s.C == 1 && s.KW <= 8 && tile_geom_ok(s)) {
+    const TileGeo g = geo(s);
+    const int Wq = (int)round_up(g.Wp, 4), kwg = s.KW <= 4 ? 1 : 2;
+    const size_t lds = (size_t)(s.KH * kwg * pick_co(Co) * 4 + g.Hp * Wq + 16);
+#define BNN_C1(CO_, KG_) BNN_TILE_LAUNCH((conv_fwd_bin_c1_k<CO_, KG_>), dim3(N), dim3(TILE_T), lds, st, x, w_latent, bias, y, g, Wq)
+    switch (pick_co(Co) * 4 + kwg) {
+      case 8 * 4 + 1: BNN_C1(8, 1); break;
+      case 8 * 4 + 2: BNN_C1(8, 2); break;
+      case 16 * 4 + 1: BNN_C1(16, 1); break;
+      case 16 * 4 + 2: BNN_C1(16, 2); break;
+      case 32 * 4 + 1: BNN_C1(32, 1); break;
+      case 32 * 4 + 2: BNN_C1(32, 2); break;
+      case 64 * 4 + 1: BNN_C1(64, 1); break;
+      default: BNN_C1(64, 2); break;
+    }
+#undef BNN_C1
     return check_launch("bnn_conv2d_fwd");
   }
   if (tile_geom_ok(s) && fwd_tile_lds(s, binarize_input != 0) <= kMaxTileLds) {
