@@ -176,10 +176,20 @@ def gpu_torch_baseline(cfg, batch, budget=4.0):
             "sample": f"{steps} steps at batch {batch}, {secs:.1f} s"}
 
 
+# Timers named after a C-ABI call rather than one kernel: the kernels one call launches (the
+# first family counts the calls; the others -- the dW fold -- add their bytes to each call).
+TIMER_KERNELS = {
+    "conv2d_bwd_filter": ("conv_bwd_filter_bf3_k<", "conv_filter_tile_reduce1_k", "conv_filter_tile_reduce2_k"),
+    "conv2d_bwd_data": ("conv_bwd_data_bf3_k<",),
+    "conv2d_fwd": ("conv_fwd_",),
+}
+
+
 def pmc_traffic(kernel):
     """HBM/fabric bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench, gfx950-corrected).  None when no pass covers the kernel."""
+    WRITE_SIZE passes of this bench, gfx950-corrected).  For a timer in TIMER_KERNELS: all bytes of
+    the call's kernels over the number of calls.  None when no pass covers the kernel."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
     prefix = kernel.rstrip(">")
@@ -187,6 +197,18 @@ def pmc_traffic(kernel):
         try:
             ks = json.load(open(f))["kernels"]
         except (OSError, ValueError, KeyError):
+            continue
+        if kernel in TIMER_KERNELS:
+            fams = TIMER_KERNELS[kernel]
+            calls, total = 0, 0
+            for name, v in ks.items():
+                for i, fam in enumerate(fams):
+                    if name.startswith(fam):
+                        n = sum(gv["launches"] for gv in v["grids"].values())
+                        total += v["traffic_bytes_per_launch"] * n
+                        calls += n if i == 0 else 0
+            if calls:
+                return int(total / calls), os.path.relpath(f, ROOT)
             continue
         for name, v in ks.items():
             if name == kernel or (name.startswith(prefix) and name[len(prefix):len(prefix) + 1] in (",", ">")):
