@@ -778,7 +778,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
             ctx.has_bias = bias is not None
             return y
         macs = N * Co * OH * OW * (C // groups) * KH * KW
-        with _timed("conv2d_fwd", 2 * macs):
+        with _timed("conv2d_fwd", 2 * macs, 4 * (x.numel() + y.numel() + w.numel())):
             L.call("bnn_conv2d_fwd", L.ptr(x), int(binarize_input), L.ptr(w), L.ptr(b), L.ptr(y),
                    N, C, H, W, Co, KH, KW, stride, padding, dilation, groups, L.stream())
         ctx.save_for_backward(x, w)
@@ -802,7 +802,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
         macs = dy.numel() * (C // groups) * KH * KW
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            with _timed("conv2d_bwd_data", 2 * macs):
+            with _timed("conv2d_bwd_data", 2 * macs, 4 * (dy.numel() + dx.numel() + w.numel())):
                 L.call("bnn_conv2d_bwd_data", L.ptr(dy), L.ptr(w), L.ptr(dx), N, C, H, W, Co, KH, KW,
                        stride, padding, dilation, groups, L.stream())
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
@@ -811,7 +811,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
             db = torch.empty((Co,), dtype=torch.float32, device=x.device) if need_db else None
             ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
                              dtype=torch.uint8, device=x.device)
-            with _timed("conv2d_bwd_filter", 2 * macs):
+            with _timed("conv2d_bwd_filter", 2 * macs, 4 * (dy.numel() + x.numel() + w.numel())):
                 L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
                        L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
                        L.stream())
