@@ -274,8 +274,8 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
 #pragma unroll
       for (int u = 0; u < FIN_B; ++u) {
         const int64_t r = rb + u * FIN_GROUPS;
-        q0[u] = r < R ? p0[r * C + c] : 0.0;
-        q1[u] = r < R ? p1[r * C + c] : 0.0;
+        q0[u] = p0[min(r, R - 1) * C + c];   // clamped, unconditional: the loads batch
+        q1[u] = p1[min(r, R - 1) * C + c];
       }
 #pragma unroll
       for (int u = 0; u < FIN_B; ++u) {
@@ -413,8 +413,8 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
 #pragma unroll
       for (int u = 0; u < FIN_B; ++u) {
         const int64_t r = rb + u * FIN_GROUPS;
-        q0[u] = r < R ? p0[r * C + c] : 0.0;
-        q1[u] = r < R ? p1[r * C + c] : 0.0;
+        q0[u] = p0[min(r, R - 1) * C + c];   // clamped, unconditional: the loads batch
+        q1[u] = p1[min(r, R - 1) * C + c];
         qg[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[r * C + c] : 0.f;
         qx[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[(R + r) * C + c] : 0.f;
       }
