@@ -701,6 +701,9 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 constexpr int B3_W = 8, B3_T = 64 * B3_W;   // 8 waves: two per SIMD, so LDS / MFMA latency overlaps
+// samples per bf16x3 workgroup: 16 once that still gives >= 256 workgroups (one round over the CUs
+// at N = 4096; the per-workgroup set-up amortises), else MF_IPB (the filter workspace's bound)
+inline int b3_ipb(int64_t N) { return N >= 16 * 256 ? 16 : MF_IPB; }
 
 struct B3Data {
   int C, H, W, Co, Cop, KH, KW, OH, OW, pad, OHp, OWp, taps, Kp, ntile_pix;
@@ -724,7 +727,8 @@ constexpr int B3_DU = 2;   // register-prefetched dY units per thread (backward 
 
 template <int NT, int MT>
 __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restrict__ dy, const float* __restrict__ w,
-                                                            float* __restrict__ dx, int64_t N, B3Data g) {
+                                                            float* __restrict__ dx, int64_t N, B3Data g,
+                                                            int ipb) {
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   unsigned short* wsb = reinterpret_cast<unsigned short*>(ldsf);          // [16 NT][ws] ternary bf16
   unsigned short* img = wsb + 16 * NT * g.ws;                              // 3 x [OHp * OWp][ps]
@@ -763,7 +767,7 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
   }
   const int my_tiles = (g.ntile_pix - wv + B3_W - 1) / B3_W;
   const int chunk = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  const int64_t n0 = (int64_t)blockIdx.x * ipb, n1 = (n0 + ipb < N) ? n0 + ipb : N;
   const float inv_ohw = 1.f / (float)ohw, inv_ow = 1.f / (float)g.OW;
   const int nunit = (g.Cop / 8) * ohw;    // staging unit = 8 channels of one pixel
   // lanes walk consecutive pixels of one 8-channel group: each of the 8 loads is coalesced, each
@@ -881,7 +885,7 @@ template <int NA, int MT>
 __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __restrict__ dy,
                                                               const float* __restrict__ x, int binarize,
                                                               float* __restrict__ part, int64_t N, B3Filt g,
-                                                              int with_bias) {
+                                                              int with_bias, int ipb) {
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   unsigned short* dyp = reinterpret_cast<unsigned short*>(ldsf);       // 3 x [Co16][Kd]
   const int PL = g.Co16 * g.Kd;
@@ -971,7 +975,7 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
     const float xv = binarize ? (float)tsign(v) : v;
     xh[(c * g.Hp + ih + g.pad) * g.Wh + iw + g.pad] = (unsigned short)(__float_as_uint(xv) >> 16);
   };
-  const int64_t n0 = (int64_t)blockIdx.x * MF_IPB, n1 = (n0 + MF_IPB < N) ? n0 + MF_IPB : N;
+  const int64_t n0 = (int64_t)blockIdx.x * ipb, n1 = (n0 + ipb < N) ? n0 + ipb : N;
   if (n0 < n1) fetch(n0);
   for (int64_t n = n0; n < n1; ++n) {
     lds_barrier();   // previous sample's fragment and xh reads are done
@@ -1517,9 +1521,10 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   int64_t blds = 0;
   if (g_conv_mfma == 1 && b3_data_geom(s, &bd, &blds)) {
     const size_t lds = (size_t)blds;
-    const dim3 grid((unsigned)((N + MF_IPB - 1) / MF_IPB));
+    const int ipb = b3_ipb(N);
+    const dim3 grid((unsigned)((N + ipb - 1) / ipb));
     const int per_wave = (bd.ntile_pix + B3_W - 1) / B3_W;
-#define BNN_B3D(NT_, MT_) BNN_TILE_LAUNCH((conv_bwd_data_bf3_k<NT_, MT_>), grid, dim3(B3_T), lds, st, dy, w_latent, dx, N, bd)
+#define BNN_B3D(NT_, MT_) BNN_TILE_LAUNCH((conv_bwd_data_bf3_k<NT_, MT_>), grid, dim3(B3_T), lds, st, dy, w_latent, dx, N, bd, ipb)
     if (bd.C <= 16) {
       if (per_wave <= 1) BNN_B3D(1, 1); else if (per_wave <= 2) BNN_B3D(1, 2); else if (per_wave <= 4) BNN_B3D(1, 4);
       else if (per_wave <= 8) BNN_B3D(1, 8); else BNN_B3D(1, 16);
@@ -1599,13 +1604,14 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   B3Filt bf;
   int64_t blds = 0;
   if (N > 0 && g_conv_mfma == 1 && b3_filt_geom(s, binarize_input, &bf, &blds)) {
-    const int64_t nblk = (N + MF_IPB - 1) / MF_IPB;
+    const int ipb = b3_ipb(N);
+    const int64_t nblk = (N + ipb - 1) / ipb;
     const int64_t parts = nblk * bf.KS;
     const int64_t nel = (int64_t)Co * bf.ncombo + Co;
     float* part = reinterpret_cast<float*>(work);
     const size_t lds = (size_t)blds;
     const int per_wave = (bf.ntn + bf.WT - 1) / bf.WT;
-#define BNN_B3F(NA_, MT_) BNN_TILE_LAUNCH((conv_bwd_filter_bf3_k<NA_, MT_>), dim3((unsigned)nblk), dim3(B3_T), lds, st, dy, x, binarize_input, part, N, bf, db != nullptr)
+#define BNN_B3F(NA_, MT_) BNN_TILE_LAUNCH((conv_bwd_filter_bf3_k<NA_, MT_>), dim3((unsigned)nblk), dim3(B3_T), lds, st, dy, x, binarize_input, part, N, bf, db != nullptr, ipb)
 #define BNN_B3F_MT(NA_) \
     if (per_wave <= 1) BNN_B3F(NA_, 1); else if (per_wave <= 2) BNN_B3F(NA_, 2); else if (per_wave <= 4) BNN_B3F(NA_, 4); \
     else BNN_B3F(NA_, 8);

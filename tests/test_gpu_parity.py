@@ -306,6 +306,31 @@ def test_conv_backward_mfma_matches_valu(F, shape):
         assert rel_err(g[2], db64) < GRAD_TOL
 
 
+@pytest.mark.parametrize("shape", [
+    (4096, 16, 14, 14, 32, 5, 2),    # BinCNN conv2 at the bench batch: 16 samples per workgroup
+    (4096, 1, 28, 28, 16, 5, 2),     # BinCNN conv1
+])
+def test_conv_backward_full_batch_vs_float64(F, shape):
+    """The bf16x3 conv backward at the bench's batch (the 16-samples-per-workgroup schedule, one
+    round over the CUs) against float64 torch convolutions of the binarised operands on the GPU."""
+    N, C, H, W, Co, K, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(N + C)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g)
+    x = torch.where(torch.rand(N, C, H, W, device="cuda", generator=g) < 0.3, torch.zeros_like(x), x)
+    w = torch.rand(Co, C, K, K, device="cuda", generator=g) * 2 - 1
+    b = torch.randn(Co, device="cuda", generator=g)
+    dy = torch.randn(N, Co, H, W, device="cuda", generator=g)
+    xt, wt, bt = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.binary_conv2d(xt, wt, bt, True, 1, pad, 1, 1).backward(dy)
+    xs, ws, d64 = torch.sign(x).double(), torch.sign(w).double(), dy.double()
+    dw64 = torch.nn.grad.conv2d_weight(xs, tuple(w.shape), d64, padding=pad)
+    dx64 = torch.nn.grad.conv2d_input(tuple(x.shape), ws, d64, padding=pad)
+    db64 = d64.sum((0, 2, 3))
+    for got, want in ((wt.grad, dw64), (xt.grad, dx64), (bt.grad, db64)):
+        err = float((got.double() - want).norm() / want.norm())
+        assert err < GRAD_TOL, err
+
+
 def test_hardtanh_backward(F):
     x = torch.tensor([-2.0, -1.0, -0.5, 0.0, 0.5, 1.0, 3.0] * 11, device="cuda")
     g = torch.randn_like(x)
