@@ -103,7 +103,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--backend", default="fp4", choices=["fp4", "mfma", "xnor"])
     ap.add_argument("--exchange", action="store_true",
-                    help="run the gradient-exchange bucket path at N=1 too (flat buckets, hooks)")
+                    help="run the gradient-exchange path at N=1 too: flat buckets, hooks and the RCCL "
+                         "bucket all-reduces / buffer broadcast on a one-rank group")
     ap.add_argument("--graph", action="store_true",
                     help="capture the training step as a HIP graph and time replays (1 GPU; bnn_amd.graph)")
     ap.add_argument("--fp32-input", action="store_true",
@@ -275,7 +276,9 @@ def main():
     batch = args.batch or CONFIGS[args.config][1]
     torch.manual_seed(0)
     model = build(args.config, args.backend).to(dev).train()
-    exchange = GradExchange(model, bucket_mb=args.bucket_mb) if use_exchange else None
+    # --exchange at N = 1: a one-rank RCCL group issuing every collective of an N-GPU step
+    exchange = (GradExchange(model, bucket_mb=args.bucket_mb, force_collectives=args.exchange)
+                if use_exchange else None)
     dstep = BF.DeviceStep(dev).activate() if args.graph else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model), device_step=dstep)
     as_u8 = args.config != "cnn" and not args.fp32_input

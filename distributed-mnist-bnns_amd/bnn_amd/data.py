@@ -23,6 +23,9 @@ ZERO_FRACTION = 0.807
 
 
 def synthetic_mnist(n, seed=1234, device="cuda", normalize=None, as_u8=False):
+    if as_u8 and normalize is not None:
+        raise ValueError("synthetic_mnist: u8 pixels carry no Normalize; pass normalize=(mean, std) to the "
+                         "model instead (nets.MLP(normalize=...) -> fc1.pixel_normalize)")
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     u = torch.rand((n, 1, 28, 28), generator=g, device=device)

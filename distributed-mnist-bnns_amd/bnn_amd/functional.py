@@ -416,10 +416,13 @@ Z16 = True
 _Z16_ATTR = "_bnn_z16"
 
 
+Z16_MIN_TILES = 512      # below this many 256x256 output tiles the fp32 epilogue is as cheap
+
+
 def z16_ok(M, N, K):
     """Whether a hidden BinarizeLinear [K -> N] over M rows may hand its output on as z16."""
     return (Z16 and Q6_HANDOFF and DIGIT_GEMM == "fp6" and N % 256 == 0 and round_up(K, 256) <= 32767
-            and (N // 256) * ((M + 255) // 256) >= 512)
+            and (N // 256) * ((M + 255) // 256) >= Z16_MIN_TILES)
 
 
 Z16_HANDOFFS = 0          # z16 placeholders produced (tests check the hand-off actually ran)
@@ -920,13 +923,20 @@ def _q6_wanted(x, C, training=True):
             and C % 64 == 0)
 
 
+Q6_HANDOFFS = 0           # FP6 digit hand-offs consumed by a linear backward (tests check they ran)
+
+
 def _q6_take(dy):
     """(rows Fp6Operand, cols Fp6Operand, colsum) attached to ``dy`` by bnn_bn_bwd_q6, or None."""
+    global Q6_HANDOFFS
     ent = getattr(dy, _Q6_ATTR, None)
     if ent is None:
         return None
     delattr(dy, _Q6_ATTR)
-    return ent[1:] if ent[0] == _q6_key(dy) else None
+    if ent[0] != _q6_key(dy):
+        return None
+    Q6_HANDOFFS += 1
+    return ent[1:]
 
 
 def _dz_placeholder(M, C, device):
@@ -1106,6 +1116,7 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
 
 
 HEAD_NOUT = 10
+HEAD_CALLS = 0            # fused drop->bn->htanh->fc heads run (tests check the path actually ran)
 
 
 class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
@@ -1118,6 +1129,8 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, weight, bias, running_mean, running_var, momentum, eps, p, seed, w4, b4):
         _check(z, weight, bias, running_mean, running_var, w4, b4)
+        global HEAD_CALLS
+        HEAD_CALLS += 1
         ctx.q6 = _q6_wanted(z, z.shape[-1])
         zz = _z16_of(z)                       # (int16, bias): the compact pre-activation
         if zz is None:

@@ -31,6 +31,9 @@ class GraphedStep:
             for _ in range(max(1, warmup)):
                 step_fn()
         torch.cuda.current_stream().wait_stream(side)
+        # the captured Adam reads its bias corrections from device tables built for the current lr
+        if hasattr(optimizer, "build_schedules"):
+            optimizer.build_schedules()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn()
@@ -47,6 +50,11 @@ class GraphedStep:
 
     def __call__(self, n=1):
         """Replay the captured step n times; returns the step function's (static) output."""
+        limit = self.opt.schedule_limit() if hasattr(self.opt, "schedule_limit") else None
+        if limit is not None and self.ds.steps + int(n) > limit:
+            # the *_sched kernels index the table by the device counter without a bound
+            raise RuntimeError(f"GraphedStep: {n} replays would run past the Adam schedule "
+                               f"({self.ds.steps} of {limit} steps used); recapture to rebuild it")
         for _ in range(n):
             self.graph.replay()
         self._shadow(n)

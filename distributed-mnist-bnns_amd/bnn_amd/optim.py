@@ -49,18 +49,20 @@ class LatentAdam(torch.optim.Optimizer):
         self._clamp = {id(p) for p in clamp_params}
         self.grad_scale = grad_scale
         self.device_step = device_step
-        self._sched = {}              # group index -> (table, lr, betas, first step, device ctr base)
+        self._sched = {}              # group index -> (device table, (lr, betas) it was built for)
 
-    def _schedule(self, gi, group, step, device):
-        """Device table for this group covering the device counter's steps: entry i holds the bias
-        corrections of Adam step (step at table build) + i - (counter at build)."""
+    def _schedule(self, gi, group, step, device, build):
+        """Device table for this group covering the device counter's steps: entry c holds the bias
+        corrections of Adam step (step at table build) + c - (counter at build).  ``build``: make
+        one if the cached table is missing or was built for another lr / betas; else None."""
         ds = self.device_step
         key = (group["lr"], tuple(group["betas"]))
         ent = self._sched.get(gi)
         if ent is None or ent[1] != key:
-            # entry c = Adam step first + c for device counter value c (build it before capturing)
+            if not build:
+                return None
             if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("LatentAdam: run one eager step with device_step before capturing")
+                raise RuntimeError("LatentAdam: build the device schedule (build_schedules) before capturing")
             first = step - ds.steps
             if first < 1:
                 raise RuntimeError("LatentAdam: device step counter ahead of the optimizer's steps")
@@ -68,20 +70,55 @@ class LatentAdam(torch.optim.Optimizer):
             ent = (tab, key)
             self._sched[gi] = ent
         if ds.steps >= ent[0].shape[0]:
-            raise RuntimeError("LatentAdam: device-step schedule exhausted")
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("LatentAdam: device-step schedule exhausted")
+            return None             # eager: per-launch bias corrections
         return ent[0]
+
+    def build_schedules(self):
+        """(Re)build every group's device table for its current lr / betas, between steps -- before
+        a HIP-graph capture (graph.GraphedStep calls it)."""
+        ds = self.device_step
+        if ds is None:
+            return
+        for gi, group in enumerate(self.param_groups):
+            steps = {self.state[p]["step"] for p in group["params"] if self.state.get(p)}
+            if not steps:
+                continue
+            if len(steps) != 1:
+                raise RuntimeError("LatentAdam: device_step needs every parameter of a group stepped together")
+            self._sched.pop(gi, None)
+            self._schedule(gi, group, steps.pop() + 1, group["params"][0].device, build=True)
+
+    def schedule_limit(self):
+        """Device counter value at which the first device table runs out (None: no table)."""
+        lens = [ent[0].shape[0] for ent in self._sched.values()]
+        return min(lens) if lens else None
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         ds = self.device_step
+        capturing = ds is not None and torch.cuda.is_current_stream_capturing()
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             sched = None
             small = []                # plain Adam + clamp tensors: one multi-tensor launch per 16
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            live = [p for p in group["params"] if p.grad is not None]
+            if ds is not None and live:
+                steps = {self.state[p]["step"] if self.state.get(p) else 0 for p in live}
+                if len(steps) != 1 or len(live) != len(group["params"]):
+                    # one table per group is indexed by the shared device counter
+                    raise RuntimeError("LatentAdam: device_step needs every parameter of a group to get a "
+                                       "gradient on every step")
+                # the table of this lr: built on the group's first step (or by build_schedules before
+                # a capture); an eager step at another lr (the trainer's lr-quirk epochs) uses the
+                # per-launch bias corrections -- bit-identical -- instead of rebuilding a table
+                sched = self._schedule(gi, group, steps.pop() + 1, live[0].device,
+                                       build=gi not in self._sched)
+                if sched is None and capturing:
+                    raise RuntimeError("LatentAdam: no device schedule for this lr (build_schedules before capturing)")
+            for p in live:
                 st = self.state[p]
                 if not st:
                     st["step"] = 0
@@ -91,18 +128,14 @@ class LatentAdam(torch.optim.Optimizer):
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 args = (g, st["exp_avg"], st["exp_avg_sq"], st["step"], group["lr"], b1, b2, group["eps"],
                         self.grad_scale, id(p) in self._clamp)
-                kw = {}
-                if ds is not None:
-                    if sched is None:
-                        sched = self._schedule(gi, group, st["step"], p.device)
-                    kw = dict(sched=sched, ctr=ds.ctr)
+                kw = dict(sched=sched, ctr=ds.ctr) if sched is not None else {}
                 # a binarized layer's weight also gets its next-forward ternary operands rewritten in
                 # the same pass (bnn_adam_clamp_pack); anything else: plain fused Adam + clamp
                 if not BF.adam_clamp_pack_(p, *args, **kw):
                     small.append((p, g, st["exp_avg"], st["exp_avg_sq"], st["step"], id(p) in self._clamp))
             if small:
                 BF.adam_clamp_multi_(small, group["lr"], b1, b2, group["eps"], self.grad_scale,
-                                     sched=sched, ctr=ds.ctr if ds is not None else None)
+                                     sched=sched, ctr=ds.ctr if sched is not None else None)
         if ds is not None:
             ds.advance()
         return loss

@@ -31,6 +31,9 @@ MI355X design:
   into the zeroed view -- one read-modify-write pass over the 563 MB of wide-MLP gradients fewer
   per step.  Valid while each weight gets one gradient per backward (no accumulation across
   micro-batches); the sink is armed by ``zero_grad`` and disarmed once the weight is written.
+* ``force_collectives=True`` issues every collective even on a one-rank group (the bucket
+  all-reduces, the per-forward buffer broadcast): the RCCL path of a multi-GPU run, exercised and
+  profiled on one GPU (an AVG over one rank leaves every gradient bit-identical).
 """
 import math
 
@@ -59,19 +62,23 @@ class _Bucket:
 
 class GradExchange:
     def __init__(self, module, process_group=None, bucket_mb=64, broadcast_buffers=True,
-                 init_broadcast=True, direct_write=True):
+                 init_broadcast=True, direct_write=True, force_collectives=False):
         if not dist.is_available() or not dist.is_initialized():
             raise RuntimeError("GradExchange needs an initialised torch.distributed process group")
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        self.force = bool(force_collectives)
+        self.collectives = 0       # collectives issued (all-reduces + buffer broadcasts)
+        # group rank 0 as a global rank: torch's src= arguments are global ranks
+        self.src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
         self.broadcast_buffers = broadcast_buffers
         self.use_avg = dist.get_backend(process_group) == "nccl"
         params = [p for p in module.parameters() if p.requires_grad]
         self._flat_buffers = self._coalesce_buffers(module)
         if init_broadcast:
             for p in params:
-                dist.broadcast(p.data, src=0, group=self.pg)
+                dist.broadcast(p.data, src=self.src, group=self.pg)
                 BF.invalidate_packed(p)     # written through .data: cached packed operands are stale
             self.sync_buffers()
         self.cap_bytes = max(1, int(bucket_mb * 2 ** 20))
@@ -172,14 +179,15 @@ class GradExchange:
     def sync_buffers(self):
         """DDP broadcast_buffers: rank 0's buffers to every rank -- packed into the staging
         buffer (one multi-tensor copy per dtype), ONE collective per device, unpacked."""
-        if self.world <= 1:
+        if self.world <= 1 and not self.force:
             return
-        root = dist.get_rank(self.pg) == 0 if self.pg is not None else dist.get_rank() == 0
+        root = dist.get_rank() == self.src
         for flat, lists in self._flat_buffers:
             if root:
                 for bufs, views in lists:
                     torch._foreach_copy_(views, bufs)
-            dist.broadcast(flat, src=0, group=self.pg)
+            dist.broadcast(flat, src=self.src, group=self.pg)
+            self.collectives += 1
             if not root:
                 for bufs, views in lists:
                     torch._foreach_copy_(bufs, views)
@@ -234,9 +242,10 @@ class GradExchange:
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
             b = self.buckets[self._next]
-            if self.world > 1:
+            if self.world > 1 or self.force:
                 op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
                 b.work = dist.all_reduce(b.view(), op=op, group=self.pg, async_op=True)
+                self.collectives += 1
             self._next += 1
 
     def finish(self):
@@ -248,7 +257,7 @@ class GradExchange:
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
-                if not self.use_avg:
+                if not self.use_avg and self.world > 1:
                     b.view().div_(self.world)
                 b.work = None
 

@@ -67,6 +67,9 @@ def parse(argv=None):
                     "instead of u8 pixels")
     ap.add_argument("--max-steps", type=int, default=0, help="stop each epoch after this many steps")
     ap.add_argument("--no-lr-quirk", action="store_true", help="drop the per-batch lr*=0.1 at epoch%%40==0")
+    ap.add_argument("--lr-quirk-period", type=int, default=40, help="the 40 of epoch%%40==0 (mnist-dist2.py:126)")
+    ap.add_argument("--device-step", action="store_true", help="eager steps on the device step counter (dropout "
+                    "seeds and Adam as --graph draws them: an eager twin of a --graph run)")
     ap.add_argument("--csv-prefix", default=None, help="write <prefix>_BATCH_TIME.csv / _EPOCH_TIME.csv")
     ap.add_argument("--checkpoint", default=None, help="write a latent-weight checkpoint here after every epoch")
     ap.add_argument("--resume", default=None, help="resume from a checkpoint written by --checkpoint")
@@ -105,7 +108,7 @@ def train(gpu, args):
     exchange = GradExchange(model) if world > 1 else None
     if args.graph and world > 1:
         raise SystemExit("--graph runs one process (the gradient exchange is not captured)")
-    dstep = BF.DeviceStep(device).activate() if args.graph else None
+    dstep = BF.DeviceStep(device).activate() if (args.graph or args.device_step) else None
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=nets.binary_params(model), device_step=dstep)
     crit = torch.nn.CrossEntropyLoss()
     first_epoch = 1
@@ -137,12 +140,13 @@ def train(gpu, args):
                 break
             sel = idx[batch_idx * args.batch_size:(batch_idx + 1) * args.batch_size]
             x, y = data.index_select(0, sel), targets.index_select(0, sel)
-            quirk = epoch % 40 == 0 and not args.no_lr_quirk
+            quirk = epoch % args.lr_quirk_period == 0 and not args.no_lr_quirk
             if args.graph and len(sel) == args.batch_size and not quirk:
                 # full batches replay one captured step on static buffers (the last, short batch
                 # and lr-quirk epochs run eagerly)
                 if graphed is None:
                     static_x, static_y = x.clone(), y.clone()
+                    loss = None             # drop the last eager step's autograd graph before capturing
                     graphed = GraphedStep(lambda: _step(static_x, static_y), opt, dstep, warmup=1)
                 else:
                     static_x.copy_(x)

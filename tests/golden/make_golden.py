@@ -178,7 +178,89 @@ def trace_case(name, gen, org_protocol, steps=3, batch=16, widths=(48, 32, 24), 
     save(name, **rec)
 
 
+def mnist_u8(gen, shape):
+    """The same synthetic MNIST-shaped pixels as bytes (80.7% exact zeros, rest 1..255)."""
+    u = torch.rand(shape, generator=gen)
+    v = torch.randint(1, 256, shape, generator=gen, dtype=torch.int64)
+    return torch.where(u < 0.807, torch.zeros_like(v), v).to(torch.uint8)
+
+
+def _bits(a):
+    """Sign pattern of a float array as packed bits (1 = positive), plus the count of zeros."""
+    a = np.asarray(a)
+    return np.packbits((a > 0).reshape(-1)), np.array(int((a == 0).sum()), np.int64)
+
+
+def trace_wide_case(name, steps=10, batch=256, widths=(256, 256, 256), lr=0.01):
+    """mnist-dist2.py:118-137 (org protocol, p = 0) at widths where every fusion of the build's
+    benched path applies (C % 256 for the fused head and the FP4 tiles, C % 64 for the FP6
+    hand-offs), input given as u8 pixels through ToTensor (x = u/255, mnist-dist2.py:96-99) so the
+    u8 pixel path reproduces it exactly.  Recorded: the loss and log-probs of every step, the
+    step-0 gradients of every parameter, the per-step gradients of the small (non-binarized)
+    parameters, the sign pattern and a float64 digest (sum, sum |.|, sum of squares) of every
+    latent weight after each step, the binarized activations of fc2 / fc3 (sign bits) per step,
+    and the final latent weights, parameters and running statistics."""
+    gen = torch.Generator().manual_seed(4321)
+    torch.manual_seed(11)
+    net = TraceNet(*widths, p_drop=0.0)
+    rec = {"init/" + k: np32(v) for k, v in net.state_dict().items()}
+    opt = torch.optim.Adam(net.parameters(), lr=lr)
+    crit = nn.CrossEntropyLoss()
+    acts = {}
+
+    def keep(nm):
+        def hook(mod, inp, out):
+            acts[nm] = np32(inp[0])
+        return hook
+
+    net.fc2.register_forward_hook(keep("fc2_in"))
+    net.fc3.register_forward_hook(keep("fc3_in"))
+    net.train()
+    named = dict(net.named_parameters())
+    small = [k for k in PARAM_NAMES if k not in ("fc1.weight", "fc2.weight", "fc3.weight")]
+    for s in range(steps):
+        u = mnist_u8(gen, (batch, 1, 28, 28))
+        t = torch.randint(0, 10, (batch,), generator=gen)
+        x = u.float().div(255.0)                   # transforms.ToTensor()
+        rec[f"s{s}/u8"] = u.numpy().reshape(batch, 784)
+        rec[f"s{s}/target"] = t.numpy().astype(np.int64)
+        opt.zero_grad()
+        out = net(x)
+        loss = crit(out, t)
+        loss.backward()
+        rec[f"s{s}/out"] = np32(out)
+        rec[f"s{s}/loss"] = np.array(loss.item(), np.float64)
+        for k, v in acts.items():
+            rec[f"s{s}/act/{k}"], rec[f"s{s}/act0/{k}"] = _bits(v)
+        for k in (PARAM_NAMES if s == 0 else small):
+            rec[f"s{s}/grad/{k}"] = np32(named[k].grad)
+        for p in net.parameters():                 # mnist-dist2.py:131-137
+            if hasattr(p, "org"):
+                p.data.copy_(p.org)
+        opt.step()
+        for p in net.parameters():
+            if hasattr(p, "org"):
+                p.org.copy_(p.data.clamp_(-1, 1))
+        for k in ("fc1.weight", "fc2.weight", "fc3.weight"):
+            o = named[k].org.double().numpy()
+            rec[f"s{s}/orgsign/{k}"], rec[f"s{s}/orgzero/{k}"] = _bits(o)
+            rec[f"s{s}/orgdigest/{k}"] = np.array([o.sum(), np.abs(o).sum(), (o * o).sum()], np.float64)
+    for k in PARAM_NAMES:
+        p = named[k]
+        rec[f"final/data/{k}"] = np32(p.org if hasattr(p, "org") else p)
+    for k, v in net.state_dict().items():
+        if "running" in k:
+            rec[f"final/buf/{k}"] = np32(v)
+    rec["meta/widths"] = np.array(widths, np.int64)
+    rec["meta/lr"] = np.array(lr, np.float64)
+    rec["meta/steps"] = np.array(steps, np.int64)
+    save(name, **rec)
+
+
 def main():
+    if sys.argv[1:] == ["trace_wide"]:        # regenerate only the wide trace
+        trace_wide_case("trace_wide")
+        return
     gen = torch.Generator().manual_seed(1234)
     # 1. first layer: input width 784 -> NOT binarised (binarized_modules.py:75)
     x = mnist_like(gen, (8, 784))
@@ -222,6 +304,8 @@ def main():
             idx = np.array(list(iter(s)), np.int64)
             rec[f"n{n}_ws{ws}_r{r}"] = idx if n < 1000 else idx[:64]
     save("sampler", **rec)
+    # 11. the wide trace (every fusion of the benched path applies)
+    trace_wide_case("trace_wide")
 
 
 if __name__ == "__main__":

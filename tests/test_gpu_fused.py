@@ -197,11 +197,19 @@ def test_bn_hardtanh_binary_linear_vs_float64(F, M, C, N, backend, training):
     assert rel_err(host(fc.bias.grad), db) < GRAD_TOL
 
 
-@pytest.mark.parametrize("M", [1024, 2048])
+@pytest.mark.parametrize("M", [1024, 2048, 65536])
 def test_wide_backward_heavy_tailed_vs_float64(F, M):
     """Config 5 width (K = N = 8192): dX = dY.W_b and dW = dY^T.X_b with dY magnitudes spread
     over e^+-9 inside every row and column, against float64 GEMMs (rocBLAS dgemm on the same
-    device: products of fp32 values and +-1/0 are exact in float64)."""
+    device: products of fp32 values and +-1/0 are exact in float64).  M = 65536 is the bench's
+    batch: dW then contracts over K = 65536 (2048 FP6 blocks per output).
+
+    Bar: 1e-5 norm-wise, and 1e-5 for EVERY row of dX and every row of dW (each output neuron).
+    Per-row bound: the FP6 operand rounds x to the step 2^(e-19) of its 32-element
+    block (max |x| in [2^(e-1), 2^e)), so the rounding error d has E|d|^2 = step^2/12 per element and
+    ||d_row||^2 <= sum_blocks 32 * (2^(e-19))^2 / 12 <= (32/12) * 2^-36 * sum_blocks max_b^2
+    <= 2.7 * 2^-36 * ||row||^2: ||d_row|| / ||row|| <= 6.2e-6 in expectation, whatever the dynamic
+    range across blocks; a random +-1 operand maps it to the output row with the same ratio."""
     torch.manual_seed(M)
     K = N = 8192
     x = torch.randn(M, K, device="cuda")
@@ -213,16 +221,23 @@ def test_wide_backward_heavy_tailed_vs_float64(F, M):
     wt = w.clone().requires_grad_(True)
     y = F.binary_linear(xt, wt, None, True, "fp4")
     y.backward(dy)
-    xb, wb = torch.sign(x).double(), torch.sign(w).double()
-    dx64 = dy.double() @ wb
+    del y
+    xb = torch.sign(x).double()
+    del x
     dw64 = dy.double().t() @ xb
-    err_dx = float(torch.linalg.norm(xt.grad.double() - dx64) / torch.linalg.norm(dx64))
+    del xb
     err_dw = float(torch.linalg.norm(wt.grad.double() - dw64) / torch.linalg.norm(dw64))
+    roww = torch.linalg.norm(wt.grad.double() - dw64, dim=1) / torch.linalg.norm(dw64, dim=1)
+    del dw64
+    dx64 = dy.double() @ torch.sign(w).double()
+    err_dx = float(torch.linalg.norm(xt.grad.double() - dx64) / torch.linalg.norm(dx64))
+    rowx = torch.linalg.norm(xt.grad.double() - dx64, dim=1) / torch.linalg.norm(dx64, dim=1)
+    print(f"\nM={M}: dX {err_dx:.2e} (worst row {float(rowx.max()):.2e}), "
+          f"dW {err_dw:.2e} (worst row {float(roww.max()):.2e})")
     assert err_dx < GRAD_TOL, err_dx
     assert err_dw < GRAD_TOL, err_dw
-    # per-row check too: the worst row of dX (each row has its own digit scale)
-    row_err = torch.linalg.norm(xt.grad.double() - dx64, dim=1) / torch.linalg.norm(dx64, dim=1)
-    assert float(row_err.max()) < 10 * GRAD_TOL, float(row_err.max())
+    assert float(rowx.max()) < GRAD_TOL, float(rowx.max())
+    assert float(roww.max()) < GRAD_TOL, float(roww.max())
 
 
 @pytest.mark.parametrize("hardtanh", [True, False])

@@ -149,3 +149,42 @@ def test_trainer_graph_mode(F):
     for p in m.parameters():
         assert torch.isfinite(p).all()
     assert int(m.bn1.num_batches_tracked.item()) == 2 * nb
+
+
+def test_trainer_graph_quirk_and_recapture(F):
+    """An lr-quirk epoch (mnist-dist2.py:126-127: lr *= 0.1 on every batch) in --graph mode runs
+    eagerly with per-launch Adam bias corrections (no device table rebuilt per batch), then the
+    next epoch recaptures at the new lr.  The whole run equals its eager twin (--device-step: same
+    device-counter dropout seeds, no graphs) bit for bit."""
+    from bnn_amd import trainer
+    base = ["--model", "small", "--epochs", "3", "--dataset-size", "640", "--batch-size", "128",
+            "--log-interval", "100", "--lr-quirk-period", "2"]
+    states = []
+    for mode in ("--graph", "--device-step"):
+        torch.manual_seed(0)
+        m = trainer.train(0, trainer.parse(base + [mode]))
+        torch.cuda.synchronize()
+        states.append({k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})
+    assert F._DEVICE_STEP is None
+    a, b = states
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_graph_replay_past_schedule_raises(F):
+    """Replays that would index past the device Adam table raise instead of reading beyond it."""
+    from bnn_amd.graph import GraphedStep
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch()
+    m = _model(3, p_drop=0.0)
+    ds = F.DeviceStep().activate()
+    try:
+        opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+        opt.SCHEDULE_STEPS = 4                  # a short table: built for counter values 0 .. 4
+        g = GraphedStep(_step_fn(m, opt, u, y), opt, ds, warmup=1)
+        g(3)
+        with pytest.raises(RuntimeError, match="past the Adam schedule"):
+            g(2)
+    finally:
+        ds.deactivate()

@@ -45,11 +45,14 @@ def run_linear(F, x, w, b, dy, binarize, backend="mfma"):
 
 
 @pytest.mark.parametrize("name", ["linear_first", "linear_hidden", "linear_nobias_zw"])
-def test_linear_matches_reference_golden(F, name):
+@pytest.mark.parametrize("backend", ["fp4", "mfma", "xnor"])
+def test_linear_matches_reference_golden(F, name, backend):
+    """The reference's own BinarizeLinear fixtures through every engine; "fp4" is the default one
+    (FP4 MFMA forward, FP6 digit-plane backward GEMMs)."""
     g = load_golden(name)
     binarize = not O.first_layer(g["x"])
     b = g["bias"] if g["has_bias"] else None
-    y, dx, dw, db = run_linear(F, g["x"], g["w_latent"], b, g["dy"], binarize)
+    y, dx, dw, db = run_linear(F, g["x"], g["w_latent"], b, g["dy"], binarize, backend)
     if binarize:
         assert np.array_equal(y, g["y"])
     else:
