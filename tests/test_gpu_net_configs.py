@@ -11,11 +11,22 @@ Both GPU paths run: the drop-in (reference call pattern: .org protocol, fp32 inp
 torch.optim.Adam + org_protocol_step) and the fused trainer path (u8 pixels, BN -> sign-pack ->
 FP4 GEMM, FP6 / int8 hand-offs, fused head, LatentAdam).
 
-Bars: loss |d| <= 1e-5; log-probs norm-wise <= 1e-5; every step-0 gradient norm-wise <= 1e-5
-(the fc biases feed BatchNorm, exact gradient 0: absolute); after the update every latent
-weight equals the oracle's to 1e-6 except where the oracle's gradient is within 1e-5 * max|g| of
-0 (Adam's first step moves a weight by lr * g / (|g| + eps) ~ +-lr, so a gradient whose sign is
-decided by rounding moves it by +-lr either way: tie-aware, as test_gpu_training.py).
+Checks:
+* fc1's output z1 (continuous: fp32 pixels, or u8 pixels through the exact integer path) against
+  float64: norm-wise <= 1e-6;
+* everything downstream of z1 against the oracle run FROM THE SAME z1 (MLPOracle.step(z1=...)).
+  fc1's input is continuous, so z1 carries fp32 rounding (the reference's own CPU sgemm differs
+  from float64 too), and an element within an ulp-scale window of bn1's batch mean takes whichever
+  sign that rounding gives it -- a handful of such BatchNorm near-ties per step at batch 4096, each
+  moving one sample's output by ~1e-3.  From the same z1 the near-ties resolve identically (libbnn
+  keeps the batch mean as an exact hi + lo pair), and the bars are: loss |d| <= 1e-5, log-probs
+  norm-wise <= 1e-5, every gradient norm-wise <= 1e-5 (the fc biases feed BatchNorm: exact
+  gradient 0, checked absolute);
+* the update: every parameter after the step equals torch's Adam (float64) + the clamp applied
+  to the GPU's own gradient, elementwise to 1e-7.  The first Adam step moves a weight by
+  lr * g / (|g| + eps): for |g| near eps it amplifies the gradient's elementwise rounding, so the
+  update is checked on the gradient the step actually had (the gradient is checked above); the
+  count of latents that land off the oracle's own update by > 1e-6 is printed.
 """
 import numpy as np
 import pytest
@@ -39,8 +50,7 @@ def host(t):
 
 
 def _case(batch):
-    """(initial state, u8 pixels, targets, oracle loss / log-probs / grads / latent weights after the
-    step), computed once per batch on the host."""
+    """(initial state, u8 pixels, targets), made once per batch on the host."""
     if batch in _CACHE:
         return _CACHE[batch]
     from bnn_amd import nets
@@ -50,12 +60,16 @@ def _case(batch):
     rng = np.random.default_rng(batch)
     u8 = np.where(rng.random((batch, 784)) < 0.807, 0, rng.integers(1, 256, (batch, 784))).astype(np.uint8)
     tgt = rng.integers(0, 10, batch).astype(np.int64)
-    orc = O.MLPOracle({k: v for k, v in state.items() if "num_batches" not in k}, lr=LR)
-    loss, out, grads = orc.step(O.to_tensor(u8), tgt)
-    res = (state, u8, tgt, loss, out, grads, {k: orc.org[k].copy() for k in BINARY_W},
-           {k: orc.p[k].copy() for k in orc.p})
-    _CACHE[batch] = res
-    return res
+    _CACHE[batch] = (state, u8, tgt)
+    return _CACHE[batch]
+
+
+def _adam1(p0, g, clamp):
+    """torch.optim.Adam's first step (lr LR, betas (0.9, 0.999), eps 1e-8) in float64, + clamp."""
+    g = np.asarray(g, np.float64)
+    m, v = 0.1 * g, 0.001 * g * g
+    new = np.asarray(p0, np.float64) - (LR / 0.1) * m / (np.sqrt(v) / np.sqrt(0.001) + 1e-8)
+    return np.clip(new, -1, 1) if clamp else new
 
 
 @pytest.mark.parametrize("path", ["dropin", "fused"])
@@ -66,7 +80,7 @@ def test_net_r3_one_step_vs_oracle(batch, path):
     from bnn_amd import functional as BF
     from bnn_amd import nets
     from bnn_amd.optim import LatentAdam, org_protocol_step
-    state, u8, tgt, loss_ref, out_ref, g_ref, org_ref, p_ref = _case(batch)
+    state, u8, tgt = _case(batch)
     fused = path == "fused"
     if fused:
         model = nets.Net(p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True)
@@ -75,6 +89,8 @@ def test_net_r3_one_step_vs_oracle(batch, path):
     model.load_state_dict({k: torch.as_tensor(v) for k, v in state.items()})
     model = model.cuda().train()
     named = dict(model.named_parameters())
+    z1 = {}
+    model.fc1.register_forward_hook(lambda mod, inp, out: z1.__setitem__("z", host(out).astype(np.float32)))
     if fused:
         opt = LatentAdam(model.parameters(), lr=LR, clamp_params=nets.binary_params(model))
         x = torch.as_tensor(u8).cuda()
@@ -90,29 +106,36 @@ def test_net_r3_one_step_vs_oracle(batch, path):
     loss.backward()
     if fused:     # the benched fusions ran: two FP6 digit hand-offs, the int8 one to fc1, the head
         assert [a - b for a, b in zip((BF.Q6_HANDOFFS, BF.I8C_HANDOFFS, BF.HEAD_CALLS), c0)] == [2, 1, 1]
+    grads = {k: host(p.grad) for k, p in named.items()}
+    # fc1 forward against float64 (x = ToTensor(u8) in fp32, as the reference's loader makes it)
+    x64 = O.to_tensor(u8).astype(np.float64)
+    z1_64 = x64 @ np.sign(state["fc1.weight"]).astype(np.float64).T + state["fc1.bias"]
+    ez1 = rel_err(z1["z"], z1_64)
+    assert ez1 <= 1e-6, ez1
+    # the oracle from the same z1
+    orc = O.MLPOracle({k: v for k, v in state.items() if "num_batches" not in k}, lr=LR)
+    loss_ref, out_ref, g_ref = orc.step(O.to_tensor(u8), tgt, z1=z1["z"])
     assert abs(loss.item() - loss_ref) <= TOL, (loss.item(), loss_ref)
     assert rel_err(host(out), out_ref) <= TOL
     errs = {}
-    for k, p in named.items():
-        got = host(p.grad)
+    for k in named:
         if k in FC_BIAS:
-            assert close(got, g_ref[k], 0.0, 1e-5), k
+            assert close(grads[k], g_ref[k], 0.0, 1e-5), k
             continue
-        errs[k] = rel_err(got, g_ref[k])
+        errs[k] = rel_err(grads[k], g_ref[k])
         assert errs[k] <= TOL, (k, errs[k])
     if fused:
         opt.step()
     else:
         org_protocol_step(model, opt)
-    flips = {}
-    for k in BINARY_W:
-        got = host(named[k] if fused else named[k].org).astype(np.float64)
-        g = g_ref[k]
-        tie = np.abs(g) <= 1e-5 * np.abs(g).max()
-        bad = np.abs(got - org_ref[k]) > 1e-6
-        assert not (bad & ~tie).any(), (k, int((bad & ~tie).sum()))
-        flips[k] = int(bad.sum())
-    for k in ("bn1.weight", "bn2.weight", "bn3.weight", "fc4.weight", "fc4.bias"):
-        assert close(host(named[k]), p_ref[k], 1e-6, 1e-7), k
-    print(f"\nNet r=3 batch {batch} {path}: dloss {abs(loss.item() - loss_ref):.1e}, "
-          f"grads {max(errs.values()):.1e}, tie-moved latents {flips}")
+    clamp = set(BINARY_W) | set(FC_BIAS)
+    moved = {}
+    for k in named:
+        got = host(named[k] if fused or k not in BINARY_W else named[k].org).astype(np.float64)
+        want = _adam1(state[k], grads[k], k in clamp)
+        d = float(np.abs(got - want).max())
+        assert d <= 1e-7, (k, d)
+        if k in BINARY_W:     # informational: latents off the oracle's own update
+            moved[k] = int((np.abs(got - orc.org[k]) > 1e-6).sum())
+    print(f"\nNet r=3 batch {batch} {path}: z1 {ez1:.1e}, dloss {abs(loss.item() - loss_ref):.1e}, "
+          f"grads {max(errs.values()):.1e}, latents off the oracle's update by >1e-6 (|g| near eps): {moved}")
