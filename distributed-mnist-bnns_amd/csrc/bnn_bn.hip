@@ -507,6 +507,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
 constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
+#ifndef Q6_HEAD_OCC
+#define Q6_HEAD_OCC 3          // waves per SIMD of the fused head's quantising backward (z16 input)
+#endif
+#if defined(Q6_DIAG_NOQUANT)
+constexpr bool Q6_DIAG_NOQUANT_ON = true;
+#else
+constexpr bool Q6_DIAG_NOQUANT_ON = false;
+#endif
 
 // Rows per workgroup of the fused apply: 512 (the parameter table is filled once per workgroup),
 // or 64 when that leaves fewer than 1024 workgroups
@@ -549,10 +557,65 @@ struct Q6Out {
   double* part;                    // [M/256 chunks][C] partial column sums, or null
 };
 
+// One sub-tile's digit records staged in LDS: rows (64 rows x 2 blocks of 32 columns) and columns
+// (64 columns x 2 blocks of 32 rows), each as its global layout slice -- 128 B lo / 64 B hi per row
+// or column (the 16-B chunk q of row i at chunk q ^ (i & 7) (lo) or q ^ (i & 3) (hi): the quantising
+// lanes' 16-B writes, 128 B apart, spread over the banks) -- and the scale bytes.
+struct Q6Stage {
+  uint8_t rlo[64][128], clo[64][128];
+  uint8_t rhi[64][64], chi[64][64];
+  uint8_t rsc[64][2], csc[64][2];
+};
+
+// q6_block_pre's sink for block b of row (column) i: plane j's lo 16 B -> chunk 4b + j, hi 8 B ->
+// half of chunk 2b + j / 2
+struct Q6StageSink {
+  uint8_t* lo;
+  uint8_t* hi;
+  uint8_t* sc;
+  int i, b;
+  __device__ __forceinline__ void plane(int j, uint4 l, uint2 h) {
+    *reinterpret_cast<uint4*>(lo + 16 * ((4 * b + j) ^ (i & 7))) = l;
+    *reinterpret_cast<uint2*>(hi + 16 * ((2 * b + (j >> 1)) ^ (i & 3)) + 8 * (j & 1)) = h;
+  }
+  __device__ __forceinline__ void scale(uint8_t v) { *sc = v; }
+};
+
+// The staged records of the sub-tile at rows m0.., columns c0.. to HBM, 16 B per thread and store:
+// row lo 64 x 128 B, row hi 64 x 64 B, column lo / hi likewise, the two 128-B scale runs.  Rows at
+// or beyond M are not stored (their scale bytes are: 0, inside the slab's padding, as it was
+// initialised).
+__device__ __forceinline__ void q6_stage_store(const Q6Stage& st, const Q6Out& o, int t, int64_t m0, int64_t M,
+                                               int64_t c0, int64_t nblk_c) {
+  const int64_t blk0 = c0 / QB, mblk0 = m0 / QB;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {            // lo: 512 chunks each
+    const int ch = t + 256 * it, i = ch >> 3, q = ch & 7;
+    const uint4 rv = *reinterpret_cast<const uint4*>(&st.rlo[i][16 * (q ^ (i & 7))]);
+    const uint4 cv = *reinterpret_cast<const uint4*>(&st.clo[i][16 * (q ^ (i & 7))]);
+    if (m0 + i < M) *reinterpret_cast<uint4*>(o.rlo + ((m0 + i) * nblk_c + blk0) * 64 + 16 * q) = rv;
+    *reinterpret_cast<uint4*>(o.clo + ((c0 + i) * o.nblk_m + mblk0) * 64 + 16 * q) = cv;
+  }
+  {                                           // hi: 256 chunks each
+    const int i = t >> 2, q = t & 3;
+    const uint4 rv = *reinterpret_cast<const uint4*>(&st.rhi[i][16 * (q ^ (i & 3))]);
+    const uint4 cv = *reinterpret_cast<const uint4*>(&st.chi[i][16 * (q ^ (i & 3))]);
+    if (m0 + i < M) *reinterpret_cast<uint4*>(o.rhi + ((m0 + i) * nblk_c + blk0) * 32 + 16 * q) = rv;
+    *reinterpret_cast<uint4*>(o.chi + ((c0 + i) * o.nblk_m + mblk0) * 32 + 16 * q) = cv;
+  }
+  if (t < 8) {                                // row scales: rows m0 .. m0+63, blocks blk0, blk0+1
+    *reinterpret_cast<uint4*>(o.rsc + (blk0 >> 1) * o.rsc_rows * 2 + m0 * 2 + 16 * t) =
+        *reinterpret_cast<const uint4*>(&st.rsc[8 * t][0]);
+  } else if (t < 16) {                        // column scales: columns c0 .. c0+63, blocks mblk0, +1
+    *reinterpret_cast<uint4*>(o.csc + (mblk0 >> 1) * o.csc_rows * 2 + c0 * 2 + 16 * (t - 8)) =
+        *reinterpret_cast<const uint4*>(&st.csc[8 * (t - 8)][0]);
+  }
+}
+
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_OCC : 3)) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
                                                          const float* __restrict__ invstd,
@@ -594,6 +657,15 @@ __global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float
   const float4 xb = xin_bias4<Z16>(xin, c);
   double csum = 0.0;                      // waves 2-3: column lane, rows of block wave-2 of each sub-tile
   const int64_t mp = o.nblk_m * QB;
+  // block maxima formed in the dz phase (|dz| bits, unsigned max: abs_bits / q6_block_pre) by LDS
+  // atomics -- rmax[b][row] over the row's 32 columns of block b, cmax[b][col] over the column's 32
+  // rows of block b -- so a quantising lane reads its block once; it zeroes its entry for the next
+  // sub-tile.  The sub-tile's digit records are staged in LDS (Q6Stage) and written out as whole
+  // lines by all 256 threads.
+  __shared__ uint32_t rmax[2][Q6T_SUB], cmax[2][Q6T_COLS];
+  __shared__ __attribute__((aligned(16))) Q6Stage st;
+  if (t < 2 * Q6T_SUB) rmax[t >> 6][t & 63] = 0u;
+  else cmax[(t >> 6) - 2][t & 63] = 0u;
   constexpr int D4LD = NOUT > 0 ? (NOUT + 3) / 4 * 4 : 4;
   __shared__ __attribute__((aligned(16))) float d4s[NOUT > 0 ? Q6T_SUB * D4LD : 4];
   // software pipeline: sub-tile s+1's x (and dY) rows are loaded into registers before sub-tile s
@@ -630,19 +702,20 @@ __global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float
     const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
     const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
     const float a0[4] = {a0v.x, a0v.y, a0v.z, a0v.w}, a1[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
-    float wc[NOUT > 0 ? NOUT : 1][4];       // the head's weight columns c..c+3
-    if constexpr (NOUT > 0) {
-#pragma unroll
-      for (int q = 0; q < NOUT; ++q) {
-        const float4 f = prm[7 + q][pg];
-        wc[q][0] = f.x, wc[q][1] = f.y, wc[q][2] = f.z, wc[q][3] = f.w;
-      }
-    }
 #pragma unroll
     for (int i = 0; i < Q6T_SUB / 16; ++i) {
       const int rr = (t >> 4) + 16 * i;
       const int64_t r = m0 + rr;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
+      float wc[NOUT > 0 ? NOUT : 1][4];     // the head's weight columns c..c+3, re-read per row (the
+      if constexpr (NOUT > 0) {             // 40 registers would otherwise stay live: spills)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) {
+          const float4 f = prm[7 + q][pg];
+          wc[q][0] = f.x, wc[q][1] = f.y, wc[q][2] = f.z, wc[q][3] = f.w;
+        }
+      }
       if (r < M) {
         const float4 xv = xin_cvt4<Z16>(xr[i], xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
@@ -662,28 +735,37 @@ __global__ __launch_bounds__(256, 3) void bn_bwd_apply_q6_k(XIn xin, const float
         if (o.dx) *reinterpret_cast<float4*>(o.dx + r * C + c) = make_float4(v[0], v[1], v[2], v[3]);
       }
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
+      const uint32_t a0b = abs_bits(v[0]), a1b = abs_bits(v[1]), a2b = abs_bits(v[2]), a3b = abs_bits(v[3]);
+      atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
+      atomicMax(&cmax[i >> 1][cq], a0b);
+      atomicMax(&cmax[i >> 1][cq + 1], a1b);
+      atomicMax(&cmax[i >> 1][cq + 2], a2b);
+      atomicMax(&cmax[i >> 1][cq + 3], a3b);
     }
     __syncthreads();
     load_sub(m0 + Q6T_SUB);
-    if (wave < 2) {
-      // row block (row m0 + lane, columns c0 + 32 wave ..)
-      const int rr = lane, b = wave;
-      const int64_t r = m0 + rr;
-      const int64_t rs = r < M ? r : 0;
-      const int64_t blk = c0 / QB + b;
-      q6_block_store_lds<1>(tile + rr * Q6T_LD + QB * b, r < M, o.rlo + (rs * nblk_c + blk) * 64,
-                            o.rhi + (rs * nblk_c + blk) * 32, o.rsc + (blk >> 1) * o.rsc_rows * 2 + rs * 2 + (blk & 1));
-    } else {
-      // column block (column c0 + lane, rows m0 + 32 (wave - 2) ..): rows beyond M are zeros
-      const int b = wave - 2;
-      const float* col = tile + QB * b * Q6T_LD + lane;
-#pragma unroll
-      for (int k = 0; k < QB; ++k) csum += (double)col[k * Q6T_LD];
-      const int64_t n = c0 + lane;
-      const int64_t mblk = m0 / QB + b;
-      q6_block_store_lds<Q6T_LD>(col, true, o.clo + (n * o.nblk_m + mblk) * 64, o.chi + (n * o.nblk_m + mblk) * 32,
-                                 o.csc + (mblk >> 1) * o.csc_rows * 2 + n * 2 + (mblk & 1));
+    // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
+    const int b = wave & 1;
+    uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
+    const uint32_t am = *amp;
+    *amp = 0u;
+    if (!Q6_DIAG_NOQUANT_ON) {
+      if (wave < 2) {
+        // row block (row m0 + lane, columns c0 + 32 b ..)
+        Q6StageSink sink{st.rlo[lane], st.rhi[lane], &st.rsc[lane][b], lane, b};
+        double unused = 0.0;
+        q6_block_pre<1, false>(tile + lane * Q6T_LD + QB * b, am, sink, unused);
+      } else {
+        // column block (column c0 + lane, rows m0 + 32 b ..): rows beyond M are zeros; its
+        // elements are added to the column sum in row order while they are quantised
+        Q6StageSink sink{st.clo[lane], st.chi[lane], &st.csc[lane][b], lane, b};
+        q6_block_pre<Q6T_LD, true>(tile + QB * b * Q6T_LD + lane, am, sink, csum);
+      }
     }
+    __syncthreads();
+    // whole-line stores: per row (column) of the sub-tile its two adjacent blocks' records are 128
+    // (lo) + 64 (hi) contiguous bytes, its two scale bytes adjacent to the next row's
+    q6_stage_store(st, o, t, m0, M, c0, nblk_c);
     __syncthreads();
   }
   if (o.part != nullptr) {

@@ -168,6 +168,69 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
   if (store) *sc_byte = (uint8_t)sbyte;
 }
 
+// q6_block_store_lds with the block's max|x| given (as the bits of |x|: an unsigned max over
+// (bits & 0x7FFFFFFF) ranks NaN above +inf above every finite value, so a block holding a NaN or an
+// inf gets the same NaN scale byte as absmax_nan gives it) -- computed while the block was formed,
+// so the block is read once.  w = rint(x 2^shift) + DIGIT_BIAS comes from ONE fma: with
+// MAGIC = 1.5 2^23 + DIGIT_BIAS, fma(x, 2^shift, MAGIC) lies in [2^23, 2^24) (|rint| <= 2^19),
+// where the float grid is the integers and round-to-nearest-even equals rint's (MAGIC is even), so
+// its bits are 0x4B400000 + w: the low 16 bits of w are the low 16 bits of the float and
+// w >> 15 = bits 15..20.  Blocks with a NaN scale or shift > 126 (max|x| < 2^-107: 2^shift is not
+// an fp32 number) take the ldexp path.  CSUM adds the block's elements to csum in element order
+// (the same double sum as a separate loop over them).  The record goes to sink.plane(j, lo 16 B,
+// hi 8 B) for planes j = 0..3 and sink.scale(byte).  Bit-identical to q6_block_store_lds.
+template <int STRIDE, bool CSUM, typename Sink>
+__device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bits, Sink& sink, double& csum) {
+  int shift;
+  const int sbyte = block_scale(__uint_as_float(amax_bits), &shift);
+  uint32_t P[QB / 2], Q[QB / 2];
+  if (sbyte != 255 && shift <= 126) {
+    const float s = __uint_as_float((uint32_t)(shift + 127) << 23);
+    constexpr float MAGIC = 12582912.f + (float)DIGIT_BIAS;
+#pragma unroll
+    for (int k = 0; k < QB / 2; ++k) {
+      const float xa = src[(2 * k) * STRIDE], xb = src[(2 * k + 1) * STRIDE];
+      if constexpr (CSUM) {
+        csum += (double)xa;
+        csum += (double)xb;
+      }
+      const uint32_t ba = __float_as_uint(__builtin_fmaf(xa, s, MAGIC));
+      const uint32_t bb = __float_as_uint(__builtin_fmaf(xb, s, MAGIC));
+      P[k] = __builtin_amdgcn_perm(bb, ba, 0x05040100u);          // low halves of (a, b)
+      Q[k] = __builtin_amdgcn_ubfe(ba, 15, 6) | (__builtin_amdgcn_ubfe(bb, 15, 6) << 16);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < QB / 2; ++k) {
+      const float xa = src[(2 * k) * STRIDE], xb = src[(2 * k + 1) * STRIDE];
+      if constexpr (CSUM) {
+        csum += (double)xa;
+        csum += (double)xb;
+      }
+      const uint32_t wa = (uint32_t)(__float2int_rn(ldexpf(xa, shift)) + DIGIT_BIAS);
+      const uint32_t wb = (uint32_t)(__float2int_rn(ldexpf(xb, shift)) + DIGIT_BIAS);
+      P[k] = (wa & 0xFFFFu) | (wb << 16);
+      Q[k] = (wa >> 15) | ((wb >> 15) << 16);
+    }
+  }
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    q6v16u hv;
+#pragma unroll
+    for (int k = 0; k < QB / 2; ++k) {
+      const uint32_t e = j < 3 ? ((P[k] >> (5 * j)) & 0x001F001Fu) | 0x64006400u : Q[k] | 0x64006400u;
+      const q6h2 d = __builtin_bit_cast(q6h2, e) - q6h2{(_Float16)1040.f, (_Float16)1040.f};
+      hv[k] = __builtin_bit_cast(uint32_t, d);
+    }
+    const q6v6i rec = __builtin_amdgcn_cvt_scalef32_pk32_fp6_f16(__builtin_bit_cast(q6v32h, hv), 8.0f);
+    sink.plane(j, make_uint4((uint32_t)rec[0], (uint32_t)rec[1], (uint32_t)rec[2], (uint32_t)rec[3]),
+               make_uint2((uint32_t)rec[4], (uint32_t)rec[5]));
+  }
+  sink.scale((uint8_t)sbyte);
+}
+
+__device__ __forceinline__ uint32_t abs_bits(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
+
 // Rows of the E8M0 scale slab [K/64][rows_pad][2] a quantised operand of `rows` rows needs: the
 // GEMM's scale piece is one 1-KiB LDS-DMA of 512 rows from the tile's first row.
 inline int64_t q6_scale_rows(int64_t rows) { return (rows + 255) / 256 * 256 + 512; }
