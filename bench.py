@@ -263,7 +263,8 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29517")
         backend = os.environ.get("BNN_BENCH_BACKEND", "nccl")   # rehearsal on one device: "gloo"
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+            from bnn_amd.parallel import init_rccl
+            init_rccl(dev, rank, world)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
 

@@ -45,6 +45,18 @@ from . import functional as BF
 _ALIGN_BYTES = 256
 
 
+def init_rccl(device, rank, world_size, init_method=None):
+    """torch.distributed over RCCL ("nccl" on ROCm), one process per GPU, bound to ``device``, with
+    RCCL's internal stream created at high priority.  HIP spreads normal-priority streams over a few
+    hardware queues (GPU_MAX_HW_QUEUES = 4): in the r03 trace of bench.py --exchange the pool stream
+    RCCL got shared hardware queue 4 with the compute stream, so every bucket reduction ran
+    strictly between two backward kernels (0 % overlap, profiles/r03_exchange_rccl_order.txt); a
+    high-priority stream is given a queue of its own."""
+    opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    kw = {"init_method": init_method} if init_method else {}
+    dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, pg_options=opts, **kw)
+
+
 class _Bucket:
     __slots__ = ("flat", "start", "end", "pending", "nparams", "work")
 

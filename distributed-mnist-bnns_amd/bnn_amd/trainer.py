@@ -100,8 +100,11 @@ def train(gpu, args):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", args.master_addr)
         os.environ.setdefault("MASTER_PORT", str(args.master_port))
-        dist.init_process_group(args.backend, init_method="env://", world_size=world, rank=rank,
-                                device_id=device if args.backend == "nccl" else None)
+        if args.backend == "nccl":
+            from .parallel import init_rccl
+            init_rccl(device, rank, world, init_method="env://")
+        else:
+            dist.init_process_group(args.backend, init_method="env://", world_size=world, rank=rank)
     torch.cuda.manual_seed(args.seed)
     model = nets.MODELS[args.model](org_protocol=False, mutate_input=False,
                                     fused_bn=True).to(device)

@@ -41,7 +41,8 @@ def _worker(port, q):
         os.environ["MASTER_PORT"] = str(port)
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        from bnn_amd.parallel import init_rccl
+        init_rccl(dev, 0, 1)                      # as bench.py / the trainer: high-priority RCCL stream
         from bnn_amd import nets
         from bnn_amd.data import synthetic_mnist
         from bnn_amd.optim import LatentAdam
