@@ -531,7 +531,7 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None):
     if M == 0 or N == 0:
         return C
     k_true = K if k_true is None else k_true
-    name = L.lib().bnn_gemm_fp6_kernel(M, N).decode() if _TIMER is not None else ""
+    name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
     wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)    # split-K partials (small grids), else 0
     ws = torch.empty((wsb,), dtype=torch.uint8, device=B4.device) if wsb > 0 else None
     with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):

@@ -245,12 +245,14 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
   }
 }
 
-// Final merges: a workgroup owns 64 columns; its 4 waves each merge every 4th chunk (r = wave,
-// wave+4, ...) and wave 0 folds the 4 group results in order -- 4x the parallelism of one thread
-// per column walking all R chunks, still a fixed (deterministic) order.
-constexpr int FIN_COLS = 16, FIN_GROUPS = 16, FIN_B = 8;
+// Forward merge: 64 chunk groups x 4 columns per workgroup.  Two independent passes over the
+// partials instead of a serial Chan merge chain (two dependent double divisions per chunk: ~15-20 us
+// for the 256-1024 chunks of a small batch): the batch sum first (its fixed-order double sum gives
+// the mean), then M2 = sum_r [M2_r + n_r (S_r / n_r - mean)^2] (the parallel-axis form, every term
+// independent).  Deterministic: fixed group split, fixed fold order.
+constexpr int FF_COLS = 4, FF_GROUPS = 64, FF_B = 16;
 
-inline dim3 fin_grid(int64_t C) { return dim3((unsigned)((C + FIN_COLS - 1) / FIN_COLS)); }
+inline dim3 ffin_grid(int64_t C) { return dim3((unsigned)((C + FF_COLS - 1) / FF_COLS)); }
 
 __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__ p0, const double* __restrict__ p1,
                                                       int64_t M, int64_t C, int64_t R, float momentum, float eps,
@@ -261,56 +263,62 @@ __global__ __launch_bounds__(256) void bn_fwd_final_k(const double* __restrict__
                                                       int64_t hw) {
   // chunk r covers rows [r*chunk_rows, min((r+1)*chunk_rows, M)) of hw elements each (hw = 1 for
   // BatchNorm1d; H*W for the NCHW BatchNorm2d); p0 = chunk sum, p1 = chunk M2 about its mean
-  __shared__ double sn[FIN_GROUPS][FIN_COLS], sm[FIN_GROUPS][FIN_COLS], sq[FIN_GROUPS][FIN_COLS],
-      ss[FIN_GROUPS][FIN_COLS];
-  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
-  const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
-  double n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
-  if (c < C) {
-    // Chan et al. merge, fixed order; the partials of FIN_B chunks are loaded before any is
-    // merged (a serial load -> merge chain is latency-bound at ~1 us per chunk)
-    for (int64_t rb = grp; rb < R; rb += FIN_B * FIN_GROUPS) {
-      double q0[FIN_B], q1[FIN_B];
+  __shared__ double red[FF_GROUPS][FF_COLS];
+  __shared__ double smean[FF_COLS];
+  const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
+  const int64_t c = (int64_t)blockIdx.x * FF_COLS + lc;
+  const bool live = c < C;
+  const int64_t cc = live ? c : C - 1;
+  // pass 1: the batch sum
+  double s = 0.0;
+  for (int64_t rb = grp; rb < R; rb += FF_B * FF_GROUPS) {
+    double q[FF_B];
 #pragma unroll
-      for (int u = 0; u < FIN_B; ++u) {
-        const int64_t r = rb + u * FIN_GROUPS;
-        q0[u] = p0[min(r, R - 1) * C + c];   // clamped, unconditional: the loads batch
-        q1[u] = p1[min(r, R - 1) * C + c];
-      }
+    for (int u = 0; u < FF_B; ++u) q[u] = p0[min(rb + u * FF_GROUPS, R - 1) * C + cc];   // loads batch
 #pragma unroll
-      for (int u = 0; u < FIN_B; ++u) {
-        const int64_t r = rb + u * FIN_GROUPS;
-        if (r >= R) break;
-        const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
-        const double nb = (double)((hi - r * chunk_rows) * hw);
-        const double mb = q0[u] / nb, m2b = q1[u];
-        const double nt = n + nb, delta = mb - mean;
-        mean += delta * nb / nt;
-        m2 += m2b + delta * delta * n * nb / nt;
-        n = nt;
-        sum += q0[u];
-      }
+    for (int u = 0; u < FF_B; ++u)
+      if (rb + u * FF_GROUPS < R) s += q[u];
+  }
+  red[grp][lc] = s;
+  __syncthreads();
+  const double n = (double)(M * hw);
+  if (grp == 0) {
+    double t = 0.0;
+    for (int g = 0; g < FF_GROUPS; ++g) t += red[g][lc];   // fixed order
+    smean[lc] = t;
+  }
+  __syncthreads();
+  const double sum = smean[lc], mean = sum / n;
+  // pass 2: M2 about the batch mean
+  const double nb_full = (double)(chunk_rows * hw), inv_full = 1.0 / nb_full;
+  double m2 = 0.0;
+  for (int64_t rb = grp; rb < R; rb += FF_B * FF_GROUPS) {
+    double q0[FF_B], q1[FF_B];
+#pragma unroll
+    for (int u = 0; u < FF_B; ++u) {
+      const int64_t r = min(rb + u * FF_GROUPS, R - 1);
+      q0[u] = p0[r * C + cc];
+      q1[u] = p1[r * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < FF_B; ++u) {
+      const int64_t r = rb + u * FF_GROUPS;
+      if (r >= R) break;
+      const int64_t hi = ((r + 1) * chunk_rows < M) ? (r + 1) * chunk_rows : M;
+      const bool full = hi - r * chunk_rows == chunk_rows;
+      const double nb = full ? nb_full : (double)((hi - r * chunk_rows) * hw);
+      const double d = (full ? q0[u] * inv_full : q0[u] / nb) - mean;
+      m2 += q1[u] + nb * d * d;
     }
   }
-  sn[grp][lc] = n;
-  sm[grp][lc] = mean;
-  sq[grp][lc] = m2;
-  ss[grp][lc] = sum;
   __syncthreads();
-  if (grp != 0 || c >= C) return;
-  n = 0.0, mean = 0.0, m2 = 0.0, sum = 0.0;
-  for (int gI = 0; gI < FIN_GROUPS; ++gI) {   // fixed order
-    const double nb = sn[gI][lc];
-    if (nb == 0.0) continue;
-    const double nt = n + nb, delta = sm[gI][lc] - mean;
-    mean += delta * nb / nt;
-    m2 += sq[gI][lc] + delta * delta * n * nb / nt;
-    n = nt;
-    sum += ss[gI][lc];
-  }
+  red[grp][lc] = m2;
+  __syncthreads();
+  if (grp != 0 || !live) return;
+  m2 = 0.0;
+  for (int g = 0; g < FF_GROUPS; ++g) m2 += red[g][lc];   // fixed order
   double var = m2 / n;
   if (var < 0.0) var = 0.0;
-  mean = sum / n;                      // the exact batch sum / n: one rounding in double
   const float mh = (float)mean;
   save_mean[c] = mh;
   if (save_mean_lo) save_mean_lo[c] = (float)(mean - (double)mh);
@@ -400,27 +408,27 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       float* __restrict__ k0, float* __restrict__ k1,
                                                       I8cBound ib = I8cBound{nullptr, nullptr, nullptr, 0.f, nullptr, nullptr}) {
-  __shared__ double sa[FIN_GROUPS][FIN_COLS], sb[FIN_GROUPS][FIN_COLS];
-  __shared__ float sg[FIN_GROUPS][FIN_COLS], sx[FIN_GROUPS][FIN_COLS];
-  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
-  const int64_t c = (int64_t)blockIdx.x * FIN_COLS + lc;
+  __shared__ double sa[FF_GROUPS][FF_COLS], sb[FF_GROUPS][FF_COLS];
+  __shared__ float sg[FF_GROUPS][FF_COLS], sx[FF_GROUPS][FF_COLS];
+  const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
+  const int64_t c = (int64_t)blockIdx.x * FF_COLS + lc;
   double s = 0.0, s2 = 0.0;
   float gm = 0.f, xm = 0.f;
   if (c < C)
-    for (int64_t rb = grp; rb < R; rb += FIN_B * FIN_GROUPS) {   // batched loads, fixed order
-      double q0[FIN_B], q1[FIN_B];
-      float qg[FIN_B], qx[FIN_B];
+    for (int64_t rb = grp; rb < R; rb += FF_B * FF_GROUPS) {   // batched loads, fixed order
+      double q0[FF_B], q1[FF_B];
+      float qg[FF_B], qx[FF_B];
 #pragma unroll
-      for (int u = 0; u < FIN_B; ++u) {
-        const int64_t r = rb + u * FIN_GROUPS;
+      for (int u = 0; u < FF_B; ++u) {
+        const int64_t r = rb + u * FF_GROUPS;
         q0[u] = p0[min(r, R - 1) * C + c];   // clamped, unconditional: the loads batch
         q1[u] = p1[min(r, R - 1) * C + c];
         qg[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[r * C + c] : 0.f;
         qx[u] = (r < R && ib.pmx != nullptr) ? ib.pmx[(R + r) * C + c] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < FIN_B; ++u) {
-        if (rb + u * FIN_GROUPS >= R) break;
+      for (int u = 0; u < FF_B; ++u) {
+        if (rb + u * FF_GROUPS >= R) break;
         s += q0[u];
         s2 += q1[u];
         gm = fmaxf(gm, qg[u]);
@@ -434,7 +442,7 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
   __syncthreads();
   if (grp != 0 || c >= C) return;
   s = 0.0, s2 = 0.0;
-  for (int gI = 0; gI < FIN_GROUPS; ++gI) {   // fixed order
+  for (int gI = 0; gI < FF_GROUPS; ++gI) {   // fixed order
     s += sa[gI][lc];
     s2 += sb[gI][lc];
     gm = fmaxf(gm, sg[gI][lc]);
@@ -777,7 +785,7 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   }
 }
 
-// colsum[n] = sum_r part[r][n]: FIN_COLS columns x FIN_GROUPS chunk groups per workgroup, the
+// colsum[n] = sum_r part[r][n]: FF_COLS columns x FF_GROUPS chunk groups per workgroup, the
 // groups folded in a fixed order (deterministic)
 // ------------------------------------------------------------------ fused head: [drop ->] bn -> htanh -> Linear
 // mnist-dist2.py:69-76: fc3 -> drop -> bn3 -> htanh3 -> fc4 (nn.Linear(C, 10)).  The fp32 hardtanh
@@ -980,39 +988,39 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
     *reinterpret_cast<float4*>(pw + (chunk * NOUT + q) * C + c) = make_float4(aw[q][0], aw[q][1], aw[q][2], aw[q][3]);
 }
 
-// dW4[q][c] = sum over chunks of the partials: FIN_COLS elements x FIN_GROUPS chunk groups per
+// dW4[q][c] = sum over chunks of the partials: FF_COLS elements x FF_GROUPS chunk groups per
 // workgroup, groups folded in a fixed order (double, deterministic)
 __global__ __launch_bounds__(256) void head_dw_final_k(const float* __restrict__ pw, int64_t R, int64_t nq, int64_t C,
                                                        float* __restrict__ dw4) {
-  __shared__ double sa[FIN_GROUPS][FIN_COLS];
-  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
-  const int64_t e = (int64_t)blockIdx.x * FIN_COLS + lc, ne = nq * C;
+  __shared__ double sa[FF_GROUPS][FF_COLS];
+  const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
+  const int64_t e = (int64_t)blockIdx.x * FF_COLS + lc, ne = nq * C;
   double s = 0.0;
   if (e < ne)
-#pragma unroll 8
-    for (int64_t r = grp; r < R; r += FIN_GROUPS) s += (double)pw[r * ne + e];
+#pragma unroll 16
+    for (int64_t r = grp; r < R; r += FF_GROUPS) s += (double)pw[r * ne + e];
   sa[grp][lc] = s;
   __syncthreads();
   if (grp != 0 || e >= ne) return;
   s = 0.0;
-  for (int gI = 0; gI < FIN_GROUPS; ++gI) s += sa[gI][lc];
+  for (int gI = 0; gI < FF_GROUPS; ++gI) s += sa[gI][lc];
   dw4[e] = (float)s;
 }
 
 __global__ __launch_bounds__(256) void q6_colsum_final_k(const double* __restrict__ part, int64_t R, int64_t N,
                                                          float* __restrict__ out) {
-  __shared__ double sa[FIN_GROUPS][FIN_COLS];
-  const int lc = threadIdx.x & (FIN_COLS - 1), grp = threadIdx.x / FIN_COLS;
-  const int64_t n = (int64_t)blockIdx.x * FIN_COLS + lc;
+  __shared__ double sa[FF_GROUPS][FF_COLS];
+  const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
+  const int64_t n = (int64_t)blockIdx.x * FF_COLS + lc;
   double s = 0.0;
   if (n < N)
-#pragma unroll 8
-    for (int64_t r = grp; r < R; r += FIN_GROUPS) s += part[r * N + n];
+#pragma unroll 16
+    for (int64_t r = grp; r < R; r += FF_GROUPS) s += part[r * N + n];
   sa[grp][lc] = s;
   __syncthreads();
   if (grp != 0 || n >= N) return;
   s = 0.0;
-  for (int gI = 0; gI < FIN_GROUPS; ++gI) s += sa[gI][lc];
+  for (int gI = 0; gI < FF_GROUPS; ++gI) s += sa[gI][lc];
   out[n] = (float)s;
 }
 
@@ -1340,7 +1348,7 @@ static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const floa
   else
     hipLaunchKernelGGL((bn_reduce_k<0, false>), reduce_grid(M, C), dim3(256), 0, s, xin,
                        nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
-  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
+  hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
                      running_var, save_mean, save_invstd, lo, bn_chunk_rows(M, C), (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
     hipLaunchKernelGGL(bn_apply_k, apply_grid(M, C), dim3(256), 0, s, x, M, C, save_mean, lo, save_invstd,
@@ -1415,7 +1423,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy,
                      M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
+  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     hipLaunchKernelGGL(bn_bwd_apply_k, apply_grid(M, C), dim3(256), 0, s, x, dy, M, C, save_mean, save_mean_lo,
@@ -1457,7 +1465,7 @@ int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const flo
     hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C,
                        save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
                        make_drop(0.f, 0));
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1,
+  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1,
                      I8cBound{pmx, save_invstd, gamma, 1.f / (float)M, scale, dsum});
   *k0_out = k0;
   *k1_out = k1;
@@ -1520,7 +1528,7 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
   else
     hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
                        save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
@@ -1533,7 +1541,7 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
     hipLaunchKernelGGL((bn_bwd_apply_q6_k<0, false>), g, dim3(256), 0, s, xin, dy, M, C, save_mean, save_mean_lo,
                        save_invstd, gamma, beta, hardtanh, k0, k1, 1.f / (float)M, o, dp, nullptr, (int)qr);
   if (colsum)
-    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
+    hipLaunchKernelGGL(q6_colsum_final_k, ffin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_bwd_q6");
 }
 
@@ -1627,8 +1635,8 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
   else
     hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
                        save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
-  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, s, pw, R,
+  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + FF_COLS - 1) / FF_COLS)), dim3(256), 0, s, pw, R,
                      (int64_t)nout, C, dw4);
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
@@ -1641,7 +1649,7 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
     hipLaunchKernelGGL((bn_bwd_apply_q6_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, dy4, M, C, save_mean,
                        save_mean_lo, save_invstd, gamma, beta, 1, k0, k1, 1.f / (float)M, o, dp, w4, (int)qr);
   if (colsum)
-    hipLaunchKernelGGL(q6_colsum_final_k, fin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
+    hipLaunchKernelGGL(q6_colsum_final_k, ffin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_head_bwd_q6");
 }
 
@@ -1716,7 +1724,7 @@ BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, 
   double* p1 = p0 + R * C;
   hipLaunchKernelGGL((bn2d_reduce_k<0, 0>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s, x, nullptr, N, C,
                      (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
-  hipLaunchKernelGGL(bn_fwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
+  hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
   BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
@@ -1758,7 +1766,7 @@ static int bn2d_bwd_impl(const float* x, const float* dy, int64_t N, int64_t C, 
   BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
                                            s, x, dy, N, C, (int)H, (int)W, CR, save_mean, save_invstd, gamma, beta,
                                            hardtanh, p0, p1));
-  hipLaunchKernelGGL(bn_bwd_final_k, fin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
+  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;

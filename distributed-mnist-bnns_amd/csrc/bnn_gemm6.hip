@@ -29,6 +29,7 @@
 // k-block l/32 of the 64-k step, element j at bits 6j..6j+5; the lane's scale byte scales its 32.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 
 #include "bnn_fp6.h"
 
@@ -208,7 +209,10 @@ __device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int G, int& tm
 //   A hi : BM rows x  64 B  (block 0: planes 01, 23; block 1: ...), chunk c at c ^ ((row >> 2) & 3)
 //   A sc : BM x 2 B        (row-major, plane-0 bytes of blocks 0, 1)
 //   B    : BN rows x  32 B  (the 64 FP4 codes), chunk c at c ^ ((row >> 3) & 1)
-// DIAG (timing-only builds, wrong results): 1 = no global->LDS staging, 2 = no LDS fragment reads.
+// DIAG (timing-only builds, wrong results): 1 = no global->LDS staging, 2 = no LDS fragment reads,
+// 3 / 4 = the MFMA stream alone (fragments read once) with / without the per-step barrier, 5 = B
+// staged from contiguous per-k-step panels (as if B were stored [N/BN][K/64][BN][32 B]), 6 = 5 +
+// A hi likewise ([M/BM][K/64][BM][64 B]): what whole-line staging loads would gain.
 // OCC = waves per SIMD the register allocation must allow (2: one 512-thread workgroup per CU;
 // 4: two, whose independent barriers let one's LDS-read phase overlap the other's MFMAs).
 // PP = 1 (WM = 2, STAGES = 3): software-pipelined k loop.  Each k-step's two A tiles are split
@@ -238,10 +242,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   int tm, tn;
   const int split = p.ksplit > 1 ? (int)(blockIdx.x % p.ksplit) : 0;
   tile6_of(p.ksplit > 1 ? (int)(blockIdx.x / p.ksplit) : (int)blockIdx.x, p.gm, p.gn, p.group, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
   const int64_t nblk = p.K / QB;
   const int ks0 = split * p.kps;                          // this workgroup's first k-step
   const int nk = min(p.K / 64 - ks0, p.kps);
+  // split-K: this split's partial, row pitch N, no bias (added once by the fold)
+  float* const Cout = p.ksplit > 1 ? p.part + (int64_t)split * p.M * p.N : p.C;
+  const int64_t ldo = p.ksplit > 1 ? p.N : p.ldc;
+  const float* const bias = p.ksplit > 1 ? nullptr : p.bias;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   // One stage = I_LO + I_HI + I_SC + I_B LDS-DMA pieces of 1 KiB (64 lanes x 16 B): lo 8 rows per
   // piece, hi 16 rows, scales 512 rows of 2-B entries (only this tile's BM rows are loaded), B 32
@@ -262,13 +270,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   for (int ii = 0; ii < P_HI; ++ii) {
     const int i = wave + ii * NW;
     const int lrow = i * 16 + (lane >> 2), c = lane & 3;
-    off_hi[ii] = (uint32_t)min(lrow, p.M - 1 - m0) * (uint32_t)(nblk * 32) + 16u * (uint32_t)(c ^ ((lrow >> 2) & 3));
+    off_hi[ii] = DIAG == 6 ? (uint32_t)lrow * 64u + 16u * (uint32_t)(c ^ ((lrow >> 2) & 3))
+                           : (uint32_t)min(lrow, p.M - 1 - m0) * (uint32_t)(nblk * 32) + 16u * (uint32_t)(c ^ ((lrow >> 2) & 3));
   }
 #pragma unroll
   for (int ii = 0; ii < P_B; ++ii) {
     const int i = wave + ii * NW;
     const int lrow = i * 32 + (lane >> 1), c = lane & 1;
-    off_b[ii] = (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
+    off_b[ii] = DIAG >= 5 ? (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1))
+                          : (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
   }
   const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64 + (int64_t)ks0 * 128;
   const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32 + (int64_t)ks0 * 64;
@@ -282,10 +292,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       glds16_6s(lo_base + (int64_t)kt * 128, off_lo[ii], base + (wave + ii * NW) * 1024);
 #pragma unroll
     for (int ii = 0; ii < P_HI; ++ii)
-      glds16_6s(hi_base + (int64_t)kt * 64, off_hi[ii], base + LO_ST + (wave + ii * NW) * 1024);
+      glds16_6s(hi_base + (int64_t)kt * (DIAG == 6 ? BM * 64 : 64), off_hi[ii], base + LO_ST + (wave + ii * NW) * 1024);
 #pragma unroll
     for (int ii = 0; ii < P_B; ++ii)
-      glds16_6s(b_base + (int64_t)kt * 32, off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
+      glds16_6s(b_base + (int64_t)kt * (DIAG >= 5 ? BN * 32 : 32), off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
     if (wave == 0)   // a whole 1-KiB piece (512 rows): the scale array has 512 rows of tail padding
       glds16_6(sc_base + (int64_t)kt * p.asc_rows * 2 + lane * 16, base + LO_ST + HI_ST);
   };
@@ -526,6 +536,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       if (kt + 1 < nk) BNN_FP6_STEP(kt + 1, b1, f1, b0, f0)
     }
 #undef BNN_FP6_STEP
+  } else if constexpr (DIAG >= 3) {
+    // timing-only: fragments read once from stage 0 and reused by every k-step -- the MFMA
+    // stream alone (3: with the per-k-step barrier, 4: without)
+    stage(0, 0);
+    wait_vmcnt6<0>();
+    barrier6();
+    v4i bf[WN];
+    AFrag fr[WM];
+    read_b(smem, bf);
+#pragma unroll
+    for (int t = 0; t < WM; ++t) read_a(smem, t, fr[t]);
+    for (int kt = 0; kt < nk; ++kt) {
+      if constexpr (DIAG == 3) barrier6();
+#pragma unroll
+      for (int t = 0; t < WM; ++t) mma_tile(fr[t], bf, acc[t]);
+    }
   } else {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -566,10 +592,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   wait_vmcnt6<0>();
   barrier6();
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
-  // split-K: this split's partial, row pitch N, no bias (added once by the fold)
-  float* const Cout = p.ksplit > 1 ? p.part + (int64_t)split * p.M * p.N : p.C;
-  const int64_t ldo = p.ksplit > 1 ? p.N : p.ldc;
-  const float* const bias = p.ksplit > 1 ? nullptr : p.bias;
   const bool vec_ok = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0);
 #pragma unroll
   for (int t = 0; t < WM; ++t) {
@@ -629,14 +651,6 @@ __global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restric
   }
 }
 
-// Split count for a grid of `tiles` workgroups over nk k-steps: none while the grid fills the chip
-// twice over; otherwise enough splits for ~3 workgroups per CU, each split >= 8 k-steps.
-inline int ksplit_for(int64_t tiles, int nk, int64_t N) {
-  if (tiles >= 512 || N % 4 != 0) return 1;
-  const int64_t want = (768 + tiles - 1) / tiles;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(want, nk / 8));
-}
-
 template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0>
 int launch6(Gemm6Params p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
@@ -692,6 +706,13 @@ const Variant6 kVariants6[] = {
     // timing-only diagnostics of variant 5 (wrong results; never picked by default)
     {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128, 512},
     {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128, 512},
+    // timing-only diagnostics of variant 7 (the wide default)
+    {93, "diag: v7 MFMA stream + barrier", launch6<2, 4, 2, 4, 2, 3>, 128, 512},
+    {94, "diag: v7 MFMA stream only", launch6<2, 4, 2, 4, 2, 4>, 128, 512},
+    {95, "diag: v7 without global->LDS staging", launch6<2, 4, 2, 4, 2, 1>, 128, 512},
+    {96, "diag: v7 without LDS fragment reads", launch6<2, 4, 2, 4, 2, 2>, 128, 512},
+    {97, "diag: v7 with B staged from contiguous panels", launch6<2, 4, 2, 4, 2, 5>, 128, 512},
+    {98, "diag: v7 with B and A hi staged from contiguous panels", launch6<2, 4, 2, 4, 2, 6>, 128, 512},
 };
 
 int g_variant6 = -1;
@@ -702,15 +723,12 @@ const Variant6* find6(int id) {
   return &kVariants6[0];      // unknown id: the first entry (the sweep skips repeated names)
 }
 
-// Default per shape (tools/gpu_fp6_sweep.py, profiles/r02_fp6_*.log): the 128 x 512 tile (the
-// FP6 operand is 6x the bytes of the FP4 one per row, so tall-N tiles move the fewest bytes per
-// MAC) when the grid still fills the chip several times over, else 128 x 256 / 128 x 128.
+// Default per shape: the 128 x 512 tile (the FP6 operand is 6x the bytes of the FP4 one per row,
+// so tall-N tiles move the fewest bytes per MAC) for every shape; grids below one round of the
+// chip are split along K (plan6).
 const Variant6* pick6(int64_t M, int64_t N) {
-  if (g_variant6 >= 0) return find6(g_variant6);
-  const int64_t t512 = ((M + 127) / 128) * ((N + 511) / 512), t256 = ((M + 127) / 128) * ((N + 255) / 256);
-  if (t512 >= 1024) return find6(7);
-  if (t256 >= 512) return find6(1);
-  return find6(2);
+  (void)M, (void)N;
+  return g_variant6 >= 0 ? find6(g_variant6) : find6(7);
 }
 
 inline hipStream_t S6(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -762,17 +780,40 @@ BNN_API int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx,
   return check_launch("bnn_quant6_cols_t");
 }
 
-// split-K count of the default variant for this shape (1 = no split; see ksplit_for)
-static int fp6_ksplit(int64_t M, int64_t N, int64_t K) {
-  const Variant6* v = pick6(M, N);
-  const int64_t tiles = ((M + v->bm - 1) / v->bm) * ((N + v->bn - 1) / v->bn);
-  return ksplit_for(tiles, (int)(K / 64), N);
+// Launch plan of the default kernel for a shape: the 128 x 512 tile, and a grid below one round of
+// the chip (the MLP's backward GEMMs at batch 4096: 18-192 tiles) split along K into
+// floor(CUs / tiles) parts of >= 4 k-steps each (the whole-round efficiency of the big tile beats a
+// smaller tile's finer grid: stream-K on 128 x 256 tiles measured 27-55 us per GEMM against 44 for
+// the unsplit 192-tile 128 x 512 grid, tools/gpu_r03_sk.sh).  Forced variants never split.
+struct Fp6Plan {
+  const Variant6* v;
+  int ksplit;
+};
+
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
+static Fp6Plan plan6(int64_t M, int64_t N, int64_t K) {
+  if (g_variant6 >= 0) return Fp6Plan{find6(g_variant6), 1};
+  const Variant6* v = find6(7);
+  const int64_t tiles = ((M + v->bm - 1) / v->bm) * ((N + v->bn - 1) / v->bn), ncu = device_cus();
+  const int64_t s = std::min<int64_t>(ncu / std::max<int64_t>(tiles, 1), (K / 64) / 4);
+  return Fp6Plan{v, (int)std::max<int64_t>(1, s)};
 }
 
 BNN_API int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 != 0) return 0;
-  const int S = fp6_ksplit(M, N, K);
-  return S > 1 ? (int64_t)S * M * N * (int64_t)sizeof(float) : 0;
+  const Fp6Plan pl = plan6(M, N, K);
+  return pl.ksplit > 1 && N % 4 == 0 ? (int64_t)pl.ksplit * M * N * (int64_t)sizeof(float) : 0;
 }
 
 static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
@@ -803,17 +844,26 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
     return kErrInval;
   }
   if (M == 0 || N == 0) return 0;
-  // split-K only with a workspace of bnn_gemm_fp6_workspace bytes (and with the default variant)
-  const int S = (work != nullptr && g_variant6 < 0) ? fp6_ksplit(M, N, K) : 1;
-  // (the result depends on the shape only -- never on C's alignment or pitch: a gradient written
-  // straight into a bucket view must equal the one AccumulateGrad would add)
-  const bool split = S > 1 && work_bytes >= (int64_t)S * M * N * (int64_t)sizeof(float) && aligned16(work);
+  // split-K only with a workspace of bnn_gemm_fp6_workspace bytes (else the whole K per tile); the
+  // result depends on the shape only -- never on C's alignment or pitch: a gradient written straight
+  // into a bucket view must equal the one AccumulateGrad would add
+  const Fp6Plan pl = plan6(M, N, K);
+  const int64_t need = bnn_gemm_fp6_workspace(M, N, K);
+  const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
-                split ? S : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr};
-  return pick6(M, N)->fn(p, S6(stream));
+                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr};
+  return pl.v->fn(p, S6(stream));
 }
 
 BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, N)->name; }
+
+BNN_API const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K) {
+  const Fp6Plan pl = plan6(M, N, K);
+  static thread_local char buf[96];
+  if (pl.ksplit <= 1) return pl.v->name;
+  snprintf(buf, sizeof buf, "%s split-K %d", pl.v->name, pl.ksplit);
+  return buf;
+}
 
 BNN_API int bnn_gemm_fp6_set_variant(int32_t v) {
   g_variant6 = v;

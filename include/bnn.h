@@ -179,15 +179,16 @@ int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int64_t
 int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
                  int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                  bnn_stream_t stream);
-/* The same product with split-K when the tile grid alone would not fill the chip (small M x N,
- * long K: the input layer's and the MLP's weight gradients): `work` of bnn_gemm_fp6_workspace(M,
- * N, K) bytes (0 = no split for this shape) holds the per-split fp32 partials, folded in split
- * order (deterministic) with the bias.  A smaller workspace falls back to the unsplit kernel. */
+/* The same product with split-K when the tile grid is below one round of the chip (small M x N:
+ * the MLP's backward GEMMs at batch 4096): `work` of bnn_gemm_fp6_workspace(M, N, K) bytes (0 = no
+ * split for this shape) holds the per-split fp32 partials, folded in split order (deterministic,
+ * shape-only) with the bias.  A smaller workspace falls back to the unsplit grid. */
 int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K);
 int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
                     int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                     void* work, int64_t work_bytes, bnn_stream_t stream);
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
+const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):

@@ -134,18 +134,21 @@ def test_gemm_fp6_every_variant(F, M, N, K):
     assert len(names) >= 3
 
 
-@pytest.mark.parametrize("M,N,K", [(768, 1536, 4096), (1536, 3072, 4096), (200, 132, 8192), (64, 64, 1024)])
+@pytest.mark.parametrize("M,N,K", [(768, 1536, 4096), (1536, 3072, 4096), (4096, 1536, 768), (200, 132, 8192),
+                                   (64, 64, 1024), (300, 520, 512), (1000, 36, 1024)])
 def test_gemm_fp6_split_k(F, M, N, K):
-    """Split-K (small tile grids over long K: the MLP's weight gradients): the per-split fp32
-    partials folded in split order, with the bias, equal the digit product within fp32 rounding;
-    the fold is deterministic (two runs bit-identical); a workspace too small falls back."""
+    """Split-K (tile grids below one round of the chip: the MLP's backward GEMMs at batch 4096,
+    config 3): per-split fp32 partials folded in split order with the bias.  Equal to the digit
+    product within fp32 rounding, deterministic (two runs bit-identical), shape-only (an unaligned,
+    strided C -- a gradient-bucket view -- gets the same bits), and a workspace too small falls
+    back to the unsplit grid.  Shapes: 2-32 splits, ragged M / N."""
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M + N + K)
     x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-6, 6, (M, 1)))).astype(np.float32)
     w = rng.integers(-1, 2, (N, K)).astype(np.float32)
     bias = rng.standard_normal(N).astype(np.float32)
     wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)
-    assert wsb > 0                                    # every shape here splits
+    assert wsb > 0 and "split-K" in L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode()
     op = F.quant6_rows(torch.as_tensor(x).cuda())
     w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
     val, _, _ = decode(op, M)
@@ -155,7 +158,11 @@ def test_gemm_fp6_split_k(F, M, N, K):
     C1, C2 = host(F.gemm_fp6(op, w4, N, bias=bt)), host(F.gemm_fp6(op, w4, N, bias=bt))
     assert np.array_equal(C1, C2)
     assert rel_err(C1, exact_q) < 2e-6 and rel_err(C1, exact_x) < 1e-5
-    C0 = torch.empty(M, N, device="cuda")               # no workspace: the unsplit kernel
+    big = torch.full((M * (N + 3) + 1,), float("nan"), device="cuda")
+    Cv = big[1:].view(M, N + 3)[:, :N]                 # 4-B aligned only, row pitch N + 3
+    F.gemm_fp6(op, w4, N, bias=bt, out=Cv)
+    assert np.array_equal(host(Cv), C1)
+    C0 = torch.empty(M, N, device="cuda")               # no workspace: the unsplit grid
     L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(w4), w4.shape[1],
            L.ptr(bt), L.ptr(C0), N, M, N, op.Kp, None, 0, L.stream())
     assert rel_err(host(C0), exact_q) < 2e-6
