@@ -92,6 +92,9 @@ SIGNATURES = {
     "bnn_gemm_fp6": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_gemm_fp6_workspace": (I64, [I64, I64, I64]),
     "bnn_gemm_fp6_ws": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
+    "bnn_fp4_panel_bytes": (I64, [I64, I64]),
+    "bnn_fp4_panelize": (I32, [P, I64, I64, I64, P, P]),
+    "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_gemm_fp6_kernel": (ctypes.c_char_p, [I64, I64]),
     "bnn_gemm_fp6_kernel_k": (ctypes.c_char_p, [I64, I64, I64]),
     "bnn_gemm_fp6_set_variant": (I32, [I32]),

@@ -523,20 +523,40 @@ def quant6_cols_t(x, want_colsum=False):
     return Fp6Operand(lo, hi, sc, N, Mp), cs
 
 
-def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None):
-    """C[A.rows, N] = A . B4^T (+ bias): A an Fp6Operand, B4 FP4 nibbles [N, >= A.Kp/2 bytes]."""
+# B operands of at least this many MACs are staged from FP4 panels (bnn_fp4_panelize): the panel
+# pass costs one read + write of B, the GEMM ~29 % less (profiles/r03_fp6_staging_diag.log)
+PANEL_MIN_MACS = 1 << 30
+
+
+def fp4_panels(B4, N, Kp):
+    """FP4 rows [N, >= Kp/2 bytes] -> the panel layout [ceil(N/512), Kp/64, 512, 32 B] (flat uint8)."""
+    P = torch.empty((L.lib().bnn_fp4_panel_bytes(N, Kp),), dtype=torch.uint8, device=B4.device)
+    with _timed("fp4_panelize_k", 0, 2 * N * Kp // 2):
+        L.call("bnn_fp4_panelize", L.ptr(B4), N, B4.shape[1], Kp, L.ptr(P), L.stream())
+    return P
+
+
+def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None):
+    """C[A.rows, N] = A . B4^T (+ bias): A an Fp6Operand, B4 FP4 nibbles [N, >= A.Kp/2 bytes].
+    panels: B4 already in the panel layout (fp4_panels); large products panelize B4 themselves."""
     M, K = A.rows, A.Kp
     assert B4.dtype == torch.uint8 and B4.shape[0] == N and 2 * B4.shape[1] >= K
     C = torch.empty((M, N), dtype=torch.float32, device=B4.device) if out is None else out
     if M == 0 or N == 0:
         return C
     k_true = K if k_true is None else k_true
+    if panels is None and M * N * K >= PANEL_MIN_MACS:
+        panels = fp4_panels(B4, N, K)
     name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
     wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)    # split-K partials (small grids), else 0
     ws = torch.empty((wsb,), dtype=torch.uint8, device=B4.device) if wsb > 0 else None
     with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):
-        L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
-               L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
+        if panels is not None:
+            L.call("bnn_gemm_fp6_panel_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(panels),
+                   L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
+        else:
+            L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
+                   L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
     return C
 
 

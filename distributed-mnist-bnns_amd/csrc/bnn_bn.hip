@@ -245,12 +245,12 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
   }
 }
 
-// Forward merge: 64 chunk groups x 4 columns per workgroup.  Two independent passes over the
-// partials instead of a serial Chan merge chain (two dependent double divisions per chunk: ~15-20 us
-// for the 256-1024 chunks of a small batch): the batch sum first (its fixed-order double sum gives
-// the mean), then M2 = sum_r [M2_r + n_r (S_r / n_r - mean)^2] (the parallel-axis form, every term
-// independent).  Deterministic: fixed group split, fixed fold order.
-constexpr int FF_COLS = 4, FF_GROUPS = 64, FF_B = 16;
+// Final merges of the per-chunk partials: 16 chunk groups x 16 columns per workgroup (128-B row
+// segments per load; 4 columns x 64 groups coalesced worse and ran 1-3x slower), a fixed group
+// split and fold order (deterministic).  The forward merge takes two independent passes instead of
+// a serial Chan chain (two dependent double divisions per chunk): the batch sum first (its
+// fixed-order double sum gives the mean), then M2 = sum_r [M2_r + n_r (S_r / n_r - mean)^2].
+constexpr int FF_COLS = 16, FF_GROUPS = 16, FF_B = 8;
 
 inline dim3 ffin_grid(int64_t C) { return dim3((unsigned)((C + FF_COLS - 1) / FF_COLS)); }
 

@@ -140,12 +140,41 @@ __global__ __launch_bounds__(256) void colsum_final_k(const double* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
+// FP4 panels: B [N][ldb] (row n = K/2 bytes of nibbles) -> [ceil(N/512)][K/64][512][32 B].  A GEMM
+// stage reads 32 B of each of its BN rows per 64-k step: from row-major B that is one quarter of a
+// 128-B line per row -- 4x the L2->L1 lines of the bytes used, 29 % of the FP6 GEMM's time
+// (profiles/r03_fp6_staging_diag.log) -- from panels one contiguous BN x 32 B run.  Workgroup = 32
+// rows x 4 k-steps (one 128-B line per source row, staged in LDS), written as 4 contiguous 1-KiB
+// runs; the rows of the last panel beyond N are zeros.
+constexpr int FP4_PANEL = 512;
+
+__global__ __launch_bounds__(256) void fp4_panelize_k(const uint8_t* __restrict__ b, int64_t N, int64_t ldb,
+                                                      int64_t nks, uint8_t* __restrict__ out) {
+  __shared__ uint4 tile[32][8];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * 32, ks0 = (int64_t)blockIdx.x * 4;
+  {
+    const int row = t >> 3, ch = t & 7;                 // 16-B chunk ch of the row's 128 B
+    const int64_t n = r0 + row, ks = ks0 + (ch >> 1);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < N && ks < nks) v = *reinterpret_cast<const uint4*>(b + n * ldb + ks * 32 + (ch & 1) * 16);
+    tile[row][ch] = v;
+  }
+  __syncthreads();
+  const int q = t >> 6, row = (t & 63) >> 1, half = t & 1;   // k-step q: 32 rows x 32 B = 1 KiB
+  const int64_t ks = ks0 + q, n = r0 + row;
+  if (ks < nks)
+    *reinterpret_cast<uint4*>(out + ((n / FP4_PANEL) * nks + ks) * (FP4_PANEL * 32) + (n % FP4_PANEL) * 32 + half * 16) =
+        tile[row][2 * q + half];
+}
+
+// ------------------------------------------------------------------------------------------
 // GEMM: C[M][N] = sum_k A[m][k] B[n][k] (+ bias[n]); A = FP6 digits (lo, hi, scales), B = FP4.
 struct Gemm6Params {
   const uint8_t* alo;   // [M][K/32][64]
   const uint8_t* ahi;   // [M][K/32][32]
   const uint8_t* asc;   // [K/64][asc_rows][2]
-  const uint8_t* b;     // [N][ldb]
+  const uint8_t* b;     // [N][ldb], or (b_panel) FP4 panels [N/512][K/64][512][32 B] (bnn_fp4_panelize)
   int64_t ldb, asc_rows;
   const float* bias;
   float* C;
@@ -158,6 +187,7 @@ struct Gemm6Params {
   // writes its fp32 partial (no bias) to part[split][M][N]; gemm6_splitk_sum_k folds the splits
   int ksplit, kps;
   float* part;
+  int b_panel;   // B in the panel layout: every stage's B piece is one contiguous run of BN x 32 B
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -277,13 +307,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   for (int ii = 0; ii < P_B; ++ii) {
     const int i = wave + ii * NW;
     const int lrow = i * 32 + (lane >> 1), c = lane & 1;
-    off_b[ii] = DIAG >= 5 ? (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1))
-                          : (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
+    off_b[ii] = (DIAG >= 5 || p.b_panel) ? (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1))
+                                         : (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
   }
   const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64 + (int64_t)ks0 * 128;
   const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32 + (int64_t)ks0 * 64;
   const uint8_t* sc_base = p.asc + (int64_t)m0 * 2 + (int64_t)ks0 * p.asc_rows * 2;
-  const uint8_t* b_base = p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
+  // panel layout: tile column n0 lies in panel n0 / 512 at row n0 % 512 (BN divides 512); rows
+  // beyond N are the panel's zero padding
+  const uint8_t* b_base = p.b_panel ? p.b + ((int64_t)(n0 / FP4_PANEL) * (p.K / 64) + ks0) * (FP4_PANEL * 32) + (n0 % FP4_PANEL) * 32
+                                    : p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
+  const int64_t b_step = (DIAG >= 5) ? BN * 32 : (p.b_panel ? FP4_PANEL * 32 : 32);
   auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
     if constexpr (DIAG == 1) return;
     char* base = smem + buf * ST;
@@ -295,7 +329,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       glds16_6s(hi_base + (int64_t)kt * (DIAG == 6 ? BM * 64 : 64), off_hi[ii], base + LO_ST + (wave + ii * NW) * 1024);
 #pragma unroll
     for (int ii = 0; ii < P_B; ++ii)
-      glds16_6s(b_base + (int64_t)kt * (DIAG >= 5 ? BN * 32 : 32), off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
+      glds16_6s(b_base + (int64_t)kt * b_step, off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
     if (wave == 0)   // a whole 1-KiB piece (512 rows): the scale array has 512 rows of tail padding
       glds16_6(sc_base + (int64_t)kt * p.asc_rows * 2 + lane * 16, base + LO_ST + HI_ST);
   };
@@ -536,7 +570,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       if (kt + 1 < nk) BNN_FP6_STEP(kt + 1, b1, f1, b0, f0)
     }
 #undef BNN_FP6_STEP
-  } else if constexpr (DIAG >= 3) {
+  } else if constexpr (DIAG == 3 || DIAG == 4) {
     // timing-only: fragments read once from stage 0 and reused by every k-step -- the MFMA
     // stream alone (3: with the per-k-step barrier, 4: without)
     stage(0, 0);
@@ -835,7 +869,8 @@ BNN_API int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_
 static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
                          const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
                          int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
-  if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || ldb < K / 2 || ldb % 16 != 0 ||
+  const bool panel = ldb == -1;   // bnn_gemm_fp6_panel_ws
+  if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || (!panel && (ldb < K / 2 || ldb % 16 != 0)) ||
       ldc < N || asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
       !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
     set_error("bnn_gemm_fp6: bad arguments (M=%lld N=%lld K=%lld ldb=%lld asc_rows=%lld; K a positive multiple of "
@@ -851,8 +886,35 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const int64_t need = bnn_gemm_fp6_workspace(M, N, K);
   const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
-                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr};
+                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? 1 : 0};
   return pl.v->fn(p, S6(stream));
+}
+
+BNN_API int64_t bnn_fp4_panel_bytes(int64_t N, int64_t Kp) {
+  if (N <= 0 || Kp <= 0 || Kp % 64 != 0) return 0;
+  return (N + FP4_PANEL - 1) / FP4_PANEL * FP4_PANEL * (Kp / 2);
+}
+
+BNN_API int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t Kp, uint8_t* panels, void* stream) {
+  if (!b || !panels || N <= 0 || Kp <= 0 || Kp % 64 != 0 || ldb < Kp / 2 || ldb % 16 != 0 || !aligned16(b) ||
+      !aligned16(panels) || (Kp / 64 + 3) / 4 > 0x7fffffff) {
+    set_error("bnn_fp4_panelize: bad arguments (N=%lld ldb=%lld Kp=%lld)", (long long)N, (long long)ldb, (long long)Kp);
+    return kErrInval;
+  }
+  const int64_t nks = Kp / 64, rows = (N + FP4_PANEL - 1) / FP4_PANEL * FP4_PANEL;
+  hipLaunchKernelGGL(fp4_panelize_k, dim3((unsigned)((nks + 3) / 4), (unsigned)(rows / 32)), dim3(256), 0, S6(stream),
+                     b, N, ldb, nks, panels);
+  return check_launch("bnn_fp4_panelize");
+}
+
+BNN_API int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                                  const uint8_t* bpanels, const float* bias, float* C, int64_t ldc, int64_t M,
+                                  int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+  if (g_variant6 >= 0 && 512 % find6(g_variant6)->bn != 0) {
+    set_error("bnn_gemm_fp6_panel_ws: the forced variant's tile width does not divide the 512-row panel");
+    return kErrInval;
+  }
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, bpanels, -1, bias, C, ldc, M, N, K, work, work_bytes, stream);
 }
 
 BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, N)->name; }

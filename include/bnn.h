@@ -187,6 +187,14 @@ int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K);
 int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
                     int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                     void* work, int64_t work_bytes, bnn_stream_t stream);
+/* FP4 panels of a B operand: [N][ldb] -> [ceil(N/512)][Kp/64][512][32 B] (rows beyond N zero), so
+ * each GEMM stage stages one contiguous run of B instead of 32 B from each of 512 rows (a quarter
+ * line per row); bnn_gemm_fp6_panel_ws = bnn_gemm_fp6_ws with B in that layout. */
+int64_t bnn_fp4_panel_bytes(int64_t N, int64_t Kp);
+int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t Kp, uint8_t* panels, bnn_stream_t stream);
+int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                          const uint8_t* bpanels, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N,
+                          int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
 const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */

@@ -177,3 +177,36 @@ def test_gemm_fp6_propagates_nan(F):
     C = F.gemm_fp6(F.quant6_rows(x), F.sign_pack_fp4(w)[0], 24)
     isn = torch.isnan(C)
     assert bool(isn[7].all()) and int(isn.sum()) == 24
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 600, 320), (2048, 1024, 8192), (768, 1536, 4096), (64, 37, 64)])
+def test_fp4_panels_and_panel_gemm(F, M, N, K):
+    """The FP4 panel layout [ceil(N/512)][K/64][512][32 B] (zero rows beyond N) equals a host
+    re-tiling of the row-major operand, and the GEMM staged from panels is bit-identical to the one
+    staged from rows (only the staging source changes), split-K shapes included."""
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M * 7 + N + K)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-4, 4, (M, 1)))).astype(np.float32)
+    w = rng.integers(-1, 2, (N, K)).astype(np.float32)
+    w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
+    P = F.fp4_panels(w4, N, K)
+    rows = host(w4)[:, :K // 2]
+    npan = (N + 511) // 512
+    ref = np.zeros((npan * 512, K // 2), np.uint8)
+    ref[:N] = rows
+    ref = ref.reshape(npan, 512, K // 64, 32).transpose(0, 2, 1, 3).reshape(-1)
+    assert np.array_equal(host(P), ref)
+    op = F.quant6_rows(torch.as_tensor(x).cuda())
+    bt = torch.as_tensor(rng.standard_normal(N).astype(np.float32)).cuda()
+    C_rows = host(F.gemm_fp6(op, w4, N, bias=bt, panels=None)) if M * N * K < F.PANEL_MIN_MACS else None
+    if C_rows is None:                                  # force the row-major staging for the comparison
+        C0 = torch.empty(M, N, device="cuda")
+        wsb = L.lib().bnn_gemm_fp6_workspace(M, N, op.Kp)
+        ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device="cuda")
+        L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(w4), w4.shape[1],
+               L.ptr(bt), L.ptr(C0), N, M, N, op.Kp, L.ptr(ws), wsb, L.stream())
+        C_rows = host(C0)
+    C_pan = host(F.gemm_fp6(op, w4, N, bias=bt, panels=P))
+    assert np.array_equal(C_pan, C_rows)
+    val, _, _ = decode(op, M)
+    assert rel_err(C_pan, val[:, :K] @ w.astype(np.float64).T + host(bt)) < 2e-6
