@@ -66,7 +66,7 @@ SIGNATURES = {
                                  P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
     "bnn_bn_fwd_train_i16": (I32, [P, P, I64, I64, P, P, P, P, F32, F32, P, P, P, F32, U64, P, P]),
-    "bnn_bn_apply_pack_i16": (I32, [P, P, I64, I64, P, P, P, P, P, P, I64, P, I64, P]),
+    "bnn_bn_apply_pack_i16": (I32, [P, P, I64, I64, P, P, P, P, P, P, I64, P, I64, I32, P]),
     "bnn_bn_bwd_q6_i16": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
                                 P, P]),
     "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
@@ -94,7 +94,7 @@ SIGNATURES = {
     "bnn_gemm_fp6_ws": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_fp4_panel_bytes": (I64, [I64, I64]),
     "bnn_fp4_panelize": (I32, [P, I64, I64, I64, P, P]),
-    "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, P, P, I64, I64, I64, I64, P, I64, P]),
+    "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_gemm_fp6_kernel": (ctypes.c_char_p, [I64, I64]),
     "bnn_gemm_fp6_kernel_k": (ctypes.c_char_p, [I64, I64, I64]),
     "bnn_gemm_fp6_set_variant": (I32, [I32]),

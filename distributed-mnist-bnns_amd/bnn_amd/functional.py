@@ -536,12 +536,20 @@ def fp4_panels(B4, N, Kp):
     return P
 
 
-def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None):
-    """C[A.rows, N] = A . B4^T (+ bias): A an Fp6Operand, B4 FP4 nibbles [N, >= A.Kp/2 bytes].
-    panels: B4 already in the panel layout (fp4_panels); large products panelize B4 themselves."""
+def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None, panel_ks=None):
+    """C[A.rows, N] = A . B4^T (+ bias): A an Fp6Operand, B4 FP4 nibbles [N, >= A.Kp/2 bytes], or
+    B4 = None and panels = the same operand in the panel layout with panel_ks 64-k steps per panel
+    (fp4_panels, or a panel transpose from bn_apply_pack); large products panelize B4 themselves."""
     M, K = A.rows, A.Kp
-    assert B4.dtype == torch.uint8 and B4.shape[0] == N and 2 * B4.shape[1] >= K
-    C = torch.empty((M, N), dtype=torch.float32, device=B4.device) if out is None else out
+    if B4 is None:
+        assert panels is not None and panel_ks is not None and panel_ks * 64 >= K
+        dev = panels.device
+    else:
+        assert B4.dtype == torch.uint8 and B4.shape[0] == N and 2 * B4.shape[1] >= K
+        dev = B4.device
+        if panel_ks is None:
+            panel_ks = K // 64
+    C = torch.empty((M, N), dtype=torch.float32, device=dev) if out is None else out
     if M == 0 or N == 0:
         return C
     k_true = K if k_true is None else k_true
@@ -549,11 +557,11 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None):
         panels = fp4_panels(B4, N, K)
     name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
     wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)    # split-K partials (small grids), else 0
-    ws = torch.empty((wsb,), dtype=torch.uint8, device=B4.device) if wsb > 0 else None
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=dev) if wsb > 0 else None
     with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):
         if panels is not None:
             L.call("bnn_gemm_fp6_panel_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(panels),
-                   L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
+                   panel_ks, L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
         else:
             L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
                    L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
@@ -1400,16 +1408,24 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         qf = "fp4" if ctx.fp6 else "i8"
         q = torch.empty((M, round_up(C, 256) // 2) if fp4 else (M, round_up(C)),
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
-        qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
+        # the weight gradient's B operand straight in the FP4 panel layout (no panel pass before the
+        # dW GEMM) when the 256x256-tile kernel runs and the GEMM is large enough to be panel-staged
+        ctx.qt_panel = (need_dw and qf == "fp4" and C % 256 == 0 and N * C * round_up(M) >= PANEL_MIN_MACS
+                        and (zz is not None or (C // 256) * ((M + 255) // 256) >= 1024))
+        if ctx.qt_panel:
+            qt = torch.empty(((C + 511) // 512 * 512, round_up(M, 256) // 2), dtype=torch.uint8, device=z.device)
+        else:
+            qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
         nx = 4 if zz is None else 2
         with _timed("bn_apply_pack", 0, nx * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
             if zz is None:
                 L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
                        L.ptr(gb), 1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
-                       1 if qf == "fp4" else 0, L.stream())
+                       (2 if ctx.qt_panel else 1) if qf == "fp4" else 0, L.stream())
             else:
                 L.call("bnn_bn_apply_pack_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
-                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], L.stream())
+                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1],
+                       1 if ctx.qt_panel else 0, L.stream())
         b = bias.detach() if bias is not None else None
         wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True, qt_fmt=qf)
         if emit_z16 and fp4 and training:
@@ -1448,7 +1464,10 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                 dt, cs = (pre[1], (pre[2] if need_db else None)) if pre is not None else \
                     quant6_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[8]:
-                    dw = gemm_fp6(dt, qt, C, k_true=M, out=sink)               # dY^T . sign(h)
+                    if ctx.qt_panel:
+                        dw = gemm_fp6(dt, None, C, k_true=M, out=sink, panels=qt, panel_ks=qt.shape[1] // 32)
+                    else:
+                        dw = gemm_fp6(dt, qt, C, k_true=M, out=sink)           # dY^T . sign(h)
                     if sink is not None:        # written into the bucket view: nothing to accumulate
                         ex.grad_written(ctx.weight_ref)
                         dw = None

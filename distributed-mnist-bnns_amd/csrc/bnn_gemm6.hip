@@ -187,7 +187,8 @@ struct Gemm6Params {
   // writes its fp32 partial (no bias) to part[split][M][N]; gemm6_splitk_sum_k folds the splits
   int ksplit, kps;
   float* part;
-  int b_panel;   // B in the panel layout: every stage's B piece is one contiguous run of BN x 32 B
+  int64_t bks;   // > 0: B in the panel layout with bks 64-k steps per panel (>= K / 64): every
+                 // stage's B piece is one contiguous run of BN x 32 B
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   for (int ii = 0; ii < P_B; ++ii) {
     const int i = wave + ii * NW;
     const int lrow = i * 32 + (lane >> 1), c = lane & 1;
-    off_b[ii] = (DIAG >= 5 || p.b_panel) ? (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1))
+    off_b[ii] = (DIAG >= 5 || p.bks > 0) ? (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1))
                                          : (uint32_t)min(lrow, p.N - 1 - n0) * (uint32_t)p.ldb + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
   }
   const uint8_t* lo_base = p.alo + (int64_t)m0 * nblk * 64 + (int64_t)ks0 * 128;
@@ -315,9 +316,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   const uint8_t* sc_base = p.asc + (int64_t)m0 * 2 + (int64_t)ks0 * p.asc_rows * 2;
   // panel layout: tile column n0 lies in panel n0 / 512 at row n0 % 512 (BN divides 512); rows
   // beyond N are the panel's zero padding
-  const uint8_t* b_base = p.b_panel ? p.b + ((int64_t)(n0 / FP4_PANEL) * (p.K / 64) + ks0) * (FP4_PANEL * 32) + (n0 % FP4_PANEL) * 32
+  const uint8_t* b_base = p.bks > 0 ? p.b + ((int64_t)(n0 / FP4_PANEL) * p.bks + ks0) * (FP4_PANEL * 32) + (n0 % FP4_PANEL) * 32
                                     : p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
-  const int64_t b_step = (DIAG >= 5) ? BN * 32 : (p.b_panel ? FP4_PANEL * 32 : 32);
+  const int64_t b_step = (DIAG >= 5) ? BN * 32 : (p.bks > 0 ? FP4_PANEL * 32 : 32);
   auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
     if constexpr (DIAG == 1) return;
     char* base = smem + buf * ST;
@@ -869,7 +870,7 @@ BNN_API int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_
 static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
                          const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
                          int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
-  const bool panel = ldb == -1;   // bnn_gemm_fp6_panel_ws
+  const bool panel = ldb < 0;   // bnn_gemm_fp6_panel_ws: ldb = -(k-steps per panel)
   if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || (!panel && (ldb < K / 2 || ldb % 16 != 0)) ||
       ldc < N || asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
       !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
@@ -886,7 +887,7 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const int64_t need = bnn_gemm_fp6_workspace(M, N, K);
   const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
-                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? 1 : 0};
+                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0};
   return pl.v->fn(p, S6(stream));
 }
 
@@ -908,13 +909,14 @@ BNN_API int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t K
 }
 
 BNN_API int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                                  const uint8_t* bpanels, const float* bias, float* C, int64_t ldc, int64_t M,
-                                  int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
-  if (g_variant6 >= 0 && 512 % find6(g_variant6)->bn != 0) {
-    set_error("bnn_gemm_fp6_panel_ws: the forced variant's tile width does not divide the 512-row panel");
+                                  const uint8_t* bpanels, int64_t bks, const float* bias, float* C, int64_t ldc,
+                                  int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+  if ((g_variant6 >= 0 && 512 % find6(g_variant6)->bn != 0) || K <= 0 || bks < K / 64) {
+    set_error("bnn_gemm_fp6_panel_ws: bad arguments (K=%lld bks=%lld; bks >= K/64, a tile width dividing 512)",
+              (long long)K, (long long)bks);
     return kErrInval;
   }
-  return gemm_fp6_impl(alo, ahi, asc, asc_rows, bpanels, -1, bias, C, ldc, M, N, K, work, work_bytes, stream);
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, bpanels, -bks, bias, C, ldc, M, N, K, work, work_bytes, stream);
 }
 
 BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, N)->name; }

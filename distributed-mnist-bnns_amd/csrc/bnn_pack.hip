@@ -246,7 +246,7 @@ __device__ __forceinline__ void nib_transpose8(uint32_t (&x)[8]) {
 template <bool Z16>
 __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, int64_t C,
                                                            ColAffine af, uint8_t* __restrict__ q, int64_t ldq,
-                                                           uint8_t* __restrict__ qt, int64_t ldqt) {
+                                                           uint8_t* __restrict__ qt, int64_t ldqt, int64_t pnks) {
   __shared__ uint32_t img[AP_T * AP_LD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t k0 = (int64_t)blockIdx.x * AP_T, m0 = (int64_t)blockIdx.y * AP_T;
@@ -291,10 +291,16 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
 #pragma unroll
     for (int c = 0; c < 8; ++c) out[c][qq] = w[c];
   }
+  // pnks > 0: the transpose in the FP4 panel layout of the FP6 GEMM's B operand (bnn_fp4_panelize:
+  // [C/512][pnks][512][32 B]) -- row n's 16 B at batch m0 + 32 mg are half mg & 1 of k-step
+  // (m0 + 32 mg) / 64; a wave's 8 rows per store are 32-B pieces of 8 lines the c loop completes
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
-    *reinterpret_cast<uint4*>(qt + (k0 + 8 * kb + c) * ldqt + m0 / 2 + 16 * mg) =
-        make_uint4(out[c][0], out[c][1], out[c][2], out[c][3]);
+  for (int c = 0; c < 8; ++c) {
+    const int64_t n = k0 + 8 * kb + c;
+    uint8_t* dst = pnks > 0 ? qt + ((n >> 9) * pnks + (m0 >> 6) + (mg >> 1)) * 16384 + (n & 511) * 32 + (mg & 1) * 16
+                            : qt + n * ldqt + m0 / 2 + 16 * mg;
+    *reinterpret_cast<uint4*>(dst) = make_uint4(out[c][0], out[c][1], out[c][2], out[c][3]);
+  }
 }
 
 __global__ __launch_bounds__(256) void sign_f32_k(const float* __restrict__ x, float* __restrict__ y,
@@ -991,8 +997,9 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
                               const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
                               int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
   const int64_t need = fmt == 1 ? round_up(C, 256) / 2 : round_up(C, TILE);
+  const int qf = qt_fmt == 2 ? 1 : qt_fmt;   // 2 = FP4 transpose in the panel layout
   if (!x || !mean || !invstd || M < 0 || C < 0 || (fmt != 0 && fmt != 1) || (!q && !qt) ||
-      (q && (ldq < need || ldq % (fmt == 1 ? 128 : TILE) != 0 || !aligned16(q))) || !qt_ok(qt, M, ldqt, qt_fmt)) {
+      (q && (ldq < need || ldq % (fmt == 1 ? 128 : TILE) != 0 || !aligned16(q))) || !qt_ok(qt, M, ldqt, qf)) {
     set_error("bnn_bn_apply_pack: bad arguments (M=%lld C=%lld fmt=%d ldq=%lld ldqt=%lld)", (long long)M,
               (long long)C, fmt, (long long)ldq, (long long)ldqt);
     return kErrInval;
@@ -1000,7 +1007,7 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   if (M == 0 && !qt) return 0;
   const int vec = aligned16(x) && (C % 4 == 0);
   const int64_t gx = q ? (fmt == 1 ? 2 * ldq : ldq) / TILE : (C + TILE - 1) / TILE;
-  const int64_t gy = qt ? qt_tiles(ldqt, qt_fmt) : (M + TILE - 1) / TILE;
+  const int64_t gy = qt ? qt_tiles(ldqt, qf) : (M + TILE - 1) / TILE;
   if (gx == 0 || gy == 0) return 0;
   if (gy > 65535) {
     set_error("bnn_bn_apply_pack: M too large for one launch (%lld)", (long long)M);
@@ -1009,10 +1016,16 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   const ColAffine af{mean, mean_lo, invstd, gamma, beta,
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
-  if (fmt == 1 && q && qt && qt_fmt == 1 && C % AP_T == 0 && af.vec && vec && (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024) {
+  const bool fast = fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && C % AP_T == 0 && af.vec && vec &&
+                    (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024;
+  if (qt_fmt == 2 && !fast) {
+    set_error("bnn_bn_apply_pack: the panel transpose (qt_fmt 2) needs FP4 rows, C %% 256 == 0 and >= 1024 tiles");
+    return kErrInval;
+  }
+  if (fast) {
     hipLaunchKernelGGL((bn_apply_pack_fp4_k<false>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                        dim3(256), 0, S(stream), XIn{x, nullptr}, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
-                       reinterpret_cast<uint8_t*>(qt), ldqt);
+                       reinterpret_cast<uint8_t*>(qt), ldqt, qt_fmt == 2 ? ldqt / 32 : (int64_t)0);
     return check_launch("bnn_bn_apply_pack");
   }
   // 4 row tiles per workgroup when that still leaves >= 8K workgroups (amortised parameter loads)
@@ -1031,7 +1044,8 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
 // output of bnn_gemm_fp4_i16): FP4 rows + FP4 transpose only, C % 256 == 0, any M.
 BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                                   const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
-                                  uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, void* stream) {
+                                  uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, int32_t qt_panel,
+                                  void* stream) {
   const ColAffine af{mean, mean_lo, invstd, gamma, beta,
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
@@ -1043,7 +1057,7 @@ BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_
     return kErrInval;
   }
   hipLaunchKernelGGL((bn_apply_pack_fp4_k<true>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
-                     dim3(256), 0, S(stream), XIn{x16, xbias}, M, C, af, q, ldq, qt, ldqt);
+                     dim3(256), 0, S(stream), XIn{x16, xbias}, M, C, af, q, ldq, qt, ldqt, qt_panel ? ldqt / 32 : (int64_t)0);
   return check_launch("bnn_bn_apply_pack_i16");
 }
 

@@ -189,12 +189,14 @@ int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, 
                     void* work, int64_t work_bytes, bnn_stream_t stream);
 /* FP4 panels of a B operand: [N][ldb] -> [ceil(N/512)][Kp/64][512][32 B] (rows beyond N zero), so
  * each GEMM stage stages one contiguous run of B instead of 32 B from each of 512 rows (a quarter
- * line per row); bnn_gemm_fp6_panel_ws = bnn_gemm_fp6_ws with B in that layout. */
+ * line per row); bnn_gemm_fp6_panel_ws = bnn_gemm_fp6_ws with B in that layout, bks = the 64-k
+ * steps stored per panel (>= K/64; Kp/64 of bnn_fp4_panelize, round_up(M,256)/64 of
+ * bnn_bn_apply_pack's panel transpose). */
 int64_t bnn_fp4_panel_bytes(int64_t N, int64_t Kp);
 int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t Kp, uint8_t* panels, bnn_stream_t stream);
 int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                          const uint8_t* bpanels, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N,
-                          int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
+                          const uint8_t* bpanels, int64_t bks, const float* bias, float* C, int64_t ldc, int64_t M,
+                          int64_t N, int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
 const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
@@ -346,7 +348,9 @@ int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_
  * 66-68: bn1 -> htanh1 -> fc2 binarises its input): y = ((x-mean)-mean_lo)*invstd*gamma+beta exactly as
  * bnn_bn_fwd_* computes it, written only as the next GEMM's ternary operand -- q rows in fmt 0
  * (int8, ldq >= round_up(C,64)) or fmt 1 (FP4 nibbles, ldq bytes >= round_up(C,256)/2, multiple
- * of 128) and/or the int8 transpose qt [C][ldqt] for the weight gradient; no fp32 activation is
+ * of 128) and/or the transpose qt for the weight gradient: qt_fmt 0 int8 [C][ldqt], 1 FP4
+ * [C][ldqt bytes], 2 FP4 in the panel layout of bnn_gemm_fp6_panel_ws ([ceil(C/512)][ldqt/32][512]
+ * [32 B], bks = ldqt/32; needs fmt 1, C % 256 == 0 and >= 1024 256x256 tiles); no fp32 activation is
  * written (Hardtanh keeps the sign; its backward mask is recomputed from x by bnn_bn_bwd). */
 int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                       const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
@@ -357,7 +361,8 @@ int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, c
  * x = fl(x16 + xbias) -- the value the fp32 GEMM epilogue stores, so every result is bit-identical
  * to the fp32 entry on that x.  Training-mode statistics passes only:
  *   bnn_bn_fwd_train_i16     = bnn_bn_dropout_fwd_train with y = NULL (p = 0: no dropout)
- *   bnn_bn_apply_pack_i16    = bnn_bn_apply_pack, fmt 1 rows + qt_fmt 1 transpose, C % 256 == 0
+ *   bnn_bn_apply_pack_i16    = bnn_bn_apply_pack, fmt 1 rows + qt_fmt 1 (qt_panel 0) or 2 (qt_panel 1)
+ *                              transpose, C % 256 == 0
  *   bnn_bn_bwd_q6_i16        = bnn_bn_bwd_q6
  *   bnn_bn_head_fwd_i16      = bnn_bn_head_fwd
  *   bnn_bn_head_bwd_q6_i16   = bnn_bn_head_bwd_q6
@@ -369,7 +374,8 @@ int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int6
                          void* work, bnn_stream_t stream);
 int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                           const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
-                          uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, bnn_stream_t stream);
+                          uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, int32_t qt_panel,
+                          bnn_stream_t stream);
 int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
                       const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                       const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx, float* dgamma,

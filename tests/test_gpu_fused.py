@@ -90,6 +90,43 @@ def test_bn_apply_pack_wide_tiles_bit_exact(F):
     _apply_pack_case(F, 8200, 8192, 1, 1)
 
 
+def test_bn_apply_pack_panel_transpose(F):
+    """qt_fmt 2: the 256 x 256-tile kernel writes the transpose straight in the FP4 panel layout of
+    the FP6 GEMM's B operand -- equal to bnn_fp4_panelize of the row-major transpose (C = 1792: a
+    half-filled last panel; M ragged; >= 1024 tiles), and the dW GEMM staged from it equals the
+    row-staged one."""
+    from bnn_amd import _lib as L
+    M, C = 40000, 1792
+    rng = np.random.default_rng(5)
+    z = (rng.integers(-30, 31, (M, C)) + rng.uniform(-1, 1, C).astype(np.float32)).astype(np.float32)
+    gamma, beta = dev(rng.uniform(0.5, 1.5, C).astype(np.float32)), dev(rng.uniform(-0.3, 0.3, C).astype(np.float32))
+    zt = dev(z)
+    mean, invstd, lo = bn_stats(F, zt, C)
+    ldqt = F.round_up(M, 256) // 2
+    outs = []
+    for fmt_t in (1, 2):
+        q = torch.empty((M, C // 2), dtype=torch.uint8, device="cuda")
+        rows = (C + 511) // 512 * 512 if fmt_t == 2 else C
+        qt = torch.full((rows, ldqt), 0x55, dtype=torch.uint8, device="cuda")
+        L.call("bnn_bn_apply_pack", L.ptr(zt), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo), L.ptr(gamma),
+               L.ptr(beta), 1, L.ptr(q), q.shape[1], L.ptr(qt), ldqt, fmt_t, L.stream())
+        outs.append(qt)
+    P = F.fp4_panels(outs[0], C, 2 * ldqt)
+    got = host(outs[1]).reshape(-1)
+    ref = host(P)
+    live = np.zeros(((C + 511) // 512, 2 * ldqt // 64, 512, 32), bool)
+    live[:, :, :, :] = True
+    live[C // 512:, :, C % 512 or 512:, :] = False        # rows beyond C: unspecified in qt_fmt 2
+    live = live.reshape(-1)
+    assert np.array_equal(got[live], ref[live])
+    N = 512
+    dy = torch.randn(M, N, device="cuda")
+    dt, _ = F.quant6_cols_t(dy)
+    a = F.gemm_fp6(dt, outs[0], C, k_true=M)
+    b = F.gemm_fp6(dt, None, C, k_true=M, panels=outs[1], panel_ks=ldqt // 32)
+    assert torch.equal(a, b)
+
+
 def _apply_pack_case(F, M, C, fmt, with_qt):
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M * 7 + C + fmt)

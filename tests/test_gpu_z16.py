@@ -93,7 +93,7 @@ def test_apply_pack_i16_bit_identical(F, M, C):
                    1, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], 1, L.stream())
         else:
             L.call("bnn_bn_apply_pack_i16", L.ptr(z16), L.ptr(bias), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo),
-                   L.ptr(gam), L.ptr(bet), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], L.stream())
+                   L.ptr(gam), L.ptr(bet), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], 0, L.stream())
         res.append((q, qt))
     assert eq(res[0][0], res[1][0]) and eq(res[0][1], res[1][1])
 
