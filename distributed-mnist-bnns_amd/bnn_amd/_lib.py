@@ -55,6 +55,9 @@ SIGNATURES = {
     "bnn_bn2d_fwd_eval": (I32, [P, I64, I64, I64, I64, P, P, P, P, F32, P, I32, I32, P, P]),
     "bnn_bn2d_bwd": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "bnn_bn2d_bwd_eval": (I32, [P, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
+    "bnn_bn2d_fwd_train_q": (I32, [P, P, I32, I64, I64, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P]),
+    "bnn_bn2d_bwd_q": (I32, [P, P, I32, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
+    "bnn_conv2d_fwd_q": (I32, [P, P, P, I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,

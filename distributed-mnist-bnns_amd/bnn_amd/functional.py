@@ -141,11 +141,18 @@ def sign_pack(x, want_q=True, want_qt=False):
     return q, qt
 
 
+_QT_CODE = {"i8": 0, "fp4": 1, "fp4p": 2}
+
+
 def _qt_buffer(K, M, qt_fmt, device):
-    """The transposed ternary operand [K, .] of an [M, K] matrix: int8 (qt_fmt "i8") or FP4
-    nibbles (qt_fmt "fp4": round_up(M, 256) / 2 bytes per row, the B operand of gemm_fp6)."""
+    """The transposed ternary operand [K, .] of an [M, K] matrix: int8 (qt_fmt "i8"), FP4
+    nibbles (qt_fmt "fp4": round_up(M, 256) / 2 bytes per row, the B operand of gemm_fp6), or those
+    nibbles in gemm_fp6's panel layout (qt_fmt "fp4p": the rows rounded up to 512, panel_ks =
+    shape[1] // 32; see fp4_panels)."""
     if qt_fmt == "fp4":
         return torch.empty((K, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
+    if qt_fmt == "fp4p":
+        return torch.empty(((K + 511) // 512 * 512, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
     return torch.empty((K, round_up(M)), dtype=torch.int8, device=device)
 
 
@@ -160,7 +167,7 @@ def sign_pack_fp4(x, want_qt=False, qt_fmt="i8", want_q=True):
     nbytes = 4 * M * K + (q4.numel() if q4 is not None else 0) + (qt.numel() if qt is not None else 0)
     with _timed("sign_pack_tile_k<1>", 0, nbytes):
         L.call("bnn_sign_pack_fp4", L.ptr(x), M, K, K, L.ptr(q4), q4.shape[1] if q4 is not None else 0,
-               L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if qt_fmt == "fp4" else 0, L.stream())
+               L.ptr(qt), qt.shape[1] if qt is not None else 0, _QT_CODE[qt_fmt], L.stream())
     return q4, qt
 
 
@@ -235,7 +242,7 @@ def packed_weight(weight, fmt, want_q, want_qt, cache=True, qt_fmt="i8"):
     if same:                                    # keep producing what earlier forwards needed
         want_q = want_q or ent["q"] is not None
         want_qt = want_qt or ent["qt"] is not None
-    if fmt == "fp4" or qt_fmt == "fp4":
+    if fmt == "fp4" or qt_fmt in ("fp4", "fp4p"):
         assert fmt == "fp4" or not want_q, "int8 rows with an FP4 transpose are not a supported pairing"
         q, qt = sign_pack_fp4(weight, want_qt=want_qt, qt_fmt=qt_fmt, want_q=want_q)
     else:
@@ -309,7 +316,7 @@ def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.
     q, qt = ent["q"], ent["qt"]
     nbytes = 28 * N * K + (q.numel() if q is not None else 0) + (qt.numel() if qt is not None else 0)
     tail = (1 if ent["fmt"] == "fp4" else 0, L.ptr(q), q.shape[1] if q is not None else 0,
-            L.ptr(qt), qt.shape[1] if qt is not None else 0, 1 if ent["qt_fmt"] == "fp4" else 0, L.stream())
+            L.ptr(qt), qt.shape[1] if qt is not None else 0, _QT_CODE[ent["qt_fmt"]], L.stream())
     with _timed("sign_pack_tile_k<adam>", 0, nbytes):
         if sched is not None:
             L.call("bnn_adam_clamp_pack_sched", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
@@ -790,9 +797,35 @@ def _pair_same(v, what):
     return int(v)
 
 
+# Compact conv outputs (zq): a binary-input BinarizeConv2d computes exact integer sums I (|I| <=
+# C*KH*KW: 25 for the BinCNN's first layer, 400 for its second) plus a per-channel bias, so when
+# its only consumer is the fused BatchNorm2d it travels as int8 / int16 sums + the bias
+# (bnn_conv2d_fwd_q; bnn_bn2d_*_q read fl(I + bias), bit-identical to the fp32 output) -- a stride-0
+# placeholder of the output shape carries them, as the MLP's z16 does.
+ZQ = True
+_ZQ_ATTR = "_bnn_zq"
+ZQ_HANDOFFS = 0
+
+
+def _zq_of(x):
+    """(int8 / int16 sums [N, C, H, W], bias [C] or None, fmt 1 / 2) carried by a zq placeholder."""
+    return getattr(x, _ZQ_ATTR, None)
+
+
+def _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, pad):
+    """1 (int8) / 2 (int16) when bnn_conv2d_fwd_q takes the shape, else 0."""
+    if not (ZQ and binarize_input and stride == 1 and dilation == 1 and groups == 1 and pad <= min(KH, KW) - 1):
+        return 0
+    if not (C == 1 and KW <= 8) and not (C % 16 == 0 and C <= 64):
+        return 0
+    n = C * KH * KW
+    return 1 if n <= 127 else (2 if n <= 32767 else 0)
+
+
 class BinaryConv2dFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, binarize_input, stride, padding, dilation, groups):
+    def forward(ctx, x, weight, bias, binarize_input, stride, padding, dilation, groups, emit_compact=False):
+        global ZQ_HANDOFFS
         _check(x, weight, bias)
         x = _c2d(x)
         w = _c2d(weight.detach())
@@ -800,9 +833,24 @@ class BinaryConv2dFunction(torch.autograd.Function):
         Co, _, KH, KW = w.shape
         OH = (H + 2 * padding - dilation * (KH - 1) - 1) // stride + 1
         OW = (W + 2 * padding - dilation * (KW - 1) - 1) // stride + 1
-        y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
         b = bias.detach() if bias is not None else None
         ctx.empty = N == 0
+        zf = _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, padding) if emit_compact else 0
+        if zf and N > 0 and Co <= 64 and (OH * OW) % 4 == 0 and OH % 2 == 0 and OW % 2 == 0:
+            yq = torch.empty((N, Co, OH, OW), dtype=torch.int8 if zf == 1 else torch.int16, device=x.device)
+            macs = N * Co * OH * OW * C * KH * KW
+            with _timed("conv2d_fwd", 2 * macs, 4 * x.numel() + yq.numel() * yq.element_size() + 4 * w.numel()):
+                L.call("bnn_conv2d_fwd_q", L.ptr(x), L.ptr(w), L.ptr(yq), zf, N, C, H, W, Co, KH, KW, stride,
+                       padding, dilation, groups, L.stream())
+            ctx.save_for_backward(x, w)
+            ctx.conf = (binarize_input, stride, padding, dilation, groups)
+            ctx.has_bias = bias is not None
+            ZQ_HANDOFFS += 1
+            ph = torch.zeros((1,), dtype=torch.float32, device=x.device).as_strided((N, Co, OH, OW), (0, 0, 0, 0))
+            # the bias as it is now: the optimizer updates the Parameter in place after backward
+            setattr(ph, _ZQ_ATTR, (yq, b.clone() if b is not None else None, zf))
+            return ph
+        y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
         if ctx.empty:             # empty batch: F.conv2d returns [0, Co, OH, OW]
             ctx.save_for_backward(x, w)
             ctx.conf = (binarize_input, stride, padding, dilation, groups)
@@ -828,7 +876,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
             return (torch.empty_like(x) if ctx.needs_input_grad[0] else None,
                     torch.zeros_like(w) if ctx.needs_input_grad[1] else None,
                     torch.zeros((Co,), dtype=torch.float32, device=x.device)
-                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None, None)
+                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None, None, None)
         dx = dw = db = None
         macs = dy.numel() * (C // groups) * KH * KW
         if ctx.needs_input_grad[0]:
@@ -848,13 +896,16 @@ class BinaryConv2dFunction(torch.autograd.Function):
                        L.stream())
             if not ctx.needs_input_grad[1]:
                 dw = None
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
-def binary_conv2d(x, weight, bias=None, binarize_input=True, stride=1, padding=0, dilation=1, groups=1):
+def binary_conv2d(x, weight, bias=None, binarize_input=True, stride=1, padding=0, dilation=1, groups=1,
+                  emit_compact=False):
+    """emit_compact: return the output as a zq placeholder when the shape allows (its consumer
+    must be batch_norm2d_hardtanh_pool in training mode)."""
     return BinaryConv2dFunction.apply(x, weight, bias, binarize_input, _pair_same(stride, "stride"),
                                       _pair_same(padding, "padding"), _pair_same(dilation, "dilation"),
-                                      int(groups))
+                                      int(groups), bool(emit_compact))
 
 
 # ----------------------------------------------------------------------------- (3) STE helpers
@@ -1304,7 +1355,11 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh, pool):
         _check(x, weight, bias, running_mean, running_var)
-        x = x if x.is_contiguous() else x.contiguous()
+        zq = _zq_of(x)                        # (int8/int16 sums, bias, fmt): x in its compact form
+        if zq is not None and not training:
+            raise RuntimeError("a compact conv output needs the training-mode BatchNorm2d")
+        if zq is None:
+            x = x if x.is_contiguous() else x.contiguous()
         N, C, H, W = x.shape
         oh, ow = (H // 2, W // 2) if pool else (H, W)
         y = torch.empty((N, C, oh, ow), dtype=torch.float32, device=x.device)
@@ -1315,35 +1370,53 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
         if training:
             mean = torch.empty((C,), dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
-            with _timed("bn2d_fwd_train", 0, 8 * nel + 4 * y.numel()):
-                L.call("bnn_bn2d_fwd_train", L.ptr(x), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(running_mean),
-                       L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
-                       L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
+            xb = 4 if zq is None else zq[0].element_size()
+            with _timed("bn2d_fwd_train", 0, 2 * xb * nel + 4 * y.numel()):
+                if zq is None:
+                    L.call("bnn_bn2d_fwd_train", L.ptr(x), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(running_mean),
+                           L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
+                           L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
+                else:
+                    L.call("bnn_bn2d_fwd_train_q", L.ptr(zq[0]), L.ptr(zq[1]), zq[2], N, C, H, W, L.ptr(w), L.ptr(b),
+                           L.ptr(running_mean), L.ptr(running_var), float(momentum if momentum is not None else -1.0),
+                           float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws),
+                           L.stream())
         else:
             mean = running_mean
             invstd = (running_var + eps).rsqrt()
             with _timed("bn2d_fwd_eval", 0, 4 * nel + 4 * y.numel()):
                 L.call("bnn_bn2d_fwd_eval", L.ptr(x), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                        L.ptr(running_var), float(eps), L.ptr(y), int(hardtanh), int(pool), L.ptr(ws), L.stream())
-        ctx.save_for_backward(x, w, b, mean, invstd)
+        if zq is None:
+            ctx.save_for_backward(x, w, b, mean, invstd, None, None)
+        else:
+            ctx.save_for_backward(zq[0], w, b, mean, invstd, zq[1], None)
+        ctx.zq_fmt = 0 if zq is None else zq[2]
+        ctx.shape = (N, C, H, W)
         ctx.hardtanh, ctx.pool = hardtanh, pool
         ctx.training = training
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, b, mean, invstd = ctx.saved_tensors
+        x, w, b, mean, invstd, xbias, _ = ctx.saved_tensors
         dy = dy if dy.is_contiguous() else dy.contiguous()
-        N, C, H, W = x.shape
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dw = torch.empty((C,), dtype=torch.float32, device=x.device) if w is not None else None
-        db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
-        ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=x.device)
+        N, C, H, W = ctx.shape
+        dx = torch.empty((N, C, H, W), dtype=torch.float32, device=dy.device) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((C,), dtype=torch.float32, device=dy.device) if w is not None else None
+        db = torch.empty((C,), dtype=torch.float32, device=dy.device) if b is not None else None
+        ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=dy.device)
         nel = N * C * H * W
-        with _timed("bn2d_bwd", 0, 12 * nel + 8 * dy.numel()):
-            L.call("bnn_bn2d_bwd" if ctx.training else "bnn_bn2d_bwd_eval", L.ptr(x), L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b), L.ptr(mean),
-                   L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
-                   L.stream())
+        xb = 4 if ctx.zq_fmt == 0 else x.element_size()
+        with _timed("bn2d_bwd", 0, (2 * xb + 4) * nel + 8 * dy.numel()):
+            if ctx.zq_fmt:
+                L.call("bnn_bn2d_bwd_q", L.ptr(x), L.ptr(xbias), ctx.zq_fmt, L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b),
+                       L.ptr(mean), L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dx), L.ptr(dw), L.ptr(db),
+                       L.ptr(ws), L.stream())
+            else:
+                L.call("bnn_bn2d_bwd" if ctx.training else "bnn_bn2d_bwd_eval", L.ptr(x), L.ptr(dy), N, C, H, W,
+                       L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dx),
+                       L.ptr(dw), L.ptr(db), L.ptr(ws), L.stream())
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, None)
 
@@ -1405,23 +1478,19 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             invstd = (rv + eps).rsqrt()
         need_dh = any(ctx.needs_input_grad[:3])
         need_dw = ctx.needs_input_grad[8] or zz is not None
-        qf = "fp4" if ctx.fp6 else "i8"
+        # FP6 backward: both GEMMs' B operands (this layer's X_b^T and W_b^T) are written straight in
+        # the FP4 panel layout gemm_fp6 stages from (no panel pass)
+        qf = "fp4p" if ctx.fp6 else "i8"
         q = torch.empty((M, round_up(C, 256) // 2) if fp4 else (M, round_up(C)),
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
-        # the weight gradient's B operand straight in the FP4 panel layout (no panel pass before the
-        # dW GEMM) when the 256x256-tile kernel runs and the GEMM is large enough to be panel-staged
-        ctx.qt_panel = (need_dw and qf == "fp4" and C % 256 == 0 and N * C * round_up(M) >= PANEL_MIN_MACS
-                        and (zz is not None or (C // 256) * ((M + 255) // 256) >= 1024))
-        if ctx.qt_panel:
-            qt = torch.empty(((C + 511) // 512 * 512, round_up(M, 256) // 2), dtype=torch.uint8, device=z.device)
-        else:
-            qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
+        ctx.qt_panel = need_dw and qf == "fp4p"
+        qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
         nx = 4 if zz is None else 2
         with _timed("bn_apply_pack", 0, nx * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
             if zz is None:
                 L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
                        L.ptr(gb), 1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
-                       (2 if ctx.qt_panel else 1) if qf == "fp4" else 0, L.stream())
+                       _QT_CODE[qf], L.stream())
             else:
                 L.call("bnn_bn_apply_pack_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
                        L.ptr(mlo), L.ptr(gw), L.ptr(gb), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1],
@@ -1478,7 +1547,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             db = cs
         if any(ctx.needs_input_grad[:3]):
             if ctx.fp6:
-                dh = gemm_fp6(pre[0] if pre is not None else quant6_rows(dy), wqt, C, k_true=N)   # dY . W_b
+                dh = gemm_fp6(pre[0] if pre is not None else quant6_rows(dy), None, C, k_true=N,
+                              panels=wqt, panel_ks=wqt.shape[1] // 32)                   # dY . W_b
             else:
                 d, s = quant_rows(dy)
                 dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)

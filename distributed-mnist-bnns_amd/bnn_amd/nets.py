@@ -139,10 +139,12 @@ class BinCNN(nn.Module):
 
     def _layer(self, seq, x):
         conv, bn, ht, pool = seq
-        z = conv(x)
-        if (self.fused_bn and BF.bn2d_fusable(z, 2) and isinstance(bn, nn.BatchNorm2d)
-                and pool.kernel_size == 2 and pool.stride == 2 and pool.padding == 0 and not pool.ceil_mode
-                and ht.min_val == -1.0 and ht.max_val == 1.0):
+        fuse = (self.fused_bn and isinstance(bn, nn.BatchNorm2d) and pool.kernel_size == 2 and pool.stride == 2
+                and pool.padding == 0 and not pool.ceil_mode and ht.min_val == -1.0 and ht.max_val == 1.0)
+        # training-mode fused layers take the conv output as its exact integer sums (int8 / int16 +
+        # bias: 1/4 or 1/2 the bytes of every BatchNorm2d pass over it)
+        z = conv(x, emit_compact=fuse and bn.training)
+        if fuse and BF.bn2d_fusable(z, 2):
             return BF.batch_norm2d_hardtanh_pool(z, bn, hardtanh=True, pool=2)
         return pool(ht(bn(z)))
 

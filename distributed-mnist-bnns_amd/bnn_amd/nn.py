@@ -130,7 +130,9 @@ class BinarizeConv2d(nn.Conv2d):
         if isinstance(self.padding, str):
             raise NotImplementedError("BinarizeConv2d: string padding is not supported")
 
-    def forward(self, input):
+    def forward(self, input, emit_compact=False):
+        # emit_compact (the build's fused BinCNN only): the output may travel as its exact int8 /
+        # int16 sums + bias to a libbnn BatchNorm2d (functional.binary_conv2d)
         binarize = input.size(1) != 3                         # :94
         if binarize and self.mutate_input:
             input.data = BF.sign(input.data)                    # :95
@@ -139,4 +141,4 @@ class BinarizeConv2d(nn.Conv2d):
             if self.bias is not None:
                 self.bias.org = self.bias.data.clone()          # :104
         return BF.binary_conv2d(input, self.weight, self.bias, binarize, self.stride, self.padding,
-                                self.dilation, self.groups)
+                                self.dilation, self.groups, emit_compact=emit_compact)

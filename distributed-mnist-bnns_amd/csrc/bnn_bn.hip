@@ -1116,10 +1116,61 @@ __device__ __forceinline__ Win bn2_window(float2 top, float2 bot, const Bn2Chan&
   return w;
 }
 
+// The NCHW input of a BatchNorm2d pass: fp32 (XF 0), or (XF 1 / 2) the int8 / int16 exact sums I of
+// the binary convolution that produced it (bnn_conv2d_fwd_q) plus its per-channel bias, read as
+// x = fl(I + bias[c]) -- the value the conv's fp32 epilogue stores, so every result is bit-identical,
+// at 1/4 (conv1: |I| <= 25) or 1/2 the bytes of every pass.
+struct X2 {
+  const void* p;
+  const float* bias;
+};
+
+template <int XF>
+__device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
+  return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
+}
+
+// 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
+template <int XF>
+__device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
+  } else if constexpr (XF == 1) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
+                       (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    return make_float4((float)(int16_t)(u.x & 0xFFFF) + b, (float)(int16_t)(u.x >> 16) + b,
+                       (float)(int16_t)(u.y & 0xFFFF) + b, (float)(int16_t)(u.y >> 16) + b);
+  }
+}
+
+// 2 consecutive elements (idx even)
+template <int XF>
+__device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) {
+    return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
+  } else if constexpr (XF == 1) {
+    const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
+  } else {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    return make_float2((float)(int16_t)(u & 0xFFFF) + b, (float)(int16_t)(u >> 16) + b);
+  }
+}
+
+template <int XF>
+__device__ __forceinline__ float x2_ld1(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) return reinterpret_cast<const float*>(x.p)[idx];
+  else if constexpr (XF == 1) return (float)reinterpret_cast<const int8_t*>(x.p)[idx] + b;
+  else return (float)reinterpret_cast<const int16_t*>(x.p)[idx] + b;
+}
+
 // MODE 0: chunk (mean, M2) of x.  MODE 1: chunk (sum g, sum g*xhat), g = masked full-resolution
 // gradient (POOL: routed to the window argmax from the pooled dy).
-template <int MODE, int POOL>
-__global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__ x, const float* __restrict__ dy,
+template <int MODE, int POOL, int XF = 0>
+__global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(X2 x, const float* __restrict__ dy,
                                                        int64_t N, int64_t C, int H, int W, int64_t CR,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
@@ -1129,15 +1180,16 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__
   const int64_t c = blockIdx.x, r = blockIdx.y;
   const int64_t n0 = r * CR, n1 = (n0 + CR < N) ? n0 + CR : N;
   const int64_t HW = (int64_t)H * W;
+  const float xb = x2_bias<XF>(x, c);
   double a = 0.0, b = 0.0;
   float fa = 0.f, fb = 0.f;
   int cnt = 0;
   if (MODE == 0) {
-    const float shift = x[(n0 * C + c) * HW];
+    const float shift = x2_ld1<XF>(x, (n0 * C + c) * HW, xb);
     const int64_t hw4 = HW / 4, total = (n1 - n0) * hw4;
     for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
       const int64_t n = n0 + i / hw4, j = i - (i / hw4) * hw4;
-      const float4 v = ld4(x + (n * C + c) * HW + 4 * j);
+      const float4 v = x2_ld4<XF>(x, (n * C + c) * HW + 4 * j, xb);
       const float d[4] = {v.x - shift, v.y - shift, v.z - shift, v.w - shift};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1168,9 +1220,8 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__
     for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
       const int64_t n = n0 + i / pp, p = i - (i / pp) * pp;
       const int ph = (int)(p / PW), pw = (int)(p - (int64_t)ph * PW);
-      const float* xp = x + (n * C + c) * HW + (int64_t)(2 * ph) * W + 2 * pw;
-      const Win w = bn2_window(*reinterpret_cast<const float2*>(xp), *reinterpret_cast<const float2*>(xp + W),
-                               k, hardtanh);
+      const int64_t xo = (n * C + c) * HW + (int64_t)(2 * ph) * W + 2 * pw;
+      const Win w = bn2_window(x2_ld2<XF>(x, xo, xb), x2_ld2<XF>(x, xo + W, xb), k, hardtanh);
       const float yv = w.y[w.arg];
       const float g = (!hardtanh || (yv > -1.f && yv < 1.f)) ? dy[(n * C + c) * pp + p] : 0.f;
       fa += g;
@@ -1187,7 +1238,7 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__
     for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
       const int64_t n = n0 + i / hw4, j = i - (i / hw4) * hw4;
       const int64_t o = (n * C + c) * HW + 4 * j;
-      const float4 xv = ld4(x + o), gv = ld4(dy + o);
+      const float4 xv = x2_ld4<XF>(x, o, xb), gv = ld4(dy + o);
       const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1215,8 +1266,8 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(const float* __restrict__
 }
 
 // Forward apply: y = clamp((x-mean)*invstd*gamma+beta) (POOL: max over each 2x2 window).
-template <int POOL>
-__global__ __launch_bounds__(256) void bn2d_apply_k(const float* __restrict__ x, int64_t N, int64_t C, int H, int W,
+template <int POOL, int XF = 0>
+__global__ __launch_bounds__(256) void bn2d_apply_k(X2 x, int64_t N, int64_t C, int H, int W,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ invstd,
                                                     const float* __restrict__ gamma,
@@ -1230,17 +1281,19 @@ __global__ __launch_bounds__(256) void bn2d_apply_k(const float* __restrict__ x,
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
       const int64_t plane = i / pp, p = i - plane * pp;
       const int ph = (int)(p / PW), pw = (int)(p - (int64_t)ph * PW);
-      const Bn2Chan k = bn2_chan(plane % C, mean, invstd, gamma, beta);
-      const float* xp = x + plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
-      y[i] = bn2_window(*reinterpret_cast<const float2*>(xp), *reinterpret_cast<const float2*>(xp + W), k,
-                        hardtanh).out;
+      const int64_t c = plane % C;
+      const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+      const float xb = x2_bias<XF>(x, c);
+      const int64_t xo = plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
+      y[i] = bn2_window(x2_ld2<XF>(x, xo, xb), x2_ld2<XF>(x, xo + W, xb), k, hardtanh).out;
     }
     return;
   }
   const int64_t n4 = N * C * HW / 4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const Bn2Chan k = bn2_chan(((4 * i) / HW) % C, mean, invstd, gamma, beta);
-    const float4 xv = ld4(x + 4 * i);
+    const int64_t c = ((4 * i) / HW) % C;
+    const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+    const float4 xv = x2_ld4<XF>(x, 4 * i, x2_bias<XF>(x, c));
     float v[4] = {fmaf((xv.x - k.mu) * k.is, k.ga, k.be), fmaf((xv.y - k.mu) * k.is, k.ga, k.be),
                   fmaf((xv.z - k.mu) * k.is, k.ga, k.be), fmaf((xv.w - k.mu) * k.is, k.ga, k.be)};
     if (hardtanh) {
@@ -1252,8 +1305,8 @@ __global__ __launch_bounds__(256) void bn2d_apply_k(const float* __restrict__ x,
 }
 
 // Backward apply: dx = gamma*invstd*(g - sum_g/n - xhat*sum_gxhat/n), g routed/masked as in reduce.
-template <int POOL>
-__global__ __launch_bounds__(256) void bn2d_bwd_apply_k(const float* __restrict__ x, const float* __restrict__ dy,
+template <int POOL, int XF = 0>
+__global__ __launch_bounds__(256) void bn2d_bwd_apply_k(X2 x, const float* __restrict__ dy,
                                                         int64_t N, int64_t C, int H, int W,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd,
@@ -1274,8 +1327,8 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_k(const float* __restrict_
       const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
       const float m0 = sg[c] * inv_n, m1 = sgx[c] * inv_n, sc = k.ga * k.is;
       const int64_t off = plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
-      const Win w = bn2_window(*reinterpret_cast<const float2*>(x + off),
-                               *reinterpret_cast<const float2*>(x + off + W), k, hardtanh);
+      const float xb = x2_bias<XF>(x, c);
+      const Win w = bn2_window(x2_ld2<XF>(x, off, xb), x2_ld2<XF>(x, off + W, xb), k, hardtanh);
       const float gp = dy[i];
       float o[4];
 #pragma unroll
@@ -1293,7 +1346,7 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_k(const float* __restrict_
     const int64_t c = ((4 * i) / HW) % C;
     const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
     const float m0 = sg[c] * inv_n, m1 = sgx[c] * inv_n, sc = k.ga * k.is;
-    const float4 xv = ld4(x + 4 * i), gv = ld4(dy + 4 * i);
+    const float4 xv = x2_ld4<XF>(x, 4 * i, x2_bias<XF>(x, c)), gv = ld4(dy + 4 * i);
     const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
     float o[4];
 #pragma unroll
@@ -1707,13 +1760,20 @@ BNN_API int64_t bnn_bn2d_workspace(int64_t N, int64_t C) {
 
 #define BN2_POOL_SWITCH(pool, ...) \
   do { if (pool) { constexpr int P = 2; __VA_ARGS__; } else { constexpr int P = 0; __VA_ARGS__; } } while (0)
+#define BN2_XF_SWITCH(xf, ...)                                               \
+  do {                                                                       \
+    if ((xf) == 1) { constexpr int XFV = 1; __VA_ARGS__; }                   \
+    else if ((xf) == 2) { constexpr int XFV = 2; __VA_ARGS__; }              \
+    else { constexpr int XFV = 0; __VA_ARGS__; }                             \
+  } while (0)
 
-BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, float momentum,
                                float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
                                int32_t pool, void* work, void* stream) {
-  if (!bn2_args_ok(x, N, C, H, W, pool) || !save_mean || !save_invstd || !work || !y ||
-      (running_mean == nullptr) != (running_var == nullptr)) {
+  if (!bn2_args_ok(reinterpret_cast<const float*>(x.p), N, C, H, W, pool) || !save_mean || !save_invstd || !work ||
+      !y || (running_mean == nullptr) != (running_var == nullptr) || xf < 0 || xf > 2 || (xf == 0 && x.bias) ||
+      (x.bias && !aligned16(x.bias))) {
     set_error("bnn_bn2d_fwd_train: bad arguments (N=%lld C=%lld H=%lld W=%lld pool=%d; H*W must be a multiple "
               "of 4, pool 0 or 2 with even H, W)", (long long)N, (long long)C, (long long)H, (long long)W, pool);
     return kErrInval;
@@ -1722,14 +1782,36 @@ BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, 
   const int64_t CR = bn2_chunk_images(N, C), R = (N + CR - 1) / CR;
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
-  hipLaunchKernelGGL((bn2d_reduce_k<0, 0>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s, x, nullptr, N, C,
-                     (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0, p1);
+  BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_reduce_k<0, 0, XFV>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s,
+                                       x, nullptr, N, C, (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0,
+                                       p1));
   hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
-  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
-                                           (int)W, save_mean, save_invstd, gamma, beta, hardtanh, y));
+  BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_apply_k<P, XFV>), dim3(grid_for(outs)), dim3(256),
+                                                             0, s, x, N, C, (int)H, (int)W, save_mean, save_invstd,
+                                                             gamma, beta, hardtanh, y)));
   return check_launch("bnn_bn2d_fwd_train");
+}
+
+BNN_API int bnn_bn2d_fwd_train(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, float momentum,
+                               float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
+                               int32_t pool, void* work, void* stream) {
+  return bn2d_fwd_train_impl(X2{x, nullptr}, 0, N, C, H, W, gamma, beta, running_mean, running_var, momentum, eps,
+                             save_mean, save_invstd, y, hardtanh, pool, work, stream);
+}
+
+BNN_API int bnn_bn2d_fwd_train_q(const void* xq, const float* xbias, int32_t xfmt, int64_t N, int64_t C, int64_t H,
+                                 int64_t W, const float* gamma, const float* beta, float* running_mean,
+                                 float* running_var, float momentum, float eps, float* save_mean, float* save_invstd,
+                                 float* y, int32_t hardtanh, int32_t pool, void* work, void* stream) {
+  if (xfmt != 1 && xfmt != 2) {
+    set_error("bnn_bn2d_fwd_train_q: xfmt must be 1 (int8) or 2 (int16)");
+    return kErrInval;
+  }
+  return bn2d_fwd_train_impl(X2{xq, xbias}, xfmt, N, C, H, W, gamma, beta, running_mean, running_var, momentum, eps,
+                             save_mean, save_invstd, y, hardtanh, pool, work, stream);
 }
 
 BNN_API int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
@@ -1743,17 +1825,18 @@ BNN_API int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, i
   float* istd = reinterpret_cast<float*>(work);
   hipLaunchKernelGGL(bn_invstd_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_var, istd, C, eps);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
-  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, N, C, (int)H,
-                                           (int)W, running_mean, istd, gamma, beta, hardtanh, y));
+  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_apply_k<P, 0>), dim3(grid_for(outs)), dim3(256), 0, s, X2{x, nullptr},
+                                           N, C, (int)H, (int)W, running_mean, istd, gamma, beta, hardtanh, y));
   return check_launch("bnn_bn2d_fwd_eval");
 }
 
-static int bn2d_bwd_impl(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
+static int bn2d_bwd_impl(X2 x, int xf, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
                          const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                          int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                          void* stream, bool batch_stats) {
-  if (!bn2_args_ok(x, N, C, H, W, pool) || !dy || !save_mean || !save_invstd || !work ||
-      (dx && !aligned16(dx)) || (!pool && !aligned16(dy))) {
+  if (!bn2_args_ok(reinterpret_cast<const float*>(x.p), N, C, H, W, pool) || !dy || !save_mean || !save_invstd ||
+      !work || (dx && !aligned16(dx)) || (!pool && !aligned16(dy)) || xf < 0 || xf > 2 || (xf == 0 && x.bias) ||
+      (x.bias && !aligned16(x.bias))) {
     set_error("bnn_bn2d_bwd: bad arguments");
     return kErrInval;
   }
@@ -1763,17 +1846,17 @@ static int bn2d_bwd_impl(const float* x, const float* dy, int64_t N, int64_t C, 
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
-                                           s, x, dy, N, C, (int)H, (int)W, CR, save_mean, save_invstd, gamma, beta,
-                                           hardtanh, p0, p1));
+  BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P, XFV>), dim3((unsigned)C, (unsigned)R),
+                                                             dim3(BN2_T), 0, s, x, dy, N, C, (int)H, (int)W, CR,
+                                                             save_mean, save_invstd, gamma, beta, hardtanh, p0, p1)));
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
     const float inv_n = batch_stats ? (float)(1.0 / ((double)N * (double)(H * W))) : 0.f;
-    BN2_POOL_SWITCH(pool, hipLaunchKernelGGL(bn2d_bwd_apply_k<P>, dim3(grid_for(outs)), dim3(256), 0, s, x, dy, N,
-                                             C, (int)H, (int)W, save_mean, save_invstd, gamma, beta, hardtanh, k0,
-                                             k1, inv_n, dx));
+    BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_bwd_apply_k<P, XFV>), dim3(grid_for(outs)),
+                                                               dim3(256), 0, s, x, dy, N, C, (int)H, (int)W, save_mean,
+                                                               save_invstd, gamma, beta, hardtanh, k0, k1, inv_n, dx)));
   }
   return check_launch("bnn_bn2d_bwd");
 }
@@ -1782,14 +1865,26 @@ BNN_API int bnn_bn2d_bwd(const float* x, const float* dy, int64_t N, int64_t C, 
                          const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                          int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                          void* stream) {
-  return bn2d_bwd_impl(x, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool, dx, dgamma, dbeta,
-                       work, stream, true);
+  return bn2d_bwd_impl(X2{x, nullptr}, 0, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool, dx,
+                       dgamma, dbeta, work, stream, true);
+}
+
+BNN_API int bnn_bn2d_bwd_q(const void* xq, const float* xbias, int32_t xfmt, const float* dy, int64_t N, int64_t C,
+                           int64_t H, int64_t W, const float* gamma, const float* beta, const float* save_mean,
+                           const float* save_invstd, int32_t hardtanh, int32_t pool, float* dx, float* dgamma,
+                           float* dbeta, void* work, void* stream) {
+  if (xfmt != 1 && xfmt != 2) {
+    set_error("bnn_bn2d_bwd_q: xfmt must be 1 (int8) or 2 (int16)");
+    return kErrInval;
+  }
+  return bn2d_bwd_impl(X2{xq, xbias}, xfmt, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool, dx,
+                       dgamma, dbeta, work, stream, true);
 }
 
 BNN_API int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
                               const float* gamma, const float* beta, const float* running_mean, const float* invstd,
                               int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                               void* stream) {
-  return bn2d_bwd_impl(x, dy, N, C, H, W, gamma, beta, running_mean, invstd, hardtanh, pool, dx, dgamma, dbeta,
-                       work, stream, false);
+  return bn2d_bwd_impl(X2{x, nullptr}, 0, dy, N, C, H, W, gamma, beta, running_mean, invstd, hardtanh, pool, dx,
+                       dgamma, dbeta, work, stream, false);
 }

@@ -8,6 +8,8 @@
 // this a latency/L2-bound kernel; the int8-MFMA implicit-GEMM form is the next step.
 #include <algorithm>
 
+#include <type_traits>
+
 #include "bnn_common.h"
 
 namespace bnn {
@@ -288,11 +290,19 @@ __global__ __launch_bounds__(TILE_T) void conv_fwd_bin_tile_k(const float* __res
 // window of row kh starts at byte b = (oh+kh)*Wq + ow: the KWG+1 dwords from b/4 and
 // v_alignbyte give its taps in order; bytes past KW meet zero weight bytes.  Integer sums, so
 // bit-identical to conv_fwd_bin_tile_k.
-template <int CO, int KWG>
+// OT = float: y = sum + bias; int8_t / int16_t (bnn_conv2d_fwd_q): the exact sum alone, the bias
+// added by the consumer (fl(I + bias) = the fp32 value).
+template <typename OT>
+__device__ __forceinline__ OT conv_out(int acc, const float* bias, int co) {
+  if constexpr (std::is_same<OT, float>::value) return (float)acc + (bias ? bias[co] : 0.f);
+  else return (OT)acc;
+}
+
+template <int CO, int KWG, typename OT = float>
 __global__ __launch_bounds__(TILE_T) void conv_fwd_bin_c1_k(const float* __restrict__ x,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
-                                                            float* __restrict__ y, TileGeo g, int Wq) {
+                                                            OT* __restrict__ y, TileGeo g, int Wq) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   int* ws = lds;                                   // [KH][KWG][CO]
   int* xw = lds + g.KH * KWG * CO;                 // [Hp][Wq / 4] words of sign bytes
@@ -345,10 +355,10 @@ __global__ __launch_bounds__(TILE_T) void conv_fwd_bin_c1_k(const float* __restr
         for (int co = 0; co < CO; ++co) acc[co] = __builtin_amdgcn_sdot4(xv, wr[kg * CO + co], acc[co], false);
       }
     }
-    float* yp = y + (int64_t)n * g.Co * g.OH * g.OW + p;
+    OT* yp = y + (int64_t)n * g.Co * g.OH * g.OW + p;
 #pragma unroll
     for (int co = 0; co < CO; ++co)
-      if (co < g.Co) yp[(int64_t)co * g.OH * g.OW] = (float)acc[co] + (bias ? bias[co] : 0.f);
+      if (co < g.Co) yp[(int64_t)co * g.OH * g.OW] = conv_out<OT>(acc[co], bias, co);
   }
 }
 
@@ -1197,9 +1207,9 @@ struct MfFwd {
 constexpr int FW_IPB = 8;    // samples per forward workgroup (the weight staging amortises)
 constexpr int FW_PX = 16;    // per-thread register slots of the next sample's input
 
-template <int COT>
+template <int COT, typename OT = float>
 __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restrict__ x, const float* __restrict__ w,
-                                                          const float* __restrict__ bias, float* __restrict__ y,
+                                                          const float* __restrict__ bias, OT* __restrict__ y,
                                                           int64_t N, MfFwd g) {
   extern __shared__ __attribute__((aligned(16))) float ldsf[];
   int8_t* ws = reinterpret_cast<int8_t*>(ldsf);                 // [COT*16][KCp*16]
@@ -1285,7 +1295,7 @@ __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restric
         for (int a = 0; a < COT; ++a)
           acc[a][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bv[m], acc[a][m], 0, 0, 0);
     }
-    float* yn = y + n * g.Co * OHW;
+    OT* yn = y + n * g.Co * OHW;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       if (m >= my_tiles) continue;
@@ -1296,7 +1306,7 @@ __global__ __launch_bounds__(MF_T) void conv_fwd_i8mfma_k(const float* __restric
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = a * 16 + 4 * h + r;
-          if (co < g.Co) yn[(int64_t)co * OHW + pix] = (float)acc[a][m][r] + (bias ? bias[co] : 0.f);
+          if (co < g.Co) yn[(int64_t)co * OHW + pix] = conv_out<OT>(acc[a][m][r], bias, co);
         }
     }
   }
@@ -1504,6 +1514,66 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
   }
   hipLaunchKernelGGL(conv_fwd_k, dim3(grid_for(total)), dim3(256), 0, st, x, binarize_input, w_latent, bias, y, s);
   return check_launch("bnn_conv2d_fwd");
+}
+
+template <typename OT>
+static void launch_c1_q(const ConvShape& s, const float* x, const float* w_latent, OT* y, hipStream_t st) {
+  const TileGeo g = geo(s);
+  const int Wq = (int)round_up(g.Wp, 4), kwg = s.KW <= 4 ? 1 : 2;
+  const size_t lds = (size_t)(s.KH * kwg * pick_co(s.Co) * 4 + g.Hp * Wq + 16);
+  const dim3 grid((unsigned)s.N);
+#define BNN_C1Q(CO_, KG_) \
+  BNN_TILE_LAUNCH((conv_fwd_bin_c1_k<CO_, KG_, OT>), grid, dim3(TILE_T), lds, st, x, w_latent, nullptr, y, g, Wq)
+  switch (pick_co(s.Co) * 4 + kwg) {
+    case 8 * 4 + 1: BNN_C1Q(8, 1); break;
+    case 8 * 4 + 2: BNN_C1Q(8, 2); break;
+    case 16 * 4 + 1: BNN_C1Q(16, 1); break;
+    case 16 * 4 + 2: BNN_C1Q(16, 2); break;
+    case 32 * 4 + 1: BNN_C1Q(32, 1); break;
+    case 32 * 4 + 2: BNN_C1Q(32, 2); break;
+    case 64 * 4 + 1: BNN_C1Q(64, 1); break;
+    default: BNN_C1Q(64, 2); break;
+  }
+#undef BNN_C1Q
+}
+
+// The binary-input forward writing the exact integer sums (no bias) as int8 (yfmt 1: C*KH*KW <= 127)
+// or int16 (yfmt 2: <= 32767) for a BatchNorm2d that reads fl(I + bias) (bnn_bn2d_*_q): the
+// int8-MFMA kernel (C % 16 == 0) or the single-channel dot4 kernel; other shapes are refused.
+BNN_API int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int32_t yfmt, int64_t N, int64_t C,
+                             int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
+                             int32_t dil, int32_t groups, void* stream) {
+  ConvShape s;
+  if (!x || !w_latent || !y || (yfmt != 1 && yfmt != 2) || !make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s) ||
+      C * KH * KW > (yfmt == 1 ? 127 : 32767)) {
+    set_error("bnn_conv2d_fwd_q: bad arguments (yfmt 1 needs C*KH*KW <= 127, 2 <= 32767)");
+    return kErrInval;
+  }
+  if (N * Co * s.OH * s.OW == 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  MfFwd mf;
+  int64_t mlds = 0;
+#define BNN_QOUT(OT_, ...) do { if (yfmt == 1) { using OT_ = int8_t; __VA_ARGS__; } else { using OT_ = int16_t; __VA_ARGS__; } } while (0)
+  if (g_conv_mfma && mf_fwd_geom(s, &mf, &mlds)) {
+    const size_t lds = (size_t)mlds;
+    const dim3 grid((unsigned)((N + FW_IPB - 1) / FW_IPB));
+    const int cot = (mf.Co + 15) / 16;
+    BNN_QOUT(OT, {
+      OT* yo = reinterpret_cast<OT*>(y);
+      if (cot == 1) BNN_TILE_LAUNCH((conv_fwd_i8mfma_k<1, OT>), grid, dim3(MF_T), lds, st, x, w_latent, nullptr, yo, N, mf);
+      else if (cot == 2) BNN_TILE_LAUNCH((conv_fwd_i8mfma_k<2, OT>), grid, dim3(MF_T), lds, st, x, w_latent, nullptr, yo, N, mf);
+      else BNN_TILE_LAUNCH((conv_fwd_i8mfma_k<4, OT>), grid, dim3(MF_T), lds, st, x, w_latent, nullptr, yo, N, mf);
+    });
+    return check_launch("bnn_conv2d_fwd_q");
+  }
+  if (g_conv_mfma && s.C == 1 && s.KW <= 8 && tile_geom_ok(s)) {
+    if (yfmt == 1) launch_c1_q<int8_t>(s, x, w_latent, reinterpret_cast<int8_t*>(y), st);
+    else launch_c1_q<int16_t>(s, x, w_latent, reinterpret_cast<int16_t*>(y), st);
+    return check_launch("bnn_conv2d_fwd_q");
+  }
+#undef BNN_QOUT
+  set_error("bnn_conv2d_fwd_q: no compact-output kernel for this shape (C %% 16 == 0 up to 64, or C == 1)");
+  return kErrInval;
 }
 
 BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* dx, int64_t N,

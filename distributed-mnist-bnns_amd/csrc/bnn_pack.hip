@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
                                                         int rtiles = 1, int64_t ntiles_y = 0,
                                                         AdamArgs ad = {}, int qt4 = 0) {
   // qt4 = 1: the transpose is written as FP4 nibbles (qt rows of ldqt BYTES, element m in byte
-  // m/2), the B operand of the FP6 digit GEMMs (bnn_gemm6.hip); else int8 (rows of ldqt elements)
+  // m/2), the B operand of the FP6 digit GEMMs (bnn_gemm6.hip); 2: the same nibbles in that GEMM's
+  // panel layout ([K/512][ldqt/32][512][32 B], bnn_fp4_panelize); else int8 (rows of ldqt elements)
   // rtiles > 1: the workgroup walks rtiles vertically adjacent 64x64 tiles of its column block
   // (the per-column BatchNorm parameters are loaded once per workgroup, not once per tile)
   __shared__ int tile[TILE][TILE + 1];
@@ -194,7 +195,10 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
           lo |= fp4_code(tile[mc + j][kk]) << (4 * j);
           hi |= fp4_code(tile[mc + 8 + j][kk]) << (4 * j);
         }
-        *reinterpret_cast<uint2*>(qt + k * ldqt + (m0 + mc) / 2) = make_uint2(lo, hi);
+        const int64_t m = m0 + mc;
+        int8_t* dst = qt4 == 2 ? qt + ((k >> 9) * (ldqt / 32) + (m >> 6)) * 16384 + (k & 511) * 32 + (m & 63) / 2
+                               : qt + k * ldqt + m / 2;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
       }
     } else if (k < K && m0 + mc < ldqt) {
       int g[16];
@@ -764,12 +768,12 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // 64-row tiles the grid must cover so every padding element is written.
 bool qt_ok(const int8_t* qt, int64_t M, int64_t ldqt, int qt_fmt) {
   if (!qt) return true;
-  if (!aligned16(qt) || (qt_fmt != 0 && qt_fmt != 1)) return false;
-  return qt_fmt == 1 ? (ldqt % 128 == 0 && 2 * ldqt >= round_up(M, 256))
+  if (!aligned16(qt) || qt_fmt < 0 || qt_fmt > 2) return false;
+  return qt_fmt >= 1 ? (ldqt % 128 == 0 && 2 * ldqt >= round_up(M, 256))
                      : (ldqt % TILE == 0 && ldqt >= round_up(M, TILE));
 }
 
-int64_t qt_tiles(int64_t ldqt, int qt_fmt) { return (qt_fmt == 1 ? 2 * ldqt : ldqt) / TILE; }
+int64_t qt_tiles(int64_t ldqt, int qt_fmt) { return (qt_fmt >= 1 ? 2 * ldqt : ldqt) / TILE; }
 
 inline int grid_cap(int64_t want) { return (int)std::max<int64_t>(1, std::min<int64_t>(want, 8192)); }
 
@@ -1018,10 +1022,6 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
   const bool fast = fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && C % AP_T == 0 && af.vec && vec &&
                     (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024;
-  if (qt_fmt == 2 && !fast) {
-    set_error("bnn_bn_apply_pack: the panel transpose (qt_fmt 2) needs FP4 rows, C %% 256 == 0 and >= 1024 tiles");
-    return kErrInval;
-  }
   if (fast) {
     hipLaunchKernelGGL((bn_apply_pack_fp4_k<false>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                        dim3(256), 0, S(stream), XIn{x, nullptr}, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,

@@ -51,7 +51,9 @@ int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, int8_t* 
 /* FP4 form of the ternary rows for bnn_gemm_fp4: q4 [M][ldq4 bytes], ldq4 a multiple of 128 with
  * 2*ldq4 >= round_up(K,256) (zero nibbles beyond K).  qt = the transpose [K][ldqt] for the
  * backward GEMMs: qt_fmt 0 = int8 as in bnn_sign_pack_i8; qt_fmt 1 = FP4 nibbles, ldqt BYTES (a
- * multiple of 128, 2*ldqt >= round_up(M,256)), the B operand of bnn_gemm_fp6. */
+ * multiple of 128, 2*ldqt >= round_up(M,256)), the B operand of bnn_gemm_fp6; qt_fmt 2 = the same
+ * nibbles in the panel layout of bnn_gemm_fp6_panel_ws ([ceil(K/512)][ldqt/32][512][32 B], bks =
+ * ldqt/32; rows beyond K unspecified). */
 int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
                       int8_t* qt, int64_t ldqt, int32_t qt_fmt, bnn_stream_t stream);
 
@@ -216,6 +218,12 @@ int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* w_latent
                    const float* bias, float* y, int64_t N, int64_t C, int64_t H, int64_t W,
                    int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
                    int32_t dil, int32_t groups, bnn_stream_t stream);
+/* The binary-input forward writing the exact sums I (no bias) as int8 (yfmt 1, C*KH*KW <= 127) or
+ * int16 (yfmt 2, <= 32767) for a BatchNorm2d that reads fl(I + bias) (bnn_bn2d_*_q): stride 1,
+ * dilation 1, groups 1, C == 1 (KW <= 8) or C % 16 == 0 (<= 64), Co <= 64; other shapes -1. */
+int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int32_t yfmt, int64_t N, int64_t C, int64_t H,
+                     int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad, int32_t dil,
+                     int32_t groups, bnn_stream_t stream);
 int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* dx, int64_t N, int64_t C,
                         int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride,
                         int32_t pad, int32_t dil, int32_t groups, bnn_stream_t stream);
@@ -295,6 +303,17 @@ int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int
                       const float* gamma, const float* beta, const float* running_mean, const float* invstd,
                       int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                       bnn_stream_t stream);
+/* The same training-mode passes on a compact input: xq = int8 (xfmt 1) or int16 (xfmt 2) sums
+ * [N][C][H][W] of bnn_conv2d_fwd_q, xbias [C] (nullable, 16-B aligned) its bias, read as
+ * x = fl(xq + xbias[c]) -- bit-identical to the fp32 entries on the conv's fp32 output. */
+int bnn_bn2d_fwd_train_q(const void* xq, const float* xbias, int32_t xfmt, int64_t N, int64_t C, int64_t H, int64_t W,
+                         const float* gamma, const float* beta, float* running_mean, float* running_var,
+                         float momentum, float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
+                         int32_t pool, void* work, bnn_stream_t stream);
+int bnn_bn2d_bwd_q(const void* xq, const float* xbias, int32_t xfmt, const float* dy, int64_t N, int64_t C, int64_t H,
+                   int64_t W, const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                   int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
+                   bnn_stream_t stream);
 
 /* nn.Dropout(p) fused in front of BatchNorm1d (+ Hardtanh) (mnist-dist2.py:69-70: fc3 -> drop ->
  * bn3): x is the pre-dropout input; the keep mask is a counter-based hash of (seed, row*C + col)
@@ -350,7 +369,7 @@ int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_
  * (int8, ldq >= round_up(C,64)) or fmt 1 (FP4 nibbles, ldq bytes >= round_up(C,256)/2, multiple
  * of 128) and/or the transpose qt for the weight gradient: qt_fmt 0 int8 [C][ldqt], 1 FP4
  * [C][ldqt bytes], 2 FP4 in the panel layout of bnn_gemm_fp6_panel_ws ([ceil(C/512)][ldqt/32][512]
- * [32 B], bks = ldqt/32; needs fmt 1, C % 256 == 0 and >= 1024 256x256 tiles); no fp32 activation is
+ * [32 B], bks = ldqt/32; rows beyond C unspecified); no fp32 activation is
  * written (Hardtanh keeps the sign; its backward mask is recomputed from x by bnn_bn_bwd). */
 int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                       const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
@@ -421,8 +440,8 @@ int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_s
  * bnn_adam_clamp does (bit-identical p, m, v), and in the same pass sign(p_new) is written as the
  * ternary rows q -- fmt 0: int8 [N][ldq] (ldq multiple of 64 >= round_up(K,64)); fmt 1: FP4
  * nibbles [N][ldq bytes] (ldq multiple of 128, 2*ldq >= round_up(K,256)) -- and/or the int8
- * transpose qt [K][ldqt] (qt_fmt 0: int8, ldqt multiple of 64 >= round_up(N,64); qt_fmt 1: FP4
- * nibbles, ldqt bytes as in bnn_sign_pack_fp4); padding zero-filled, as
+ * transpose qt [K][ldqt] (qt_fmt 0: int8, ldqt multiple of 64 >= round_up(N,64); qt_fmt 1 / 2: FP4
+ * nibbles, ldqt bytes, rows or panels as in bnn_sign_pack_fp4); padding zero-filled, as
  * bnn_sign_pack_i8 / bnn_sign_pack_fp4 of p_new would write them.  q or qt may be NULL (not both).
  * replaces: p.data.copy_(p.org); Adam.step(); p.org.copy_(p.data.clamp_(-1,1)) (mnist-dist2.py:
  * 131-137) and the weight sign of the next forward (binarized_modules.py:79). */

@@ -127,6 +127,22 @@ def test_bn_apply_pack_panel_transpose(F):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,K", [(300, 700), (1536, 3072), (64, 1024)])
+def test_sign_pack_panel_transpose(F, M, K):
+    """qt_fmt "fp4p" of the 64 x 64-tile sign-pack (the weights' W_b^T that the fused Adam re-pack
+    rewrites, and small-batch BatchNorm apply-packs): equal to bnn_fp4_panelize of the row-major
+    FP4 transpose on every row < K."""
+    x = torch.randn(M, K, device="cuda")
+    x[3, :7] = 0.0
+    _, qt_rows = F.sign_pack_fp4(x, want_qt=True, qt_fmt="fp4")
+    _, qt_pan = F.sign_pack_fp4(x, want_qt=True, qt_fmt="fp4p")
+    ref = host(F.fp4_panels(qt_rows, K, 2 * qt_rows.shape[1])).reshape((K + 511) // 512, -1, 512, 32)
+    got = host(qt_pan).reshape(ref.shape)
+    live = np.arange((K + 511) // 512 * 512).reshape(-1, 1, 512, 1) < K
+    live = np.broadcast_to(live.reshape((K + 511) // 512, 1, 512, 1), ref.shape)
+    assert np.array_equal(got[live], ref[live])
+
+
 def _apply_pack_case(F, M, C, fmt, with_qt):
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M * 7 + C + fmt)

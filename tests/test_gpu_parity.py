@@ -496,6 +496,55 @@ def test_fused_cnn_step_matches_torch_modules(F):
         assert close(host(ba), host(bb), 1e-5, 1e-6), n
 
 
+@pytest.mark.parametrize("shape", [(37, 1, 28, 28, 16, 5, 2), (19, 16, 14, 14, 32, 5, 2), (5, 32, 8, 8, 24, 3, 1)])
+def test_conv_fwd_compact_sums(F, shape):
+    """bnn_conv2d_fwd_q writes the exact binary-conv sums as int8 (C*KH*KW <= 127) / int16: adding
+    the bias in fp32 reproduces bnn_conv2d_fwd's fp32 output bit for bit (the BinCNN's conv1 / conv2
+    and a 3x3 shape)."""
+    from bnn_amd import _lib as L
+    N, C, H, W, Co, K, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(N * C)
+    x = torch.randn(N, C, H, W, generator=g, device="cuda")
+    x[0, 0, 3, :5] = 0.0                                  # exact zeros: sign 0
+    w = torch.randn(Co, C, K, K, generator=g, device="cuda")
+    b = torch.randn(Co, generator=g, device="cuda")
+    y = torch.empty(N, Co, H + 2 * pad - K + 1, W + 2 * pad - K + 1, device="cuda")
+    L.call("bnn_conv2d_fwd", L.ptr(x), 1, L.ptr(w), L.ptr(b), L.ptr(y), N, C, H, W, Co, K, K, 1, pad, 1, 1, L.stream())
+    fmt = 1 if C * K * K <= 127 else 2
+    yq = torch.empty(y.shape, dtype=torch.int8 if fmt == 1 else torch.int16, device="cuda")
+    L.call("bnn_conv2d_fwd_q", L.ptr(x), L.ptr(w), L.ptr(yq), fmt, N, C, H, W, Co, K, K, 1, pad, 1, 1, L.stream())
+    assert torch.equal(yq.float() + b.view(1, -1, 1, 1), y)
+
+
+def test_fused_cnn_compact_outputs_bit_identical(F):
+    """The fused BinCNN with its conv outputs travelling as int8 (conv1) / int16 (conv2) sums + bias
+    (functional.ZQ) against the same net with fp32 conv outputs: loss, every gradient and the
+    BatchNorm running buffers bit-identical, two hand-offs per forward."""
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    torch.manual_seed(6)
+    a = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    b = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    b.load_state_dict(a.state_dict())
+    x, y = synthetic_mnist(200, seed=9, device="cuda")
+    try:
+        F.ZQ = False
+        la = torch.nn.functional.cross_entropy(a(x), y)
+        la.backward()
+        F.ZQ = True
+        n0 = F.ZQ_HANDOFFS
+        lb = torch.nn.functional.cross_entropy(b(x), y)
+        lb.backward()
+        assert F.ZQ_HANDOFFS - n0 == 2
+    finally:
+        F.ZQ = True
+    assert la.item() == lb.item()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad), n
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(ba, bb), n
+
+
 def test_fused_mlp_step_matches_unfused(F):
     """The build's trainer path (fused BN+Hardtanh, latent Adam) against the drop-in path
     (torch BatchNorm1d/Hardtanh, torch Adam + .org protocol) on one step, dropout off."""
