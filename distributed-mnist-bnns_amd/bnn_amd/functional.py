@@ -799,7 +799,7 @@ def _pair_same(v, what):
 
 # Compact conv outputs (zq): a binary-input BinarizeConv2d computes exact integer sums I (|I| <=
 # C*KH*KW: 25 for the BinCNN's first layer, 400 for its second) plus a per-channel bias, so when
-# its only consumer is the fused BatchNorm2d it travels as int8 / int16 sums + the bias
+# its only consumer is the fused BatchNorm2d it travels as int16 sums + the bias
 # (bnn_conv2d_fwd_q; bnn_bn2d_*_q read fl(I + bias), bit-identical to the fp32 output) -- a stride-0
 # placeholder of the output shape carries them, as the MLP's z16 does.
 ZQ = True
@@ -818,8 +818,10 @@ def _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, pad):
         return 0
     if not (C == 1 and KW <= 8) and not (C % 16 == 0 and C <= 64):
         return 0
-    n = C * KH * KW
-    return 1 if n <= 127 else (2 if n <= 32767 else 0)
+    # int16 even where int8 would hold the sums (the first layer's |I| <= 25): the pooled BatchNorm2d
+    # passes read 2 elements per lane, and 2-byte loads made them slower than on fp32 (int8 conv1:
+    # apply 33 -> 46 us, backward 115 -> 139 us; int16 conv2: backward 115 -> 78 us, tools/gpu_r03_q6b.sh)
+    return 2 if C * KH * KW <= 32767 else 0
 
 
 class BinaryConv2dFunction(torch.autograd.Function):

@@ -668,8 +668,10 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   // block maxima formed in the dz phase (|dz| bits, unsigned max: abs_bits / q6_block_pre) by LDS
   // atomics -- rmax[b][row] over the row's 32 columns of block b, cmax[b][col] over the column's 32
   // rows of block b -- so a quantising lane reads its block once; it zeroes its entry for the next
-  // sub-tile.  The sub-tile's digit records are staged in LDS (Q6Stage) and written out as whole
-  // lines by all 256 threads.
+  // sub-tile.  (Shuffle reductions + plain stores instead measured no faster and pushed the head
+  // variant into spills: ab/r03_q6_noatomics_bn2d_byrow.patch, tools/gpu_r03_q6b.sh.)  The
+  // sub-tile's digit records are staged in LDS (Q6Stage) and written out as whole lines by all 256
+  // threads.
   __shared__ uint32_t rmax[2][Q6T_SUB], cmax[2][Q6T_COLS];
   __shared__ __attribute__((aligned(16))) Q6Stage st;
   if (t < 2 * Q6T_SUB) rmax[t >> 6][t & 63] = 0u;
@@ -1186,21 +1188,32 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(X2 x, const float* __rest
   int cnt = 0;
   if (MODE == 0) {
     const float shift = x2_ld1<XF>(x, (n0 * C + c) * HW, xb);
-    const int64_t hw4 = HW / 4, total = (n1 - n0) * hw4;
-    for (int64_t i = threadIdx.x; i < total; i += BN2_T) {
-      const int64_t n = n0 + i / hw4, j = i - (i / hw4) * hw4;
-      const float4 v = x2_ld4<XF>(x, (n * C + c) * HW + 4 * j, xb);
-      const float d[4] = {v.x - shift, v.y - shift, v.z - shift, v.w - shift};
+    // thread -> (image lane li, 4-element group j): ipi images per sweep of the workgroup when a
+    // plane has fewer than BN2_T groups, the index split paid once per thread (not per element)
+    const int hw4 = (int)(HW / 4);
+    const bool wide = hw4 >= BN2_T;
+    const int ipi = wide ? 1 : BN2_T / hw4;
+    const int li = wide ? 0 : (int)threadIdx.x / hw4;
+    const int j0 = wide ? (int)threadIdx.x : (int)threadIdx.x - li * hw4;
+    const int jstep = wide ? BN2_T : hw4;
+    if (li < ipi) {
+      for (int64_t n = n0 + li; n < n1; n += ipi) {
+        const int64_t base = (n * C + c) * HW;
+        for (int j = j0; j < hw4; j += jstep) {
+          const float4 v = x2_ld4<XF>(x, base + 4 * j, xb);
+          const float d[4] = {v.x - shift, v.y - shift, v.z - shift, v.w - shift};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        fa += d[q];
-        fb = fmaf(d[q], d[q], fb);
-      }
-      if (++cnt == 8) {
-        a += (double)fa;
-        b += (double)fb;
-        fa = fb = 0.f;
-        cnt = 0;
+          for (int q = 0; q < 4; ++q) {
+            fa += d[q];
+            fb = fmaf(d[q], d[q], fb);
+          }
+          if (++cnt == 8) {
+            a += (double)fa;
+            b += (double)fb;
+            fa = fb = 0.f;
+            cnt = 0;
+          }
+        }
       }
     }
     a += (double)fa;
@@ -1789,8 +1802,8 @@ static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, in
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
   BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_apply_k<P, XFV>), dim3(grid_for(outs)), dim3(256),
-                                                             0, s, x, N, C, (int)H, (int)W, save_mean, save_invstd,
-                                                             gamma, beta, hardtanh, y)));
+                                                               0, s, x, N, C, (int)H, (int)W, save_mean, save_invstd,
+                                                               gamma, beta, hardtanh, y)));
   return check_launch("bnn_bn2d_fwd_train");
 }
 
@@ -1847,16 +1860,17 @@ static int bn2d_bwd_impl(X2 x, int xf, const float* dy, int64_t N, int64_t C, in
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P, XFV>), dim3((unsigned)C, (unsigned)R),
-                                                             dim3(BN2_T), 0, s, x, dy, N, C, (int)H, (int)W, CR,
-                                                             save_mean, save_invstd, gamma, beta, hardtanh, p0, p1)));
+                                                               dim3(BN2_T), 0, s, x, dy, N, C, (int)H, (int)W, CR,
+                                                               save_mean, save_invstd, gamma, beta, hardtanh, p0, p1)));
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
     const float inv_n = batch_stats ? (float)(1.0 / ((double)N * (double)(H * W))) : 0.f;
     BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_bwd_apply_k<P, XFV>), dim3(grid_for(outs)),
-                                                               dim3(256), 0, s, x, dy, N, C, (int)H, (int)W, save_mean,
-                                                               save_invstd, gamma, beta, hardtanh, k0, k1, inv_n, dx)));
+                                                                 dim3(256), 0, s, x, dy, N, C, (int)H, (int)W,
+                                                                 save_mean, save_invstd, gamma, beta, hardtanh, k0, k1,
+                                                                 inv_n, dx)));
   }
   return check_launch("bnn_bn2d_bwd");
 }

@@ -517,7 +517,7 @@ def test_conv_fwd_compact_sums(F, shape):
 
 
 def test_fused_cnn_compact_outputs_bit_identical(F):
-    """The fused BinCNN with its conv outputs travelling as int8 (conv1) / int16 (conv2) sums + bias
+    """The fused BinCNN with its conv outputs travelling as int16 sums + bias
     (functional.ZQ) against the same net with fp32 conv outputs: loss, every gradient and the
     BatchNorm running buffers bit-identical, two hand-offs per forward."""
     from bnn_amd import nets
