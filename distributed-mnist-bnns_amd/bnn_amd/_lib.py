@@ -77,6 +77,14 @@ SIGNATURES = {
                                      P, P, P, P]),
     "bnn_bn_bwd_i8cols_workspace": (I64, [I64, I64]),
     "bnn_bn_bwd_i8cols": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
+    "bnn_bn_bwd_i8cols_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
+    "bnn_bn_bwd_stats_pre": (I32, [P, I64, I64, I64, I32, P, P, P, P, P, P, P, P]),
+    "bnn_bn_bwd_q6_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "bnn_bn_bwd_q6_i16_pre": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
+                                    P, P]),
+    "bnn_gemm_fp6_bnstats_rows": (I64, [I64]),
+    "bnn_gemm_fp6_bnstats": (I32, [P, P, P, I64, P, I64, P, I64, I64, I64, I64, P, P, I32, P, P, P, P, P, I32, I32,
+                                   P, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,

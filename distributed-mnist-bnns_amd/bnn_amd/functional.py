@@ -13,6 +13,8 @@ Every op here runs on ROCm tensors through libbnn.so; there is no CPU fallback.
 """
 import contextlib
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -575,6 +577,38 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None, panel_ks=N
     return C
 
 
+# The BatchNorm-backward statistics in the dX GEMM's epilogue (bnn_gemm_fp6_bnstats): the fused
+# BN -> linear layer's backward takes sum g, sum g*xhat (and the i8cols bound's maxima) from the
+# GEMM that writes dy instead of a separate pass over (x, dy).  Off by default: on the wide step
+# every CU reaches its tile epilogue in the same round, so the epilogue's x reads are not hidden
+# behind MFMA work and cost as much as the pass they replace (BNN_BN_EPI=1 enables).
+BN_EPI = os.environ.get("BNN_BN_EPI", "0") == "1"
+BN_EPI_USES = 0           # epilogue-statistics backward passes run (tests check the path ran)
+
+
+def gemm_fp6_bnstats(A, panels, panel_ks, N, x, xbias, x_i16, mean, mlo, invstd, gamma, beta, mode):
+    """(C = A . B^T with B in panels, the per-128-row partials [2|4, R, N] of the BatchNorm-backward
+    statistics of C over x [A.rows, N], R)."""
+    global BN_EPI_USES
+    M, K = A.rows, A.Kp
+    dev = panels.device
+    C = torch.empty((M, N), dtype=torch.float32, device=dev)
+    R = L.lib().bnn_gemm_fp6_bnstats_rows(M)
+    part = torch.empty(((4 if mode == 2 else 2) * R * N,), dtype=torch.float32, device=dev)
+    name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * K, 3 * M * K + N * K // 2 + 4 * M * N + (2 if x_i16 else 4) * M * N):
+        L.call("bnn_gemm_fp6_bnstats", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(panels), panel_ks,
+               L.ptr(C), N, M, N, K, L.ptr(x), L.ptr(xbias), int(bool(x_i16)), L.ptr(mean), L.ptr(mlo), L.ptr(invstd),
+               L.ptr(gamma), L.ptr(beta), 1, int(mode), L.ptr(part), L.stream())
+    BN_EPI_USES += 1
+    return C, part, R
+
+
+def _bn_epi_ok(M, N, K):
+    """Whether the dX GEMM of this shape can carry the statistics epilogue (the unsplit default)."""
+    return BN_EPI and N % 4 == 0 and L.lib().bnn_gemm_fp6_workspace(M, N, K) == 0
+
+
 # ----------------------------------------------------------------------------- linear
 class BinaryLinearFunction(torch.autograd.Function):
     """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
@@ -1034,10 +1068,11 @@ def _q6_take_required(dy):
     return pre
 
 
-def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name, z16=None):
+def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, ws, name, z16=None, pre=None):
     """BatchNorm(+Dropout) backward that also quantises dz (returned, with the digits attached).
     z16 = (int16, bias): the input in its compact form (x unused); dz is then not written (the
-    returned gradient is a placeholder carrying only the digits, _dz_placeholder)."""
+    returned gradient is a placeholder carrying only the digits, _dz_placeholder).  pre = (part, R):
+    the statistics from the dX GEMM's epilogue (gemm_fp6_bnstats mode 1; p = 0)."""
     dev = dy.device
     dx = torch.empty((M, C), dtype=torch.float32, device=dev) if z16 is None else _dz_placeholder(M, C, dev)
     dx_ptr = L.ptr(dx) if z16 is None else None
@@ -1046,14 +1081,20 @@ def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, 
     cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
     xb, dzb = (8, 4) if z16 is None else (4, 0)   # bytes per element: two passes over x, the dz write
-    with _timed(name, 0, xb * M * C + 8 * M * C + dzb * M * C + 3 * M * C + 3 * C * Mp + M * C // 16):
+    if pre is not None:
+        xb //= 2                                    # one pass over x and dy: the statistics came with dy
+        L.call("bnn_bn_bwd_stats_pre", L.ptr(pre[0]), pre[1], M, C, 1, L.ptr(w), L.ptr(invstd), L.ptr(dw), L.ptr(db),
+               None, None, L.ptr(ws), L.stream())
+    sfx = "_pre" if pre is not None else ""
+    with _timed(name, 0, xb * M * C + (4 if pre is not None else 8) * M * C + dzb * M * C + 3 * M * C + 3 * C * Mp
+                + M * C // 16):
         if z16 is None:
-            L.call("bnn_bn_bwd_q6", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+            L.call("bnn_bn_bwd_q6" + sfx, L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                    L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
                    L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
                    L.ptr(ws), L.stream())
         else:
-            L.call("bnn_bn_bwd_q6_i16", L.ptr(z16[0]), L.ptr(z16[1]), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
+            L.call("bnn_bn_bwd_q6_i16" + sfx, L.ptr(z16[0]), L.ptr(z16[1]), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
                    L.ptr(mean), L.ptr(invstd), L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw),
                    L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi),
                    L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
@@ -1070,7 +1111,9 @@ I8C_HANDOFF = True
 I8C_HANDOFFS = 0          # hand-offs made (tests check the path actually ran)
 
 
-def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db):
+def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db, pre=None):
+    """pre = (part, R): the statistics and the digit bound's maxima from the dX GEMM's epilogue
+    (gemm_fp6_bnstats mode 2)."""
     dev = x.device
     ldqt = round_up(M)
     dg = torch.empty((3, C, ldqt), dtype=torch.int8, device=dev)
@@ -1078,10 +1121,13 @@ def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db):
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
     ds = torch.empty((C,), dtype=torch.int64, device=dev)
     ws = torch.empty((L.lib().bnn_bn_bwd_i8cols_workspace(M, C),), dtype=torch.uint8, device=dev)
-    with _timed("bn_bwd_i8cols", 0, 16 * M * C + dg.numel()):
-        L.call("bnn_bn_bwd_i8cols", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
-               L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc), L.ptr(cs), L.ptr(ds),
-               L.ptr(ws), L.stream())
+    if pre is not None:
+        L.call("bnn_bn_bwd_stats_pre", L.ptr(pre[0]), pre[1], M, C, 2, L.ptr(w), L.ptr(invstd), L.ptr(dw), L.ptr(db),
+               L.ptr(sc), L.ptr(ds), L.ptr(ws), L.stream())
+    with _timed("bn_bwd_i8cols", 0, (8 if pre is not None else 16) * M * C + dg.numel()):
+        L.call("bnn_bn_bwd_i8cols" + ("_pre" if pre is not None else ""), L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
+               L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc),
+               L.ptr(cs), L.ptr(ds), L.ptr(ws), L.stream())
     dz = _dz_placeholder(M, C, dev)
     setattr(dz, _I8C_ATTR, (_q6_key(dz), dg, sc, cs, ds))
     global I8C_HANDOFFS
@@ -1548,9 +1594,17 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                     dw = gemm_i8(dt, 3, qt, 1, N, C, a_scale=sc, k_true=M)
             db = cs
         if any(ctx.needs_input_grad[:3]):
+            st = None
             if ctx.fp6:
-                dh = gemm_fp6(pre[0] if pre is not None else quant6_rows(dy), None, C, k_true=N,
-                              panels=wqt, panel_ks=wqt.shape[1] // 32)                   # dY . W_b
+                A = pre[0] if pre is not None else quant6_rows(dy)
+                if ctx.training and (ctx.q6 or ctx.i8c) and _bn_epi_ok(M, C, A.Kp):
+                    # the BatchNorm backward's statistics come with dh from the GEMM's epilogue
+                    dh, part, R = gemm_fp6_bnstats(A, wqt, wqt.shape[1] // 32, C, z, zb if ctx.z16 else None,
+                                                   ctx.z16, mean, mlo, invstd, gw, gb, 1 if ctx.q6 else 2)
+                    st = (part, R)
+                else:
+                    dh = gemm_fp6(A, None, C, k_true=N, panels=wqt, panel_ks=wqt.shape[1] // 32)   # dY . W_b
+                del A
             else:
                 d, s = quant_rows(dy)
                 dh = gemm_i8(d, 3, wqt, 1, M, C, a_scale=s, k_true=N)
@@ -1560,9 +1614,9 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             ws = _bn_ws(M, C, z.device)
             if ctx.q6:
                 dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6",
-                                z16=(z, zb) if ctx.z16 else None)
+                                z16=(z, zb) if ctx.z16 else None, pre=st)
             elif ctx.i8c:
-                dz = _bn_bwd_i8c(z, dh, M, C, gw, gb, mean, invstd, mlo, dgw, dgb)
+                dz = _bn_bwd_i8c(z, dh, M, C, gw, gb, mean, invstd, mlo, dgw, dgb, pre=st)
             else:
                 dz = torch.empty_like(z)
                 with _timed("bn_bwd", 0, 16 * M * C):

@@ -403,11 +403,14 @@ struct I8cBound {
   int64_t* dsum;
 };
 
-__global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__ p0,
-                                                      const double* __restrict__ p1, int64_t C, int64_t R,
+// PT = double: bn_reduce_k's per-chunk partials; float: the FP6 dX GEMM's per-tile-row epilogue
+// statistics (bnn_gemm_fp6_bnstats -> bnn_bn_bwd_stats_pre)
+template <typename PT>
+__device__ __forceinline__ void bn_bwd_final_body(const PT* __restrict__ p0,
+                                                      const PT* __restrict__ p1, int64_t C, int64_t R,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       float* __restrict__ k0, float* __restrict__ k1,
-                                                      I8cBound ib = I8cBound{nullptr, nullptr, nullptr, 0.f, nullptr, nullptr}) {
+                                                      I8cBound ib) {
   __shared__ double sa[FF_GROUPS][FF_COLS], sb[FF_GROUPS][FF_COLS];
   __shared__ float sg[FF_GROUPS][FF_COLS], sx[FF_GROUPS][FF_COLS];
   const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
   float gm = 0.f, xm = 0.f;
   if (c < C)
     for (int64_t rb = grp; rb < R; rb += FF_B * FF_GROUPS) {   // batched loads, fixed order
-      double q0[FF_B], q1[FF_B];
+      PT q0[FF_B], q1[FF_B];
       float qg[FF_B], qx[FF_B];
 #pragma unroll
       for (int u = 0; u < FF_B; ++u) {
@@ -464,6 +467,21 @@ __global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__
     ib.scale[c] = sc;
     if (ib.dsum != nullptr) ib.dsum[c] = 0;
   }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_final_k(const double* __restrict__ p0, const double* __restrict__ p1,
+                                                      int64_t C, int64_t R, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta, float* __restrict__ k0,
+                                                      float* __restrict__ k1,
+                                                      I8cBound ib = I8cBound{nullptr, nullptr, nullptr, 0.f, nullptr, nullptr}) {
+  bn_bwd_final_body<double>(p0, p1, C, R, dgamma, dbeta, k0, k1, ib);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_final_pre_k(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                          int64_t C, int64_t R, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, float* __restrict__ k0,
+                                                          float* __restrict__ k1, I8cBound ib) {
+  bn_bwd_final_body<float>(p0, p1, C, R, dgamma, dbeta, k0, k1, ib);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ x, const float* __restrict__ dy,
@@ -1500,6 +1518,14 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
 
 namespace bnn {
 int64_t bn_workspace_bytes(int64_t M, int64_t C) { return bnn_bn_workspace(M, C); }
+// where bn_bwd_sums / bnn_bn_bwd_stats_pre leave k0 = sum g, k1 = sum g*xhat in the workspace
+void bn_stat_slots(void* work, int64_t M, int64_t C, const float** k0, const float** k1) {
+  const int64_t R = bn_chunks(M, C);
+  double* p1 = reinterpret_cast<double*>(work) + R * C;
+  float* a = reinterpret_cast<float*>(p1 + R * C);
+  *k0 = a;
+  *k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(a) + round_up(C * 4, 256));
+}
 int64_t bn_reduce_chunks(int64_t M, int64_t C) { return bn_chunks(M, C); }
 
 // The statistics half of the training-mode backward (bnn_bn_bwd without its apply pass): k0 =
@@ -1566,11 +1592,13 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
                      work, stream, make_drop(p, seed), true);
 }
 
+// pre: the statistics are already in `work` (bnn_bn_bwd_stats_pre from the dX GEMM's epilogue
+// partials): only the quantising apply pass runs
 static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,
                           const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
                           float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
-                          uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
+                          uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream, bool pre = false) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % Q6T_COLS != 0 || !dy || !aligned16(dy) ||
       !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) ||
@@ -1588,13 +1616,19 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  if (z16)
-    hipLaunchKernelGGL((bn_reduce_k<1, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
-                       save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
-  else
-    hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
-                       save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
-  hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  if (pre && p > 0.f) {
+    set_error("bnn_bn_bwd_q6_pre: the epilogue statistics carry no dropout mask (p must be 0)");
+    return kErrInval;
+  }
+  if (!pre) {
+    if (z16)
+      hipLaunchKernelGGL((bn_reduce_k<1, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+                         save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
+    else
+      hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+                         save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
+    hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
+  }
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
@@ -1618,6 +1652,48 @@ BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C,
                           uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_bwd_q6_impl(XIn{x, nullptr}, false, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
                         p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream);
+}
+
+BNN_API int bnn_bn_bwd_q6_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                              const float* beta, const float* save_mean, const float* save_invstd,
+                              const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                              uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
+  return bn_bwd_q6_impl(XIn{x, nullptr}, false, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream, true);
+}
+
+BNN_API int bnn_bn_bwd_q6_i16_pre(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
+                                  const float* gamma, const float* beta, const float* save_mean,
+                                  const float* save_invstd, const float* save_mean_lo, int32_t hardtanh, float p,
+                                  uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
+                                  uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                                  void* stream) {
+  return bn_bwd_q6_impl(XIn{x16, xbias}, true, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream, true);
+}
+
+// The statistics half of a training-mode BatchNorm(+Hardtanh) backward from the per-tile-row partials
+// the FP6 dX GEMM's epilogue wrote (bnn_gemm_fp6_bnstats: part [2 or 4][R][C] floats): k0 = sum g,
+// k1 = sum g*xhat into `work` (bnn_bn_workspace(M, C) bytes, where the *_pre apply entries read them),
+// dgamma / dbeta, and (mode 2) the int8 column-digit scale from the max|g| / max|xhat| bound + zeroed
+// digit sums, as bn_bwd_final_k does for bn_reduce_k's partials.
+BNN_API int bnn_bn_bwd_stats_pre(const float* part, int64_t R, int64_t M, int64_t C, int32_t mode, const float* gamma,
+                                 const float* save_invstd, float* dgamma, float* dbeta, float* scale, int64_t* dsum,
+                                 void* work, void* stream) {
+  if (!part || R <= 0 || M <= 0 || C <= 0 || (mode != 1 && mode != 2) || !work || (mode == 2 && (!scale || !save_invstd))) {
+    set_error("bnn_bn_bwd_stats_pre: bad arguments");
+    return kErrInval;
+  }
+  const int64_t Rb = bn_chunks(M, C);
+  double* p1 = reinterpret_cast<double*>(work) + Rb * C;
+  float* k0 = reinterpret_cast<float*>(p1 + Rb * C);
+  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
+  const I8cBound ib = mode == 2 ? I8cBound{part + 2 * R * C, save_invstd, gamma, 1.f / (float)M, scale, dsum}
+                                : I8cBound{nullptr, nullptr, nullptr, 0.f, nullptr, nullptr};
+  hipLaunchKernelGGL(bn_bwd_final_pre_k, ffin_grid(C), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), part,
+                     part + R * C, C, R, dgamma, dbeta, k0, k1, ib);
+  return check_launch("bnn_bn_bwd_stats_pre");
 }
 
 BNN_API int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,

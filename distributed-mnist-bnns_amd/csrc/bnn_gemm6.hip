@@ -189,6 +189,18 @@ struct Gemm6Params {
   float* part;
   int64_t bks;   // > 0: B in the panel layout with bks 64-k steps per panel (>= K / 64): every
                  // stage's B piece is one contiguous run of BN x 32 B
+  // BatchNorm-backward statistics of C in the epilogue (bnn_gemm_fp6_bnstats; mode 0 = off): C is the
+  // gradient dy reaching a training-mode BatchNorm(+Hardtanh) whose input x [M][N] (fp32, or int16
+  // + xbias) is read here; per 128-row tile row tm and column n the epilogue writes
+  // part[0][tm][n] = sum g, part[1] = sum g*xhat (mode 2: part[2] = max|g|, part[3] = max|xhat|),
+  // g = dy masked by -1 < BN(x) < 1 -- bn_reduce_k's MODE 1 / 2 sums, without its pass over x and dy
+  struct Bn {
+    const void* x;
+    const float* xbias;
+    const float *mean, *mean_lo, *invstd, *gamma, *beta;
+    float* part;
+    int z16, hardtanh, mode;
+  } bn;
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -623,19 +635,62 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   }
 
   // epilogue: C/D map of the 32x32 MFMA (reg i -> row (i&3)+8(i>>2)+4h, col lane&31), transposed
-  // through a per-wave LDS patch and written as 16-B row segments (as bnn_gemm.hip)
+  // through a per-wave LDS patch and written as 16-B row segments (as bnn_gemm.hip); with p.bn.mode
+  // the BatchNorm-backward column statistics of the tile ride along (Gemm6Params::Bn)
   wait_vmcnt6<0>();
   barrier6();
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
   const bool vec_ok = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0);
+  // the statistics epilogue exists in the 2-wave-row, 2-tile-row forms (the default 128 x 512 tile)
+  constexpr bool BNE = WAVES_M == 2 && WM == 2 && DIAG == 0;
+  const int bnmode = BNE ? p.bn.mode : 0;
+  __shared__ float bnred[BNE ? 2 : 1][BNE ? WAVES_N : 1][BNE ? WN : 1][32][4];   // per wave row: its column statistics
 #pragma unroll
-  for (int t = 0; t < WM; ++t) {
-    const int trow0 = m0 + wm * WM * 32 + t * 32;
+  for (int u = 0; u < WN; ++u) {
+    const int tcol0 = n0 + wn * WN * 32 + u * 32;
+    const int col = tcol0 + r;
+    const float bb = (bias && col < p.N) ? bias[col] : 0.f;
+    const int c4 = lane & 7, cs = tcol0 + 4 * c4;          // this lane's 4 columns in the row phase
+    float st0[4] = {0.f, 0.f, 0.f, 0.f}, st1[4] = {0.f, 0.f, 0.f, 0.f};
+    float stg[4] = {0.f, 0.f, 0.f, 0.f}, stx[4] = {0.f, 0.f, 0.f, 0.f};
+    float bm[4], bl[4], bi[4], bg[4], bbt[4], bx[4];
+    if (bnmode && cs + 3 < p.N) {
+      const float4 m4 = *reinterpret_cast<const float4*>(p.bn.mean + cs);
+      const float4 i4 = *reinterpret_cast<const float4*>(p.bn.invstd + cs);
+      const float4 l4 = p.bn.mean_lo ? *reinterpret_cast<const float4*>(p.bn.mean_lo + cs) : make_float4(0, 0, 0, 0);
+      const float4 g4 = p.bn.gamma ? *reinterpret_cast<const float4*>(p.bn.gamma + cs) : make_float4(1, 1, 1, 1);
+      const float4 b4 = p.bn.beta ? *reinterpret_cast<const float4*>(p.bn.beta + cs) : make_float4(0, 0, 0, 0);
+      const float4 x4 = (p.bn.z16 && p.bn.xbias) ? *reinterpret_cast<const float4*>(p.bn.xbias + cs) : make_float4(0, 0, 0, 0);
+      bm[0] = m4.x, bm[1] = m4.y, bm[2] = m4.z, bm[3] = m4.w;
+      bi[0] = i4.x, bi[1] = i4.y, bi[2] = i4.z, bi[3] = i4.w;
+      bl[0] = l4.x, bl[1] = l4.y, bl[2] = l4.z, bl[3] = l4.w;
+      bg[0] = g4.x, bg[1] = g4.y, bg[2] = g4.z, bg[3] = g4.w;
+      bbt[0] = b4.x, bbt[1] = b4.y, bbt[2] = b4.z, bbt[3] = b4.w;
+      bx[0] = x4.x, bx[1] = x4.y, bx[2] = x4.z, bx[3] = x4.w;
+    }
+    // this lane's x values of both tile rows, all loads issued before any is used (one memory
+    // latency per column group instead of one per row phase); rows past M clamped, never summed
+    float xv[WM][4][4];
+    if (bnmode && cs + 3 < p.N) {
 #pragma unroll
-    for (int u = 0; u < WN; ++u) {
-      const int tcol0 = n0 + wn * WN * 32 + u * 32;
-      const int col = tcol0 + r;
-      const float bb = (bias && col < p.N) ? bias[col] : 0.f;
+      for (int t = 0; t < WM; ++t)
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) {
+          const int rr = m0 + wm * WM * 32 + t * 32 + (lane >> 3) + 8 * ps;
+          const int64_t xi = (int64_t)(rr < p.M ? rr : p.M - 1) * p.N + cs;
+          if (p.bn.z16) {
+            const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(p.bn.x) + xi);
+            xv[t][ps][0] = (float)(int16_t)(q.x & 0xFFFFu) + bx[0], xv[t][ps][1] = (float)(int16_t)(q.x >> 16) + bx[1];
+            xv[t][ps][2] = (float)(int16_t)(q.y & 0xFFFFu) + bx[2], xv[t][ps][3] = (float)(int16_t)(q.y >> 16) + bx[3];
+          } else {
+            const float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.bn.x) + xi);
+            xv[t][ps][0] = q.x, xv[t][ps][1] = q.y, xv[t][ps][2] = q.z, xv[t][ps][3] = q.w;
+          }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < WM; ++t) {
+      const int trow0 = m0 + wm * WM * 32 + t * 32;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -646,9 +701,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int ps = 0; ps < 4; ++ps) {
-        const int lr = (lane >> 3) + 8 * ps, c4 = lane & 7;
+        const int lr = (lane >> 3) + 8 * ps;
         const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
-        const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
+        const int row = trow0 + lr, c0 = cs;
         if (row >= p.M) continue;
         float* dst = Cout + (int64_t)row * ldo + c0;
         if (vec_ok && c0 + 3 < p.N) {
@@ -659,8 +714,68 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
           for (int j = 0; j < 4; ++j)
             if (c0 + j < p.N) dst[j] = vs[j];
         }
+        if (bnmode && c0 + 3 < p.N) {
+          // bn_reduce_k MODE 1 / 2 on these 4 elements (the same xhat, y, mask and products)
+          const float* xs = xv[t][ps];
+          const float gs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xh = ((xs[j] - bm[j]) - bl[j]) * bi[j];
+            const float y = fmaf(xh, bg[j], bbt[j]);
+            const float g = (!p.bn.hardtanh || (y > -1.f && y < 1.f)) ? gs[j] : 0.f;
+            st0[j] += g;
+            st1[j] = fmaf(g, xh, st1[j]);
+            if (bnmode == 2) {   // NaN -> inf: the bound (and the scale) become non-finite
+              const float ag = fabsf(g), ax = fabsf(xh);
+              stg[j] = (ag == ag) ? fmaxf(stg[j], ag) : __builtin_inff();
+              stx[j] = (ax == ax) ? fmaxf(stx[j], ax) : __builtin_inff();
+            }
+          }
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (BNE && bnmode) {
+      // the 8 lanes holding these columns (lane bits 3-5: 8 row phases): a fixed xor tree
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st0[j] += __shfl_xor(st0[j], o, 64);
+          st1[j] += __shfl_xor(st1[j], o, 64);
+          if (bnmode == 2) {
+            stg[j] = fmaxf(stg[j], __shfl_xor(stg[j], o, 64));
+            stx[j] = fmaxf(stx[j], __shfl_xor(stx[j], o, 64));
+          }
+        }
+      if (lane < 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bnred[wm][wn][u][4 * c4 + j][0] = st0[j];
+          bnred[wm][wn][u][4 * c4 + j][1] = st1[j];
+          bnred[wm][wn][u][4 * c4 + j][2] = stg[j];
+          bnred[wm][wn][u][4 * c4 + j][3] = stx[j];
+        }
+      }
+    }
+  }
+  if (BNE && bnmode) {
+    __syncthreads();
+    // wave row 0 folds the two wave rows (fixed order) and writes this tile row's partials
+    if (wm == 0 && lane < 32) {
+      const int64_t RN = (int64_t)p.gm * p.N;
+#pragma unroll
+      for (int u = 0; u < WN; ++u) {
+        const int c = n0 + wn * WN * 32 + u * 32 + lane;
+        if (c >= p.N) continue;
+        float* pp = p.bn.part + (int64_t)tm * p.N + c;
+        pp[0] = bnred[0][wn][u][lane][0] + bnred[1][wn][u][lane][0];
+        pp[RN] = bnred[0][wn][u][lane][1] + bnred[1][wn][u][lane][1];
+        if (bnmode == 2) {
+          pp[2 * RN] = fmaxf(bnred[0][wn][u][lane][2], bnred[1][wn][u][lane][2]);
+          pp[3 * RN] = fmaxf(bnred[0][wn][u][lane][3], bnred[1][wn][u][lane][3]);
+        }
+      }
     }
   }
 }
@@ -887,7 +1002,7 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const int64_t need = bnn_gemm_fp6_workspace(M, N, K);
   const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
-                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0};
+                split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0, {}};
   return pl.v->fn(p, S6(stream));
 }
 
@@ -917,6 +1032,37 @@ BNN_API int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const 
     return kErrInval;
   }
   return gemm_fp6_impl(alo, ahi, asc, asc_rows, bpanels, -bks, bias, C, ldc, M, N, K, work, work_bytes, stream);
+}
+
+// The panel GEMM with the BatchNorm-backward statistics of C in its epilogue (Gemm6Params::Bn), for
+// the dX product that feeds a training-mode BatchNorm(+Hardtanh) backward: part = [2 or 4][gm][N]
+// floats, gm = bnn_gemm_fp6_bnstats_rows(M) (one row per 128-row tile row); no bias, no split-K.
+BNN_API int64_t bnn_gemm_fp6_bnstats_rows(int64_t M) { return (M + 127) / 128; }
+
+BNN_API int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                                 const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc, int64_t M, int64_t N,
+                                 int64_t K, const void* x, const float* xbias, int32_t x_i16, const float* mean,
+                                 const float* mean_lo, const float* invstd, const float* gamma, const float* beta,
+                                 int32_t hardtanh, int32_t mode, float* part, void* stream) {
+  const Fp6Plan pl = plan6(M, N, K);
+  if (!x || !mean || !invstd || !part || (mode != 1 && mode != 2) || N % 4 != 0 || pl.ksplit != 1 ||
+      pl.v->bm != 128 || pl.v->id != 7 || K <= 0 || bks < K / 64 || !aligned16(x) || !aligned16(mean) ||
+      !aligned16(invstd) || (mean_lo && !aligned16(mean_lo)) || (gamma && !aligned16(gamma)) ||
+      (beta && !aligned16(beta)) || (xbias && !aligned16(xbias)) || !aligned16(part)) {
+    set_error("bnn_gemm_fp6_bnstats: bad arguments (M=%lld N=%lld K=%lld mode=%d; N %% 4 == 0, an unsplit 128x512 "
+              "default plan, 16-B aligned vectors)", (long long)M, (long long)N, (long long)K, mode);
+    return kErrInval;
+  }
+  if (!alo || !ahi || !asc || !bpanels || !C || M <= 0 || N <= 0 || K % 64 != 0 || ldc < N ||
+      asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
+      !aligned16(asc) || !aligned16(bpanels) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
+    set_error("bnn_gemm_fp6_bnstats: bad GEMM arguments");
+    return kErrInval;
+  }
+  Gemm6Params p{alo, ahi, asc, bpanels, -bks, asc_rows, nullptr, C, ldc, (int)M, (int)N, (int)K, 0, 0,
+                K >= 32768 ? 8 : 4, 1, 0, nullptr, bks};
+  p.bn = Gemm6Params::Bn{x, xbias, mean, mean_lo, invstd, gamma, beta, part, x_i16 ? 1 : 0, hardtanh ? 1 : 0, mode};
+  return pl.v->fn(p, S6(stream));
 }
 
 BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, N)->name; }

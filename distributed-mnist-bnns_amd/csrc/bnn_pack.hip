@@ -1067,6 +1067,7 @@ int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const flo
                 float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out,
                 float* pmx = nullptr, float* scale = nullptr, int64_t* dsum = nullptr);
 int64_t bn_workspace_bytes(int64_t M, int64_t C);
+void bn_stat_slots(void* work, int64_t M, int64_t C, const float** k0, const float** k1);
 int64_t bn_reduce_chunks(int64_t M, int64_t C);
 }  // namespace bnn
 
@@ -1080,11 +1081,11 @@ BNN_API int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C) {
   return round_up(bn_workspace_bytes(M, C), 256) + i8c_pmx_bytes(M, C) + qc_strips(M) * C * (int64_t)sizeof(double);
 }
 
-BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+static int bn_bwd_i8cols_impl(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                               const float* beta, const float* save_mean, const float* save_invstd,
                               const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
                               int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
-                              int64_t* dsum, void* work, void* stream) {
+                              int64_t* dsum, void* work, void* stream, bool pre) {
   if (!x || !dy || !digits_t || !scale || !work || M <= 0 || C <= 0 || C % 4 != 0 || !aligned16(x) ||
       !aligned16(dy) || ldqt % TILE != 0 || ldqt < round_up(M, TILE) || plane < C * ldqt || plane % 16 != 0 ||
       !aligned16(digits_t) || col_chunks(M, C) > 65535 || ldqt / TILE > 65535 || !aligned16(save_mean) ||
@@ -1099,14 +1100,39 @@ BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_
   char* qw = reinterpret_cast<char*>(work) + round_up(bn_workspace_bytes(M, C), 256);
   float* pmx = reinterpret_cast<float*>(qw);
   double* part = reinterpret_cast<double*>(qw + i8c_pmx_bytes(M, C));
-  // statistics pass + its final merge, which also writes scale (from the bound) and zeroes dsum
-  int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta, work, s,
-                       &k0, &k1, pmx, scale, dsum);
-  if (rc) return rc;
+  // statistics pass + its final merge, which also writes scale (from the bound) and zeroes dsum;
+  // pre: bnn_bn_bwd_stats_pre (mode 2) already did, from the dX GEMM's epilogue partials
+  if (pre) {
+    bn_stat_slots(work, M, C, &k0, &k1);
+  } else {
+    const int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
+                               work, s, &k0, &k1, pmx, scale, dsum);
+    if (rc) return rc;
+  }
   const BnCols bc{save_mean, save_mean_lo, save_invstd, gamma, beta, k0, k1, 1.f / (float)M, hardtanh};
   hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT)),
                      dim3(256), 0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum, colsum ? part : nullptr);
   if (colsum)
     hipLaunchKernelGGL(bn_dz_colsum_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, qc_strips(M), C, colsum);
   return check_launch("bnn_bn_bwd_i8cols");
+}
+
+BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                              const float* beta, const float* save_mean, const float* save_invstd,
+                              const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
+                              int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
+                              int64_t* dsum, void* work, void* stream) {
+  return bn_bwd_i8cols_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
+                            digits_t, ldqt, plane, scale, colsum, dsum, work, stream, false);
+}
+
+// bnn_bn_bwd_i8cols after bnn_bn_bwd_stats_pre (mode 2): the statistics, the digit scale and the
+// zeroed digit sums are already in place; only the quantising pass runs
+BNN_API int bnn_bn_bwd_i8cols_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                                  const float* beta, const float* save_mean, const float* save_invstd,
+                                  const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
+                                  int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
+                                  int64_t* dsum, void* work, void* stream) {
+  return bn_bwd_i8cols_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
+                            digits_t, ldqt, plane, scale, colsum, dsum, work, stream, true);
 }

@@ -199,6 +199,17 @@ int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t Kp, uint8
 int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
                           const uint8_t* bpanels, int64_t bks, const float* bias, float* C, int64_t ldc, int64_t M,
                           int64_t N, int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
+/* bnn_gemm_fp6_panel_ws (no bias, the unsplit default plan only) with the BatchNorm-backward column
+ * statistics of C in its epilogue: C is the dy of a training-mode BatchNorm(+Hardtanh) over x
+ * [M][N] (fp32, or int16 + xbias when x_i16) with save_mean / mean_lo / invstd and gamma / beta;
+ * part = [2 (mode 1) or 4 (mode 2)][bnn_gemm_fp6_bnstats_rows(M)][N] floats (sum g, sum g*xhat,
+ * max|g|, max|xhat| per 128-row tile row), folded by bnn_bn_bwd_stats_pre. */
+int64_t bnn_gemm_fp6_bnstats_rows(int64_t M);
+int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                         const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                         const void* x, const float* xbias, int32_t x_i16, const float* mean, const float* mean_lo,
+                         const float* invstd, const float* gamma, const float* beta, int32_t hardtanh, int32_t mode,
+                         float* part, bnn_stream_t stream);
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
 const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
@@ -423,6 +434,33 @@ int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, con
                       const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                       float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale,
                       float* colsum, int64_t* dsum, void* work, bnn_stream_t stream);
+
+/* The BatchNorm(+Hardtanh) backward statistics from the FP6 dX GEMM's epilogue instead of their own
+ * pass over (x, dy): bnn_gemm_fp6_bnstats (below) writes per-128-row-tile-row partials of sum g,
+ * sum g*xhat (mode 2: + max|g|, max|xhat|) while it writes dy; bnn_bn_bwd_stats_pre folds them
+ * (fixed order) into `work` (bnn_bn_workspace(M, C) bytes -- for i8cols the first
+ * bnn_bn_workspace bytes of its workspace) with dgamma / dbeta (mode 2: the digit scale + zeroed
+ * dsum); the *_pre entries then run only the apply pass (same arguments as their plain forms;
+ * p = 0).  Same math as the plain entries, the statistics summed in another order.
+ * replaces: the statistics reduction of BatchNorm1d's backward (mnist-dist2.py:66-74) */
+int bnn_bn_bwd_stats_pre(const float* part, int64_t R, int64_t M, int64_t C, int32_t mode, const float* gamma,
+                         const float* save_invstd, float* dgamma, float* dbeta, float* scale, int64_t* dsum,
+                         void* work, bnn_stream_t stream);
+int bnn_bn_bwd_q6_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                      const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
+                      float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
+                      uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                      bnn_stream_t stream);
+int bnn_bn_bwd_q6_i16_pre(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
+                          const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                          const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          uint8_t* chi, uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
+int bnn_bn_bwd_i8cols_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+                          const float* beta, const float* save_mean, const float* save_invstd,
+                          const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta, int8_t* digits_t,
+                          int64_t ldqt, int64_t plane, float* scale, float* colsum, int64_t* dsum, void* work,
+                          bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */

@@ -229,8 +229,10 @@ def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
     u[:, :, :3] = 0                                   # dead pixels: exact-zero weight gradients
     y = torch.randint(0, 10, (2048,), generator=g, device="cuda")
     grads = []
+    epi0 = F.BN_EPI
     for on in (True, False):
         F.I8C_HANDOFF = on
+        F.BN_EPI = False          # both steps reduce the BatchNorm statistics in the same order
         try:
             torch.manual_seed(0)
             m = nets.MLP(1024, 512, 256, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
@@ -241,6 +243,7 @@ def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
             grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
         finally:
             F.I8C_HANDOFF = True
+            F.BN_EPI = epi0
     for k in grads[0]:
         if k in ("fc1.weight", "fc1.bias"):
             assert rel_err(host(grads[0][k]), host(grads[1][k]).astype(np.float64)) < 1e-6, k

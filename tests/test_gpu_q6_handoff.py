@@ -67,9 +67,11 @@ def test_bn_bwd_q6_matches_separate_passes(F, M, C, p):
     assert F._q6_take(dz2) is None                   # taken once
 
 
-def _wide_step(F, handoff, M=512, width=1024, seed=0):
+def _wide_step(F, handoff, M=512, width=1024, seed=0, bn_epi=False):
     from bnn_amd import nets
+    epi0 = F.BN_EPI
     F.Q6_HANDOFF = handoff
+    F.BN_EPI = bn_epi           # the statistics' summation order must match for bit-equality
     try:
         torch.manual_seed(seed)
         m = nets.MLP(width, width, width, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
@@ -83,6 +85,7 @@ def _wide_step(F, handoff, M=512, width=1024, seed=0):
         return {k: host(p.grad) for k, p in m.named_parameters()}, names
     finally:
         F.Q6_HANDOFF = True
+        F.BN_EPI = epi0
 
 
 def test_training_step_with_handoff_equals_without(F):
@@ -96,3 +99,63 @@ def test_training_step_with_handoff_equals_without(F):
             assert rel_err(g1[k], g0[k]) <= 1e-6, k
         else:
             assert np.array_equal(g1[k], g0[k]), k
+
+
+@pytest.mark.parametrize("x_i16,mode", [(False, 1), (True, 1), (False, 2)])
+def test_gemm_fp6_bnstats_epilogue(F, x_i16, mode):
+    """bnn_gemm_fp6_bnstats: C bit-identical to the plain panel GEMM; its per-tile-row partials of
+    sum g, sum g*xhat (g = dy masked by -1 < BN(x) < 1) within 1e-6 of float64 sums of the same
+    fp32 quantities; mode 2's max|g| / max|xhat| exact; the folded statistics (bnn_bn_bwd_stats_pre)
+    within 1e-6 of bn_bwd's own reduction."""
+    from bnn_amd import _lib as L
+    M, N, K = 4100, 8192, 2048                    # ragged last tile row; >= 1 round of tiles (unsplit)
+    g = torch.Generator(device="cuda").manual_seed(11 + mode)
+    dyq = torch.randn(M, K, generator=g, device="cuda")
+    w = torch.randint(-1, 2, (N, K), generator=g, device="cuda").float()
+    A = F.quant6_rows(dyq)
+    P = F.fp4_panels(F.sign_pack_fp4(w)[0], N, K)
+    xi = torch.randint(-300, 301, (M, N), generator=g, device="cuda").to(torch.int16)
+    xb = torch.randn(N, generator=g, device="cuda")
+    x = xi.float() + xb if x_i16 else torch.randn(M, N, generator=g, device="cuda") * 3
+    mean, invstd, mlo = F._bn_stat_buffers(N, "cuda")
+    rm, rv = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    gam = torch.rand(N, generator=g, device="cuda") + 0.5
+    bet = torch.randn(N, generator=g, device="cuda") * 0.2
+    L.call("bnn_bn_fwd_train", L.ptr(x), M, N, L.ptr(gam), L.ptr(bet), L.ptr(rm), L.ptr(rv), 0.1, 1e-5,
+           L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
+    C0 = F.gemm_fp6(A, None, N, panels=P, panel_ks=K // 64)
+    C1, part, R = F.gemm_fp6_bnstats(A, P, K // 64, N, xi if x_i16 else x, xb if x_i16 else None, x_i16, mean,
+                                     mlo, invstd, gam, bet, mode)
+    assert torch.equal(C0, C1)
+    xh = ((x - mean) - mlo) * invstd
+    yv = (xh.double() * gam.double() + bet.double()).float()   # fmaf(xh, gamma, beta): one rounding
+    gg = torch.where((yv > -1) & (yv < 1), C0, torch.zeros_like(C0))
+    pr = part.view(-1, R, N)
+    assert rel_err(host(pr[0]).astype(np.float64).sum(0), host(gg).astype(np.float64).sum(0)) < 1e-6
+    assert rel_err(host(pr[1]).astype(np.float64).sum(0), (host(gg).astype(np.float64) * host(xh)).sum(0)) < 1e-6
+    if mode == 2:
+        assert torch.equal(pr[2].max(0).values, gg.abs().max(0).values)
+        assert torch.equal(pr[3].max(0).values, xh.abs().max(0).values)
+    # the fold against bn_bwd's own statistics (dgamma = sum g*xhat, dbeta = sum g)
+    ws = F._bn_ws(M, N, "cuda")
+    dg0, db0, dg1, db1 = (torch.empty(N, device="cuda") for _ in range(4))
+    L.call("bnn_bn_bwd", L.ptr(x), L.ptr(C0), M, N, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(mlo),
+           1, None, L.ptr(dg0), L.ptr(db0), L.ptr(ws), L.stream())
+    sc, ds = torch.empty(N, device="cuda"), torch.empty(N, dtype=torch.int64, device="cuda")
+    L.call("bnn_bn_bwd_stats_pre", L.ptr(part), R, M, N, mode, L.ptr(gam), L.ptr(invstd), L.ptr(dg1), L.ptr(db1),
+           L.ptr(sc) if mode == 2 else None, L.ptr(ds) if mode == 2 else None, L.ptr(F._bn_ws(M, N, "cuda")),
+           L.stream())
+    assert rel_err(host(dg1), host(dg0)) < 1e-6 and rel_err(host(db1), host(db0)) < 1e-6
+
+
+def test_training_step_bn_epilogue_statistics(F):
+    """A fused wide step with the BatchNorm-backward statistics taken from the dX GEMMs' epilogues
+    (functional.BN_EPI) against the same step with the separate statistics pass: the forward and
+    loss identical, every gradient within 1e-6 norm-wise (the sums differ only in order)."""
+    n0 = F.BN_EPI_USES
+    # 64 x 4 tiles of 128 x 512 on the dX GEMMs: one round of the chip, so their plan is unsplit
+    g1, names1 = _wide_step(F, True, M=8192, width=2048, bn_epi=True)
+    assert F.BN_EPI_USES - n0 >= 1
+    g0, _ = _wide_step(F, True, M=8192, width=2048, bn_epi=False)
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) <= 1e-6 or np.abs(g1[k] - g0[k]).max() <= 1e-7, k
