@@ -32,6 +32,9 @@ SIGNATURES = {
     "bnn_gemm_i8": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, I64, I64, I64, I64, P]),
     "bnn_gemm_i8_affine": (I32, [P, I64, I64, I32, P, I64, I64, I32, P, P, P, P, P, ctypes.c_double, P, I64,
                                  I64, I64, I64, P]),
+    "bnn_gemm_i8_bnstats_chunk": (I64, [I64, I64]),
+    "bnn_gemm_i8_affine_bnstats": (I32, [P, I64, P, I64, P, P, P, ctypes.c_double, P, I64, I64, I64, I64, P, I64,
+                                         P]),
     "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
@@ -47,6 +50,7 @@ SIGNATURES = {
     "bnn_conv_set_mfma": (I32, [I32]),
     "bnn_bn_workspace": (I64, [I64, I64]),
     "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, P, P]),
+    "bnn_bn_fwd_final_parts": (I32, [P, I64, I64, I64, I64, P, P, F32, F32, P, P, P, P]),
     "bnn_bn_fwd_eval": (I32, [P, I64, I64, P, P, P, P, F32, P, I32, P, P]),
     "bnn_bn_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, P, P]),
     "bnn_bn_bwd_eval": (I32, [P, P, I64, I64, P, P, P, P, I32, P, P, P, P, P]),

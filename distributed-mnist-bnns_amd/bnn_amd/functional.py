@@ -756,6 +756,38 @@ def _const_vec(val, n, device):
     return t
 
 
+# fc1 -> bn1 (mnist-dist2.py:64-65): in training the pixel GEMM's epilogue also forms bn1's
+# forward statistics (chunk sums and M2 of z from its exact integer sums,
+# bnn_gemm_i8_affine_bnstats), carried on the output; the fused BatchNorm then runs only the final
+# (bnn_bn_fwd_final_parts) instead of a statistics pass over z.
+PIX_STATS = os.environ.get("BNN_PIX_STATS", "1") != "0"      # BNN_PIX_STATS=0: the statistics pass
+_FSTATS_ATTR = "_bnn_fstats"
+PIX_STATS_USES = 0
+
+
+def _pixels_fwd_with_stats(q, wq, M, N, K, bscale, bias, R, s0):
+    chunk = int(L.lib().bnn_gemm_i8_bnstats_chunk(M, N))
+    rows = (M + chunk - 1) // chunk
+    part = torch.empty((2, rows, N), dtype=torch.float64, device=q.device)
+    y = torch.empty((M, N), dtype=torch.float32, device=q.device)
+    Kp = q.shape[1]
+    assert wq.shape[1] == Kp and Kp % ALIGN == 0
+    name = f"{gemm_kernel_name(1, 1, M, N, Kp)} [pixels]" if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * K, M * Kp + N * Kp + 4 * M * N):
+        L.call("bnn_gemm_i8_affine_bnstats", L.ptr(q), Kp, L.ptr(wq), Kp, L.ptr(bscale), L.ptr(bias), L.ptr(R),
+               float(s0), L.ptr(y), N, M, N, Kp, L.ptr(part), rows, L.stream())
+    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N))
+    return y
+
+
+def _fstats_of(z, M, C):
+    """The forward-statistics partials a pixel GEMM attached to z (None if absent or stale)."""
+    fs = getattr(z, _FSTATS_ATTR, None)
+    if fs is None or fs[3] != M or fs[4] != C or z._version != 0:
+        return None
+    return fs
+
+
 class BinaryLinearPixelsFunction(torch.autograd.Function):
     """fc1 on u8 pixels: y = F.linear(x, sign(w)) + b with x = a*(u - 128 + s0), the reference's
     first BinarizeLinear (models/binarized_modules.py:68-85 with size(1) == 784: input not
@@ -777,9 +809,12 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
             return torch.empty((0, N), dtype=torch.float32, device=u.device)
         wq, _ = packed_weight(weight, "i8", True, False, cache)
         R = row_sums(wq, K)
-        y = gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=_const_vec(a, N, u.device),
-                           bias=bias.detach() if bias is not None else None, col_off=R, off_mul=s0, k_true=K,
-                           label="pixels")
+        bvec = bias.detach() if bias is not None else None
+        if PIX_STATS and need_dw and K <= q.shape[1]:
+            y = _pixels_fwd_with_stats(q, wq, M, N, K, _const_vec(a, N, u.device), bvec, R, s0)
+        else:
+            y = gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=_const_vec(a, N, u.device), bias=bvec, col_off=R,
+                               off_mul=s0, k_true=K, label="pixels")
         ctx.save_for_backward(qt)
         if I8C_HANDOFF and need_dw:
             setattr(y, _I8C_WANT, True)
@@ -1514,7 +1549,13 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             ws = _bn_ws(M, C, z.device)
             mom = float(momentum if momentum is not None else -1.0)
             with _timed("bn_fwd_stats", 0, (4 if zz is None else 2) * M * C):
-                if zz is None:
+                fs = _fstats_of(z, M, C) if zz is None else None
+                if fs is not None:
+                    global PIX_STATS_USES
+                    PIX_STATS_USES += 1
+                    L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(rm), L.ptr(rv), mom,
+                           float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
+                elif zz is None:
                     L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv), mom,
                            float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
                 else:

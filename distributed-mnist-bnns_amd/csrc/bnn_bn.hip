@@ -1440,6 +1440,24 @@ static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const floa
   return check_launch("bnn_bn_fwd_train");
 }
 
+// The forward statistics from chunk partials another kernel formed (bnn_gemm_i8_affine_bnstats):
+// part = [2][R][C] doubles (chunk sums, M2 about the chunk means), chunk r = rows
+// [r*chunk_rows, min((r+1)*chunk_rows, M)); the same final as bnn_bn_fwd_train
+BNN_API int bnn_bn_fwd_final_parts(const double* part, int64_t R, int64_t chunk_rows, int64_t M, int64_t C,
+                                   float* running_mean, float* running_var, float momentum, float eps,
+                                   float* save_mean, float* save_invstd, float* save_mean_lo, void* stream) {
+  if (!part || M <= 0 || C <= 0 || chunk_rows <= 0 || R != (M + chunk_rows - 1) / chunk_rows || !save_mean ||
+      !save_invstd || !save_mean_lo || (running_mean == nullptr) != (running_var == nullptr)) {
+    set_error("bnn_bn_fwd_final_parts: bad arguments (R=%lld chunk_rows=%lld M=%lld C=%lld)", (long long)R,
+              (long long)chunk_rows, (long long)M, (long long)C);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), part,
+                     part + R * C, M, C, R, momentum, eps, running_mean, running_var, save_mean, save_invstd,
+                     save_mean_lo, chunk_rows, (int64_t)1);
+  return check_launch("bnn_bn_fwd_final_parts");
+}
+
 BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,

@@ -43,6 +43,10 @@ struct GemmParams {
   // int16 output (ternary x ternary forms without scales, offsets or bias): the exact dot products
   // |sum| <= K < 2^15 as int16 [M][ldc] instead of fp32 C (bnn_gemm_fp4_i16)
   int16_t* C16 = nullptr;
+  // the next BatchNorm's forward statistics from the (1,1) 32x32 forms' epilogue
+  // (bnn_gemm_i8_affine_bnstats): [2][stat_rows][N] doubles, chunk = this tile row's wave row
+  double* stat = nullptr;
+  int64_t stat_rows = 0;
 };
 
 __device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
@@ -575,6 +579,44 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
   // 16-B stores (4 per lane instead of 16 dword stores).
   wait_vmcnt_c<0>();  // no LDS-DMA piece may land in the epilogue's patches
   block_barrier();  // every wave is done reading the last operand stage
+  if constexpr (DA == 1 && DB == 1 && !F4 && !S16 && DIAG == 0) {
+    if (p.stat != nullptr) {
+      // BatchNorm forward statistics of z = a*(S + coff) + b (the pixel layer; a = b_scale, no
+      // a_scale / row_off: host check) per column over this wave row's WM*32 rows of the tile --
+      // one chunk of bn_fwd_final_k: the chunk sum and the M2 about the chunk mean, formed in double
+      // from the exact integer sums S (sum S, sum S^2 as int32 / int64), with no extra HBM traffic
+      const int cr0 = m0 + wm * WM * 32;
+      const int cnt = min(WM * 32, p.M - cr0);
+      const int64_t chunk = (int64_t)tm * WAVES_M + wm, RN = p.stat_rows * (int64_t)p.N;
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const int col = n0 + wn * WN * 32 + u * 32 + r;
+        // integer sums (|S| <= 128 K: a lane's 16 WM values fit int32, their squares int64)
+        int i1 = 0;
+        long long i2 = 0;
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int i = 0; i < TR; ++i) {
+            const int row = cr0 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const int v = row < p.M ? (int)acc[0][t][u][i] : 0;
+            i1 += v;
+            i2 += (long long)v * v;
+          }
+        i1 += __shfl_xor(i1, 32, 64);
+        i2 += __shfl_xor(i2, 32, 64);
+        const double s1 = (double)i1, s2 = (double)i2;
+        if (h == 0 && cnt > 0 && col < p.N) {
+          const double a = p.b_scale ? (double)p.b_scale[col] : 1.0;
+          const double coff = p.col_off ? (double)p.col_off[col] * p.off_mul : 0.0;
+          const double b = p.bias ? (double)p.bias[col] : 0.0;
+          p.stat[chunk * p.N + col] = a * (s1 + cnt * coff) + cnt * b;
+          const double m2 = s2 - s1 * s1 / cnt;
+          p.stat[RN + chunk * p.N + col] = a * a * (m2 > 0.0 ? m2 : 0.0);
+        }
+      }
+    }
+  }
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
   const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
   constexpr int SUB = S16 ? 2 : 1;   // MFMA tiles per patch edge
@@ -826,6 +868,39 @@ BNN_API int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, in
   if (lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31))
     return find_variant(a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20))->fn(p, reinterpret_cast<hipStream_t>(stream));
   return pick_kernel(a_digits, b_digits, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+// The statistics form runs the 32x32 (1,1) kernels only: 128x128 tiles (64-row chunks) on grids
+// below 512 of the 256x256 tiles (128-row chunks), as pick_kernel's BK=64 choices
+static const Variant* i8_bnstats_variant(int64_t M, int64_t N) {
+  const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
+  return find_variant(big ? 2 : 1);
+}
+
+BNN_API int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N) {
+  return i8_bnstats_variant(M, N)->id == 2 ? 128 : 64;
+}
+
+BNN_API int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
+                                       const float* b_scale, const float* bias, const int64_t* col_off,
+                                       double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                       double* stat, int64_t stat_rows, void* stream) {
+  const int64_t chunk = M > 0 ? bnn_gemm_i8_bnstats_chunk(M, N) : 1;
+  if (!A || !B || !C || !stat || M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K ||
+      lda % 16 != 0 || ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) || M > 0x7fffffff ||
+      N > 0x7fffffff || K > 0x7fffffff || lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31) ||
+      stat_rows != (M + chunk - 1) / chunk ||
+      // |S| <= 128 K: sum S^2 over a column stays an exact double below 2^53
+      (double)M * (128.0 * K) * (128.0 * K) >= 9007199254740992.0) {
+    set_error("bnn_gemm_i8_affine_bnstats: bad arguments (M=%lld N=%lld K=%lld stat_rows=%lld; want %lld)",
+              (long long)M, (long long)N, (long long)K, (long long)stat_rows, (long long)((M + chunk - 1) / chunk));
+    return kErrInval;
+  }
+  GemmParams p{A, B, lda, ldb, 0, 0, nullptr, b_scale, bias, C, ldc,
+               (int)M, (int)N, (int)K, 0, 0, nullptr, col_off, off_mul};
+  p.stat = stat;
+  p.stat_rows = stat_rows;
+  return i8_bnstats_variant(M, N)->fn(p, reinterpret_cast<hipStream_t>(stream));
 }
 
 BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,

@@ -117,6 +117,18 @@ int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_
                        const int64_t* row_off, const int64_t* col_off, double off_mul, float* C,
                        int64_t ldc, int64_t M, int64_t N, int64_t K, bnn_stream_t stream);
 
+/* fc1 on u8 pixels (digits (1,1), no a_scale / row_off) that also hands the next BatchNorm its
+ * forward statistics (mnist-dist2.py:64-65, fc1 -> bn1): stat = [2][stat_rows][N] doubles, per
+ * column and chunk of bnn_gemm_i8_bnstats_chunk(M, N) rows the sum of z = b_scale*(S + off_mul*
+ * col_off) + bias and its M2 about the chunk mean, formed in the GEMM epilogue from the exact
+ * integer sums S (no pass over C); stat_rows = ceil(M / chunk).  Feed to bnn_bn_fwd_final_parts.
+ * The statistics are those of the unrounded z (C holds its fp32 rounding). */
+int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N);
+int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
+                               const float* b_scale, const float* bias, const int64_t* col_off,
+                               double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                               double* stat, int64_t stat_rows, bnn_stream_t stream);
+
 /* ---------------------------------------------------------------- u8 pixels (first layer)
  * Replaces the fp32 pixel tensor the reference's loader builds (ToTensor = u8/255, optionally
  * Normalize; mnist-dist2.py:96-99, mnist-distributed-BNNS2.py:82) as the operand of fc1
@@ -275,6 +287,12 @@ int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, c
                      float* running_mean, float* running_var, float momentum, float eps,
                      float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
                      void* work, bnn_stream_t stream);
+/* bnn_bn_fwd_train's final step (mean hi/lo, invstd, running statistics) from chunk partials
+ * another kernel formed: part = [2][R][C] doubles (chunk sums, then M2 about each chunk's mean),
+ * chunk r = rows [r*chunk_rows, min((r+1)*chunk_rows, M)), R = ceil(M / chunk_rows). */
+int bnn_bn_fwd_final_parts(const double* part, int64_t R, int64_t chunk_rows, int64_t M, int64_t C,
+                           float* running_mean, float* running_var, float momentum, float eps,
+                           float* save_mean, float* save_invstd, float* save_mean_lo, bnn_stream_t stream);
 int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                     const float* running_mean, const float* running_var, float eps, float* y,
                     int32_t hardtanh, void* work, bnn_stream_t stream);

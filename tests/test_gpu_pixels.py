@@ -251,3 +251,82 @@ def test_mlp_step_with_i8cols_handoff_equals_unfused(F):
             assert torch.equal(grads[0][k], grads[1][k]), k
     dead = grads[0]["fc1.weight"].view(1024, 28, 28)[:, :3]
     assert not dead.any()
+
+
+@pytest.mark.parametrize("M,N,normalize", [(8192, 4096, None), (1000, 3072, None), (4100, 1024, (0.1307, 0.3081)),
+                                           (77, 200, None)])
+def test_pixels_gemm_bn_forward_statistics(F, t10k, M, N, normalize):
+    """bnn_gemm_i8_affine_bnstats: C bit-identical to bnn_gemm_i8_affine; the chunk partials equal
+    float64 chunk sums / M2 of z = a*(S + s0*R) + b computed from the exact integer sums; the
+    final (bnn_bn_fwd_final_parts) within 1e-6 of bnn_bn_fwd_train's statistics of the stored z
+    (which differ only by z's fp32 rounding), running statistics likewise."""
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M + N)
+    u = t10k[rng.integers(0, 10000, M)]
+    w = rng.uniform(-1, 1, (N, 784)).astype(np.float32)
+    w[:, ::97] = 0.0
+    b = rng.standard_normal(N).astype(np.float32)
+    ut, wt, bt = (torch.as_tensor(v).cuda() for v in (u, w, b))
+    a, s0 = F.pixel_affine(normalize)
+    q, _ = F.pixels_pack(ut, want_q=True, want_qt=False)
+    wq, _ = F.packed_weight(wt, "i8", True, False, False)
+    R = F.row_sums(wq, 784)
+    bs = F._const_vec(a, N, "cuda")
+    y0 = F.gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=bs, bias=bt, col_off=R, off_mul=s0, k_true=784)
+    y1 = F._pixels_fwd_with_stats(q, wq, M, N, 784, bs, bt, R, s0)
+    assert torch.equal(y0, y1)
+    part, rows, chunk = getattr(y1, F._FSTATS_ATTR)[:3]
+    # exact integer sums (|S| <= 128*784: exact in the float64 product)
+    S = (u.astype(np.float64) - 128) @ np.sign(w).astype(np.float64).T
+    z = float(np.float32(a)) * (S + float(s0) * host(R).astype(np.float64)[None, :]) + b.astype(np.float64)
+    ph = host(part)
+    for r in range(rows):
+        zc = z[r * chunk:(r + 1) * chunk]
+        assert rel_err(ph[0, r], zc.sum(0)) <= 1e-12
+        assert rel_err(ph[1, r], ((zc - zc.mean(0)) ** 2).sum(0)) <= 1e-9
+    mean0, istd0, lo0 = F._bn_stat_buffers(N, "cuda")
+    mean1, istd1, lo1 = (t.clone() for t in F._bn_stat_buffers(N, "cuda"))
+    rm0, rv0 = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    L.call("bnn_bn_fwd_train", L.ptr(y0), M, N, None, None, L.ptr(rm0), L.ptr(rv0), 0.1, 1e-5, L.ptr(mean0),
+           L.ptr(istd0), L.ptr(lo0), None, 1, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
+    L.call("bnn_bn_fwd_final_parts", L.ptr(part), rows, chunk, M, N, L.ptr(rm1), L.ptr(rv1), 0.1, 1e-5,
+           L.ptr(mean1), L.ptr(istd1), L.ptr(lo1), L.stream())
+    m0 = host(mean0).astype(np.float64) + host(lo0)
+    m1 = host(mean1).astype(np.float64) + host(lo1)
+    assert np.abs(m1 - z.mean(0)).max() <= 1e-12 * np.abs(z).max() + 1e-12
+    sd = z.std(0)
+    assert np.all(np.abs(m1 - m0) <= 1e-6 * sd + 1e-30)
+    assert rel_err(host(istd1), host(istd0)) <= 1e-6
+    assert rel_err(host(rm1), host(rm0)) <= 1e-6 and rel_err(host(rv1), host(rv0)) <= 1e-6
+
+
+def test_mlp_step_pixel_statistics_epilogue(F):
+    """A fused MLP training step on pixels with bn1's forward statistics from the fc1 epilogue
+    (functional.PIX_STATS) against the same step with the statistics pass: loss within 1e-6, bn1's
+    batch statistics within 1e-6, every gradient within 1e-4 norm-wise (a BatchNorm near-tie may
+    resolve differently: the two means differ by z's fp32 rounding)."""
+    from bnn_amd import nets
+    g = torch.Generator(device="cuda").manual_seed(3)
+    u = torch.randint(0, 256, (4096, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    y = torch.randint(0, 10, (4096,), generator=g, device="cuda")
+    out = []
+    on0 = F.PIX_STATS
+    for on in (True, False):
+        F.PIX_STATS = on
+        try:
+            torch.manual_seed(0)
+            m = nets.MLP(2048, 1024, 512, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+            n0 = F.PIX_STATS_USES
+            loss = torch.nn.CrossEntropyLoss()(m(u), y)
+            loss.backward()
+            assert F.PIX_STATS_USES - n0 == (1 if on else 0)
+            out.append((float(loss), {k: host(p.grad) for k, p in m.named_parameters()},
+                        host(m.bn1.running_mean), host(m.bn1.running_var)))
+        finally:
+            F.PIX_STATS = on0
+    (l1, g1, rm1, rv1), (l0, g0, rm0, rv0) = out
+    assert abs(l1 - l0) <= 1e-6 * abs(l0)
+    assert rel_err(rm1, rm0) <= 1e-6 and rel_err(rv1, rv0) <= 1e-6
+    for k in g0:   # fc1.bias: analytically zero ahead of a batch-statistics BatchNorm (~1e-11 noise)
+        assert rel_err(g1[k], g0[k]) <= 1e-4 or np.abs(g1[k] - g0[k]).max() <= 1e-9, k
