@@ -283,7 +283,7 @@ __device__ __forceinline__ void block_barrier() {
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
-          int DIAG = 0, int F4 = 0, int S16 = 0>
+          int DIAG = 0, int F4 = 0, int S16 = 0, int BST = 0>
 __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
   // F4 = 1: both operands are ternary FP4 (e2m1) nibbles, 2 per byte; K and the LDS tiles are
   // counted in bytes (BKT bytes = 2*BKT elements); v_mfma_scale_f32_32x32x64_f8f6f4 with unit
@@ -579,7 +579,8 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
   // 16-B stores (4 per lane instead of 16 dword stores).
   wait_vmcnt_c<0>();  // no LDS-DMA piece may land in the epilogue's patches
   block_barrier();  // every wave is done reading the last operand stage
-  if constexpr (DA == 1 && DB == 1 && !F4 && !S16 && DIAG == 0) {
+  // BST = 1: the statistics instance (bnn_gemm_i8_affine_bnstats); the plain kernels carry none of it
+  if constexpr (BST && DA == 1 && DB == 1 && !F4 && !S16 && DIAG == 0) {
     if (p.stat != nullptr) {
       // BatchNorm forward statistics of z = a*(S + coff) + b (the pixel layer; a = b_scale, no
       // a_scale / row_off: host check) per column over this wave row's WM*32 rows of the tile --
@@ -594,19 +595,30 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         // integer sums (|S| <= 128 K: a lane's 16 WM values fit int32, their squares int64)
         int i1 = 0;
         long long i2 = 0;
+        if (cr0 + WM * 32 <= p.M) {              // a full chunk (wave-uniform): no row tests
 #pragma unroll
-        for (int t = 0; t < TM; ++t)
+          for (int t = 0; t < TM; ++t)
 #pragma unroll
-          for (int i = 0; i < TR; ++i) {
-            const int row = cr0 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            const int v = row < p.M ? (int)acc[0][t][u][i] : 0;
-            i1 += v;
-            i2 += (long long)v * v;
-          }
+            for (int i = 0; i < TR; ++i) {
+              const int v = (int)acc[0][t][u][i];
+              i1 += v;
+              i2 += (long long)v * v;
+            }
+        } else {
+          const int lim = p.M - cr0 - 4 * h;     // this lane's rows below M: offsets < lim
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int i = 0; i < TR; ++i) {
+              const int v = (t * 32 + (i & 3) + 8 * (i >> 2)) < lim ? (int)acc[0][t][u][i] : 0;
+              i1 += v;
+              i2 += (long long)v * v;
+            }
+        }
         i1 += __shfl_xor(i1, 32, 64);
         i2 += __shfl_xor(i2, 32, 64);
-        const double s1 = (double)i1, s2 = (double)i2;
         if (h == 0 && cnt > 0 && col < p.N) {
+          const double s1 = (double)i1, s2 = (double)i2;
           const double a = p.b_scale ? (double)p.b_scale[col] : 1.0;
           const double coff = p.col_off ? (double)p.col_off[col] * p.off_mul : 0.0;
           const double b = p.bias ? (double)p.bias[col] : 0.0;
@@ -707,9 +719,9 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
-          int DIAG = 0, int S16 = 0>
+          int DIAG = 0, int S16 = 0, int BST = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParams p) {
-  gemm_v2_body<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, 0, S16>(p);
+  gemm_v2_body<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, 0, S16, BST>(p);
 }
 
 // FP4 (e2m1) ternary x ternary form: its own kernel name, so traces and the bench's peak lookup
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp4_k(GemmParams 
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
-          int DIAG = 0, int F4 = 0, int S16 = 0>
+          int DIAG = 0, int F4 = 0, int S16 = 0, int BST = 0>
 int launch_v2(GemmParams p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
@@ -732,7 +744,7 @@ int launch_v2(GemmParams p, hipStream_t s) {
                        dim3(64 * WAVES_M * WAVES_N), 0, s, p);
     return check_launch("bnn_gemm_fp4");
   } else {
-    hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, S16>),
+    hipLaunchKernelGGL((gemm_i8_v2_k<DA, DB, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, DIAG, S16, BST>),
                        dim3((unsigned)nblk), dim3(64 * WAVES_M * WAVES_N), 0, s, p);
     return check_launch("bnn_gemm_i8");
   }
@@ -900,7 +912,9 @@ BNN_API int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_
                (int)M, (int)N, (int)K, 0, 0, nullptr, col_off, off_mul};
   p.stat = stat;
   p.stat_rows = stat_rows;
-  return i8_bnstats_variant(M, N)->fn(p, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return i8_bnstats_variant(M, N)->id == 2 ? launch_v2<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 0, 0, 1>(p, st)
+                                           : launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 0, 0, 1>(p, st);
 }
 
 BNN_API int bnn_gemm_i8(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_digits,
