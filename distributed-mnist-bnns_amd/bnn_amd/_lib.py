@@ -35,6 +35,9 @@ SIGNATURES = {
     "bnn_gemm_i8_bnstats_chunk": (I64, [I64, I64]),
     "bnn_gemm_i8_affine_bnstats": (I32, [P, I64, P, I64, P, P, P, ctypes.c_double, P, I64, I64, I64, I64, P, I64,
                                          P]),
+    "bnn_linear_nsmall_workspace": (I64, [I64, I64, I64]),
+    "bnn_linear_nsmall_fwd": (I32, [P, I64, I64, P, P, I64, P, P]),
+    "bnn_linear_nsmall_bwd": (I32, [P, P, P, I64, I64, I64, P, P, P, P, I64, P]),
     "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),

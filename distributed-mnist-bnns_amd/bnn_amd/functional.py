@@ -857,6 +857,55 @@ def binary_linear_pixels(u, weight, bias=None, normalize=None, cache=False):
     return y if len(lead) == 1 else y.reshape(*lead, weight.shape[0])
 
 
+# ----------------------------------------------------------------------------- narrow Linear
+LINEAR_NSMALL = (1, 2, 4, 8, 10, 16)
+
+
+class LinearNSmallFunction(torch.autograd.Function):
+    """y = F.linear(x, w, b) for a narrow fp32 classifier (bnn_linear_nsmall_*): the BinCNN's
+    nn.Linear(7*7*32, 10), which a library GEMM runs at ~16 us per product on this shape."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _check(x, weight, bias)
+        x = x.contiguous()
+        w = weight.detach().contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        with _timed("linear_nsmall_fwd", 2.0 * M * N * K, 4 * M * K):
+            L.call("bnn_linear_nsmall_fwd", L.ptr(x), M, K, L.ptr(w), L.ptr(bias.detach() if bias is not None else None),
+                   N, L.ptr(y), L.stream())
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        M, K = x.shape
+        N = w.shape[0]
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        db = torch.empty((N,), dtype=torch.float32, device=x.device) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        nb = int(L.lib().bnn_linear_nsmall_workspace(M, N, K)) if dw is not None or db is not None else 0
+        work = torch.empty((nb,), dtype=torch.uint8, device=x.device) if nb else None
+        with _timed("linear_nsmall_bwd", 4.0 * M * N * K, 8 * M * K):
+            L.call("bnn_linear_nsmall_bwd", L.ptr(x), L.ptr(w), L.ptr(dy), M, K, N, L.ptr(dx), L.ptr(dw), L.ptr(db),
+                   L.ptr(work), nb, L.stream())
+        return dx, dw, db
+
+
+def linear_nsmall_ok(x, weight):
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and weight.shape[0] in LINEAR_NSMALL
+            and x.shape[1] % 4 == 0 and x.shape[1] == weight.shape[1] and weight.numel() <= 16384)
+
+
+def linear_nsmall(x, weight, bias=None):
+    return LinearNSmallFunction.apply(x, weight, bias)
+
+
 # ----------------------------------------------------------------------------- conv2d
 def _pair_same(v, what):
     if isinstance(v, (tuple, list)):

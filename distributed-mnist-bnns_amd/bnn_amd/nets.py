@@ -151,6 +151,9 @@ class BinCNN(nn.Module):
     def forward(self, x):
         out = self._layer(self.layer2, self._layer(self.layer1, x))
         out = out.reshape(out.size(0), -1)
+        if self.fused_bn and BF.linear_nsmall_ok(out, self.fc.weight):
+            # the fp32 classifier through libbnn's narrow-Linear kernels (same parameters and math)
+            return self.logsoftmax(BF.linear_nsmall(out, self.fc.weight, self.fc.bias))
         return self.logsoftmax(self.fc(out))
 
 

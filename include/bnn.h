@@ -480,6 +480,19 @@ int bnn_bn_bwd_i8cols_pre(const float* x, const float* dy, int64_t M, int64_t C,
                           int64_t ldqt, int64_t plane, float* scale, float* colsum, int64_t* dsum, void* work,
                           bnn_stream_t stream);
 
+/* ---------------------------------------------------------------- narrow fp32 Linear
+ * The binarized CNN's classifier nn.Linear(7*7*32, 10) (BASELINE config 4; fp32, not binarized):
+ * y = x.w^T + b for x [M][K], w [N][K], y [M][N] (N in {1,2,4,8,10,16}, K % 4 == 0, N*K <= 16384
+ * (w is staged whole in LDS), x and w 16-B aligned, b nullable).  Backward: dx = dy.w, dw = dy^T.x,
+ * db = column sums of dy (each output nullable); dw / db need `work` of
+ * bnn_linear_nsmall_workspace(M, N, K) bytes.  fp32 products
+ * and sums in a fixed order (deterministic), the numerics class of torch's F.linear. */
+int64_t bnn_linear_nsmall_workspace(int64_t M, int64_t N, int64_t K);
+int bnn_linear_nsmall_fwd(const float* x, int64_t M, int64_t K, const float* w, const float* b, int64_t N,
+                          float* y, bnn_stream_t stream);
+int bnn_linear_nsmall_bwd(const float* x, const float* w, const float* dy, int64_t M, int64_t K, int64_t N,
+                          float* dx, float* dw, float* db, void* work, int64_t work_bytes, bnn_stream_t stream);
+
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */
 int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_stream_t stream);
