@@ -776,7 +776,7 @@ def _pixels_fwd_with_stats(q, wq, M, N, K, bscale, bias, R, s0):
     with _timed(name, 2.0 * M * N * K, M * Kp + N * Kp + 4 * M * N):
         L.call("bnn_gemm_i8_affine_bnstats", L.ptr(q), Kp, L.ptr(wq), Kp, L.ptr(bscale), L.ptr(bias), L.ptr(R),
                float(s0), L.ptr(y), N, M, N, Kp, L.ptr(part), rows, L.stream())
-    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N))
+    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N, "pixels"))
     return y
 
 
@@ -786,6 +786,27 @@ def _fstats_of(z, M, C):
     if fs is None or fs[3] != M or fs[4] != C or z._version != 0:
         return None
     return fs
+
+
+# fc2 -> bn2 (mnist-dist2.py:66-67): the FP4 forward's epilogue forms bn2's forward statistics from
+# the stored z = fl(sum + bias) (bnn_gemm_fp4_bnstats), carried on its output like fc1's.
+FP4_STATS = os.environ.get("BNN_FP4_STATS", "1") != "0"      # BNN_FP4_STATS=0: the statistics pass
+FP4_STATS_USES = 0
+
+
+def _fp4_fwd_with_stats(q, wq, M, N, k_true, bias, zbias, chunk, i16):
+    """(C [M, N] fp32 with bias, or int16 sums without; the statistics tuple for _FSTATS_ATTR)."""
+    Kb = q.shape[1]
+    assert wq.shape[1] == Kb and Kb % ALIGN == 0
+    rows = (M + chunk - 1) // chunk
+    part = torch.empty((2, rows, N), dtype=torch.float64, device=q.device)
+    C = torch.empty((M, N), dtype=torch.int16 if i16 else torch.float32, device=q.device)
+    name = (gemm_kernel_name(0, 0, M, N, Kb) + (" [i16]" if i16 else "")) if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * k_true, (M + N) * Kb + (2 if i16 else 4) * M * N):
+        L.call("bnn_gemm_fp4_bnstats", L.ptr(q), Kb, L.ptr(wq), Kb, L.ptr(None if i16 else bias),
+               None if i16 else L.ptr(C), L.ptr(C) if i16 else None, N, L.ptr(zbias), M, N, Kb, L.ptr(part), rows,
+               L.stream())
+    return C, (part, rows, chunk, M, N, "fp4")
 
 
 class BinaryLinearPixelsFunction(torch.autograd.Function):
@@ -1577,7 +1598,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
     dW = dY^T.sign(h) on the digit GEMM, then the fused BatchNorm+Hardtanh backward."""
 
     @staticmethod
-    def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend, emit_z16=False):
+    def forward(ctx, z, bn_w, bn_b, rm, rv, training, momentum, eps, weight, bias, backend, emit_z16=False,
+                emit_stats=False):
         _check(z, bn_w, bn_b, rm, rv, weight, bias)
         ctx.q6 = _q6_wanted(z, z.shape[-1], training)
         ctx.i8c = (I8C_HANDOFF and bool(getattr(z, _I8C_WANT, False)) and training and not ctx.q6
@@ -1598,10 +1620,13 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             ws = _bn_ws(M, C, z.device)
             mom = float(momentum if momentum is not None else -1.0)
             with _timed("bn_fwd_stats", 0, (4 if zz is None else 2) * M * C):
-                fs = _fstats_of(z, M, C) if zz is None else None
+                fs = _fstats_of(z, M, C)
                 if fs is not None:
-                    global PIX_STATS_USES
-                    PIX_STATS_USES += 1
+                    global PIX_STATS_USES, FP4_STATS_USES
+                    if fs[5] == "pixels":
+                        PIX_STATS_USES += 1
+                    else:
+                        FP4_STATS_USES += 1
                     L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(rm), L.ptr(rv), mom,
                            float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
                 elif zz is None:
@@ -1635,10 +1660,21 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                        1 if ctx.qt_panel else 0, L.stream())
         b = bias.detach() if bias is not None else None
         wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True, qt_fmt=qf)
+        chunk = (int(L.lib().bnn_gemm_fp4_bnstats_chunk(M, N, q.shape[1]))
+                 if emit_stats and FP4_STATS and fp4 and M > 0 and N % 4 == 0 else 0)
         if emit_z16 and fp4 and training:
             # the next BatchNorm reads z = fl(I + bias) from int16 I: a snapshot of the bias (the
             # optimizer updates the Parameter in place after this step's backward)
-            y = _z16_carrier(gemm_fp4_i16(q, wq, M, N, k_true=C), b.clone() if b is not None else None)
+            bs = b.clone() if b is not None else None
+            if chunk:
+                y16, fst = _fp4_fwd_with_stats(q, wq, M, N, C, None, bs, chunk, True)
+                y = _z16_carrier(y16, bs)
+                setattr(y, _FSTATS_ATTR, fst)
+            else:
+                y = _z16_carrier(gemm_fp4_i16(q, wq, M, N, k_true=C), bs)
+        elif fp4 and chunk:
+            y, fst = _fp4_fwd_with_stats(q, wq, M, N, C, b, b, chunk, False)
+            setattr(y, _FSTATS_ATTR, fst)
         elif fp4:
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
@@ -1712,14 +1748,14 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                 with _timed("bn_bwd", 0, 16 * M * C):
                     _bn_bwd_call(ctx.training, z, dh, M, C, gw, gb, mean, invstd, mlo, True, dz, dgw, dgb, ws)
         return (dz, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, dw, db, None, None)
+                None, None, None, None, None, dw, db, None, None, None)
 
 
-def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4", emit_z16=False):
+def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4", emit_z16=False, emit_stats=False):
     """fc(hardtanh(bn(z))) through BNHardtanhBinaryLinearFunction (bn: nn.BatchNorm1d, fc: a
     BinarizeLinear holding its latent weight, i.e. ``org_protocol = False``).  emit_z16: return
     fc's output as a z16 placeholder (its consumer must be a z16-aware libbnn BatchNorm pass:
     bn_hardtanh_binary_linear or dropout_bn_hardtanh_linear in training mode; see z16_ok)."""
     rm, rv, bn_training, factor = _bn_module_args(bn)
     return BNHardtanhBinaryLinearFunction.apply(z, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
-                                                fc.weight, fc.bias, backend, bool(emit_z16))
+                                                fc.weight, fc.bias, backend, bool(emit_z16), bool(emit_stats))

@@ -63,11 +63,12 @@ class MLP(nn.Module):
         return (self.fused_bn and z.is_cuda and z.dim() == 2 and z.shape[1] % 4 == 0 and not fc.org_protocol
                 and fc.backend in ("fp4", "mfma"))
 
-    def _bnh_fc(self, bn, ht, fc, z, emit_z16=False):
+    def _bnh_fc(self, bn, ht, fc, z, emit_z16=False, emit_stats=False):
         """fc(ht(bn(z))); fused into one libbnn op (no fp32 hardtanh output) when the fc keeps
-        its latent weight in the Parameter and runs an MFMA backend."""
+        its latent weight in the Parameter and runs an MFMA backend.  emit_stats: fc's FP4 forward
+        also forms the next (training-mode, fused) BatchNorm's forward statistics."""
         if self._fusable(fc, z):
-            return BF.bn_hardtanh_binary_linear(z, bn, fc, fc.backend, emit_z16=emit_z16)
+            return BF.bn_hardtanh_binary_linear(z, bn, fc, fc.backend, emit_z16=emit_z16, emit_stats=emit_stats)
         return fc(self._bnh(bn, ht, z))
 
     def _z16(self, fc, M, consumer):
@@ -89,7 +90,9 @@ class MLP(nn.Module):
         # fc2's output feeds the fused bn2 -> fc3 op; fc3's the fused head
         z16_2 = fuse2 and self._z16(self.fc2, M, self._fusable(self.fc3, z1) and self.fc3.backend == "fp4"
                                     and self.bn2.training)
-        x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, z1, emit_z16=z16_2)
+        # bn2 (no dropout ahead of it) takes its forward statistics from fc2's epilogue
+        st2 = fuse2 and self._fusable(self.fc3, z1) and self.bn2.training and self.training
+        x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, z1, emit_z16=z16_2, emit_stats=st2)
         z16_3 = (self._fusable(self.fc3, x) and self._z16(self.fc3, M, self._head_fused(self.fc3.out_features))
                  and x.is_cuda)
         x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x, emit_z16=z16_3)

@@ -47,6 +47,7 @@ struct GemmParams {
   // (bnn_gemm_i8_affine_bnstats): [2][stat_rows][N] doubles, chunk = this tile row's wave row
   double* stat = nullptr;
   int64_t stat_rows = 0;
+  const float* stat_bias = nullptr;   // FP4 statistics form: z = fl(sum + stat_bias[n]) (the int16 carrier's bias)
 };
 
 __device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
@@ -629,6 +630,56 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
       }
     }
   }
+  if constexpr (BST && F4 && DIAG == 0) {
+    if (p.stat != nullptr) {
+      // the next BatchNorm's forward statistics (bnn_gemm_fp4_bnstats): per column over this wave
+      // row's WM*32 rows, the chunk sum of the stored z = fl(sum + b) (the value the C / C16 + bias
+      // consumers see) and its M2 about the chunk mean, both from double sums in a fixed order --
+      // the sum is exact as bn_reduce_k's is, so the batch mean is the same double
+      const int cr0 = m0 + wm * WM * 32;
+      const int cnt = min(WM * 32, p.M - cr0);
+      const int64_t chunk = (int64_t)tm * WAVES_M + wm, RN = p.stat_rows * (int64_t)p.N;
+      const bool full = cr0 + WM * 32 <= p.M;
+      const int lim = p.M - cr0 - 4 * h;     // this lane's rows below M: offsets < lim
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const int col = n0 + wn * WN * 32 + u * TS + r;
+        const float sb = (p.stat_bias && col < p.N) ? p.stat_bias[col] : 0.f;
+        double s1 = 0.0, s2 = 0.0;
+        if (full) {
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int i = 0; i < TR; ++i) {
+              const double d = (double)(acc[0][t][u][i] + sb);
+              s1 += d;
+              s2 = fma(d, d, s2);
+            }
+        } else {
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int i = 0; i < TR; ++i) {
+              const int off = S16 ? t * 16 + i : t * 32 + (i & 3) + 8 * (i >> 2);
+              const double d = off < lim ? (double)(acc[0][t][u][i] + sb) : 0.0;
+              s1 += d;
+              s2 = fma(d, d, s2);
+            }
+        }
+        if constexpr (S16) {
+          s1 += __shfl_xor(s1, 16, 64);
+          s2 += __shfl_xor(s2, 16, 64);
+        }
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (h == 0 && cnt > 0 && col < p.N) {
+          p.stat[chunk * p.N + col] = s1;
+          const double m2 = s2 - s1 * s1 / cnt;
+          p.stat[RN + chunk * p.N + col] = m2 > 0.0 ? m2 : 0.0;
+        }
+      }
+    }
+  }
   float* patch = reinterpret_cast<float*>(smem) + wave * 1024;
   const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
   constexpr int SUB = S16 ? 2 : 1;   // MFMA tiles per patch edge
@@ -726,9 +777,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_i8_v2_k(GemmParam
 
 // FP4 (e2m1) ternary x ternary form: its own kernel name, so traces and the bench's peak lookup
 // tell it apart from the int8 forms
-template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0, int S16 = 0>
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0, int S16 = 0, int BST = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp4_k(GemmParams p) {
-  gemm_v2_body<1, 1, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, 0, 1, S16>(p);
+  gemm_v2_body<1, 1, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, 0, 1, S16, BST>(p);
 }
 
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
@@ -740,7 +791,7 @@ int launch_v2(GemmParams p, hipStream_t s) {
   const int64_t nblk = (int64_t)p.gm * p.gn;
   if constexpr (F4) {
     static_assert(DA == 1 && DB == 1 && DIAG == 0, "FP4 form");
-    hipLaunchKernelGGL((gemm_fp4_k<WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, S16>), dim3((unsigned)nblk),
+    hipLaunchKernelGGL((gemm_fp4_k<WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, S16, BST>), dim3((unsigned)nblk),
                        dim3(64 * WAVES_M * WAVES_N), 0, s, p);
     return check_launch("bnn_gemm_fp4");
   } else {
@@ -960,6 +1011,38 @@ BNN_API int bnn_gemm_fp4_i16(const uint8_t* A, int64_t lda, const uint8_t* B, in
   GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
                nullptr, nullptr, nullptr, nullptr, ldc, (int)M, (int)N, (int)K, 0, 0, nullptr, nullptr, 0.0, C16};
   return pick_kernel(0, 0, M, N, K)->fn(p, reinterpret_cast<hipStream_t>(stream));
+}
+
+// The FP4 forward with the next BatchNorm's forward statistics (its own instances of the default
+// choices: 256x256 tiles with 128-row chunks on big grids, 128x128 with 64-row chunks otherwise)
+// 0: no statistics form for this shape (the big-grid BK=64 fallback, K % 128 != 0, would spill)
+BNN_API int64_t bnn_gemm_fp4_bnstats_chunk(int64_t M, int64_t N, int64_t K) {
+  const int id = pick_kernel(0, 0, M, N, K)->id;
+  return id == 31 ? 64 : (id == 36 ? 128 : 0);
+}
+
+BNN_API int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
+                                 float* C, int16_t* C16, int64_t ldc, const float* zbias, int64_t M, int64_t N,
+                                 int64_t K, double* stat, int64_t stat_rows, void* stream) {
+  const int64_t chunk = (M > 0 && N > 0 && K > 0) ? bnn_gemm_fp4_bnstats_chunk(M, N, K) : 1;
+  const bool c16 = C16 != nullptr;
+  if (chunk <= 0 || !A || !B || (C == nullptr) == (C16 == nullptr) || (c16 && bias) || !stat || M <= 0 || N <= 0 || K <= 0 ||
+      K % BK != 0 || lda < K || ldb < K || lda % 16 != 0 || ldb % 16 != 0 || ldc < N || !aligned16(A) ||
+      !aligned16(B) || M > 0x7fffffff || N > 0x7fffffff || lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31) ||
+      (c16 && (ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(C16) & 7) != 0 || 2 * K > 32767)) ||
+      stat_rows != (M + chunk - 1) / chunk) {
+    set_error("bnn_gemm_fp4_bnstats: bad arguments (M=%lld N=%lld K=%lld bytes, stat_rows=%lld; one of C / C16, "
+              "no bias with C16)", (long long)M, (long long)N, (long long)K, (long long)stat_rows);
+    return kErrInval;
+  }
+  GemmParams p{reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B), lda, ldb, 0, 0,
+               nullptr, nullptr, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, nullptr, nullptr, 0.0, C16};
+  p.stat = stat;
+  p.stat_rows = stat_rows;
+  p.stat_bias = zbias;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return chunk == 128 ? launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1, 1>(p, st)
+                      : launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 1, 0, 1>(p, st);
 }
 
 BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, int64_t N,

@@ -124,6 +124,18 @@ int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_
  * integer sums S (no pass over C); stat_rows = ceil(M / chunk).  Feed to bnn_bn_fwd_final_parts.
  * The statistics are those of the unrounded z (C holds its fp32 rounding). */
 int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N);
+
+/* The FP4 forward (bnn_gemm_fp4 with C, or bnn_gemm_fp4_i16 with C16 and bias NULL) that also hands
+ * the next BatchNorm (no dropout in between: mnist-dist2.py:66-67, fc2 -> bn2) its forward
+ * statistics: stat = [2][stat_rows][N] doubles, per column and chunk of
+ * bnn_gemm_fp4_bnstats_chunk(M, N, K) rows the sum of the stored z = fl(sum + zbias[n]) (exact in
+ * double, as bnn_bn_fwd_train's) and its M2 about the chunk mean; stat_rows = ceil(M / chunk).
+ * chunk 0 = no statistics form for the shape (use the statistics pass).  Feed the partials to
+ * bnn_bn_fwd_final_parts. */
+int64_t bnn_gemm_fp4_bnstats_chunk(int64_t M, int64_t N, int64_t K);
+int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
+                         float* C, int16_t* C16, int64_t ldc, const float* zbias, int64_t M, int64_t N, int64_t K,
+                         double* stat, int64_t stat_rows, bnn_stream_t stream);
 int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
                                const float* b_scale, const float* bias, const int64_t* col_off,
                                double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,

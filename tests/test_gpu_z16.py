@@ -11,7 +11,14 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import rel_err
+
 pytestmark = pytest.mark.gpu
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
 
 
 @pytest.fixture(scope="module")
@@ -210,3 +217,79 @@ def test_mlp_step_with_z16_equals_fp32(F):
     assert la == lb
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("M,K,N,i16", [(65536 // 4, 2048, 4096, True), (65536 // 4, 2048, 4096, False),
+                                       (1000, 768, 1536, True), (333, 512, 256, False)])
+def test_gemm_fp4_bnstats_epilogue(F, M, K, N, i16):
+    """bnn_gemm_fp4_bnstats: C (fp32 + bias) / C16 bit-identical to bnn_gemm_fp4 / bnn_gemm_fp4_i16;
+    chunk sums of the stored z = fl(I + b) equal float64 sums of the same fp32 values (the double
+    sum is exact), M2 within 1e-9; the final (bnn_bn_fwd_final_parts) mean hi/lo bit-identical to
+    bnn_bn_fwd_train's on the same z, invstd and running statistics within 1e-6."""
+    from bnn_amd import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    h = torch.randint(-1, 2, (M, K), generator=g, device="cuda").float()
+    w = torch.randint(-1, 2, (N, K), generator=g, device="cuda").float()
+    b = torch.randn(N, generator=g, device="cuda")
+    q, _ = F.sign_pack_fp4(h)
+    wq, _ = F.sign_pack_fp4(w)
+    chunk = int(L.lib().bnn_gemm_fp4_bnstats_chunk(M, N, q.shape[1]))
+    assert chunk in (64, 128)
+    if i16:
+        c0 = F.gemm_fp4_i16(q, wq, M, N, k_true=K)
+        c1, fst = F._fp4_fwd_with_stats(q, wq, M, N, K, None, b, chunk, True)
+        z = c0.float() + b
+    else:
+        c0 = F.gemm_fp4(q, wq, M, N, bias=b, k_true=K)
+        c1, fst = F._fp4_fwd_with_stats(q, wq, M, N, K, b, b, chunk, False)
+        z = c0
+    assert torch.equal(c0, c1)
+    part, rows = fst[0], fst[1]
+    zh = host(z).astype(np.float64)
+    ph = host(part)
+    for r in range(rows):
+        zc = zh[r * chunk:(r + 1) * chunk]
+        assert np.array_equal(ph[0, r], zc.sum(0)) or rel_err(ph[0, r], zc.sum(0)) <= 1e-15
+        assert rel_err(ph[1, r], ((zc - zc.mean(0)) ** 2).sum(0)) <= 1e-9
+    mean0, istd0, lo0 = F._bn_stat_buffers(N, "cuda")
+    mean1, istd1, lo1 = (t.clone() for t in F._bn_stat_buffers(N, "cuda"))
+    rm0, rv0 = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    L.call("bnn_bn_fwd_train", L.ptr(z.contiguous()), M, N, None, None, L.ptr(rm0), L.ptr(rv0), 0.1, 1e-5,
+           L.ptr(mean0), L.ptr(istd0), L.ptr(lo0), None, 1, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
+    L.call("bnn_bn_fwd_final_parts", L.ptr(part), rows, chunk, M, N, L.ptr(rm1), L.ptr(rv1), 0.1, 1e-5,
+           L.ptr(mean1), L.ptr(istd1), L.ptr(lo1), L.stream())
+    assert torch.equal(mean0, mean1) and torch.equal(lo0, lo1)
+    assert rel_err(host(istd1), host(istd0)) <= 1e-6
+    assert rel_err(host(rm1), host(rm0)) <= 1e-6 and rel_err(host(rv1), host(rv0)) <= 1e-6
+
+
+def test_mlp_step_fp4_statistics_epilogue(F):
+    """A fused MLP training step with bn2's forward statistics from fc2's FP4 epilogue
+    (functional.FP4_STATS) against the statistics pass: loss within 1e-6, bn2's running buffers
+    within 1e-6, gradients within 1e-4 norm-wise (invstd may differ in its last bit)."""
+    from bnn_amd import nets
+    g = torch.Generator(device="cuda").manual_seed(4)
+    u = torch.randint(0, 256, (8192, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    y = torch.randint(0, 10, (8192,), generator=g, device="cuda")
+    out = []
+    on0 = F.FP4_STATS
+    for on in (True, False):
+        F.FP4_STATS = on
+        try:
+            torch.manual_seed(0)
+            m = nets.MLP(2048, 2048, 1024, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+            n0 = F.FP4_STATS_USES
+            loss = torch.nn.CrossEntropyLoss()(m(u), y)
+            loss.backward()
+            uses = F.FP4_STATS_USES - n0
+            out.append((float(loss), {k: host(p.grad) for k, p in m.named_parameters()},
+                        host(m.bn2.running_mean), host(m.bn2.running_var), uses))
+        finally:
+            F.FP4_STATS = on0
+    (l1, g1, rm1, rv1, u1), (l0, g0, rm0, rv0, u0) = out
+    assert u1 == 1 and u0 == 0              # bn2 took fc2's epilogue statistics
+    assert abs(l1 - l0) <= 1e-6 * abs(l0)
+    assert rel_err(rm1, rm0) <= 1e-6 and rel_err(rv1, rv0) <= 1e-6
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) <= 1e-4 or np.abs(g1[k] - g0[k]).max() <= 1e-9, k
