@@ -48,6 +48,9 @@ struct GemmParams {
   double* stat = nullptr;
   int64_t stat_rows = 0;
   const float* stat_bias = nullptr;   // FP4 statistics form: z = fl(sum + stat_bias[n]) (the int16 carrier's bias)
+  // 1: row-major tile order (consecutive tiles along N: concurrent tiles write adjacent segments of
+  // the same C rows) instead of the grouped raster
+  int raster = 0;
 };
 
 __device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
@@ -321,7 +324,15 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   int tm, tn;
-  tile_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  if (p.raster == 1) {   // XCD remap only, then row-major
+    const int nwg = p.gm * p.gn, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int L = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    tm = L / p.gn;
+    tn = L - tm * p.gn;
+  } else {
+    tile_of(blockIdx.x, p.gm, p.gn, tm, tn);
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // chunk swizzle: BK=64 -> chunk ^ ((row>>2)&3); BK=128 -> chunk ^ ((row>>1)&7).  Applied to the
@@ -802,6 +813,7 @@ int launch_v2(GemmParams p, hipStream_t s) {
 }
 
 int g_variant = -1;  // tuning hook (bnn_gemm_set_variant); -1 = default table
+int g_raster = 0;    // tuning hook (bnn_gemm_set_raster): GemmParams::raster of the affine entry
 
 template <int DA, int DB, int WM, int WN>
 int launch(GemmParams p, hipStream_t s) {
@@ -927,6 +939,7 @@ BNN_API int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, in
   if (M == 0 || N == 0) return 0;
   GemmParams p{A, B, lda, ldb, a_plane, b_plane, a_scale, b_scale, bias, C, ldc,
                (int)M, (int)N, (int)K, 0, 0, row_off, col_off, off_mul};
+  p.raster = g_raster;
   // v2 kernels address a tile's rows with 32-bit per-lane offsets (< 256 rows x ld)
   if (lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31))
     return find_variant(a_digits == 1 ? 0 : (b_digits == 1 ? 10 : 20))->fn(p, reinterpret_cast<hipStream_t>(stream));
@@ -1055,6 +1068,11 @@ BNN_API const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64
 
 // Tuning hook: select a kernel variant for every later bnn_gemm_i8 call in this process
 // (-1 = built-in default).  Not part of the stable ABI contract; used by tools/gemm_sweep.py.
+BNN_API int bnn_gemm_set_raster(int32_t r) {
+  g_raster = r;
+  return 0;
+}
+
 BNN_API int bnn_gemm_set_variant(int32_t v) {
   g_variant = v;
   return 0;

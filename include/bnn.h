@@ -172,6 +172,8 @@ int bnn_gemm_fp4_i16(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ld
 /* Tuning hook (not part of the stable contract): select the bnn_gemm_i8 kernel variant for all
  * later calls in this process; -1 restores the built-in default table (tools/gemm_sweep.py). */
 int bnn_gemm_set_variant(int32_t variant);
+/* Tuning hook: tile order of later bnn_gemm_i8_affine calls (0 = grouped raster, 1 = row-major). */
+int bnn_gemm_set_raster(int32_t raster);
 /* Name of the kernel instance bnn_gemm_i8 launches for this configuration (as rocprofv3 lists
  * it), so host-side HIP-event timings can be matched with profiles; a_digits = b_digits = 0
  * names the bnn_gemm_fp4 kernel (K in bytes). */
