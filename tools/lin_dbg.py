@@ -1,3 +1,7 @@
+"""Quick check of bnn_linear_nsmall_fwd against float64 at a few shapes (prints the max error).
+
+    python tools/lin_dbg.py
+"""
 import sys, os
 sys.path.insert(0, "distributed-mnist-bnns_amd")
 import torch
