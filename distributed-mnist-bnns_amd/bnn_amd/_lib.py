@@ -34,7 +34,8 @@ SIGNATURES = {
                                  I64, I64, I64, P]),
     "bnn_gemm_i8_bnstats_chunk": (I64, [I64, I64]),
     "bnn_gemm_fp4_bnstats_chunk": (I64, [I64, I64, I64]),
-    "bnn_gemm_fp4_bnstats": (I32, [P, I64, P, I64, P, P, P, I64, P, I64, I64, I64, P, I64, P]),
+    "bnn_gemm_fp4_bnstats": (I32, [P, I64, P, I64, P, P, P, I64, P, I64, I64, I64, F32, ctypes.c_uint64, P, I64,
+                                   P]),
     "bnn_gemm_i8_affine_bnstats": (I32, [P, I64, P, I64, P, P, P, ctypes.c_double, P, I64, I64, I64, I64, P, I64,
                                          P]),
     "bnn_linear_nsmall_workspace": (I64, [I64, I64, I64]),

@@ -776,14 +776,18 @@ def _pixels_fwd_with_stats(q, wq, M, N, K, bscale, bias, R, s0):
     with _timed(name, 2.0 * M * N * K, M * Kp + N * Kp + 4 * M * N):
         L.call("bnn_gemm_i8_affine_bnstats", L.ptr(q), Kp, L.ptr(wq), Kp, L.ptr(bscale), L.ptr(bias), L.ptr(R),
                float(s0), L.ptr(y), N, M, N, Kp, L.ptr(part), rows, L.stream())
-    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N, "pixels"))
+    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N, "pixels", 0.0, 0))
     return y
 
 
-def _fstats_of(z, M, C):
-    """The forward-statistics partials a pixel GEMM attached to z (None if absent or stale)."""
+def _fstats_of(z, M, C, drop=(0.0, 0)):
+    """The forward-statistics partials a GEMM epilogue attached to z (None if absent, stale, or
+    formed for another dropout (p, seed) than the consuming BatchNorm's)."""
     fs = getattr(z, _FSTATS_ATTR, None)
     if fs is None or fs[3] != M or fs[4] != C or z._version != 0:
+        return None
+    p, seed = float(drop[0]), int(drop[1])
+    if fs[6] != p or (p > 0 and fs[7] != seed):
         return None
     return fs
 
@@ -794,8 +798,9 @@ FP4_STATS = os.environ.get("BNN_FP4_STATS", "1") != "0"      # BNN_FP4_STATS=0: 
 FP4_STATS_USES = 0
 
 
-def _fp4_fwd_with_stats(q, wq, M, N, k_true, bias, zbias, chunk, i16):
-    """(C [M, N] fp32 with bias, or int16 sums without; the statistics tuple for _FSTATS_ATTR)."""
+def _fp4_fwd_with_stats(q, wq, M, N, k_true, bias, zbias, chunk, i16, drop=(0.0, 0)):
+    """(C [M, N] fp32 with bias, or int16 sums without; the statistics tuple for _FSTATS_ATTR).
+    drop = (p, seed): the statistics of drop(z) for a fused dropout BatchNorm with that seed."""
     Kb = q.shape[1]
     assert wq.shape[1] == Kb and Kb % ALIGN == 0
     rows = (M + chunk - 1) // chunk
@@ -804,9 +809,9 @@ def _fp4_fwd_with_stats(q, wq, M, N, k_true, bias, zbias, chunk, i16):
     name = (gemm_kernel_name(0, 0, M, N, Kb) + (" [i16]" if i16 else "")) if _TIMER is not None else ""
     with _timed(name, 2.0 * M * N * k_true, (M + N) * Kb + (2 if i16 else 4) * M * N):
         L.call("bnn_gemm_fp4_bnstats", L.ptr(q), Kb, L.ptr(wq), Kb, L.ptr(None if i16 else bias),
-               None if i16 else L.ptr(C), L.ptr(C) if i16 else None, N, L.ptr(zbias), M, N, Kb, L.ptr(part), rows,
-               L.stream())
-    return C, (part, rows, chunk, M, N, "fp4")
+               None if i16 else L.ptr(C), L.ptr(C) if i16 else None, N, L.ptr(zbias), M, N, Kb, float(drop[0]),
+               int(drop[1]), L.ptr(part), rows, L.stream())
+    return C, (part, rows, chunk, M, N, "fp4", float(drop[0]), int(drop[1]))
 
 
 class BinaryLinearPixelsFunction(torch.autograd.Function):
@@ -1373,15 +1378,22 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         ws = _bn_ws(M, C, z.device)
         mean, invstd, mlo = _bn_stat_buffers(C, z.device)
         mom = float(momentum if momentum is not None else -1.0)
-        with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
-            if zz is None:
-                L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
-                       L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p),
-                       int(seed), L.ptr(ws), L.stream())
-            else:
-                L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
-                       L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
-                       L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
+        fs = _fstats_of(z, M, C, (float(p), int(seed)))
+        if fs is not None and float(p) > 0:
+            global FP4_STATS_USES
+            FP4_STATS_USES += 1
+            L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(running_mean),
+                   L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
+        else:
+            with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
+                if zz is None:
+                    L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
+                           L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1,
+                           float(p), int(seed), L.ptr(ws), L.stream())
+                else:
+                    L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
+                           L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
+                           L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
         w4c = w4.detach().contiguous()
         y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
         b4d = b4.detach() if b4 is not None else None
@@ -1446,10 +1458,15 @@ def head_fusable(x, bn, fc):
             and fc.in_features == x.shape[1] and bn.momentum is not None)
 
 
+def dropout_seed():
+    """The seed of a fused dropout: the graph step's base seed, else one draw of torch's CPU RNG."""
+    return _DEVICE_STEP.base_seed if _DEVICE_STEP is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
 def dropout_bn_hardtanh_linear(x, p, bn, fc, seed=None):
     """fc(hardtanh(bn(nn.Dropout(p)(x)))) through libbnn (training mode; see head_fusable)."""
     if seed is None:
-        seed = _DEVICE_STEP.base_seed if _DEVICE_STEP is not None else int(torch.randint(0, 2 ** 62, (1,)).item())
+        seed = dropout_seed()
     rm, rv, bn_training, factor = _bn_module_args(bn)
     if not bn_training:
         raise ValueError("dropout_bn_hardtanh_linear is the training-mode fusion")
@@ -1662,18 +1679,19 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         wq, wqt = packed_weight(weight, "fp4" if fp4 else "i8", True, need_dh, cache=True, qt_fmt=qf)
         chunk = (int(L.lib().bnn_gemm_fp4_bnstats_chunk(M, N, q.shape[1]))
                  if emit_stats and FP4_STATS and fp4 and M > 0 and N % 4 == 0 else 0)
+        drop = tuple(emit_stats) if isinstance(emit_stats, tuple) else (0.0, 0)   # (p, seed) of a fused dropout
         if emit_z16 and fp4 and training:
             # the next BatchNorm reads z = fl(I + bias) from int16 I: a snapshot of the bias (the
             # optimizer updates the Parameter in place after this step's backward)
             bs = b.clone() if b is not None else None
             if chunk:
-                y16, fst = _fp4_fwd_with_stats(q, wq, M, N, C, None, bs, chunk, True)
+                y16, fst = _fp4_fwd_with_stats(q, wq, M, N, C, None, bs, chunk, True, drop)
                 y = _z16_carrier(y16, bs)
                 setattr(y, _FSTATS_ATTR, fst)
             else:
                 y = _z16_carrier(gemm_fp4_i16(q, wq, M, N, k_true=C), bs)
         elif fp4 and chunk:
-            y, fst = _fp4_fwd_with_stats(q, wq, M, N, C, b, b, chunk, False)
+            y, fst = _fp4_fwd_with_stats(q, wq, M, N, C, b, b, chunk, False, drop)
             setattr(y, _FSTATS_ATTR, fst)
         elif fp4:
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
@@ -1758,4 +1776,5 @@ def bn_hardtanh_binary_linear(z, bn, fc, backend="fp4", emit_z16=False, emit_sta
     bn_hardtanh_binary_linear or dropout_bn_hardtanh_linear in training mode; see z16_ok)."""
     rm, rv, bn_training, factor = _bn_module_args(bn)
     return BNHardtanhBinaryLinearFunction.apply(z, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
-                                                fc.weight, fc.bias, backend, bool(emit_z16), bool(emit_stats))
+                                                fc.weight, fc.bias, backend, bool(emit_z16),
+                                                emit_stats if isinstance(emit_stats, tuple) else bool(emit_stats))

@@ -95,6 +95,9 @@ class MLP(nn.Module):
         x = self._bnh_fc(self.bn1, self.htanh1, self.fc2, z1, emit_z16=z16_2, emit_stats=st2)
         z16_3 = (self._fusable(self.fc3, x) and self._z16(self.fc3, M, self._head_fused(self.fc3.out_features))
                  and x.is_cuda)
+        # (bn3's statistics of drop(z3) could come from fc3's epilogue too -- emit_stats=(p, seed) with
+        # the head's seed drawn first -- but the mask hash in the epilogue costs more than the pass:
+        # DESIGN §5)
         x = self._bnh_fc(self.bn2, self.htanh2, self.fc3, x, emit_z16=z16_3)
         if (self.fused_bn and self.fused_head and self.training and self.bn3.training
                 and BF.head_fusable(x, self.bn3, self.fc4)):

@@ -22,6 +22,7 @@
 #include "bnn_fp6.h"
 
 namespace bnn {
+const int64_t* g_seed_ctr = nullptr;   // bnn_set_seed_counter (declared in bnn_common.h)
 namespace {
 
 constexpr int BN_ROWS = 256;  // most rows per partial-statistics chunk
@@ -44,50 +45,8 @@ inline dim3 reduce_grid(int64_t M, int64_t C) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// Fused nn.Dropout(p) in front of a BatchNorm (mnist-dist2.py:69-70: fc3 -> drop -> bn3).  The
-// keep mask is a counter-based hash of (seed, element index), so forward statistics, forward
-// apply and both backward passes regenerate the same mask without storing it; kept elements are
-// scaled by 1/(1-p) exactly as torch's dropout does (x * scale, grad * scale).
-struct Drop {
-  uint64_t seed;
-  uint32_t thresh;  // keep iff hash < thresh
-  int on;
-  float scale;      // 1 / (1 - p)
-  const int64_t* ctr = nullptr;   // device step counter folded into the seed (bnn_set_seed_counter)
-};
-
-// Process-wide device step counter for graph-captured training steps: dropout launches made
-// while it is set draw their mask from seed + ctr[0] * golden, so one captured graph replays with
-// a fresh mask per step (forward and backward of a step read the same counter value).
-const int64_t* g_seed_ctr = nullptr;
-
-__device__ __forceinline__ Drop drop_resolve(Drop d) {
-  if (d.on && d.ctr != nullptr) d.seed += (uint64_t)d.ctr[0] * 0xD1B54A32D192ED03ull;
-  return d;
-}
-
-// 32-bit arithmetic only: one murmur3 fmix32 round of (element index * golden) XOR a 32-bit key
-// folded from the 64-bit seed (the key is loop-invariant: the compiler hoists it, so an element
-// costs one multiply-xor and the round).  The element index is taken mod 2^32; the mask of every
-// pass over the same tensor is the same function of it.  XOR keying (not a Weyl offset) so two
-// seeds never give shifted copies of one mask.
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  return h ^ (h >> 16);
-}
-
-__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
-  return (uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x5BD1E995u);
-}
-
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
-  return fmix32((uint32_t)i * 0x9E3779B1u ^ drop_key(seed));
-}
-
-__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
+// Drop, drop_hash, drop_resolve, g_seed_ctr: bnn_common.h (the FP4 statistics epilogue evaluates
+// the same mask)
 
 // keep bits of elements i0 .. i0+3 (bit j), evaluated once and applied to both the input and the
 // gradient where a pass needs both
@@ -109,16 +68,6 @@ __device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4])
   drop4m(d, drop_bits4(d, i0), v);
 }
 
-inline Drop make_drop(float p, uint64_t seed) {
-  Drop d{seed, 0u, 0, 1.f, g_seed_ctr};
-  if (p > 0.f && p < 1.f) {
-    const double t = (1.0 - (double)p) * 4294967296.0;
-    d.thresh = t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
-    d.on = 1;
-    d.scale = 1.f / (1.f - p);
-  }
-  return d;
-}
 
 // MODE 0: per-chunk (mean, M2), accumulated as deviations from the chunk's first row so the
 //         float partials see deviations rather than raw magnitudes; merged with Chan's formula.

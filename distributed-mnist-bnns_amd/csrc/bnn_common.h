@@ -183,4 +183,61 @@ __device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v,
   return pi;
 }
 
+// Fused nn.Dropout(p) in front of a BatchNorm (mnist-dist2.py:69-70: fc3 -> drop -> bn3).  The
+// keep mask is a counter-based hash of (seed, element index), so forward statistics, forward
+// apply and both backward passes regenerate the same mask without storing it; kept elements are
+// scaled by 1/(1-p) exactly as torch's dropout does (x * scale, grad * scale).
+struct Drop {
+  uint64_t seed;
+  uint32_t thresh;  // keep iff hash < thresh
+  int on;
+  float scale;      // 1 / (1 - p)
+  const int64_t* ctr = nullptr;   // device step counter folded into the seed (bnn_set_seed_counter)
+};
+
+// Process-wide device step counter for graph-captured training steps: dropout launches made
+// while it is set draw their mask from seed + ctr[0] * golden, so one captured graph replays with
+// a fresh mask per step (forward and backward of a step read the same counter value).
+extern const int64_t* g_seed_ctr;   // defined in bnn_bn.hip
+
+__device__ __forceinline__ Drop drop_resolve(Drop d) {
+  if (d.on && d.ctr != nullptr) d.seed += (uint64_t)d.ctr[0] * 0xD1B54A32D192ED03ull;
+  return d;
+}
+
+// 32-bit arithmetic only: one murmur3 fmix32 round of (element index * golden) XOR a 32-bit key
+// folded from the 64-bit seed (the key is loop-invariant: the compiler hoists it, so an element
+// costs one multiply-xor and the round).  The element index is taken mod 2^32; the mask of every
+// pass over the same tensor is the same function of it.  XOR keying (not a Weyl offset) so two
+// seeds never give shifted copies of one mask.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+  return (uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x5BD1E995u);
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
+  return fmix32((uint32_t)i * 0x9E3779B1u ^ drop_key(seed));
+}
+
+__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
+
+
+inline Drop make_drop(float p, uint64_t seed) {
+  Drop d{seed, 0u, 0, 1.f, g_seed_ctr};
+  if (p > 0.f && p < 1.f) {
+    const double t = (1.0 - (double)p) * 4294967296.0;
+    d.thresh = t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+    d.on = 1;
+    d.scale = 1.f / (1.f - p);
+  }
+  return d;
+}
+
 }  // namespace bnn

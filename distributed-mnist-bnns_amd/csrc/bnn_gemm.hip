@@ -48,6 +48,7 @@ struct GemmParams {
   double* stat = nullptr;
   int64_t stat_rows = 0;
   const float* stat_bias = nullptr;   // FP4 statistics form: z = fl(sum + stat_bias[n]) (the int16 carrier's bias)
+  Drop stat_drop{0, 0u, 0, 1.f, nullptr};   // ... of drop(z) when a fused dropout precedes the BatchNorm
   // 1: row-major tile order (consecutive tiles along N: concurrent tiles write adjacent segments of
   // the same C rows) instead of the grouped raster
   int raster = 0;
@@ -652,12 +653,27 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
       const int64_t chunk = (int64_t)tm * WAVES_M + wm, RN = p.stat_rows * (int64_t)p.N;
       const bool full = cr0 + WM * 32 <= p.M;
       const int lim = p.M - cr0 - 4 * h;     // this lane's rows below M: offsets < lim
+      const Drop dp = drop_resolve(p.stat_drop);
 #pragma unroll
       for (int u = 0; u < TN; ++u) {
         const int col = n0 + wn * WN * 32 + u * TS + r;
         const float sb = (p.stat_bias && col < p.N) ? p.stat_bias[col] : 0.f;
         double s1 = 0.0, s2 = 0.0;
-        if (full) {
+        if (dp.on) {
+          // the BatchNorm sees drop(z): the element-index mask of its own passes, x * scale kept
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int i = 0; i < TR; ++i) {
+              const int off = S16 ? t * 16 + i : t * 32 + (i & 3) + 8 * (i >> 2);
+              const int64_t idx = (int64_t)(cr0 + 4 * h + off) * p.N + col;
+              const float xv = acc[0][t][u][i] + sb;
+              const float xd = drop_keep(dp, (uint64_t)idx) ? xv * dp.scale : 0.f;
+              const double d = (full || off < lim) ? (double)xd : 0.0;
+              s1 += d;
+              s2 = fma(d, d, s2);
+            }
+        } else if (full) {
 #pragma unroll
           for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -1036,7 +1052,12 @@ BNN_API int64_t bnn_gemm_fp4_bnstats_chunk(int64_t M, int64_t N, int64_t K) {
 
 BNN_API int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
                                  float* C, int16_t* C16, int64_t ldc, const float* zbias, int64_t M, int64_t N,
-                                 int64_t K, double* stat, int64_t stat_rows, void* stream) {
+                                 int64_t K, float drop_p, uint64_t drop_seed, double* stat, int64_t stat_rows,
+                                 void* stream) {
+  if (!(drop_p >= 0.f && drop_p < 1.f)) {
+    set_error("bnn_gemm_fp4_bnstats: drop_p must be in [0, 1) (got %g)", (double)drop_p);
+    return kErrInval;
+  }
   const int64_t chunk = (M > 0 && N > 0 && K > 0) ? bnn_gemm_fp4_bnstats_chunk(M, N, K) : 1;
   const bool c16 = C16 != nullptr;
   if (chunk <= 0 || !A || !B || (C == nullptr) == (C16 == nullptr) || (c16 && bias) || !stat || M <= 0 || N <= 0 || K <= 0 ||
@@ -1053,6 +1074,7 @@ BNN_API int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B
   p.stat = stat;
   p.stat_rows = stat_rows;
   p.stat_bias = zbias;
+  p.stat_drop = make_drop(drop_p, drop_seed);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return chunk == 128 ? launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 2, 0, 1, 1, 1>(p, st)
                       : launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 1, 0, 1>(p, st);

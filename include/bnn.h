@@ -126,16 +126,18 @@ int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, int32_t a_
 int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N);
 
 /* The FP4 forward (bnn_gemm_fp4 with C, or bnn_gemm_fp4_i16 with C16 and bias NULL) that also hands
- * the next BatchNorm (no dropout in between: mnist-dist2.py:66-67, fc2 -> bn2) its forward
- * statistics: stat = [2][stat_rows][N] doubles, per column and chunk of
- * bnn_gemm_fp4_bnstats_chunk(M, N, K) rows the sum of the stored z = fl(sum + zbias[n]) (exact in
- * double, as bnn_bn_fwd_train's) and its M2 about the chunk mean; stat_rows = ceil(M / chunk).
+ * the next BatchNorm (mnist-dist2.py:66-67, fc2 -> bn2; or fc3 -> drop -> bn3 with drop_p > 0 and
+ * the seed the fused dropout BatchNorm passes will use, :68-70) its forward statistics:
+ * stat = [2][stat_rows][N] doubles, per column and chunk of bnn_gemm_fp4_bnstats_chunk(M, N, K)
+ * rows the sum of the stored z = fl(sum + zbias[n]) (dropped: fl(z * 1/(1-p)) or 0, the mask of
+ * bnn_bn_dropout_fwd_train) -- exact in double, as bnn_bn_fwd_train's -- and its M2 about the
+ * chunk mean; stat_rows = ceil(M / chunk).
  * chunk 0 = no statistics form for the shape (use the statistics pass).  Feed the partials to
  * bnn_bn_fwd_final_parts. */
 int64_t bnn_gemm_fp4_bnstats_chunk(int64_t M, int64_t N, int64_t K);
 int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
                          float* C, int16_t* C16, int64_t ldc, const float* zbias, int64_t M, int64_t N, int64_t K,
-                         double* stat, int64_t stat_rows, bnn_stream_t stream);
+                         float drop_p, uint64_t drop_seed, double* stat, int64_t stat_rows, bnn_stream_t stream);
 int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
                                const float* b_scale, const float* bias, const int64_t* col_off,
                                double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,

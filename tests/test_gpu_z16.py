@@ -293,3 +293,38 @@ def test_mlp_step_fp4_statistics_epilogue(F):
     assert rel_err(rm1, rm0) <= 1e-6 and rel_err(rv1, rv0) <= 1e-6
     for k in g0:
         assert rel_err(g1[k], g0[k]) <= 1e-4 or np.abs(g1[k] - g0[k]).max() <= 1e-9, k
+
+
+@pytest.mark.parametrize("i16", [True, False])
+def test_gemm_fp4_bnstats_dropout(F, i16):
+    """The dropout form of bnn_gemm_fp4_bnstats: its final (bnn_bn_fwd_final_parts) against
+    bnn_bn_dropout_fwd_train on the fp32 z with the same p and seed -- mean hi / lo bit-identical
+    (both sum the same dropped fp32 values exactly in double), invstd and running statistics within
+    1e-6; a different seed gives other statistics."""
+    from bnn_amd import _lib as L
+    M, K, N, p, seed = 8192, 2048, 1024, 0.3, 123456789
+    g = torch.Generator(device="cuda").manual_seed(99)
+    h = torch.randint(-1, 2, (M, K), generator=g, device="cuda").float()
+    w = torch.randint(-1, 2, (N, K), generator=g, device="cuda").float()
+    b = torch.randn(N, generator=g, device="cuda")
+    q, _ = F.sign_pack_fp4(h)
+    wq, _ = F.sign_pack_fp4(w)
+    chunk = int(L.lib().bnn_gemm_fp4_bnstats_chunk(M, N, q.shape[1]))
+    z = F.gemm_fp4(q, wq, M, N, bias=b, k_true=K)
+    res = []
+    for sd in (seed, seed + 1):
+        c1, fst = F._fp4_fwd_with_stats(q, wq, M, N, K, None if i16 else b, b, chunk, i16, (p, sd))
+        mean1, istd1, lo1 = (t.clone() for t in F._bn_stat_buffers(N, "cuda"))
+        rm1, rv1 = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+        L.call("bnn_bn_fwd_final_parts", L.ptr(fst[0]), fst[1], chunk, M, N, L.ptr(rm1), L.ptr(rv1), 0.1, 1e-5,
+               L.ptr(mean1), L.ptr(istd1), L.ptr(lo1), L.stream())
+        res.append((mean1, istd1, lo1, rm1, rv1))
+    mean0, istd0, lo0 = F._bn_stat_buffers(N, "cuda")
+    rm0, rv0 = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, N, None, None, L.ptr(rm0), L.ptr(rv0), 0.1, 1e-5, L.ptr(mean0),
+           L.ptr(istd0), L.ptr(lo0), None, 1, p, seed, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
+    mean1, istd1, lo1, rm1, rv1 = res[0]
+    assert torch.equal(mean0, mean1) and torch.equal(lo0, lo1)
+    assert rel_err(host(istd1), host(istd0)) <= 1e-6
+    assert rel_err(host(rm1), host(rm0)) <= 1e-6 and rel_err(host(rv1), host(rv0)) <= 1e-6
+    assert not torch.equal(res[1][0], mean0)
