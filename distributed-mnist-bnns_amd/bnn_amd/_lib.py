@@ -47,6 +47,7 @@ SIGNATURES = {
     "bnn_gemm_fp4_i16": (I32, [P, I64, P, I64, P, I64, I64, I64, I64, P]),
     "bnn_gemm_set_variant": (I32, [I32]),
     "bnn_gemm_set_raster": (I32, [I32]),
+    "bnn_adam_pack_set_tile256": (I32, [I32]),
     "bnn_gemm_i8_kernel": (ctypes.c_char_p, [I32, I32, I64, I64, I64]),
     "bnn_gemm_xnor": (I32, [P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_conv2d_fwd": (I32, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),

@@ -303,10 +303,18 @@ def adam_schedule(lr, beta1, beta2, step0, n, device):
     return host.to(device)
 
 
+# BNN_ADAM_TILE256=1 / 0: the 256 x 256-tile form of bnn_adam_clamp_pack on / off (A/B timing);
+# unset: the library's default
+_ADAM_TILE256 = [os.environ.get("BNN_ADAM_TILE256")]
+
+
 def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
                      grad_scale=1.0, clamp=True, sched=None, ctr=None):
     """bnn_adam_clamp on a 2-D latent weight that also rewrites its cached packed operands (see
     packed_weight).  Returns False (nothing done) when ``p`` has no valid cache."""
+    if _ADAM_TILE256[0] is not None:
+        L.call("bnn_adam_pack_set_tile256", int(_ADAM_TILE256[0] != "0"))
+        _ADAM_TILE256[0] = None
     ent = getattr(p, "_bnn_pack", None)
     if ent is None or ent["key"] != _pack_key(p) or p.dim() != 2:
         return False

@@ -307,6 +307,66 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
   }
 }
 
+// bnn_adam_clamp_pack on 256 x 256 tiles (the layout of bn_apply_pack_fp4_k): phase 1 updates
+// each 1-KiB row run of p with Adam + clamp (p, g, m, v read and p, m, v written as whole-line
+// float4 runs; sign_pack_tile_k's 64 x 64 tiles move 64-B pieces), packs the new signs into the FP4
+// rows and the LDS nibble image; phase 2 writes the FP4 transpose (plain or panel layout) exactly
+// as bn_apply_pack_fp4_k does.  Same element arithmetic (adam_elem) as sign_pack_tile_k<1, 0, 1>.
+__global__ __launch_bounds__(256) void adam_pack_fp4_k(float* __restrict__ p, AdamArgs a0, int64_t N, int64_t K,
+                                                       uint8_t* __restrict__ q, int64_t ldq,
+                                                       uint8_t* __restrict__ qt, int64_t ldqt, int64_t pnks) {
+  __shared__ uint32_t img[AP_T * AP_LD];
+  const AdamArgs a = adam_resolve(a0);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t k0 = (int64_t)blockIdx.x * AP_T, m0 = (int64_t)blockIdx.y * AP_T;
+  const int64_t cb = k0 + 4 * lane;
+  uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
+#pragma unroll 4
+  for (int i = 0; i < AP_T / 4; ++i) {
+    const int r = wave + 4 * i;
+    const int64_t off = (m0 + r) * K + cb;            // N % 256 == 0: every row is in range
+    const float4 pv = *reinterpret_cast<const float4*>(p + off);
+    const float4 gv = *reinterpret_cast<const float4*>(a.g + off);
+    float4 mv = *reinterpret_cast<const float4*>(a.m + off);
+    float4 vv = *reinterpret_cast<const float4*>(a.v + off);
+    float4 np;
+    np.x = adam_elem(pv.x, gv.x, mv.x, vv.x, a);
+    np.y = adam_elem(pv.y, gv.y, mv.y, vv.y, a);
+    np.z = adam_elem(pv.z, gv.z, mv.z, vv.z, a);
+    np.w = adam_elem(pv.w, gv.w, mv.w, vv.w, a);
+    *reinterpret_cast<float4*>(p + off) = np;
+    *reinterpret_cast<float4*>(a.m + off) = mv;
+    *reinterpret_cast<float4*>(a.v + off) = vv;
+    const uint32_t code = fp4_code(tsign(np.x)) | (fp4_code(tsign(np.y)) << 4) | (fp4_code(tsign(np.z)) << 8) |
+                          (fp4_code(tsign(np.w)) << 12);
+    *reinterpret_cast<uint16_t*>(q + (m0 + r) * ldq + k0 / 2 + 2 * lane) = (uint16_t)code;
+    const int slot = (lane >> 1) ^ (((r >> 6) & 3) << 3);
+    img16[(r * AP_LD + slot) * 2 + (lane & 1)] = (uint16_t)code;
+  }
+  __syncthreads();
+  const int mg = t & 7, kb = t >> 3;
+  uint32_t out[8][4];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 32 * mg + 8 * qq + i;
+      w[i] = img[r * AP_LD + (kb ^ ((mg >> 1) << 3))];
+    }
+    nib_transpose8(w);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) out[c][qq] = w[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int64_t n = k0 + 8 * kb + c;
+    uint8_t* dst = pnks > 0 ? qt + ((n >> 9) * pnks + (m0 >> 6) + (mg >> 1)) * 16384 + (n & 511) * 32 + (mg & 1) * 16
+                            : qt + n * ldqt + m0 / 2 + 16 * mg;
+    *reinterpret_cast<uint4*>(dst) = make_uint4(out[c][0], out[c][1], out[c][2], out[c][3]);
+  }
+}
+
 __global__ __launch_bounds__(256) void sign_f32_k(const float* __restrict__ x, float* __restrict__ y,
                                                   int64_t n, int vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -844,6 +904,14 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
   return check_launch("bnn_sign_pack_fp4");
 }
 
+// tuning hook (bnn_adam_pack_set_tile256): 0 forces the 64 x 64 tile kernel (A/B timing)
+static int ADAM_TILE256 = 0;   // on once validated on the GPU (bnn_adam_pack_set_tile256)
+
+BNN_API int bnn_adam_pack_set_tile256(int32_t on) {
+  ADAM_TILE256 = on != 0;
+  return 0;
+}
+
 static int adam_clamp_pack_impl(float* p, const AdamArgs& a, int64_t N, int64_t K, int32_t fmt, void* q,
                                 int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
   const float* grad = a.g;
@@ -872,6 +940,14 @@ static int adam_clamp_pack_impl(float* p, const AdamArgs& a, int64_t N, int64_t 
     return kErrInval;
   }
   const int vec = aligned16(p) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq) && (K % 4 == 0);
+  if (fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && vec && N % AP_T == 0 && K % AP_T == 0 &&
+      2 * ldq == K && 2 * ldqt == N && ADAM_TILE256) {
+    // whole 256 x 256 tiles, no padding: the 1-KiB-run form
+    hipLaunchKernelGGL(adam_pack_fp4_k, dim3((unsigned)(K / AP_T), (unsigned)(N / AP_T)), dim3(256), 0, S(stream), p,
+                       a, N, K, reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(qt), ldqt,
+                       qt_fmt == 2 ? ldqt / 32 : (int64_t)0);
+    return check_launch("bnn_adam_clamp_pack");
+  }
   if (fmt == 0)
     hipLaunchKernelGGL((sign_pack_tile_k<0, 0, 1>), dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, S(stream), p, N,
                        K, K, reinterpret_cast<int8_t*>(q), ldq, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, a, qt_fmt);

@@ -516,6 +516,9 @@ int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_
 /* Fused latent update (replaces mnist-dist2.py:131-137 around torch.optim.Adam, :91):
  * p <- Adam(p, grad*grad_scale) with torch's bias-corrected formula, then, if clamp != 0,
  * p <- clamp(p, -1, 1).  step = 1-based Adam step count after this update. */
+/* Tuning hook: 0 makes bnn_adam_clamp_pack use its 64 x 64-tile kernel even for whole 256 x 256
+ * tiles (A/B timing and the equality test); 1 (default) the 1-KiB-run form. */
+int bnn_adam_pack_set_tile256(int32_t on);
 int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,
                    int32_t clamp, bnn_stream_t stream);

@@ -35,6 +35,7 @@ Tolerances:
   Those biases (and the BatchNorm running means, which carry them) are checked for range /
   loosely, as tests/test_oracle_golden.py does for the CPU oracle.
 """
+import os
 import numpy as np
 import pytest
 import torch
@@ -263,7 +264,7 @@ def test_fused_trainer_uses_repacked_weights(nets):
         assert np.array_equal(np.asarray(a), np.asarray(b))
 
 
-@pytest.mark.parametrize("N,K", [(300, 1000), (64, 784), (8192, 784), (100, 37)])
+@pytest.mark.parametrize("N,K", [(300, 1000), (64, 784), (8192, 784), (100, 37), (512, 768), (2048, 4096)])
 @pytest.mark.parametrize("fmt", [0, 1])
 @pytest.mark.parametrize("qt_fmt", [0, 1])
 def test_adam_clamp_pack_matches_unfused(nets, N, K, fmt, qt_fmt):
@@ -299,3 +300,31 @@ def test_adam_clamp_pack_matches_unfused(nets, N, K, fmt, qt_fmt):
     _, qt_ref = F.sign_pack_fp4(a[0], want_qt=True, qt_fmt="fp4" if qt_fmt == 1 else "i8", want_q=False)
     assert torch.equal(q, q_ref)
     assert torch.equal(qt, qt_ref)
+
+
+@pytest.mark.parametrize("N,K,qt_fmt", [(512, 768, 1), (1024, 2048, 2), (8192, 8192, 2), (768, 1536, 1)])
+def test_adam_pack_tile256_equals_tile64(nets, N, K, qt_fmt):
+    """The 256 x 256-tile form of bnn_adam_clamp_pack (whole tiles, FP4 rows + FP4 / panel
+    transpose) against the 64 x 64-tile kernel (bnn_adam_pack_set_tile256(0)): p, m, v, q, qt
+    bit-identical."""
+    from bnn_amd import _lib as L
+    torch.manual_seed(N + K)
+    p0 = torch.empty(N, K, device="cuda").uniform_(-1.1, 1.1)
+    p0[torch.rand_like(p0) < 0.01] = 0.0
+    g = torch.randn_like(p0)
+    m0 = torch.randn_like(p0) * 0.1
+    v0 = torch.rand_like(p0) * 0.01
+    outs = []
+    try:
+        for tile256 in (1, 0):
+            L.call("bnn_adam_pack_set_tile256", tile256)
+            b = [p0.clone(), m0.clone(), v0.clone()]
+            q = torch.full((N, K // 2), 0x77, dtype=torch.uint8, device="cuda")
+            qt = torch.full((K, N // 2), 0x77, dtype=torch.uint8, device="cuda")
+            L.call("bnn_adam_clamp_pack", L.ptr(b[0]), L.ptr(g), L.ptr(b[1]), L.ptr(b[2]), N, K, 0.01, 0.9, 0.999,
+                   1e-8, 3, 1.0, 1, 1, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], qt_fmt, L.stream())
+            outs.append(b + [q, qt])
+    finally:
+        L.call("bnn_adam_pack_set_tile256", int(os.environ.get("BNN_ADAM_TILE256", "0") != "0"))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
