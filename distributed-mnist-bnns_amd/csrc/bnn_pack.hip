@@ -905,7 +905,7 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
 }
 
 // tuning hook (bnn_adam_pack_set_tile256): 0 forces the 64 x 64 tile kernel (A/B timing)
-static int ADAM_TILE256 = 0;   // on once validated on the GPU (bnn_adam_pack_set_tile256)
+static int ADAM_TILE256 = 1;
 
 BNN_API int bnn_adam_pack_set_tile256(int32_t on) {
   ADAM_TILE256 = on != 0;

@@ -325,6 +325,6 @@ def test_adam_pack_tile256_equals_tile64(nets, N, K, qt_fmt):
                    1e-8, 3, 1.0, 1, 1, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1], qt_fmt, L.stream())
             outs.append(b + [q, qt])
     finally:
-        L.call("bnn_adam_pack_set_tile256", int(os.environ.get("BNN_ADAM_TILE256", "0") != "0"))
+        L.call("bnn_adam_pack_set_tile256", int(os.environ.get("BNN_ADAM_TILE256", "1") != "0"))
     for x, y in zip(*outs):
         assert torch.equal(x, y)
