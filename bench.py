@@ -317,10 +317,23 @@ def main():
     if use_exchange:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    dist_info = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        ranks = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ranks, t)
+        per_rank = [float(v.item()) for v in ranks]
+        elapsed = max(per_rank)
+        try:
+            nccl_v = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:     # noqa: BLE001 -- informational only
+            nccl_v = None
+        dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                     "rccl_version": nccl_v, "devices": world,
+                     "rank_ms_per_step_min": round(min(per_rank) / args.steps * 1e3, 3),
+                     "rank_ms_per_step_max": round(max(per_rank) / args.steps * 1e3, 3),
+                     "collectives_per_step": (exchange.collectives / max(1, args.warmup + args.steps)
+                                              if exchange is not None else None)}
     final_loss = float(loss.item())
 
     # instrumented steps (outside the timed region): per-launch HIP events -> roofline
@@ -376,6 +389,8 @@ def main():
         result["roofline"] = roofline_of(ksum, tsteps)
     else:
         result["roofline"] = None
+    if dist_info is not None:
+        result["distributed"] = dist_info
     result["cpu_baseline"] = cpu_main
     if cpu_main:
         result["cpu_baselines_other"] = cpu_extra

@@ -36,6 +36,7 @@ SIGNATURES = {
     "bnn_gemm_fp4_bnstats_chunk": (I64, [I64, I64, I64]),
     "bnn_gemm_fp4_bnstats": (I32, [P, I64, P, I64, P, P, P, I64, P, I64, I64, I64, F32, ctypes.c_uint64, P, I64,
                                    P]),
+    "bnn_gemm_i8_bnstats_ok": (I32, [I64, I64, I64, I64, I64]),
     "bnn_gemm_i8_affine_bnstats": (I32, [P, I64, P, I64, P, P, P, ctypes.c_double, P, I64, I64, I64, I64, P, I64,
                                          P]),
     "bnn_linear_nsmall_workspace": (I64, [I64, I64, I64]),
@@ -70,6 +71,7 @@ SIGNATURES = {
     "bnn_bn2d_fwd_train_q": (I32, [P, P, I32, I64, I64, I64, I64, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P]),
     "bnn_bn2d_bwd_q": (I32, [P, P, I32, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "bnn_conv2d_fwd_q": (I32, [P, P, P, I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
+    "bnn_conv2d_fwd_q_ok": (I32, [I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32]),
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,

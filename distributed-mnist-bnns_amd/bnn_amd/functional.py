@@ -154,7 +154,12 @@ def _qt_buffer(K, M, qt_fmt, device):
     if qt_fmt == "fp4":
         return torch.empty((K, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
     if qt_fmt == "fp4p":
-        return torch.empty(((K + 511) // 512 * 512, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
+        buf = torch.empty(((K + 511) // 512 * 512, round_up(M, 256) // 2), dtype=torch.uint8, device=device)
+        if buf.shape[0] > K:
+            # the packing kernels write rows < K only; the panel GEMM stages whole 512-row panels,
+            # so the pad rows are zeroed here (e2m1 zeros: they add nothing to any column)
+            buf[K:].zero_()
+        return buf
     return torch.empty((K, round_up(M)), dtype=torch.int8, device=device)
 
 
@@ -844,7 +849,8 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
         wq, _ = packed_weight(weight, "i8", True, False, cache)
         R = row_sums(wq, K)
         bvec = bias.detach() if bias is not None else None
-        if PIX_STATS and need_dw and K <= q.shape[1]:
+        if (PIX_STATS and need_dw and K <= q.shape[1]
+                and L.lib().bnn_gemm_i8_bnstats_ok(M, N, q.shape[1], q.shape[1], wq.shape[1])):
             y = _pixels_fwd_with_stats(q, wq, M, N, K, _const_vec(a, N, u.device), bvec, R, s0)
         else:
             y = gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=_const_vec(a, N, u.device), bias=bvec, col_off=R,
@@ -964,8 +970,9 @@ def _zq_of(x):
     return getattr(x, _ZQ_ATTR, None)
 
 
-def _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, pad):
-    """1 (int8) / 2 (int16) when bnn_conv2d_fwd_q takes the shape, else 0."""
+def _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, pad, N, Co):
+    """1 (int8) / 2 (int16) when bnn_conv2d_fwd_q takes the shape, else 0 (then the fp32 output is
+    written: the library's own geometry check, bnn_conv2d_fwd_q_ok, has the last word)."""
     if not (ZQ and binarize_input and stride == 1 and dilation == 1 and groups == 1 and pad <= min(KH, KW) - 1):
         return 0
     if not (C == 1 and KW <= 8) and not (C % 16 == 0 and C <= 64):
@@ -973,7 +980,10 @@ def _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, pad):
     # int16 even where int8 would hold the sums (the first layer's |I| <= 25): the pooled BatchNorm2d
     # passes read 2 elements per lane, and 2-byte loads made them slower than on fp32 (int8 conv1:
     # apply 33 -> 46 us, backward 115 -> 139 us; int16 conv2: backward 115 -> 78 us, tools/gpu_r03_q6b.sh)
-    return 2 if C * KH * KW <= 32767 else 0
+    fmt = 2 if C * KH * KW <= 32767 else 0
+    if fmt and not L.lib().bnn_conv2d_fwd_q_ok(fmt, N, C, H, W, Co, KH, KW, stride, pad, dilation, groups):
+        return 0
+    return fmt
 
 
 class BinaryConv2dFunction(torch.autograd.Function):
@@ -989,7 +999,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
         OW = (W + 2 * padding - dilation * (KW - 1) - 1) // stride + 1
         b = bias.detach() if bias is not None else None
         ctx.empty = N == 0
-        zf = _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, padding) if emit_compact else 0
+        zf = _zq_fmt(x, binarize_input, stride, dilation, groups, C, KH, KW, H, W, padding, N, Co) if emit_compact else 0
         if zf and N > 0 and Co <= 64 and (OH * OW) % 4 == 0 and OH % 2 == 0 and OW % 2 == 0:
             yq = torch.empty((N, Co, OH, OW), dtype=torch.int8 if zf == 1 else torch.int16, device=x.device)
             macs = N * Co * OH * OW * C * KH * KW

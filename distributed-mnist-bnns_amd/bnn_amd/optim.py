@@ -105,15 +105,17 @@ class LatentAdam(torch.optim.Optimizer):
             sched = None
             small = []                # plain Adam + clamp tensors: one multi-tensor launch per 16
             live = [p for p in group["params"] if p.grad is not None]
-            if ds is not None and live:
-                steps = {self.state[p]["step"] if self.state.get(p) else 0 for p in live}
-                if len(steps) != 1 or len(live) != len(group["params"]):
-                    # one table per group is indexed by the shared device counter
-                    raise RuntimeError("LatentAdam: device_step needs every parameter of a group to get a "
-                                       "gradient on every step")
+            steps = {self.state[p]["step"] if self.state.get(p) else 0 for p in live}
+            uniform = len(steps) == 1 and len(live) == len(group["params"])
+            if ds is not None and live and not uniform and capturing:
+                # one table per group is indexed by the shared device counter
+                raise RuntimeError("LatentAdam: a captured device step needs every parameter of a group to "
+                                   "get a gradient on every step")
+            if ds is not None and live and uniform:
                 # the table of this lr: built on the group's first step (or by build_schedules before
-                # a capture); an eager step at another lr (the trainer's lr-quirk epochs) uses the
-                # per-launch bias corrections -- bit-identical -- instead of rebuilding a table
+                # a capture); an eager step at another lr (the trainer's lr-quirk epochs) -- or an
+                # eager step where some parameter got no gradient -- uses the per-launch bias
+                # corrections (bit-identical) instead of a table
                 sched = self._schedule(gi, group, steps.pop() + 1, live[0].device,
                                        build=gi not in self._sched)
                 if sched is None and capturing:

@@ -50,8 +50,10 @@ def init_rccl(device, rank, world_size, init_method=None):
     RCCL's internal stream created at high priority.  HIP spreads normal-priority streams over a few
     hardware queues (GPU_MAX_HW_QUEUES = 4): in the r03 trace of bench.py --exchange the pool stream
     RCCL got shared hardware queue 4 with the compute stream, so every bucket reduction ran
-    strictly between two backward kernels (0 % overlap, profiles/r03_exchange_rccl_order.txt); a
-    high-priority stream is given a queue of its own."""
+    strictly between two backward kernels (profiles/r03_exchange_rccl_overlap_normalprio.txt: the
+    last 24 collectives, 1,599.5 us, 0.00 % overlapped by compute kernels); a high-priority stream
+    is given a queue of its own (profiles/r03_exchange_rccl_overlap_hiprio.txt: 5,886.1 us, 85.37 %
+    overlapped -- one-rank collectives, so the durations are not xGMI traffic)."""
     opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
     kw = {"init_method": init_method} if init_method else {}
     dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, pg_options=opts, **kw)
@@ -82,6 +84,7 @@ class GradExchange:
         self.world = dist.get_world_size(process_group)
         self.force = bool(force_collectives)
         self.collectives = 0       # collectives issued (all-reduces + buffer broadcasts)
+        self.launch_log = []       # (bucket, start, end) of this step's all-reduces, in launch order
         # group rank 0 as a global rank: torch's src= arguments are global ranks
         self.src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
         self.broadcast_buffers = broadcast_buffers
@@ -216,6 +219,7 @@ class GradExchange:
             b.pending = b.nparams
             b.work = None
         self._next = 0
+        self.launch_log = []
         if self.direct_write:
             self._armed = {id(p) for _, plist, _ in self._flats for p in plist}
 
@@ -258,6 +262,7 @@ class GradExchange:
                 op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
                 b.work = dist.all_reduce(b.view(), op=op, group=self.pg, async_op=True)
                 self.collectives += 1
+                self.launch_log.append((self._next, b.start, b.end))
             self._next += 1
 
     def finish(self):

@@ -1537,15 +1537,41 @@ static void launch_c1_q(const ConvShape& s, const float* x, const float* w_laten
 #undef BNN_C1Q
 }
 
+// Which compact-output kernel bnn_conv2d_fwd_q runs for a shape: 1 = int8 MFMA, 2 = single-channel
+// dot4, 0 = none (the shape is refused).  Shared by the entry and its query so they cannot disagree.
+static int fwd_q_path(const ConvShape& s, MfFwd* mf, int64_t* mlds) {
+  if (g_conv_mfma && mf_fwd_geom(s, mf, mlds)) return 1;
+  if (g_conv_mfma && s.C == 1 && s.KW <= 8 && tile_geom_ok(s)) return 2;
+  return 0;
+}
+
+static bool fwd_q_args_ok(int32_t yfmt, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH,
+                          int64_t KW, int32_t stride, int32_t pad, int32_t dil, int32_t groups, ConvShape* s) {
+  return (yfmt == 1 || yfmt == 2) && make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, s) &&
+         C * KH * KW <= (yfmt == 1 ? 127 : 32767);
+}
+
+// 1 when bnn_conv2d_fwd_q accepts the shape (same geometry checks, nothing launched), else 0: the
+// host asks before it emits a compact conv output, so an unsupported shape takes the fp32 output
+// instead of failing.
+BNN_API int bnn_conv2d_fwd_q_ok(int32_t yfmt, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH,
+                                int64_t KW, int32_t stride, int32_t pad, int32_t dil, int32_t groups) {
+  ConvShape s;
+  if (!fwd_q_args_ok(yfmt, N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s)) return 0;
+  MfFwd mf;
+  int64_t mlds = 0;
+  return fwd_q_path(s, &mf, &mlds) != 0 ? 1 : 0;
+}
+
 // The binary-input forward writing the exact integer sums (no bias) as int8 (yfmt 1: C*KH*KW <= 127)
 // or int16 (yfmt 2: <= 32767) for a BatchNorm2d that reads fl(I + bias) (bnn_bn2d_*_q): the
-// int8-MFMA kernel (C % 16 == 0) or the single-channel dot4 kernel; other shapes are refused.
+// int8-MFMA kernel (C % 16 == 0) or the single-channel dot4 kernel; other shapes are refused
+// (bnn_conv2d_fwd_q_ok tells which).
 BNN_API int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int32_t yfmt, int64_t N, int64_t C,
                              int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
                              int32_t dil, int32_t groups, void* stream) {
   ConvShape s;
-  if (!x || !w_latent || !y || (yfmt != 1 && yfmt != 2) || !make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s) ||
-      C * KH * KW > (yfmt == 1 ? 127 : 32767)) {
+  if (!x || !w_latent || !y || !fwd_q_args_ok(yfmt, N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s)) {
     set_error("bnn_conv2d_fwd_q: bad arguments (yfmt 1 needs C*KH*KW <= 127, 2 <= 32767)");
     return kErrInval;
   }
@@ -1553,8 +1579,9 @@ BNN_API int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   MfFwd mf;
   int64_t mlds = 0;
+  const int path = fwd_q_path(s, &mf, &mlds);
 #define BNN_QOUT(OT_, ...) do { if (yfmt == 1) { using OT_ = int8_t; __VA_ARGS__; } else { using OT_ = int16_t; __VA_ARGS__; } } while (0)
-  if (g_conv_mfma && mf_fwd_geom(s, &mf, &mlds)) {
+  if (path == 1) {
     const size_t lds = (size_t)mlds;
     const dim3 grid((unsigned)((N + FW_IPB - 1) / FW_IPB));
     const int cot = (mf.Co + 15) / 16;
@@ -1566,7 +1593,7 @@ BNN_API int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int
     });
     return check_launch("bnn_conv2d_fwd_q");
   }
-  if (g_conv_mfma && s.C == 1 && s.KW <= 8 && tile_geom_ok(s)) {
+  if (path == 2) {
     if (yfmt == 1) launch_c1_q<int8_t>(s, x, w_latent, reinterpret_cast<int8_t*>(y), st);
     else launch_c1_q<int16_t>(s, x, w_latent, reinterpret_cast<int16_t*>(y), st);
     return check_launch("bnn_conv2d_fwd_q");

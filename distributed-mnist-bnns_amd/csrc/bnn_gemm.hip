@@ -973,17 +973,26 @@ BNN_API int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N) {
   return i8_bnstats_variant(M, N)->id == 2 ? 128 : 64;
 }
 
+// The shape bounds of the statistics form (the plain kernel has fallbacks where it has none)
+static bool i8_bnstats_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  return M > 0 && N > 0 && K > 0 && K % BK == 0 && lda >= K && ldb >= K && lda % 16 == 0 && ldb % 16 == 0 &&
+         M <= 0x7fffffff && N <= 0x7fffffff && K <= 0x7fffffff && lda * 256 < (1LL << 31) &&
+         ldb * 256 < (1LL << 31) &&
+         // |S| <= 128 K: sum S^2 over a column stays an exact double below 2^53
+         (double)M * (128.0 * K) * (128.0 * K) < 9007199254740992.0;
+}
+
+BNN_API int bnn_gemm_i8_bnstats_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  return i8_bnstats_shape_ok(M, N, K, lda, ldb) ? 1 : 0;
+}
+
 BNN_API int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
                                        const float* b_scale, const float* bias, const int64_t* col_off,
                                        double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                                        double* stat, int64_t stat_rows, void* stream) {
   const int64_t chunk = M > 0 ? bnn_gemm_i8_bnstats_chunk(M, N) : 1;
-  if (!A || !B || !C || !stat || M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || lda < K || ldb < K ||
-      lda % 16 != 0 || ldb % 16 != 0 || ldc < N || !aligned16(A) || !aligned16(B) || M > 0x7fffffff ||
-      N > 0x7fffffff || K > 0x7fffffff || lda * 256 >= (1LL << 31) || ldb * 256 >= (1LL << 31) ||
-      stat_rows != (M + chunk - 1) / chunk ||
-      // |S| <= 128 K: sum S^2 over a column stays an exact double below 2^53
-      (double)M * (128.0 * K) * (128.0 * K) >= 9007199254740992.0) {
+  if (!A || !B || !C || !stat || !i8_bnstats_shape_ok(M, N, K, lda, ldb) || ldc < N || !aligned16(A) ||
+      !aligned16(B) || stat_rows != (M + chunk - 1) / chunk) {
     set_error("bnn_gemm_i8_affine_bnstats: bad arguments (M=%lld N=%lld K=%lld stat_rows=%lld; want %lld)",
               (long long)M, (long long)N, (long long)K, (long long)stat_rows, (long long)((M + chunk - 1) / chunk));
     return kErrInval;

@@ -328,7 +328,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   const uint8_t* hi_base = p.ahi + (int64_t)m0 * nblk * 32 + (int64_t)ks0 * 64;
   const uint8_t* sc_base = p.asc + (int64_t)m0 * 2 + (int64_t)ks0 * p.asc_rows * 2;
   // panel layout: tile column n0 lies in panel n0 / 512 at row n0 % 512 (BN divides 512); rows
-  // beyond N are the panel's zero padding
+  // beyond N are the panel's padding, staged unclamped: zero in every producer's buffer
+  // (bnn_fp4_panelize writes them, functional._qt_buffer zeroes them for the packing kernels) and
+  // in any case only ever multiplied into output columns >= N, which are neither stored nor reduced
   const uint8_t* b_base = p.bks > 0 ? p.b + ((int64_t)(n0 / FP4_PANEL) * p.bks + ks0) * (FP4_PANEL * 32) + (n0 % FP4_PANEL) * 32
                                     : p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
   const int64_t b_step = (DIAG >= 5) ? BN * 32 : (p.bks > 0 ? FP4_PANEL * 32 : 32);

@@ -142,6 +142,10 @@ int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, in
                                const float* b_scale, const float* bias, const int64_t* col_off,
                                double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                                double* stat, int64_t stat_rows, bnn_stream_t stream);
+/* 1 when bnn_gemm_i8_affine_bnstats takes the shape (no 32-bit tile offsets overflow, the column
+ * sum of S^2 stays an exact double: M (128 K)^2 < 2^53), else 0 -- then run bnn_gemm_i8_affine and
+ * the statistics pass. */
+int bnn_gemm_i8_bnstats_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 
 /* ---------------------------------------------------------------- u8 pixels (first layer)
  * Replaces the fp32 pixel tensor the reference's loader builds (ToTensor = u8/255, optionally
@@ -263,6 +267,10 @@ int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* w_latent
 int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int32_t yfmt, int64_t N, int64_t C, int64_t H,
                      int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad, int32_t dil,
                      int32_t groups, bnn_stream_t stream);
+/* 1 when bnn_conv2d_fwd_q takes the shape (the same geometry checks, nothing launched; depends on
+ * bnn_conv_set_mfma), else 0: the host asks before emitting a compact conv output. */
+int bnn_conv2d_fwd_q_ok(int32_t yfmt, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                        int32_t stride, int32_t pad, int32_t dil, int32_t groups);
 int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* dx, int64_t N, int64_t C,
                         int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride,
                         int32_t pad, int32_t dil, int32_t groups, bnn_stream_t stream);

@@ -257,9 +257,88 @@ def trace_wide_case(name, steps=10, batch=256, widths=(256, 256, 256), lr=0.01):
     save(name, **rec)
 
 
+class TraceCNN(nn.Module):
+    """The build's BinCNN (BASELINE config 4) with the reference's own BinarizeConv2d
+    (binarized_modules.py:87-107), on the ConvNet template of mnist-dist.py:31-51 (conv5x5 p2 ->
+    BatchNorm2d -> MaxPool2d(2), twice, then Linear(7*7*32, 10)) with Hardtanh in place of ReLU,
+    as in mnist-dist2.py's Net.  Module names follow nets.BinCNN so the state_dicts match."""
+
+    def __init__(self):
+        super().__init__()
+        self.layer1 = nn.Sequential(BinarizeConv2d(1, 16, kernel_size=5, stride=1, padding=2),
+                                    nn.BatchNorm2d(16), nn.Hardtanh(), nn.MaxPool2d(kernel_size=2, stride=2))
+        self.layer2 = nn.Sequential(BinarizeConv2d(16, 32, kernel_size=5, stride=1, padding=2),
+                                    nn.BatchNorm2d(32), nn.Hardtanh(), nn.MaxPool2d(kernel_size=2, stride=2))
+        self.fc = nn.Linear(7 * 7 * 32, 10)
+        self.logsoftmax = nn.LogSoftmax(dim=1)
+
+    def forward(self, x):
+        out = self.layer2(self.layer1(x))
+        return self.logsoftmax(self.fc(out.reshape(out.size(0), -1)))
+
+
+CNN_PARAMS = ["layer1.0.weight", "layer1.0.bias", "layer1.1.weight", "layer1.1.bias", "layer2.0.weight",
+              "layer2.0.bias", "layer2.1.weight", "layer2.1.bias", "fc.weight", "fc.bias"]
+
+
+def trace_cnn_case(name, steps=8, batch=256, lr=0.01):
+    """The BinCNN trained by the reference loop (mnist-dist2.py:118-137: CrossEntropy on the
+    log-probs, org restore -> Adam -> clamp), input = ToTensor of u8 pixels (conv1 binarises it:
+    C = 1 != 3, binarized_modules.py:94-95).  Recorded per step: the u8 batch and targets, loss,
+    log-probs, every gradient, the latent conv weights (.org) and their sign bits after the
+    update, the binarized input of conv2 (sign bits + zero count), every parameter after the
+    update and the running statistics."""
+    gen = torch.Generator().manual_seed(8642)
+    torch.manual_seed(13)
+    net = TraceCNN()
+    rec = {"init/" + k: np32(v) for k, v in net.state_dict().items()}
+    opt = torch.optim.Adam(net.parameters(), lr=lr)
+    crit = nn.CrossEntropyLoss()
+    acts = {}
+    net.layer2[0].register_forward_hook(lambda mod, inp, out: acts.__setitem__("conv2_in", np32(inp[0])))
+    net.train()
+    named = dict(net.named_parameters())
+    for s in range(steps):
+        u = mnist_u8(gen, (batch, 1, 28, 28))
+        t = torch.randint(0, 10, (batch,), generator=gen)
+        x = u.float().div(255.0)                   # transforms.ToTensor()
+        rec[f"s{s}/u8"] = u.numpy().reshape(batch, 784)
+        rec[f"s{s}/target"] = t.numpy().astype(np.int64)
+        opt.zero_grad()
+        out = net(x)
+        loss = crit(out, t)
+        loss.backward()
+        rec[f"s{s}/out"] = np32(out)
+        rec[f"s{s}/loss"] = np.array(loss.item(), np.float64)
+        rec[f"s{s}/act/conv2_in"], rec[f"s{s}/act0/conv2_in"] = _bits(acts["conv2_in"])
+        for k in CNN_PARAMS:
+            rec[f"s{s}/grad/{k}"] = np32(named[k].grad)
+        for p in net.parameters():                 # mnist-dist2.py:131-137
+            if hasattr(p, "org"):
+                p.data.copy_(p.org)
+        opt.step()
+        for p in net.parameters():
+            if hasattr(p, "org"):
+                p.org.copy_(p.data.clamp_(-1, 1))
+        for k in CNN_PARAMS:
+            p = named[k]
+            rec[f"s{s}/data/{k}"] = np32(p.org if hasattr(p, "org") else p)
+        for k in ("layer1.0.weight", "layer2.0.weight"):
+            rec[f"s{s}/orgsign/{k}"], rec[f"s{s}/orgzero/{k}"] = _bits(named[k].org.numpy())
+        for k, v in net.state_dict().items():
+            if "running" in k:
+                rec[f"s{s}/buf/{k}"] = np32(v)
+    rec["meta/lr"] = np.array(lr, np.float64)
+    rec["meta/steps"] = np.array(steps, np.int64)
+    save(name, **rec)
+
+
 def main():
     if sys.argv[1:] == ["trace_wide"]:        # regenerate only the wide trace
         trace_wide_case("trace_wide")
+        return
+    if sys.argv[1:] == ["trace_cnn"]:         # regenerate only the BinCNN trace
+        trace_cnn_case("trace_cnn")
         return
     gen = torch.Generator().manual_seed(1234)
     # 1. first layer: input width 784 -> NOT binarised (binarized_modules.py:75)
@@ -306,6 +385,8 @@ def main():
     save("sampler", **rec)
     # 11. the wide trace (every fusion of the benched path applies)
     trace_wide_case("trace_wide")
+    # 12. the BinCNN (config 4) trace on the reference's BinarizeConv2d
+    trace_cnn_case("trace_cnn")
 
 
 if __name__ == "__main__":

@@ -81,6 +81,33 @@ def test_device_step_adam_equals_per_launch(F):
         assert np.array_equal(a[k], b[k]), k
 
 
+def test_device_step_eager_with_missing_gradients(F):
+    """An eager device-step LatentAdam step where a parameter got no gradient (a frozen fc4 bias)
+    takes the per-launch bias corrections for its group instead of raising (only a captured step
+    needs one schedule per group): equal to LatentAdam without a device step, bit for bit."""
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch()
+    states = []
+    for dev_step in (False, True):
+        m = _model(12, p_drop=0.0)
+        m.fc4.bias.requires_grad_(False)
+        ds = F.DeviceStep().activate() if dev_step else None
+        try:
+            opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+            step = _step_fn(m, opt, u, y)
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            states.append(_state(m, opt))
+        finally:
+            if ds is not None:
+                ds.deactivate()
+    a, b = states
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("widths,M", [((256, 128, 64), 256), ((192, 192, 192), 64)])
 def test_graph_replays_equal_eager_device_steps(F, widths, M):
     from bnn_amd.graph import GraphedStep

@@ -19,6 +19,11 @@ Runs, on this GPU:
 Bars: over 25-step windows, the mean loss of L is within max(2 x the largest
 window gap |T1 - T|, 0.02) of T's; both learn (last window's mean loss below half of the
 first's); training-set accuracy after the 300 steps within 1.5 points of T's.
+
+With dropout on (p = 0.3 before bn3, mnist-dist2.py:69; test_mnist_loss_curve_dropout): L draws
+its keep masks from the build's hash, T from torch's Philox stream, so no two runs
+share a mask; the calibration T2 is T with another dropout seed, and the same windowed bars hold
+with T2 in place of T1 (accuracy measured in eval mode, dropout off).
 """
 import os
 
@@ -61,10 +66,11 @@ def _accuracy(model, x, y, fp32):
     return correct / len(x)
 
 
-def _run_libbnn(state, x, y, order):
+def _run_libbnn(state, x, y, order, p_drop=0.0, seed=0):
     from bnn_amd import nets
     from bnn_amd.optim import LatentAdam
-    m = nets.MLP(*WIDTHS, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True)
+    torch.manual_seed(seed)                 # the fused dropout draws its seeds from torch's CPU RNG
+    m = nets.MLP(*WIDTHS, p_drop=p_drop, org_protocol=False, mutate_input=False, fused_bn=True)
     m.load_state_dict(state)
     m = m.cuda().train()
     opt = LatentAdam(m.parameters(), lr=LR, clamp_params=nets.binary_params(m))
@@ -79,9 +85,10 @@ def _run_libbnn(state, x, y, order):
     return np.array([float(v) for v in losses]), _accuracy(m, x, y, fp32=False)
 
 
-def _run_torch(state, x, y, order, flip=False):
+def _run_torch(state, x, y, order, flip=False, p_drop=0.0, seed=0):
     from oracle.bnn_torch import RefMLP, train_step
-    m = RefMLP(*WIDTHS, p_drop=0.0)
+    torch.manual_seed(seed)                 # torch's dropout masks (the CUDA generator)
+    m = RefMLP(*WIDTHS, p_drop=p_drop)
     m.load_state_dict(state)
     if flip:
         with torch.no_grad():
@@ -94,6 +101,10 @@ def _run_torch(state, x, y, order, flip=False):
     return np.array(losses), _accuracy(m, x, y, fp32=True)
 
 
+def _windows(a):
+    return a[: len(a) // WIN * WIN].reshape(-1, WIN).mean(1)
+
+
 def test_mnist_loss_curve_matches_reference_semantics():
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
@@ -104,7 +115,7 @@ def test_mnist_loss_curve_matches_reference_semantics():
     L, accL = _run_libbnn(state, x, y, order)
     T, accT = _run_torch(state, x, y, order)
     T1, accT1 = _run_torch(state, x, y, order, flip=True)
-    w = lambda a: a[: len(a) // WIN * WIN].reshape(-1, WIN).mean(1)   # noqa: E731
+    w = _windows
     wl, wt, wt1 = w(L), w(T), w(T1)
     band = max(2 * float(np.abs(wt1 - wt).max()), 0.02)
     print("\nwindow mean loss  libbnn:", " ".join(f"{v:.3f}" for v in wl))
@@ -117,3 +128,27 @@ def test_mnist_loss_curve_matches_reference_semantics():
     assert np.abs(wl - wt).max() <= band
     assert wl[-1] < 0.5 * wl[0] and wt[-1] < 0.5 * wt[0]
     assert abs(accL - accT) <= 0.015
+
+
+def test_mnist_loss_curve_dropout():
+    """p = 0.3 (mnist-dist2.py:69), the bench's dropout: the fused path's hash masks against torch's
+    dropout; the band is the gap between two torch runs that differ only in their dropout seed."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import nets
+    torch.manual_seed(5)
+    state = {k: v.clone() for k, v in nets.MLP(*WIDTHS, p_drop=0.3).state_dict().items()}
+    x, y, order = _data()
+    L, accL = _run_libbnn(state, x, y, order, p_drop=0.3, seed=11)
+    T, accT = _run_torch(state, x, y, order, p_drop=0.3, seed=21)
+    T2, accT2 = _run_torch(state, x, y, order, p_drop=0.3, seed=31)
+    wl, wt, wt2 = _windows(L), _windows(T), _windows(T2)
+    band = max(2 * float(np.abs(wt2 - wt).max()), 0.02)
+    print("\nwindow mean loss, p=0.3  libbnn:", " ".join(f"{v:.3f}" for v in wl))
+    print("window mean loss, p=0.3  torch :", " ".join(f"{v:.3f}" for v in wt))
+    print("window mean loss, p=0.3  torch2:", " ".join(f"{v:.3f}" for v in wt2))
+    print(f"max window gap libbnn {np.abs(wl - wt).max():.4f}, torch2 {np.abs(wt2 - wt).max():.4f} (band {band:.4f}); "
+          f"accuracy libbnn {accL:.4f}, torch {accT:.4f}, torch2 {accT2:.4f}")
+    assert np.abs(wl - wt).max() <= band
+    assert wl[-1] < 0.5 * wl[0] and wt[-1] < 0.5 * wt[0]
+    assert abs(accL - accT) <= max(0.015, 2 * abs(accT2 - accT))

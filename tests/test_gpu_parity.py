@@ -545,6 +545,40 @@ def test_fused_cnn_compact_outputs_bit_identical(F):
         assert torch.equal(ba, bb), n
 
 
+def test_compact_conv_falls_back_when_refused(F):
+    """emit_compact only when bnn_conv2d_fwd_q takes the shape (bnn_conv2d_fwd_q_ok, the kernel
+    choice itself): with the MFMA conv kernels switched off (bnn_conv_set_mfma(0)) and for a
+    C = 16 layer whose 20x20 output exceeds the MFMA forward's 256-pixel tile, the fused BinCNN
+    block takes the fp32 conv output instead of raising, with the same loss."""
+    from bnn_amd import _lib as L
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    assert L.lib().bnn_conv2d_fwd_q_ok(2, 8, 16, 14, 14, 32, 5, 5, 1, 2, 1, 1) == 1
+    assert L.lib().bnn_conv2d_fwd_q_ok(2, 8, 16, 20, 20, 32, 5, 5, 1, 2, 1, 1) == 0
+    torch.manual_seed(6)
+    a = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+    x, y = synthetic_mnist(64, seed=9, device="cuda")
+    la = torch.nn.functional.cross_entropy(a(x), y).item()
+    try:
+        L.call("bnn_conv_set_mfma", 0)
+        assert L.lib().bnn_conv2d_fwd_q_ok(2, 8, 16, 14, 14, 32, 5, 5, 1, 2, 1, 1) == 0
+        n0 = F.ZQ_HANDOFFS
+        lb = torch.nn.functional.cross_entropy(a(x), y).item()
+        assert F.ZQ_HANDOFFS == n0
+    finally:
+        L.call("bnn_conv_set_mfma", 1)
+    assert abs(la - lb) <= 1e-6 * max(1.0, abs(la))
+    # a C = 16 input whose 20x20 output the compact kernels refuse: the fp32 path, no error
+    conv = nets.BinarizeConv2d(16, 32, 5, padding=2).cuda()
+    conv.org_protocol = False
+    xb = torch.randn(4, 16, 20, 20, device="cuda")
+    n0 = F.ZQ_HANDOFFS
+    out = conv(xb, emit_compact=True)
+    assert F.ZQ_HANDOFFS == n0 and out.stride() != (0, 0, 0, 0)
+    ref = F.binary_conv2d(xb, conv.weight, conv.bias, True, 1, 2, 1, 1)
+    assert torch.equal(out, ref)
+
+
 def test_fused_mlp_step_matches_unfused(F):
     """The build's trainer path (fused BN+Hardtanh, latent Adam) against the drop-in path
     (torch BatchNorm1d/Hardtanh, torch Adam + .org protocol) on one step, dropout off."""

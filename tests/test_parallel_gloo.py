@@ -111,6 +111,7 @@ def _worker_chunks(rank, world, port, q):
         out["max_bucket"] = max(sizes)
         out["fc1_slices"] = len(ex._param_buckets[model.fc1.weight])
         params = list(model.parameters())
+        out["launch_logs"] = []
         for step in range(2):
             ex.zero_grad()
             coefs = []
@@ -120,6 +121,7 @@ def _worker_chunks(rank, world, port, q):
             loss = sum((p * c).sum() for p, c in zip(params, coefs[rank]))
             loss.backward()
             ex.finish()
+            out["launch_logs"].append(list(ex.launch_log))
             for i, p in enumerate(params):
                 want = sum(coefs[r][i] for r in range(world)) / world
                 assert torch.allclose(p.grad, want, rtol=1e-6, atol=1e-7), (step, i)
@@ -152,6 +154,11 @@ def test_gradexchange_chunked_buckets_world2():
     assert out[0]["max_bucket"] * 4 <= 0.002 * 2 ** 20
     assert out[0]["fc1_slices"] == 72
     assert out[0]["nbuckets"] > 72
+    # RCCL pairs the i-th collective of every rank: both ranks launch the same buckets (same
+    # slices) in the same order, every bucket once per step, in bucket order
+    assert out[0]["launch_logs"] == out[1]["launch_logs"]
+    for log in out[0]["launch_logs"]:
+        assert [b for b, _, _ in log] == list(range(out[0]["nbuckets"]))
 
 
 def test_shard_indices_match_distributed_sampler_golden():
