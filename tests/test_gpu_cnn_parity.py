@@ -24,8 +24,10 @@ gradients of BatchNorm2d and the classifier <= 1e-4.
 test_cnn_one_step_bench_batch_vs_float64: one training step of the bench's CNN workload (batch
 4096, bench.build("cnn"), bench's synthetic data) against the float64 oracle (oracle/bnn_t64.py
 CNNOracle) on the GPU -- no continuous-input layer exists in this net (conv1 binarises the
-pixels), so the whole step is compared from the raw input: loss / log-probs / every gradient
-<= 1e-5, the update = Adam (float64) + clamp on the GPU's own gradient elementwise <= 1e-7.
+pixels), so the whole step is compared from the raw input: loss / log-probs <= 1e-5, every
+gradient <= 1e-5 or within 2x of the reference's own fp32 arithmetic (RefCNN on torch fp32, same
+state and batch) where that is further from float64 (the conv weight gradients: ~2e-5), the update
+= Adam (float64) + clamp on the GPU's own gradient elementwise <= 1e-7.
 """
 import numpy as np
 import pytest
@@ -161,8 +163,13 @@ def test_cnn_trace_fused(trace):
         _check(row, lambda k: named[k], g)
     bufs = dict(model.named_buffers())
     last = int(g["meta/steps"]) - 1
-    for k in ("layer1.1.running_var", "layer2.1.running_var", "layer1.1.running_mean", "layer2.1.running_mean"):
+    for k in ("layer1.1.running_var", "layer2.1.running_var"):
         assert close(host(bufs[k]), g[f"s{last}/buf/{k}"], 1e-4, 1e-7), k
+    # the running means carry the conv biases, whose true gradient is 0 (BatchNorm removes the
+    # mean): Adam turns their rounding-noise gradients into +-lr steps of either sign, in every
+    # implementation differently (as the MLP's fc biases: test_oracle_golden.py) -- a loose check
+    for k in ("layer1.1.running_mean", "layer2.1.running_mean"):
+        assert close(host(bufs[k]), g[f"s{last}/buf/{k}"], 2e-2, 1e-6), (k, rel_err(host(bufs[k]), g[f"s{last}/buf/{k}"]))
 
 
 def test_cnn_one_step_bench_batch_vs_float64():
@@ -193,15 +200,32 @@ def test_cnn_one_step_bench_batch_vs_float64():
     orc = T.CNNOracle(state, lr=LR, device="cuda")
     loss_ref, out_ref, g_ref = orc.step(x, y, update=False)
     dloss, eout = abs(float(loss) - loss_ref), T.rel_err(out.detach(), out_ref)
+
+    def errors(gr):
+        return {k: float(torch.linalg.vector_norm(gr[k].double() - g_ref[k])) if k in CONV_B
+                else T.rel_err(gr[k], g_ref[k]) for k in named}
+
+    errs = errors(grads)
+    # calibration: the reference's own arithmetic (torch fp32 convolutions, BatchNorm2d, autograd:
+    # oracle/bnn_torch.py RefCNN) on the same state and batch against the same float64 step.  The
+    # conv weight gradients contract B*28*28 (conv1) / B*14*14 products of a BatchNorm gradient
+    # that sums to 0 per channel: fp32 arithmetic itself lands ~2e-5 from float64 there
+    from oracle.bnn_torch import RefCNN
+    ref = RefCNN()
+    ref.load_state_dict({k.replace("layer1.0", "c1").replace("layer1.1", "b1").replace("layer2.0", "c2")
+                         .replace("layer2.1", "b2"): v.cpu() for k, v in state.items()})
+    ref = ref.cuda().train()
+    torch.nn.functional.cross_entropy(ref(x.clone()), y).backward()
+    rg = {k.replace("c1", "layer1.0").replace("b1", "layer1.1").replace("c2", "layer2.0").replace("b2", "layer2.1"):
+          p.grad.detach() for k, p in ref.named_parameters()}
+    terrs = errors(rg)
+    print(f"\nBinCNN step B={batch}: loss {float(loss):.6f} vs {loss_ref:.6f} (d {dloss:.1e}), log-probs {eout:.1e}")
+    print("  libbnn vs float64:    ", {k: f"{v:.1e}" for k, v in errs.items()})
+    print("  torch fp32 vs float64:", {k: f"{v:.1e}" for k, v in terrs.items()})
     assert dloss <= 1e-5, (float(loss), loss_ref)
     assert eout <= 1e-5, eout
-    errs = {}
-    for k in named:
-        if k in CONV_B:
-            errs[k] = float(torch.linalg.vector_norm(grads[k].double() - g_ref[k]))
-        else:
-            errs[k] = T.rel_err(grads[k], g_ref[k])
-        assert errs[k] <= 1e-5, (k, errs[k])
+    for k, v in errs.items():
+        assert v <= max(1e-5, 2 * terrs[k]), (k, v, terrs[k])
     upd = {}
     for k in named:
         gk = grads[k].double()
@@ -211,5 +235,4 @@ def test_cnn_one_step_bench_batch_vs_float64():
             want.clamp_(-1, 1)
         upd[k] = float((named[k].detach().double() - want).abs().max())
         assert upd[k] <= 1e-7, (k, upd[k])
-    print(f"\nBinCNN step B={batch}: loss {float(loss):.6f} vs {loss_ref:.6f} (d {dloss:.1e}), log-probs {eout:.1e}, "
-          f"grads { {k: f'{v:.1e}' for k, v in errs.items()} }, update max {max(upd.values()):.1e}")
+    print(f"  update max {max(upd.values()):.1e}")
