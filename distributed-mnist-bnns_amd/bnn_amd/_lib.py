@@ -77,9 +77,6 @@ SIGNATURES = {
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
                             P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
-    "bnn_dropout_bits": (I32, [I64, F32, U64, P, P]),
-    "bnn_dropout_bits_use": (I32, [P, I64, F32, U64]),
-    "bnn_dropout_bits_clear": (I32, []),
     "bnn_bn_head_workspace": (I64, [I64, I64, I32]),
     "bnn_bn_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
     "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P,

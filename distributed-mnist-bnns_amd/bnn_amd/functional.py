@@ -1340,14 +1340,12 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         b = bias.detach() if bias is not None else None
         ws = _bn_ws(M, C, x.device)
         mean, invstd, mlo = _bn_stat_buffers(C, x.device)
-        bits = _drop_bits_make(M * C, p, seed, x.device)
-        with _timed("bn_dropout_fwd_train", 0, 12 * M * C), _drop_bits_scope(bits, M * C, p, seed):
+        with _timed("bn_dropout_fwd_train", 0, 12 * M * C):
             L.call("bnn_bn_dropout_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                    L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
                    L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(y), 1, float(p), int(seed), L.ptr(ws), L.stream())
         ctx.save_for_backward(x, w, b, mean, invstd, mlo)
         ctx.p, ctx.seed = p, seed
-        ctx.bits = bits
         return y
 
     @staticmethod
@@ -1360,12 +1358,11 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         db = torch.empty((C,), dtype=torch.float32, device=x.device) if b is not None else None
         ws = _bn_ws(M, C, x.device)
         if ctx.q6 and dx is not None:
-            with _drop_bits_scope(ctx.bits, M * C, ctx.p, ctx.seed):
-                dx = _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, True, ctx.p, ctx.seed, dw, db, ws,
-                                "bn_dropout_bwd_q6")
+            dx = _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, True, ctx.p, ctx.seed, dw, db, ws,
+                            "bn_dropout_bwd_q6")
             return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                     None, None, None, None, None, None)
-        with _timed("bn_dropout_bwd", 0, 16 * M * C), _drop_bits_scope(ctx.bits, M * C, ctx.p, ctx.seed):
+        with _timed("bn_dropout_bwd", 0, 16 * M * C):
             L.call("bnn_bn_dropout_bwd", L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                    L.ptr(mlo), 1, float(ctx.p), int(ctx.seed), L.ptr(dx), L.ptr(dw), L.ptr(db), L.ptr(ws),
                    L.stream())
@@ -1375,37 +1372,6 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
 
 HEAD_NOUT = 10
 HEAD_CALLS = 0            # fused drop->bn->htanh->fc heads run (tests check the path actually ran)
-
-# The dropout keep mask materialised once per forward as bits (bnn_dropout_bits: n / 8 bytes, one
-# hash per element) and read by the statistics, apply and backward passes instead of each of them
-# evaluating the hash per element -- the same mask bit for bit.  BNN_DROP_BITS=0: the hash in every
-# pass.
-DROP_BITS = os.environ.get("BNN_DROP_BITS", "1") != "0"
-DROP_BITS_USES = 0        # masks materialised (tests check the path ran)
-
-
-def _drop_bits_make(n, p, seed, device):
-    """The keep bits of elements 0..n-1 (registered for the calls that follow), or None."""
-    global DROP_BITS_USES
-    if not DROP_BITS or float(p) <= 0.0 or n <= 0:
-        return None
-    bits = torch.empty(((n + 63) // 64 * 2,), dtype=torch.int32, device=device)
-    with _timed("dropout_bits", 0, n / 8):
-        L.call("bnn_dropout_bits", n, float(p), int(seed), L.ptr(bits), L.stream())
-    DROP_BITS_USES += 1
-    return bits
-
-
-@contextlib.contextmanager
-def _drop_bits_scope(bits, n, p, seed):
-    """Register ``bits`` (None: nothing) for the libbnn calls inside the block."""
-    if bits is not None:
-        L.call("bnn_dropout_bits_use", L.ptr(bits), n, float(p), int(seed))
-    try:
-        yield
-    finally:
-        if bits is not None:
-            L.call("bnn_dropout_bits_clear")
 
 
 class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
@@ -1431,35 +1397,32 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         mean, invstd, mlo = _bn_stat_buffers(C, z.device)
         mom = float(momentum if momentum is not None else -1.0)
         fs = _fstats_of(z, M, C, (float(p), int(seed)))
-        bits = _drop_bits_make(M * C, p, seed, z.device)
-        with _drop_bits_scope(bits, M * C, p, seed):
-            if fs is not None and float(p) > 0:
-                global FP4_STATS_USES
-                FP4_STATS_USES += 1
-                L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(running_mean),
-                       L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
-            else:
-                with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
-                    if zz is None:
-                        L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
-                               L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1,
-                               float(p), int(seed), L.ptr(ws), L.stream())
-                    else:
-                        L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
-                               L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
-                               L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
-            w4c = w4.detach().contiguous()
-            y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
-            b4d = b4.detach() if b4 is not None else None
-            with _timed("bn_head_fwd", 0, (4 if zz is None else 2) * M * C + 4 * M * HEAD_NOUT):
+        if fs is not None and float(p) > 0:
+            global FP4_STATS_USES
+            FP4_STATS_USES += 1
+            L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(running_mean),
+                   L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
+        else:
+            with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
                 if zz is None:
-                    L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
-                           L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d), L.ptr(y4), L.stream())
+                    L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
+                           L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1,
+                           float(p), int(seed), L.ptr(ws), L.stream())
                 else:
-                    L.call("bnn_bn_head_fwd_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
-                           L.ptr(mlo), L.ptr(gw), L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d),
-                           L.ptr(y4), L.stream())
-        ctx.bits = bits
+                    L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
+                           L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
+                           L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
+        w4c = w4.detach().contiguous()
+        y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
+        b4d = b4.detach() if b4 is not None else None
+        with _timed("bn_head_fwd", 0, (4 if zz is None else 2) * M * C + 4 * M * HEAD_NOUT):
+            if zz is None:
+                L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
+                       L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d), L.ptr(y4), L.stream())
+            else:
+                L.call("bnn_bn_head_fwd_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
+                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d),
+                       L.ptr(y4), L.stream())
         if zz is None:
             ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, w4c, None)
         else:
@@ -1486,8 +1449,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
         cs = torch.empty((C,), dtype=torch.float32, device=dev)
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, HEAD_NOUT),), dtype=torch.uint8, device=dev)
-        with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + (0 if ctx.z16 else 4) * M * C + 6 * M * C), \
-                _drop_bits_scope(ctx.bits, M * C, ctx.p, ctx.seed):
+        with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + (0 if ctx.z16 else 4) * M * C + 6 * M * C):
             if not ctx.z16:
                 L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw),
                        L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx),

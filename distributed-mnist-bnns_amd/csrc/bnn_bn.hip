@@ -23,7 +23,6 @@
 
 namespace bnn {
 const int64_t* g_seed_ctr = nullptr;   // bnn_set_seed_counter (declared in bnn_common.h)
-DropBits g_drop_bits{nullptr, 0, 0.f, 0, nullptr};   // bnn_dropout_bits (declared in bnn_common.h)
 namespace {
 
 constexpr int BN_ROWS = 256;  // most rows per partial-statistics chunk
@@ -52,8 +51,6 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // keep bits of elements i0 .. i0+3 (bit j), evaluated once and applied to both the input and the
 // gradient where a pass needs both
 __device__ __forceinline__ uint32_t drop_bits4(const Drop& d, uint64_t i0) {
-  // i0 % 4 == 0 at every caller (element r * C + c, C % 4 == 0, c % 4 == 0): the 4 bits share a word
-  if (d.bits != nullptr) return (d.bits[i0 >> 5] >> (i0 & 31)) & 0xFu;
   uint32_t m = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) m |= (uint32_t)drop_keep(d, i0 + j) << j;
@@ -1427,7 +1424,7 @@ BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const
     return kErrInval;
   }
   return bn_fwd_train_impl(XIn{x, nullptr}, false, M, C, gamma, beta, running_mean, running_var, momentum, eps,
-                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed, M * C));
+                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed));
 }
 
 BNN_API int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* gamma,
@@ -1439,7 +1436,7 @@ BNN_API int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t
     return kErrInval;
   }
   return bn_fwd_train_impl(XIn{x16, xbias}, true, M, C, gamma, beta, running_mean, running_var, momentum, eps,
-                           save_mean, save_invstd, save_mean_lo, nullptr, 0, work, stream, make_drop(p, seed, M * C));
+                           save_mean, save_invstd, save_mean_lo, nullptr, 0, work, stream, make_drop(p, seed));
 }
 
 BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -1559,7 +1556,7 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
     return kErrInval;
   }
   return bn_bwd_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dx, dgamma, dbeta,
-                     work, stream, make_drop(p, seed, M * C), true);
+                     work, stream, make_drop(p, seed), true);
 }
 
 // pre: the statistics are already in `work` (bnn_bn_bwd_stats_pre from the dX GEMM's epilogue
@@ -1580,7 +1577,7 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Drop dp = make_drop(p, seed, M * C);
+  const Drop dp = make_drop(p, seed);
   const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
@@ -1696,10 +1693,10 @@ static int bn_head_fwd_impl(XIn xin, bool z16, int64_t M, int64_t C, const float
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (z16)
     hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, true>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
-                       beta, w4, b4, y4, make_drop(p, seed, M * C));
+                       beta, w4, b4, y4, make_drop(p, seed));
   else
     hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
-                       beta, w4, b4, y4, make_drop(p, seed, M * C));
+                       beta, w4, b4, y4, make_drop(p, seed));
   return check_launch("bnn_bn_head_fwd");
 }
 
@@ -1734,7 +1731,7 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Drop dp = make_drop(p, seed, M * C);
+  const Drop dp = make_drop(p, seed);
   const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
@@ -1797,59 +1794,6 @@ __global__ __launch_bounds__(256) void dropout_mask_k(int64_t n, Drop d0, float*
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     out[i] = (!d.on || drop_keep(d, (uint64_t)i)) ? d.scale : 0.f;   // p == 0: the fused passes never mask
-}
-
-// The keep mask as bits: each wave covers 64 groups of 64 consecutive elements, one ballot per group;
-// lane j keeps group j's 64 bits and the wave stores them as one coalesced 512-B run.
-__global__ __launch_bounds__(256) void dropout_bits_k(int64_t n, Drop d0, uint2* __restrict__ out) {
-  const Drop d = drop_resolve(d0);
-  const int lane = threadIdx.x & 63;
-  const int64_t ngroups = (n + 63) / 64;
-  const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w * 64 < ngroups; w += wstride) {
-    uint64_t mine = 0;
-    for (int k = 0; k < 64; ++k) {
-      const int64_t i = (w * 64 + k) * 64 + lane;
-      const uint64_t m = __ballot(i < n && drop_hash_keep(d, (uint64_t)i));
-      if (lane == k) mine = m;
-    }
-    if (w * 64 + lane < ngroups) out[w * 64 + lane] = make_uint2((uint32_t)mine, (uint32_t)(mine >> 32));
-  }
-}
-
-// Materialise the keep mask of elements 0..n-1 for (p, seed) as bits (bits: ceil(n / 64) * 2 words,
-// 8-B aligned) and register them: the dropout BatchNorm / head passes launched until
-// bnn_dropout_bits_clear read their mask from the bits instead of evaluating the hash per element
-// and pass -- the same mask bit for bit.  p == 0 registers nothing.
-BNN_API int bnn_dropout_bits(int64_t n, float p, uint64_t seed, uint32_t* bits, void* stream) {
-  if (n < 0 || (n > 0 && !bits) || (reinterpret_cast<uintptr_t>(bits) & 7) != 0 || !(p >= 0.f && p < 1.f)) {
-    set_error("bnn_dropout_bits: bad arguments");
-    return kErrInval;
-  }
-  g_drop_bits = DropBits{nullptr, 0, 0.f, 0, nullptr};
-  if (n == 0 || p == 0.f) return 0;
-  const Drop d = make_drop(p, seed);
-  const int64_t waves = ((n + 63) / 64 + 63) / 64;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 8192));
-  hipLaunchKernelGGL(dropout_bits_k, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, d,
-                     reinterpret_cast<uint2*>(bits));
-  g_drop_bits = DropBits{bits, n, p, seed, g_seed_ctr};
-  return check_launch("bnn_dropout_bits");
-}
-
-// Register bits bnn_dropout_bits wrote earlier (the backward of the pass that made them).
-BNN_API int bnn_dropout_bits_use(const uint32_t* bits, int64_t n, float p, uint64_t seed) {
-  if (!bits || n <= 0 || (reinterpret_cast<uintptr_t>(bits) & 7) != 0 || !(p > 0.f && p < 1.f)) {
-    set_error("bnn_dropout_bits_use: bad arguments");
-    return kErrInval;
-  }
-  g_drop_bits = DropBits{bits, n, p, seed, g_seed_ctr};
-  return 0;
-}
-
-BNN_API int bnn_dropout_bits_clear() {
-  g_drop_bits = DropBits{nullptr, 0, 0.f, 0, nullptr};
-  return 0;
 }
 
 BNN_API int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, void* stream) {

@@ -193,9 +193,6 @@ struct Drop {
   int on;
   float scale;      // 1 / (1 - p)
   const int64_t* ctr = nullptr;   // device step counter folded into the seed (bnn_set_seed_counter)
-  // the same mask materialised as bits (element i: bit i % 32 of word i / 32; bnn_dropout_bits) for
-  // the passes launched while it is registered, or null: every pass evaluates the hash
-  const uint32_t* bits = nullptr;
 };
 
 // Process-wide device step counter for graph-captured training steps: dropout launches made
@@ -229,36 +226,16 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
   return fmix32((uint32_t)i * 0x9E3779B1u ^ drop_key(seed));
 }
 
-__device__ __forceinline__ bool drop_hash_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
+__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
 
-__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) {
-  if (d.bits != nullptr) return (d.bits[i >> 5] >> (i & 31)) & 1u;
-  return drop_hash_keep(d, i);
-}
 
-// The registered materialised mask (bnn_dropout_bits / _use / _clear; defined in bnn_bn.hip): the
-// keep bits of elements 0..n-1 for (p, seed) under the device step counter ctr
-struct DropBits {
-  const uint32_t* bits;
-  int64_t n;
-  float p;
-  uint64_t seed;
-  const int64_t* ctr;
-};
-extern DropBits g_drop_bits;
-
-// n: the element count the launch's passes index (0..n-1); the registered bits are attached when
-// they were made for the same (p, seed, step counter) and cover n elements
-inline Drop make_drop(float p, uint64_t seed, int64_t n = -1) {
+inline Drop make_drop(float p, uint64_t seed) {
   Drop d{seed, 0u, 0, 1.f, g_seed_ctr};
   if (p > 0.f && p < 1.f) {
     const double t = (1.0 - (double)p) * 4294967296.0;
     d.thresh = t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
     d.on = 1;
     d.scale = 1.f / (1.f - p);
-    if (n >= 0 && g_drop_bits.bits != nullptr && g_drop_bits.p == p && g_drop_bits.seed == seed &&
-        g_drop_bits.ctr == g_seed_ctr && n <= g_drop_bits.n)
-      d.bits = g_drop_bits.bits;
   }
   return d;
 }

@@ -395,15 +395,6 @@ int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const f
                   uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                   bnn_stream_t stream);
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
-/* The same keep mask materialised as bits (element i: bit i % 32 of word i / 32; bits holds
- * ceil(n / 64) * 2 words, 8-B aligned), registered process-wide for (p, seed, the step counter):
- * every dropout BatchNorm / head entry launched until bnn_dropout_bits_clear whose passes index at
- * most n elements reads its mask from the bits instead of evaluating the hash per element and pass
- * -- the same mask bit for bit.  _use re-registers bits written earlier (the backward of the
- * forward that made them).  p == 0 registers nothing. */
-int bnn_dropout_bits(int64_t n, float p, uint64_t seed, uint32_t* bits, bnn_stream_t stream);
-int bnn_dropout_bits_use(const uint32_t* bits, int64_t n, float p, uint64_t seed);
-int bnn_dropout_bits_clear(void);
 
 /* The network's head fused with its BatchNorm (mnist-dist2.py:69-76: fc3 -> drop -> bn3 -> htanh3
  * -> fc4 = nn.Linear(C, nout)), training mode, nout == 10, C % 256 == 0 (the forward: C % 128): the fp32 hardtanh

@@ -41,11 +41,20 @@ def rel_err(a, b):
 
 
 # --------------------------------------------------------------------------- layers
-def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5):
+# Hardtanh-boundary window: an element whose BatchNorm output lies within TAU of +-1 gets the
+# strict mask 1[-1 < y < 1] (hardtanh backward) from whichever rounding its implementation applies
+# -- fp32 arithmetic (the reference's, libbnn's) and float64 can decide it differently, as they do a
+# BatchNorm near-tie's sign.  TAU = 2^-20: 8 fp32 ulps at 1.0, well above the fp32 rounding of
+# y = (x - mean) * invstd * gamma + beta.  Such elements are recorded per column (MLPOracle.boundary).
+TAU = 2.0 ** -20
+
+
+def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5, boundary=None):
     """nn.BatchNorm1d / 2d in training mode followed by nn.Hardtanh (mnist-dist2.py:52-53): batch
     statistics over ``dims`` (biased variance normalises, the unbiased one feeds the running
     estimate).  Returns (hardtanh output, cache, new running mean, new running var); z is
-    consumed (overwritten by x_hat)."""
+    consumed (overwritten by x_hat).  ``boundary`` (a list): the per-column count of elements
+    within TAU of the Hardtanh boundary is appended."""
     m = z.numel() // z.shape[1]
     shape = [1] * z.dim()
     shape[1] = -1
@@ -55,6 +64,8 @@ def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5):
     xhat = z.sub_(mu.view(shape)).mul_(inv.view(shape))
     y = xhat * gamma.view(shape) + beta.view(shape)
     mask = (y > -1.0) & (y < 1.0)              # Hardtanh backward: strict
+    if boundary is not None:
+        boundary.append(((y.abs() - 1.0).abs() < TAU).sum(dims))
     y.clamp_(-1.0, 1.0)
     new_rm = (1 - momentum) * rmean + momentum * mu
     new_rv = (1 - momentum) * rvar + momentum * var * (m / max(m - 1, 1))
@@ -126,7 +137,8 @@ class MLPOracle:
     runs from it: fc1's input is continuous, see bnn_np.MLPOracle.step); ``drop`` -- the scaled keep
     mask (1/(1-p) or 0, fp32 [B, h3]) of the Dropout before bn3 (torch's dropout multiplies the
     fp32 pre-activation by it); ``update`` -- run the latent-weight protocol (restore -> Adam ->
-    clamp); ``need_grads`` -- which gradients to return (None = all)."""
+    clamp).  After a step, ``boundary[i]`` counts per column the elements of hidden layer i's
+    BatchNorm output within TAU of the Hardtanh boundary."""
 
     def __init__(self, state, lr=0.01, org_protocol=True, device="cpu"):
         self.dev = torch.device(device)
@@ -137,6 +149,7 @@ class MLPOracle:
 
     def step(self, x, target, z1=None, drop=None, update=True):
         p = self.p
+        self.boundary = []         # per hidden layer: [h_i] counts of elements within TAU of +-1
         x = torch.as_tensor(x).to(self.dev)
         target = torch.as_tensor(target).to(self.dev, torch.int64)
         a = x.reshape(x.shape[0], -1).to(F64)
@@ -154,7 +167,8 @@ class MLPOracle:
                 z = (z.to(F32) * torch.as_tensor(drop).to(self.dev, F32)).to(F64)
             bn = f"bn{i + 1}"
             a, cache, rm, rv = batchnorm_train(z, p[f"{bn}.weight"], p[f"{bn}.bias"],
-                                               p[f"{bn}.running_mean"], p[f"{bn}.running_var"], (0,))
+                                               p[f"{bn}.running_mean"], p[f"{bn}.running_var"], (0,),
+                                               boundary=self.boundary)
             p[f"{bn}.running_mean"], p[f"{bn}.running_var"] = rm, rv
             caches.append((xu, wb, cache))
         logits = a @ p["fc4.weight"].T + p["fc4.bias"]

@@ -25,9 +25,10 @@ test_cnn_one_step_bench_batch_vs_float64: one training step of the bench's CNN w
 4096, bench.build("cnn"), bench's synthetic data) against the float64 oracle (oracle/bnn_t64.py
 CNNOracle) on the GPU -- no continuous-input layer exists in this net (conv1 binarises the
 pixels), so the whole step is compared from the raw input: loss / log-probs <= 1e-5, every
-gradient <= 1e-5 or within 2x of the reference's own fp32 arithmetic (RefCNN on torch fp32, same
-state and batch) where that is further from float64 (the conv weight gradients: ~2e-5), the update
-= Adam (float64) + clamp on the GPU's own gradient elementwise <= 1e-7.
+gradient <= 1e-5 except the two conv weight gradients (<= 5e-5: fp32-cancellation-limited, see
+CONV_W_F64_TOL; the reference's own fp32 arithmetic, RefCNN on torch fp32 with the same state and
+batch, is printed beside them: 1.6e-4 / 2.5e-4), the update = Adam (float64) + clamp on the GPU's
+own gradient elementwise <= 1e-7.
 """
 import numpy as np
 import pytest
@@ -43,6 +44,11 @@ CONV_B = ("layer1.0.bias", "layer2.0.bias")
 SMALL = ("layer1.1.weight", "layer1.1.bias", "layer2.1.weight", "layer2.1.bias", "fc.weight", "fc.bias")
 SIGN_BUDGET = 4
 LR = 0.01
+# The conv weight gradients contract B*28*28 (conv1: 3.2 M at B = 4096) / B*14*14 products of a
+# BatchNorm2d gradient that sums to 0 per channel: fp32 arithmetic is ~1e-4 from float64 there
+# (the reference's own, RefCNN on torch fp32: 1.6e-4 / 2.5e-4 at B = 4096, profiles/
+# r04_cnn_parity.log; 2.2e-5 on its own trace at B = 256).  libbnn measured 2.2e-5 / 6.2e-6.
+CONV_W_F64_TOL = {"layer1.0.weight": 5e-5, "layer2.0.weight": 5e-5}
 
 
 @pytest.fixture(scope="module")
@@ -225,7 +231,7 @@ def test_cnn_one_step_bench_batch_vs_float64():
     assert dloss <= 1e-5, (float(loss), loss_ref)
     assert eout <= 1e-5, eout
     for k, v in errs.items():
-        assert v <= max(1e-5, 2 * terrs[k]), (k, v, terrs[k])
+        assert v <= CONV_W_F64_TOL.get(k, 1e-5), (k, v, terrs[k])
     upd = {}
     for k in named:
         gk = grads[k].double()

@@ -112,52 +112,3 @@ def test_wide_step_with_fused_head_equals_unfused(F):
             assert np.linalg.norm(a - b) <= 1e-5 * ref, k
         else:
             assert rel_err(a, b) <= 2e-5, (k, rel_err(a, b))
-
-
-def test_dropout_bits_equal_hash_mask(F):
-    """bnn_dropout_bits: bit i of the materialised mask = keep(i) of the hash the passes evaluate
-    (bnn_dropout_mask), for a ragged n and a seed with all 64 bits used."""
-    from bnn_amd import _lib as L
-    for n, p, seed in ((1000003, 0.3, 0x9E3779B97F4A7C15), (64 * 64 * 8, 0.5, 7), (77, 0.3, 1)):
-        bits = torch.empty(((n + 63) // 64 * 2,), dtype=torch.int32, device="cuda")
-        L.call("bnn_dropout_bits", n, p, seed, L.ptr(bits), L.stream())
-        L.call("bnn_dropout_bits_clear")
-        keep = (F.dropout_mask(n, p, seed) > 0).cpu().numpy()
-        w = bits.cpu().numpy().view(np.uint32)
-        got = ((w[np.arange(n) >> 5] >> (np.arange(n) & 31).astype(np.uint32)) & 1).astype(bool)
-        assert np.array_equal(got, keep), (n, p)
-
-
-@pytest.mark.parametrize("M,C,z16", [(4096, 768, False), (2048, 1024, True)])
-def test_head_with_dropout_bits_bit_identical(F, M, C, z16, monkeypatch):
-    """The fused head (and the unfused dropout BatchNorm) with the mask materialised as bits
-    (functional.DROP_BITS) equals the per-pass hash bit for bit: output, every gradient, the FP6
-    digit hand-off and the running statistics."""
-    g = torch.Generator(device="cuda").manual_seed(M)
-    z0 = (torch.randint(-30, 31, (M, C), generator=g, device="cuda").float() + 0.25)
-    dy = torch.randn(M, 10, generator=g, device="cuda")
-    runs = []
-    for bits in (False, True):
-        monkeypatch.setattr(F, "DROP_BITS", bits)
-        for fused in (True, False):
-            bn, fc = _modules(C, 5)
-            z = z0.clone().requires_grad_(True)
-            zin = z
-            if z16:     # an int16-carried pre-activation, as fc3's FP4 GEMM hands it to the head
-                zin = F._z16_carrier(z0.round().to(torch.int16), torch.full((C,), 0.25, device="cuda"))
-            torch.manual_seed(78)
-            n0 = F.DROP_BITS_USES
-            if fused:
-                y = F.dropout_bn_hardtanh_linear(zin if z16 else z, 0.3, bn, fc)
-            else:
-                y = fc(F.dropout_batch_norm_hardtanh(z, 0.3, bn))
-            assert F.DROP_BITS_USES - n0 == int(bits)
-            y.backward(dy)
-            out = {"y": host(y), "dgw": host(bn.weight.grad), "dgb": host(bn.bias.grad), "dw4": host(fc.weight.grad),
-                   "rm": host(bn.running_mean), "rv": host(bn.running_var)}
-            if not (fused and z16):
-                out["dz"] = host(z.grad)
-            runs.append(out)
-    for a, b in zip(runs[:2], runs[2:]):
-        for k in a:
-            assert np.array_equal(a[k], b[k]), k
