@@ -762,7 +762,17 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
 // into the head on the f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation,
 // the numerics class of the reference's F.linear); the backward forms dh3 = dY4 . W4 per element
 // inside the BatchNorm passes and accumulates dW4 = dY4^T . h3 there (h3 recomputed from z).
-constexpr int HD_ROWS = 64, HD_COLS = 128, HD_LD = HD_COLS + 4;
+#ifndef HEAD_RED_LDS
+#define HEAD_RED_LDS 0
+#endif
+#ifndef HEAD_RED_RB
+#define HEAD_RED_RB 8
+#endif
+// Row pitches of the LDS images (floats).  W4's: = 2 mod 32, so the B-fragment reads -- lane (r, k)
+// at row r = lane & 15, column k0 + (lane >> 4) -- fall on banks 2r + k, 32 distinct per 32-lane
+// group (a pitch of 128 put W4's 10 rows on ONE bank: the head forward spent ~40 % of its time in
+// LDS bank conflicts, profiles/r04_pmc_bn.txt).  h3's stays 132 (float4 stores; 2-way on reads).
+constexpr int HD_ROWS = 64, HD_COLS = 128, HD_LD = HD_COLS + 4, HD_WLD = HD_COLS + 2;
 // elementwise map of a 64 x 128 chunk: thread -> 4 columns 4 (t % 32), rows t / 32 + 8 i
 constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
 
@@ -778,8 +788,8 @@ __global__ __launch_bounds__(256, Z16 ? 4 : 2) void bn_head_fwd_k(XIn xin, int64
   __shared__ __attribute__((aligned(16))) float ht[HD_ROWS * HD_LD];
   // W4's NOUT real rows only (the MFMA's B columns NOUT..15 read as zero): with <= 128 registers
   // (4 waves per SIMD) the 1024 workgroups of a 65536-row batch are resident at once (4 per CU,
-  // 38.8 KiB of LDS each) instead of running in two rounds at 3 per CU
-  __shared__ float ws[NOUT * HD_COLS];
+  // 38.4 KiB of LDS each) instead of running in two rounds at 3 per CU
+  __shared__ float ws[NOUT * HD_WLD];
   const Drop dp = drop_resolve(dp0);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * HD_ROWS;
@@ -833,13 +843,16 @@ __global__ __launch_bounds__(256, Z16 ? 4 : 2) void bn_head_fwd_k(XIn xin, int64
     }
 #pragma unroll
     for (int u = 0; u < (NOUT * HD_COLS + 255) / 256; ++u)
-      if (t + 256 * u < NOUT * HD_COLS) ws[t + 256 * u] = w4c[u];
+      if (t + 256 * u < NOUT * HD_COLS) {
+        const int i = t + 256 * u, q = i / HD_COLS;
+        ws[q * HD_WLD + (i - q * HD_COLS)] = w4c[u];
+      }
     __syncthreads();
     // wave wv: rows 16 wv .. +15 of the tile; A = h3 rows, B = W4^T (16 x 16 of which NOUT real)
 #pragma unroll
     for (int k0 = 0; k0 < HD_COLS; k0 += 4) {
       const float a = ht[(16 * wv + (lane & 15)) * HD_LD + k0 + (lane >> 4)];
-      const float b = (lane & 15) < NOUT ? ws[(lane & 15) * HD_COLS + k0 + (lane >> 4)] : 0.f;
+      const float b = (lane & 15) < NOUT ? ws[(lane & 15) * HD_WLD + k0 + (lane >> 4)] : 0.f;
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
     }
   }
@@ -870,8 +883,17 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
   const int64_t chunk = id / C4;
   const int64_t c = (id - chunk * C4) * 4;
   const int64_t r0 = chunk * chunk_rows;
-  if (r0 >= M) return;
   const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
+#if HEAD_RED_LDS
+  // C % 256 == 0 (host check): a wave's 64 column groups share one chunk, whose dY4 rows the wave
+  // stages in its own LDS slice once (chunk_rows x NOUT floats) and then reads as broadcasts
+  __shared__ float d4s[4][BN_ROWS * NOUT];
+  float* myd4 = d4s[threadIdx.x >> 6];
+  if (r0 < M)
+    for (int64_t i = threadIdx.x & 63; i < (r1 - r0) * NOUT; i += 64) myd4[i] = d4[r0 * NOUT + i];
+  __syncthreads();     // before any return: every wave of the workgroup reaches it
+#endif
+  if (r0 >= M) return;
   float mu[4], lo[4], is[4], ga[4], be[4];
   float wc[NOUT][4], aw[NOUT][4];
 #pragma unroll
@@ -894,7 +916,7 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
-    constexpr int RB = 8;   // rows whose x loads are issued together (as bn_reduce_k)
+    constexpr int RB = HEAD_RED_RB;   // rows whose x loads are issued together (as bn_reduce_k)
     for (int64_t rb = r; rb < re; rb += RB) {
     float4 xv8[RB];
 #pragma unroll
@@ -906,12 +928,17 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
       const float4 xv = xv8[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
+      float dq[NOUT];
+#if HEAD_RED_LDS
+#pragma unroll
+      for (int q = 0; q < NOUT; ++q) dq[q] = myd4[(rr - r0) * NOUT + q];
+#else
       // C % 256 == 0 (host check): a wave's 64 column groups share the chunk, so the row is
       // wave-uniform and dY4's row comes in through scalar loads
       const int64_t ru = (int64_t)__builtin_amdgcn_readfirstlane((int)rr);
-      float dq[NOUT];
 #pragma unroll
       for (int q = 0; q < NOUT; ++q) dq[q] = d4[ru * NOUT + q];
+#endif
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {   // column pairs: the q-sums on the packed FMA
         pf2 gs2 = {0.f, 0.f};

@@ -8,8 +8,8 @@ import subprocess
 import sys
 import tempfile
 
-LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "distributed-mnist-bnns_amd", "lib",
-                   "libbnn.so")
+LIB = os.environ.get("BNN_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "distributed-mnist-bnns_amd", "lib", "libbnn.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
