@@ -482,6 +482,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
 constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
+#ifndef Q6_SHFL_MAX
+#define Q6_SHFL_MAX 0          // 1: block maxima by DPP / shuffle trees and per-wave partials (no LDS atomics)
+#endif
 #ifndef Q6_HEAD_OCC
 #define Q6_HEAD_OCC 3          // waves per SIMD of the fused head's quantising backward (z16 input)
 #endif
@@ -640,6 +643,10 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   // sub-tile's digit records are staged in LDS (Q6Stage) and written out as whole lines by all 256
   // threads.
   __shared__ uint32_t rmax[2][Q6T_SUB], cmax[2][Q6T_COLS];
+  // the head form keeps the atomics: the shuffle form's registers spill it (18 spills)
+  constexpr bool SHM = Q6_SHFL_MAX && NOUT == 0;
+  // per-wave partial column maxima (no atomics): [wave][block][column]
+  __shared__ __attribute__((aligned(16))) uint32_t cmaxp[SHM ? 4 : 1][2][Q6T_COLS];
   __shared__ __attribute__((aligned(16))) Q6Stage st;
   if (t < 2 * Q6T_SUB) rmax[t >> 6][t & 63] = 0u;
   else cmax[(t >> 6) - 2][t & 63] = 0u;
@@ -673,6 +680,7 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     }
     asm volatile("" ::: "memory");   // the table reads stay inside the loop
     const int pg = t & 15;
+    uint32_t cmx[2][4];               // SHM: this thread's column maxima over its two rows of each block
     const float4 mv = prm[0][pg], iv = prm[1][pg], lv = prm[2][pg], gav = prm[3][pg], bev = prm[4][pg];
     const float4 a0v = prm[5][pg], a1v = prm[6][pg];
     const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -713,19 +721,51 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       }
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
       const uint32_t a0b = abs_bits(v[0]), a1b = abs_bits(v[1]), a2b = abs_bits(v[2]), a3b = abs_bits(v[3]);
-      atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
-      atomicMax(&cmax[i >> 1][cq], a0b);
-      atomicMax(&cmax[i >> 1][cq + 1], a1b);
-      atomicMax(&cmax[i >> 1][cq + 2], a2b);
-      atomicMax(&cmax[i >> 1][cq + 3], a3b);
+      if constexpr (SHM) {
+        // row block (row rr, columns of block (t & 15) >> 3): lanes t & 7 = 0..7, one DPP tree
+        uint32_t rm = max(max(a0b, a1b), max(a2b, a3b));
+        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0xB1, 0xF, 0xF, false));   // quad xor 1
+        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0x4E, 0xF, 0xF, false));   // quad xor 2
+        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0x141, 0xF, 0xF, false));  // half mirror
+        if ((t & 7) == 0) rmax[(t & 15) >> 3][rr] = rm;
+        const uint32_t ab4[4] = {a0b, a1b, a2b, a3b};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cmx[i >> 1][j] = (i & 1) ? max(cmx[i >> 1][j], ab4[j]) : ab4[j];
+      } else {
+        atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
+        atomicMax(&cmax[i >> 1][cq], a0b);
+        atomicMax(&cmax[i >> 1][cq + 1], a1b);
+        atomicMax(&cmax[i >> 1][cq + 2], a2b);
+        atomicMax(&cmax[i >> 1][cq + 3], a3b);
+      }
+    }
+    if constexpr (SHM) {
+      // the 4 lanes of a wave holding the same columns (t >> 4 & 3) fold theirs; lane group 0 stores
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cmx[b][j] = max(cmx[b][j], (uint32_t)__shfl_xor((int)cmx[b][j], 16, 64));
+          cmx[b][j] = max(cmx[b][j], (uint32_t)__shfl_xor((int)cmx[b][j], 32, 64));
+        }
+      if (((t >> 4) & 3) == 0) {
+        *reinterpret_cast<uint4*>(&cmaxp[wave][0][cq]) = make_uint4(cmx[0][0], cmx[0][1], cmx[0][2], cmx[0][3]);
+        *reinterpret_cast<uint4*>(&cmaxp[wave][1][cq]) = make_uint4(cmx[1][0], cmx[1][1], cmx[1][2], cmx[1][3]);
+      }
     }
     __syncthreads();
     load_sub(m0 + Q6T_SUB);
     // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
     const int b = wave & 1;
-    uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
-    const uint32_t am = *amp;
-    *amp = 0u;
+    uint32_t am;
+    if constexpr (SHM) {
+      am = wave < 2 ? rmax[b][lane]
+                    : max(max(cmaxp[0][b][lane], cmaxp[1][b][lane]), max(cmaxp[2][b][lane], cmaxp[3][b][lane]));
+    } else {
+      uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
+      am = *amp;
+      *amp = 0u;
+    }
     if (!Q6_DIAG_NOQUANT_ON) {
       if (wave < 2) {
         // row block (row m0 + lane, columns c0 + 32 b ..)
@@ -762,12 +802,6 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
 // into the head on the f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation,
 // the numerics class of the reference's F.linear); the backward forms dh3 = dY4 . W4 per element
 // inside the BatchNorm passes and accumulates dW4 = dY4^T . h3 there (h3 recomputed from z).
-#ifndef HEAD_RED_LDS
-#define HEAD_RED_LDS 0
-#endif
-#ifndef HEAD_RED_RB
-#define HEAD_RED_RB 8
-#endif
 // Row pitches of the LDS images (floats).  W4's: = 2 mod 32, so the B-fragment reads -- lane (r, k)
 // at row r = lane & 15, column k0 + (lane >> 4) -- fall on banks 2r + k, 32 distinct per 32-lane
 // group (a pitch of 128 put W4's 10 rows on ONE bank: the head forward spent ~40 % of its time in
@@ -884,15 +918,15 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
   const int64_t c = (id - chunk * C4) * 4;
   const int64_t r0 = chunk * chunk_rows;
   const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
-#if HEAD_RED_LDS
   // C % 256 == 0 (host check): a wave's 64 column groups share one chunk, whose dY4 rows the wave
-  // stages in its own LDS slice once (chunk_rows x NOUT floats) and then reads as broadcasts
+  // stages in its own LDS slice once (chunk_rows x NOUT floats) and then reads as broadcasts (per-row
+  // scalar loads of dY4 left the loop waiting on the scalar cache: 677 -> 584 us on the wide step,
+  // profiles/r04_ab_head_*)
   __shared__ float d4s[4][BN_ROWS * NOUT];
   float* myd4 = d4s[threadIdx.x >> 6];
   if (r0 < M)
     for (int64_t i = threadIdx.x & 63; i < (r1 - r0) * NOUT; i += 64) myd4[i] = d4[r0 * NOUT + i];
   __syncthreads();     // before any return: every wave of the workgroup reaches it
-#endif
   if (r0 >= M) return;
   float mu[4], lo[4], is[4], ga[4], be[4];
   float wc[NOUT][4], aw[NOUT][4];
@@ -916,7 +950,7 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
-    constexpr int RB = HEAD_RED_RB;   // rows whose x loads are issued together (as bn_reduce_k)
+    constexpr int RB = 8;   // rows whose x loads are issued together (as bn_reduce_k; 4: slower)
     for (int64_t rb = r; rb < re; rb += RB) {
     float4 xv8[RB];
 #pragma unroll
@@ -929,16 +963,8 @@ __global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
       drop4(dp, (uint64_t)(rr * C + c), xs);
       float dq[NOUT];
-#if HEAD_RED_LDS
 #pragma unroll
       for (int q = 0; q < NOUT; ++q) dq[q] = myd4[(rr - r0) * NOUT + q];
-#else
-      // C % 256 == 0 (host check): a wave's 64 column groups share the chunk, so the row is
-      // wave-uniform and dY4's row comes in through scalar loads
-      const int64_t ru = (int64_t)__builtin_amdgcn_readfirstlane((int)rr);
-#pragma unroll
-      for (int q = 0; q < NOUT; ++q) dq[q] = d4[ru * NOUT + q];
-#endif
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {   // column pairs: the q-sums on the packed FMA
         pf2 gs2 = {0.f, 0.f};
