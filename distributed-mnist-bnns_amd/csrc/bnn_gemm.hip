@@ -392,7 +392,11 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
   // fragment lane map: 32x32 -> row lane&31, 16-B chunk (lane>>5) of a 32-B k-step;
   //                    16x16 -> row lane&15, 16-B chunk (lane>>4) of a 64-B k-step
   const int r = S16 ? (lane & 15) : (lane & 31), h = S16 ? (lane >> 4) : (lane >> 5), sw = swz(r);
+#ifdef GEMM_DIAG_NOMAIN   // timing-only build: no k loop (the epilogue of zero accumulators)
+  const int nk = p.K > (1 << 30) ? p.K / BKT : 0;
+#else
   const int nk = p.K / BKT;
+#endif
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s, s);
@@ -782,6 +786,9 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
           continue;
         }
         float* dst = p.C + (int64_t)row * p.ldc + c0;
+#ifdef GEMM_DIAG_NOSTORE     // timing-only build: the epilogue without its global stores
+        if (p.M > 0) continue;
+#endif
         if (vec_ok && c0 + 3 < p.N) {
           *reinterpret_cast<float4*>(dst) = v;
         } else {
