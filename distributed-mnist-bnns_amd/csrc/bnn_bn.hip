@@ -482,9 +482,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
 // the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
 constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
-#ifndef Q6_SHFL_MAX
-#define Q6_SHFL_MAX 0          // 1: block maxima by DPP / shuffle trees and per-wave partials (no LDS atomics)
-#endif
 #ifndef Q6_HEAD_OCC
 #define Q6_HEAD_OCC 3          // waves per SIMD of the fused head's quantising backward (z16 input)
 #endif
@@ -639,14 +636,11 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   // atomics -- rmax[b][row] over the row's 32 columns of block b, cmax[b][col] over the column's 32
   // rows of block b -- so a quantising lane reads its block once; it zeroes its entry for the next
   // sub-tile.  (Shuffle reductions + plain stores instead measured no faster and pushed the head
-  // variant into spills: ab/r03_q6_noatomics_bn2d_byrow.patch, tools/gpu_r03_q6b.sh.)  The
+  // variant into spills: ab/r03_q6_noatomics_bn2d_byrow.patch, tools/gpu_r03_q6b.sh; round 4's DPP
+  // row-maximum trees + per-wave column partials: 1765 vs 1761 us, profiles/r04_ab_q6shfl_pixdiag.log.)  The
   // sub-tile's digit records are staged in LDS (Q6Stage) and written out as whole lines by all 256
   // threads.
   __shared__ uint32_t rmax[2][Q6T_SUB], cmax[2][Q6T_COLS];
-  // the head form keeps the atomics: the shuffle form's registers spill it (18 spills)
-  constexpr bool SHM = Q6_SHFL_MAX && NOUT == 0;
-  // per-wave partial column maxima (no atomics): [wave][block][column]
-  __shared__ __attribute__((aligned(16))) uint32_t cmaxp[SHM ? 4 : 1][2][Q6T_COLS];
   __shared__ __attribute__((aligned(16))) Q6Stage st;
   if (t < 2 * Q6T_SUB) rmax[t >> 6][t & 63] = 0u;
   else cmax[(t >> 6) - 2][t & 63] = 0u;
@@ -680,7 +674,6 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     }
     asm volatile("" ::: "memory");   // the table reads stay inside the loop
     const int pg = t & 15;
-    uint32_t cmx[2][4];               // SHM: this thread's column maxima over its two rows of each block
     const float4 mv = prm[0][pg], iv = prm[1][pg], lv = prm[2][pg], gav = prm[3][pg], bev = prm[4][pg];
     const float4 a0v = prm[5][pg], a1v = prm[6][pg];
     const float ms[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -721,51 +714,19 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       }
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
       const uint32_t a0b = abs_bits(v[0]), a1b = abs_bits(v[1]), a2b = abs_bits(v[2]), a3b = abs_bits(v[3]);
-      if constexpr (SHM) {
-        // row block (row rr, columns of block (t & 15) >> 3): lanes t & 7 = 0..7, one DPP tree
-        uint32_t rm = max(max(a0b, a1b), max(a2b, a3b));
-        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0xB1, 0xF, 0xF, false));   // quad xor 1
-        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0x4E, 0xF, 0xF, false));   // quad xor 2
-        rm = max(rm, (uint32_t)__builtin_amdgcn_mov_dpp((int)rm, 0x141, 0xF, 0xF, false));  // half mirror
-        if ((t & 7) == 0) rmax[(t & 15) >> 3][rr] = rm;
-        const uint32_t ab4[4] = {a0b, a1b, a2b, a3b};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cmx[i >> 1][j] = (i & 1) ? max(cmx[i >> 1][j], ab4[j]) : ab4[j];
-      } else {
-        atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
-        atomicMax(&cmax[i >> 1][cq], a0b);
-        atomicMax(&cmax[i >> 1][cq + 1], a1b);
-        atomicMax(&cmax[i >> 1][cq + 2], a2b);
-        atomicMax(&cmax[i >> 1][cq + 3], a3b);
-      }
-    }
-    if constexpr (SHM) {
-      // the 4 lanes of a wave holding the same columns (t >> 4 & 3) fold theirs; lane group 0 stores
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          cmx[b][j] = max(cmx[b][j], (uint32_t)__shfl_xor((int)cmx[b][j], 16, 64));
-          cmx[b][j] = max(cmx[b][j], (uint32_t)__shfl_xor((int)cmx[b][j], 32, 64));
-        }
-      if (((t >> 4) & 3) == 0) {
-        *reinterpret_cast<uint4*>(&cmaxp[wave][0][cq]) = make_uint4(cmx[0][0], cmx[0][1], cmx[0][2], cmx[0][3]);
-        *reinterpret_cast<uint4*>(&cmaxp[wave][1][cq]) = make_uint4(cmx[1][0], cmx[1][1], cmx[1][2], cmx[1][3]);
-      }
+      atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
+      atomicMax(&cmax[i >> 1][cq], a0b);
+      atomicMax(&cmax[i >> 1][cq + 1], a1b);
+      atomicMax(&cmax[i >> 1][cq + 2], a2b);
+      atomicMax(&cmax[i >> 1][cq + 3], a3b);
     }
     __syncthreads();
     load_sub(m0 + Q6T_SUB);
     // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
     const int b = wave & 1;
-    uint32_t am;
-    if constexpr (SHM) {
-      am = wave < 2 ? rmax[b][lane]
-                    : max(max(cmaxp[0][b][lane], cmaxp[1][b][lane]), max(cmaxp[2][b][lane], cmaxp[3][b][lane]));
-    } else {
-      uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
-      am = *amp;
-      *amp = 0u;
-    }
+    uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
+    const uint32_t am = *amp;
+    *amp = 0u;
     if (!Q6_DIAG_NOQUANT_ON) {
       if (wave < 2) {
         // row block (row m0 + lane, columns c0 + 32 b ..)
