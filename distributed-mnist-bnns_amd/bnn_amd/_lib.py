@@ -37,6 +37,14 @@ SIGNATURES = {
     "bnn_gemm_fp4_bnstats": (I32, [P, I64, P, I64, P, P, P, I64, P, I64, I64, I64, F32, ctypes.c_uint64, P, I64,
                                    P]),
     "bnn_gemm_i8_bnstats_ok": (I32, [I64, I64, I64, I64, I64]),
+    "bnn_gemm_i8_s20_ok": (I32, [I64, I64, I64, I64, ctypes.c_double]),
+    "bnn_gemm_i8_affine_bnstats_s20": (I32, [P, I64, P, I64, P, ctypes.c_double, I64, P, P, I64, I64, I64, I64, P,
+                                             I64, P, P, P]),
+    "bnn_bn_apply_pack_s20": (I32, [P, P, P, F32, I64, I64, P, P, P, P, P, P, I64, P, I64, I32, P]),
+    "bnn_bn_bwd_i8cols_s20": (I32, [P, P, P, F32, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P,
+                                    P]),
+    "bnn_bn_bwd_i8cols_s20_pre": (I32, [P, P, P, F32, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P,
+                                        P, P]),
     "bnn_gemm_i8_affine_bnstats": (I32, [P, I64, P, I64, P, P, P, ctypes.c_double, P, I64, I64, I64, I64, P, I64,
                                          P]),
     "bnn_linear_nsmall_workspace": (I64, [I64, I64, I64]),
@@ -57,6 +65,7 @@ SIGNATURES = {
     "bnn_conv2d_bwd_filter": (I32, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32,
                                     I32, P]),
     "bnn_conv_set_mfma": (I32, [I32]),
+    "bnn_conv_set_c1_filter": (I32, [I32]),
     "bnn_bn_workspace": (I64, [I64, I64]),
     "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, P, P]),
     "bnn_bn_fwd_final_parts": (I32, [P, I64, I64, I64, I64, P, P, F32, F32, P, P, P, P]),

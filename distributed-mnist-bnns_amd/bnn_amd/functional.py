@@ -109,8 +109,8 @@ def _check(*ts, dtype=torch.float32):
 
 def _c2d(x):
     """Contiguous fp32 2-D view."""
-    if getattr(x, "_bnn_z16", None) is not None:
-        raise RuntimeError("a z16 pre-activation placeholder reached an op that reads fp32 values")
+    if getattr(x, "_bnn_z16", None) is not None or getattr(x, "_bnn_s20", None) is not None:
+        raise RuntimeError("a compact pre-activation placeholder reached an op that reads fp32 values")
     return x if x.is_contiguous() else x.contiguous()
 
 
@@ -793,6 +793,70 @@ def _pixels_fwd_with_stats(q, wq, M, N, K, bscale, bias, R, s0):
     return y
 
 
+# fc1 -> bn1 in its compact form (s20): the pixel layer's output z1 = fl(fl(S * a) + b) is carried
+# as the exact integer S = sum_k u_k sign(w_k) (|S| < 2^19 for ToTensor pixels at K = 784) in 20 bits
+# -- an int16 plane and a nibble plane, 2.5 B per element instead of 4 -- when its only reader is the
+# fused bn1 -> fc2 op in training (apply-pack forward, int8-column-digit backward), whose *_s20
+# entries form the same fp32 z1 bit for bit.  The statistics still come from the GEMM epilogue.
+# Autograd sees a stride-0 placeholder (as for z16); dense_preact() rebuilds the fp32 tensor.
+S20 = os.environ.get("BNN_S20", "1") != "0"    # BNN_S20=0: fc1 writes the fp32 z1
+_S20_ATTR = "_bnn_s20"
+S20_HANDOFFS = 0          # s20 placeholders produced (tests check the hand-off ran)
+
+
+def _s20_carrier(lo, hi, bias, scale):
+    global S20_HANDOFFS
+    S20_HANDOFFS += 1
+    ph = torch.zeros((1,), dtype=torch.float32, device=lo.device).as_strided(tuple(lo.shape), (0, 0))
+    setattr(ph, _S20_ATTR, (lo, hi, bias, float(scale)))
+    return ph
+
+
+def _s20_of(x):
+    """(int16 low bits [M, C], uint8 nibbles [M, C/2], bias [C] or None, scale) of an s20
+    placeholder, or None."""
+    return getattr(x, _S20_ATTR, None)
+
+
+def dense_preact(z):
+    """The fp32 tensor a compact pre-activation placeholder (s20 or z16) stands for, formed with
+    the same fp32 roundings as the kernels that read it; any other tensor is returned as is (test
+    and debugging aid -- the training path never materialises it)."""
+    zs = _s20_of(z)
+    if zs is not None:
+        lo, hi, bias, scale = zs
+        nib = torch.stack(((hi & 15), (hi >> 4) & 15), dim=-1).reshape(lo.shape).to(torch.int32)
+        S = ((lo.to(torch.int32) & 0xFFFF) | (nib << 16))
+        S = torch.where(S >= (1 << 19), S - (1 << 20), S)
+        y = S.to(torch.float32) * torch.tensor(scale, dtype=torch.float32, device=lo.device)
+        return y + bias if bias is not None else y
+    zz = _z16_of(z)
+    if zz is not None:
+        y = zz[0].to(torch.float32)
+        return y + zz[1] if zz[1] is not None else y
+    return z
+
+
+def _pixels_fwd_s20(q, wq, M, N, K, a, bias, R, s0):
+    chunk = int(L.lib().bnn_gemm_i8_bnstats_chunk(M, N))
+    rows = (M + chunk - 1) // chunk
+    dev = q.device
+    part = torch.empty((2, rows, N), dtype=torch.float64, device=dev)
+    lo = torch.empty((M, N), dtype=torch.int16, device=dev)
+    hi = torch.empty((M, N // 2), dtype=torch.uint8, device=dev)
+    Kp = q.shape[1]
+    assert wq.shape[1] == Kp and Kp % ALIGN == 0
+    # a snapshot of the bias: the optimizer updates the Parameter in place after this step's backward
+    bs = bias.clone() if bias is not None else None
+    name = f"{gemm_kernel_name(1, 1, M, N, Kp)} [pixels s20]" if _TIMER is not None else ""
+    with _timed(name, 2.0 * M * N * K, M * Kp + N * Kp + 2.5 * M * N):
+        L.call("bnn_gemm_i8_affine_bnstats_s20", L.ptr(q), Kp, L.ptr(wq), Kp, L.ptr(R), float(s0), K, L.ptr(lo),
+               L.ptr(hi), N, M, N, Kp, L.ptr(part), rows, L.ptr(_const_vec(a, N, dev)), L.ptr(bias), L.stream())
+    y = _s20_carrier(lo, hi, bs, a)
+    setattr(y, _FSTATS_ATTR, (part, rows, chunk, M, N, "pixels", 0.0, 0))
+    return y
+
+
 def _fstats_of(z, M, C, drop=(0.0, 0)):
     """The forward-statistics partials a GEMM epilogue attached to z (None if absent, stale, or
     formed for another dropout (p, seed) than the consuming BatchNorm's)."""
@@ -833,7 +897,7 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
     binarised) fed by ToTensor[/Normalize].  No gradient flows to the pixels."""
 
     @staticmethod
-    def forward(ctx, u, weight, bias, a, s0, cache=False):
+    def forward(ctx, u, weight, bias, a, s0, cache=False, emit_s20=False):
         _check(u, dtype=torch.uint8)
         _check(weight, bias)
         M, K = u.shape
@@ -849,8 +913,12 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
         wq, _ = packed_weight(weight, "i8", True, False, cache)
         R = row_sums(wq, K)
         bvec = bias.detach() if bias is not None else None
-        if (PIX_STATS and need_dw and K <= q.shape[1]
-                and L.lib().bnn_gemm_i8_bnstats_ok(M, N, q.shape[1], q.shape[1], wq.shape[1])):
+        stats_ok = (PIX_STATS and need_dw and K <= q.shape[1]
+                    and L.lib().bnn_gemm_i8_bnstats_ok(M, N, q.shape[1], q.shape[1], wq.shape[1]))
+        if (stats_ok and emit_s20 and S20 and I8C_HANDOFF and N % 256 == 0
+                and L.lib().bnn_gemm_i8_s20_ok(M, N, q.shape[1], K, float(s0))):
+            y = _pixels_fwd_s20(q, wq, M, N, K, a, bvec, R, s0)
+        elif stats_ok:
             y = _pixels_fwd_with_stats(q, wq, M, N, K, _const_vec(a, N, u.device), bvec, R, s0)
         else:
             y = gemm_i8_affine(q, 1, wq, 1, M, N, b_scale=_const_vec(a, N, u.device), bias=bvec, col_off=R,
@@ -882,16 +950,20 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
                 dw = gemm_i8_affine(dt, 3, qt, 1, N, K, a_scale=sc, b_scale=_const_vec(ctx.a, K, dev),
                                     row_off=ds, off_mul=ctx.s0, k_true=M, label="pixels")
             db = cs
-        return None, dw, db, None, None, None
+        return None, dw, db, None, None, None, None
 
 
-def binary_linear_pixels(u, weight, bias=None, normalize=None, cache=False):
-    """fc1 on u8 pixels [.., K] (leading dims flattened); ``normalize`` = (mean, std) or None."""
+def binary_linear_pixels(u, weight, bias=None, normalize=None, cache=False, emit_compact=False):
+    """fc1 on u8 pixels [.., K] (leading dims flattened); ``normalize`` = (mean, std) or None.
+    emit_compact: the output may travel as an s20 placeholder (its consumer must be the
+    training-mode fused bn_hardtanh_binary_linear with the FP4/FP6 backend; see nets.MLP)."""
     if u.dtype != torch.uint8:
         raise TypeError("binary_linear_pixels: expects uint8 pixels")
     a, s0 = pixel_affine(normalize)
     lead = u.shape[:-1]
-    y = BinaryLinearPixelsFunction.apply(u.reshape(-1, u.shape[-1]), weight, bias, a, s0, cache)
+    if emit_compact and len(lead) != 1:
+        raise ValueError("binary_linear_pixels: a compact output needs a 2-D batch")
+    y = BinaryLinearPixelsFunction.apply(u.reshape(-1, u.shape[-1]), weight, bias, a, s0, cache, bool(emit_compact))
     # a 2-D batch returns the Function's own output: it carries the int8 column-digit hand-off
     # marker (_I8C_WANT) a reshape view would drop
     return y if len(lead) == 1 else y.reshape(*lead, weight.shape[0])
@@ -953,6 +1025,11 @@ def _pair_same(v, what):
             raise NotImplementedError(f"bnn_amd: asymmetric {what} {v} is not supported")
         return int(v[0])
     return int(v)
+
+
+# BNN_CONV_C1F=1 / 0: the one-input-channel VALU filter-gradient kernel on / off (A/B timing);
+# unset: the library's default
+_CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
 
 
 # Compact conv outputs (zq): a binary-input BinarizeConv2d computes exact integer sums I (|I| <=
@@ -1055,6 +1132,9 @@ class BinaryConv2dFunction(torch.autograd.Function):
             ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
                              dtype=torch.uint8, device=x.device)
             with _timed("conv2d_bwd_filter", 2 * macs, 4 * (dy.numel() + x.numel() + w.numel())):
+                if _CONV_C1F[0] is not None:
+                    L.call("bnn_conv_set_c1_filter", int(_CONV_C1F[0] != "0"))
+                    _CONV_C1F[0] = None
                 L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
                        L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
                        L.stream())
@@ -1239,9 +1319,10 @@ I8C_HANDOFF = True
 I8C_HANDOFFS = 0          # hand-offs made (tests check the path actually ran)
 
 
-def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db, pre=None):
+def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db, pre=None, s20=None):
     """pre = (part, R): the statistics and the digit bound's maxima from the dX GEMM's epilogue
-    (gemm_fp6_bnstats mode 2)."""
+    (gemm_fp6_bnstats mode 2).  s20 = (low bits, nibbles, bias, scale): x in its compact form
+    (x unused)."""
     dev = x.device
     ldqt = round_up(M)
     dg = torch.empty((3, C, ldqt), dtype=torch.int8, device=dev)
@@ -1252,10 +1333,17 @@ def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db, pre=None):
     if pre is not None:
         L.call("bnn_bn_bwd_stats_pre", L.ptr(pre[0]), pre[1], M, C, 2, L.ptr(w), L.ptr(invstd), L.ptr(dw), L.ptr(db),
                L.ptr(sc), L.ptr(ds), L.ptr(ws), L.stream())
-    with _timed("bn_bwd_i8cols", 0, (8 if pre is not None else 16) * M * C + dg.numel()):
-        L.call("bnn_bn_bwd_i8cols" + ("_pre" if pre is not None else ""), L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
-               L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc),
-               L.ptr(cs), L.ptr(ds), L.ptr(ws), L.stream())
+    xb = 2.5 if s20 is not None else 4
+    with _timed("bn_bwd_i8cols", 0, (xb + 4) * (1 if pre is not None else 2) * M * C + dg.numel()):
+        sfx = "_pre" if pre is not None else ""
+        if s20 is not None:
+            L.call("bnn_bn_bwd_i8cols_s20" + sfx, L.ptr(s20[0]), L.ptr(s20[1]), L.ptr(s20[2]), s20[3], L.ptr(dy), M, C,
+                   L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt,
+                   C * ldqt, L.ptr(sc), L.ptr(cs), L.ptr(ds), L.ptr(ws), L.stream())
+        else:
+            L.call("bnn_bn_bwd_i8cols" + sfx, L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
+                   L.ptr(mlo), 1, L.ptr(dw), L.ptr(db), L.ptr(dg), ldqt, C * ldqt, L.ptr(sc), L.ptr(cs), L.ptr(ds),
+                   L.ptr(ws), L.stream())
     dz = _dz_placeholder(M, C, dev)
     setattr(dz, _I8C_ATTR, (_q6_key(dz), dg, sc, cs, ds))
     global I8C_HANDOFFS
@@ -1640,7 +1728,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         ctx.i8c = (I8C_HANDOFF and bool(getattr(z, _I8C_WANT, False)) and training and not ctx.q6
                    and z.dim() == 2 and z.shape[-1] % 4 == 0)
         zz = _z16_of(z)                       # (int16, bias): z in its compact form
-        if zz is None:
+        zs = _s20_of(z)                       # (int16 low bits, nibbles, bias, scale): fc1's compact z1
+        if zz is None and zs is None:
             z = _c2d(z)
         M, C = z.shape
         N = weight.shape[0]
@@ -1648,6 +1737,9 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
         ctx.fp6 = fp4 and DIGIT_GEMM == "fp6"
         if zz is not None and not (training and ctx.fp6 and ctx.q6 and C % 256 == 0):
             raise RuntimeError("a z16 pre-activation needs the training-mode FP4/FP6 consumer (z16_ok)")
+        if zs is not None and not (training and ctx.fp6 and ctx.i8c and C % 256 == 0 and _fstats_of(z, M, C)):
+            raise RuntimeError("an s20 pre-activation needs the training-mode FP4/FP6 consumer with the "
+                               "int8 column-digit backward and the GEMM-epilogue statistics")
         gw = bn_w.detach() if bn_w is not None else None
         gb = bn_b.detach() if bn_b is not None else None
         if training:
@@ -1665,6 +1757,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                     L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(rm), L.ptr(rv), mom,
                            float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
                 elif zz is None:
+                    assert zs is None
                     L.call("bnn_bn_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv), mom,
                            float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
                 else:
@@ -1683,9 +1776,13 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                         dtype=torch.uint8 if fp4 else torch.int8, device=z.device)
         ctx.qt_panel = need_dw and qf == "fp4p"
         qt = _qt_buffer(C, M, qf, z.device) if need_dw else None
-        nx = 4 if zz is None else 2
+        nx = 2.5 if zs is not None else (4 if zz is None else 2)
         with _timed("bn_apply_pack", 0, nx * M * C + q.numel() + (qt.numel() if qt is not None else 0)):
-            if zz is None:
+            if zs is not None:
+                L.call("bnn_bn_apply_pack_s20", L.ptr(zs[0]), L.ptr(zs[1]), L.ptr(zs[2]), zs[3], M, C, L.ptr(mean),
+                       L.ptr(invstd), L.ptr(mlo), L.ptr(gw), L.ptr(gb), L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1],
+                       1 if ctx.qt_panel else 0, L.stream())
+            elif zz is None:
                 L.call("bnn_bn_apply_pack", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
                        L.ptr(gb), 1 if fp4 else 0, L.ptr(q), q.shape[1], L.ptr(qt), qt.shape[1] if qt is not None else 0,
                        _QT_CODE[qf], L.stream())
@@ -1715,10 +1812,15 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             y = gemm_fp4(q, wq, M, N, bias=b, k_true=C)
         else:
             y = gemm_i8(q, 1, wq, 1, M, N, bias=b, k_true=C)
-        if zz is None:
+        if zs is not None:
+            ctx.save_for_backward(zs[0], gw, gb, mean, invstd, mlo, qt, wqt, zs[2])
+            ctx.s20 = (zs[1], zs[3])          # the nibble plane and the scale
+        elif zz is None:
             ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, qt, wqt, None)
         else:
             ctx.save_for_backward(zz[0], gw, gb, mean, invstd, mlo, qt, wqt, zz[1])
+        if zs is None:
+            ctx.s20 = None
         ctx.z16 = zz is not None
         ctx.weight_ref = weight
         ctx.training = training
@@ -1759,7 +1861,7 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
             st = None
             if ctx.fp6:
                 A = pre[0] if pre is not None else quant6_rows(dy)
-                if ctx.training and (ctx.q6 or ctx.i8c) and _bn_epi_ok(M, C, A.Kp):
+                if ctx.training and (ctx.q6 or ctx.i8c) and ctx.s20 is None and _bn_epi_ok(M, C, A.Kp):
                     # the BatchNorm backward's statistics come with dh from the GEMM's epilogue
                     dh, part, R = gemm_fp6_bnstats(A, wqt, wqt.shape[1] // 32, C, z, zb if ctx.z16 else None,
                                                    ctx.z16, mean, mlo, invstd, gw, gb, 1 if ctx.q6 else 2)
@@ -1778,7 +1880,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                 dz = _bn_bwd_q6(z, dh, M, C, gw, gb, mean, invstd, mlo, True, 0.0, 0, dgw, dgb, ws, "bn_bwd_q6",
                                 z16=(z, zb) if ctx.z16 else None, pre=st)
             elif ctx.i8c:
-                dz = _bn_bwd_i8c(z, dh, M, C, gw, gb, mean, invstd, mlo, dgw, dgb, pre=st)
+                dz = _bn_bwd_i8c(z, dh, M, C, gw, gb, mean, invstd, mlo, dgw, dgb, pre=st,
+                                 s20=(z, ctx.s20[0], zb, ctx.s20[1]) if ctx.s20 is not None else None)
             else:
                 dz = torch.empty_like(z)
                 with _timed("bn_bwd", 0, 16 * M * C):

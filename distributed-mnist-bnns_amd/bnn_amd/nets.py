@@ -12,6 +12,7 @@
   Hardtanh in place of ReLU: conv5x5(1->16,p2)-BN-Hardtanh-MaxPool2, conv5x5(16->32,p2)-BN-
   Hardtanh-MaxPool2, Linear(1568->10), LogSoftmax.
 """
+import torch
 import torch.nn as nn
 
 from . import functional as BF
@@ -82,9 +83,16 @@ class MLP(nn.Module):
                 and x_width % 256 == 0 and self.fc4.out_features == BF.HEAD_NOUT and self.bn3.track_running_stats
                 and self.bn3.momentum is not None)
 
+    def _s20(self, x):
+        """fc1 (on u8 pixels) may hand z1 on as its exact integer sums (functional S20): its consumer
+        is the training-mode fused bn1 -> fc2 op on the FP4/FP6 backend."""
+        return (x.dtype == torch.uint8 and x.is_cuda and self.fused_bn and self.training and self.bn1.training
+                and self.bn1.track_running_stats and self.fc2.backend == "fp4" and BF.DIGIT_GEMM == "fp6"
+                and not self.fc2.org_protocol and self.fc1.out_features % 256 == 0)
+
     def forward(self, x):
         x = x.view(-1, 28 * 28)
-        z1 = self.fc1(x)
+        z1 = self.fc1(x, emit_compact=True) if self._s20(x) else self.fc1(x)
         M = z1.shape[0]
         fuse2 = self._fusable(self.fc2, z1)
         # fc2's output feeds the fused bn2 -> fc3 op; fc3's the fused head

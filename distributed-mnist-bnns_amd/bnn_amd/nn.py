@@ -98,7 +98,9 @@ class BinarizeLinear(nn.Linear):
 
     pixel_normalize = None   # (mean, std) of a Normalize after ToTensor, for uint8 inputs
 
-    def forward(self, input):
+    def forward(self, input, emit_compact=False):
+        # emit_compact (the build's fused MLP only): a u8-pixel layer's output may travel as its
+        # exact integer sums (functional.binary_linear_pixels, s20)
         binarize = input.size(1) != 784                       # :75
         if input.dtype == torch.uint8:
             if binarize:
@@ -108,7 +110,7 @@ class BinarizeLinear(nn.Linear):
                 if self.bias is not None:
                     self.bias.org = self.bias.data.clone()
             return BF.binary_linear_pixels(input, self.weight, self.bias, self.pixel_normalize,
-                                           cache=not self.org_protocol)
+                                           cache=not self.org_protocol, emit_compact=emit_compact)
         if binarize and self.mutate_input:
             input.data = BF.sign(input.data)                    # :76
         if self.org_protocol:

@@ -76,7 +76,7 @@ __device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4])
 //         ([chunks][C] each, max|xhat| R*C floats after max|g|): the a-priori bound on |dz| that
 //         bnn_bn_bwd_i8cols scales its int8 column digits by (no column-max pass over dz).
 // One thread = 4 adjacent columns (float4), rows walked in 16-row float partials folded to double.
-template <int MODE, bool Z16 = false>
+template <int MODE, int XF = 0>
 __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restrict__ dy,
                                                    int64_t M, int64_t C, const float* __restrict__ mean,
                                                    const float* __restrict__ mean_lo,
@@ -99,9 +99,9 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
   float mu[4], lo[4] = {0, 0, 0, 0}, is[4] = {1, 1, 1, 1}, ga[4] = {1, 1, 1, 1}, be[4] = {0, 0, 0, 0};
   float gmx[4] = {0, 0, 0, 0}, xmx[4] = {0, 0, 0, 0};   // MODE 2
-  const float4 xb = xin_bias4<Z16>(xin, c);
+  const float4 xb = xin_bias4<XF>(xin, c);
   if (MODE == 0) {
-    const float4 sv = xin_load4<Z16>(xin, r0 * C + c, xb);
+    const float4 sv = xin_load4<XF>(xin, r0 * C + c, xb);
     mu[0] = sv.x;
     mu[1] = sv.y;
     mu[2] = sv.z;
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u < re ? rb + u : re - 1;
-      xv8[u] = xin_load4<Z16>(xin, rr * C + c, xb);
+      xv8[u] = xin_load4<XF>(xin, rr * C + c, xb);
       if constexpr (BWD) gb[u] = ld4(dy + rr * C + c);
     }
 #pragma unroll
@@ -1024,6 +1024,16 @@ bool bn_args_ok16(const XIn& in, int64_t M, int64_t C) {
          (C / 4) * bn_chunks(M, C) < (1LL << 31) && (M + apply_rows(M, C) - 1) / apply_rows(M, C) <= 65535;
 }
 
+// the s20 form (XIn XF 2): the int16 plane as above, the nibble plane 2-B aligned (4 per 2-B load)
+bool bn_args_ok20(const XIn& in, int64_t M, int64_t C) {
+  return bn_args_ok16(in, M, C) && in.hi && (reinterpret_cast<uintptr_t>(in.hi) & 1) == 0;
+}
+
+bool bn_args_okf(const XIn& in, int xf, int64_t M, int64_t C) {
+  return xf == 2 ? bn_args_ok20(in, M, C)
+                 : (xf == 1 ? bn_args_ok16(in, M, C) : bn_args_ok(reinterpret_cast<const float*>(in.p), M, C));
+}
+
 
 // ------------------------------------------------------------------ BatchNorm2d (+ Hardtanh, + MaxPool2d(2))
 // NCHW [N][C][H][W] activations of the binarized CNN (conv -> BatchNorm2d -> Hardtanh -> MaxPool2d(2),
@@ -1390,10 +1400,10 @@ static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const floa
   // without a caller buffer the lo part of the mean lives in the workspace (the bwd's k0 slot)
   float* lo = save_mean_lo ? save_mean_lo : reinterpret_cast<float*>(p1 + R * C);
   if (z16)
-    hipLaunchKernelGGL((bn_reduce_k<0, true>), reduce_grid(M, C), dim3(256), 0, s, xin,
+    hipLaunchKernelGGL((bn_reduce_k<0, 1>), reduce_grid(M, C), dim3(256), 0, s, xin,
                        nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
   else
-    hipLaunchKernelGGL((bn_reduce_k<0, false>), reduce_grid(M, C), dim3(256), 0, s, xin,
+    hipLaunchKernelGGL((bn_reduce_k<0, 0>), reduce_grid(M, C), dim3(256), 0, s, xin,
                        nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
                      running_var, save_mean, save_invstd, lo, bn_chunk_rows(M, C), (int64_t)1);
@@ -1486,7 +1496,7 @@ static int bn_bwd_impl(const float* x, const float* dy, int64_t M, int64_t C, co
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy,
+  hipLaunchKernelGGL((bn_reduce_k<1, 0>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy,
                      M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
@@ -1512,12 +1522,13 @@ int64_t bn_reduce_chunks(int64_t M, int64_t C) { return bn_chunks(M, C); }
 // The statistics half of the training-mode backward (bnn_bn_bwd without its apply pass): k0 =
 // sum g, k1 = sum g*xhat per column (and dgamma / dbeta) in `work` (bnn_bn_workspace bytes).
 // For passes in other files that form dz themselves (bnn_bn_bwd_i8cols, bnn_pack.hip).
-int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+int bn_bwd_sums(XIn xin, int xf, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                 const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                 float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out,
                 float* pmx, float* scale, int64_t* dsum) {
-  if (!bn_args_ok(x, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd || !work || !vec_ok(gamma) ||
-      !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo)) {
+  if ((xf != 0 && xf != 2) || !bn_args_okf(xin, xf, M, C) || !dy || !aligned16(dy) || !save_mean || !save_invstd ||
+      !work || !vec_ok(gamma) || !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) ||
+      !vec_ok(save_mean_lo)) {
     set_error("bn_bwd_sums: bad arguments");
     return kErrInval;
   }
@@ -1530,12 +1541,20 @@ int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const flo
     set_error("bn_bwd_sums: the bound pass needs the scale output");
     return kErrInval;
   }
-  if (pmx)
-    hipLaunchKernelGGL((bn_reduce_k<2, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C,
+  if (pmx && xf == 2)
+    hipLaunchKernelGGL((bn_reduce_k<2, 2>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C,
                        save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
                        make_drop(0.f, 0), pmx);
+  else if (pmx)
+    hipLaunchKernelGGL((bn_reduce_k<2, 0>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
+                       make_drop(0.f, 0), pmx);
+  else if (xf == 2)
+    hipLaunchKernelGGL((bn_reduce_k<1, 2>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C,
+                       save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
+                       make_drop(0.f, 0));
   else
-    hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, XIn{x, nullptr}, dy, M, C,
+    hipLaunchKernelGGL((bn_reduce_k<1, 0>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C,
                        save_mean, save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C),
                        make_drop(0.f, 0));
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1,
@@ -1603,10 +1622,10 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
   }
   if (!pre) {
     if (z16)
-      hipLaunchKernelGGL((bn_reduce_k<1, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+      hipLaunchKernelGGL((bn_reduce_k<1, 1>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
                          save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
     else
-      hipLaunchKernelGGL((bn_reduce_k<1, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
+      hipLaunchKernelGGL((bn_reduce_k<1, 0>), reduce_grid(M, C), dim3(256), 0, s, xin, dy, M, C, save_mean,
                          save_mean_lo, save_invstd, gamma, beta, hardtanh, p0, p1, bn_chunk_rows(M, C), dp);
     hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   }

@@ -31,50 +31,86 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // +1 for x>0, -1 for x<0, 0 for x==0 (NaN maps to 0 here; the reference would propagate NaN).
 __device__ __forceinline__ int tsign(float x) { return (x > 0.f) - (x < 0.f); }
 
-// The input of a BatchNorm pass: fp32 x [M][C], or (z16) the int16 exact dot products I of the
-// ternary BinarizeLinear that produced it (bnn_gemm_fp4_i16) plus that layer's fp32 bias, read as
-// x = fl(I + bias) -- bit-identical to the fp32 value the GEMM epilogue would have stored (it
-// computes the same one rounding), at half the bytes.  bias may be null (a bias-free Linear).
+// The input of a BatchNorm pass, in one of three forms (XF):
+//  0  fp32 x [M][C];
+//  1  (z16) the int16 exact dot products I of the ternary BinarizeLinear that produced it
+//     (bnn_gemm_fp4_i16) plus that layer's fp32 bias, read as x = fl(I + bias) -- bit-identical to
+//     the fp32 value the GEMM epilogue would have stored (it computes the same one rounding), at
+//     half the bytes;
+//  2  (s20) the exact integer sums S = sum_k u_k sign(w_k) of the u8-pixel layer (bnn_gemm_i8_affine
+//     _s20), |S| < 2^19, as 20-bit two's complement: the low 16 bits [M][C] int16 at p and the high
+//     4 bits as nibbles [M][C/2] at hi (column 2j in the low nibble of byte j), read as
+//     x = fl(fl(S * scale) + bias) -- bit-identical to the fp32 z of bnn_gemm_i8_affine (whose
+//     double (S * a) rounds once, as the fp32 product of the exact fl(S) does), at 2.5 bytes.
+// bias may be null (a bias-free Linear).
 struct XIn {
   const void* p;
   const float* bias;
+  const uint8_t* hi = nullptr;   // XF 2: the high nibbles
+  float scale = 1.f;             // XF 2: the pixel scale a
 };
 
-template <bool Z16>
+template <int XF>
 __device__ __forceinline__ float4 xin_bias4(const XIn& in, int64_t c) {
-  if constexpr (Z16) {
+  if constexpr (XF != 0) {
     if (in.bias != nullptr) return *reinterpret_cast<const float4*>(in.bias + c);
   }
   return make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// 4 consecutive elements from flat index idx (a multiple of 4) in two steps -- the raw load
-// (uint2 of 4 int16, or float4) and the conversion with b = xin_bias4 of their columns -- so a
-// software-pipelined pass can issue the load early and convert at use (converting at issue would
-// make the load's first use, and its wait, immediate).
-template <bool Z16>
-using XRaw = typename std::conditional<Z16, uint2, float4>::type;
+struct S20Raw {
+  uint2 lo;
+  uint32_t hi;   // 4 nibbles in the low 16 bits
+};
 
-template <bool Z16>
-__device__ __forceinline__ XRaw<Z16> xin_raw4(const XIn& in, int64_t idx) {
-  if constexpr (Z16)
+// 4 consecutive elements from flat index idx (a multiple of 4) in two steps -- the raw load
+// (uint2 of 4 int16, float4, or the s20 pieces) and the conversion with b = xin_bias4 of their
+// columns -- so a software-pipelined pass can issue the load early and convert at use (converting
+// at issue would make the load's first use, and its wait, immediate).
+template <int XF>
+using XRaw = typename std::conditional<XF == 1, uint2, typename std::conditional<XF == 2, S20Raw, float4>::type>::type;
+
+template <int XF>
+__device__ __forceinline__ XRaw<XF> xin_raw4(const XIn& in, int64_t idx) {
+  if constexpr (XF == 1) {
     return *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(in.p) + idx);
-  else
+  } else if constexpr (XF == 2) {
+    S20Raw r;
+    r.lo = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(in.p) + idx);
+    r.hi = *reinterpret_cast<const uint16_t*>(in.hi + (idx >> 1));
+    return r;
+  } else {
     return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(in.p) + idx);
+  }
 }
 
-template <bool Z16>
-__device__ __forceinline__ float4 xin_cvt4(const XRaw<Z16>& u, const float4& b) {
-  if constexpr (Z16)
+// S from a 32-bit window whose bits 0-15 are its low 16 bits and bits 16-19 its nibble (one
+// v_alignbit_b32 builds it), sign-extended from bit 19 (v_bfe_i32)
+__device__ __forceinline__ int s20_sext(uint32_t w) { return ((int)(w << 12)) >> 12; }
+
+template <int XF>
+__device__ __forceinline__ float4 xin_cvt4(const XRaw<XF>& u, const float4& b, float scale = 1.f) {
+  if constexpr (XF == 1) {
     return make_float4((float)(int16_t)(u.x & 0xFFFFu) + b.x, (float)(int16_t)(u.x >> 16) + b.y,
                        (float)(int16_t)(u.y & 0xFFFFu) + b.z, (float)(int16_t)(u.y >> 16) + b.w);
-  else
+  } else if constexpr (XF == 2) {
+    // no mul+add contraction: fl(fl(S * scale) + bias), the GEMM epilogue's two roundings
+#pragma clang fp contract(off)
+    // ({hi >> 4k, lo} >> 16)[31:0]: the element's 16 low bits, then its nibble at bit 16
+    const int s0 = s20_sext(__builtin_amdgcn_alignbit(u.hi, u.lo.x << 16, 16));
+    const int s1 = s20_sext(__builtin_amdgcn_alignbit(u.hi >> 4, u.lo.x, 16));
+    const int s2 = s20_sext(__builtin_amdgcn_alignbit(u.hi >> 8, u.lo.y << 16, 16));
+    const int s3 = s20_sext(__builtin_amdgcn_alignbit(u.hi >> 12, u.lo.y, 16));
+    return make_float4((float)s0 * scale + b.x, (float)s1 * scale + b.y, (float)s2 * scale + b.z,
+                       (float)s3 * scale + b.w);
+  } else {
     return u;
+  }
 }
 
-template <bool Z16>
+template <int XF>
 __device__ __forceinline__ float4 xin_load4(const XIn& in, int64_t idx, const float4& b) {
-  return xin_cvt4<Z16>(xin_raw4<Z16>(in, idx), b);
+  return xin_cvt4<XF>(xin_raw4<XF>(in, idx), b, in.scale);
 }
 
 // The training-mode BatchNorm(+Hardtanh) backward for one element (mnist-dist2.py:66-74): with
@@ -122,6 +158,25 @@ __device__ __forceinline__ Digits to_digits(float x, int shift) {
   const int d1 = ((v1 + 128) & 255) - 128;
   const int d2 = (v1 - d1) >> 8;
   return Digits{(int8_t)d0, (int8_t)d1, (int8_t)d2};
+}
+
+// to_digits' three digits packed as bytes d0 | d1 << 8 | d2 << 16 in one add and one xor: every byte
+// of u = v + 0x808080 is d_i + 128 (d0 + 128, d1 + 128 in [0, 255]: no carries), and
+// d_i & 255 = (d_i + 128) ^ 0x80 -- bit-identical to packing to_digits' bytes for every v (the top
+// digit wraps the same way; unsigned arithmetic: no overflow).
+__device__ __forceinline__ uint32_t digits24(float x, int shift) {
+  const int v = __float2int_rn(ldexpf(x, shift));
+  return (((uint32_t)v + 0x808080u) ^ 0x808080u) & 0xFFFFFFu;
+}
+
+// d0 + 256 d1 + 65536 d2 of a packed digit word (the signed bytes' combination) in two ops
+__device__ __forceinline__ int digits24_value(uint32_t g) { return (int)((g & 0xFFFFFFu) ^ 0x808080u) - 0x808080; }
+
+// byte b of each of 4 words, packed [w0.b, w1.b, w2.b, w3.b] (three v_perm_b32)
+__device__ __forceinline__ uint32_t gather_byte4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int b) {
+  const uint32_t sel = (uint32_t)b | ((uint32_t)(4 + b) << 8) | 0x0C0C0000u;
+  const uint32_t lo = __builtin_amdgcn_perm(w1, w0, sel), hi = __builtin_amdgcn_perm(w3, w2, sel);
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 // From the absolute maximum of a vector: the shift 22-E and the scale 2^(E-22).

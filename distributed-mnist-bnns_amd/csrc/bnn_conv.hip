@@ -577,6 +577,110 @@ __global__ __launch_bounds__(256) void conv_filter_tile_reduce2_k(const double* 
   }
 }
 
+// ------------------------------------------------------------------ one-input-channel filter gradient (VALU)
+// dW[co][kh][kw] = sum_{n,oh,ow} dY[n][co][oh][ow] * Xb[n][oh + kh - pad][ow + kw - pad] (+ dB = sum dY)
+// for a layer with ONE input channel (the BinCNN's conv1, 16 x 1 x 5 x 5 over 28 x 28; binarized_
+// modules.py:100-101 binarises its input): KH*KW MACs per dY element, 1.3 G MACs at B = 4096 -- ~20 us
+// of VALU, so the pass is bound by reading dY once (205 MB), which it does with coalesced 16-B loads
+// (a channel plane's 4-pixel units walked by consecutive lanes).  The bf16x3 MFMA form spent its
+// time staging dY into LDS three planes at a time (106 us).  Per sample the (binarised) input plane
+// sits in LDS with a zero halo, double-buffered (the next sample's plane is loaded into registers
+// while this one is used); thread = (channel co = t / TPC, the units r, r + TPC, ... of its plane),
+// keeping its channel's KH*KW sums and the bias sum in fp32 registers over the workgroup's samples;
+// the TPC threads of a channel are folded in a fixed order into the workgroup's partial row
+// (conv_filter_tile_reduce{1,2}_k, double).  Deterministic.
+constexpr int C1F_T = 256, C1F_SPB = 4, C1F_PX = 4;
+
+struct C1Filt {
+  int H, W, OH, OW, Co, pad, XR, XW, TPC;   // XR x XW: the haloed input plane in LDS
+};
+
+template <int KH, int KW>
+__global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1_k(const float* __restrict__ dy,
+                                                              const float* __restrict__ x, int binarize,
+                                                              float* __restrict__ part, int64_t N, C1Filt g,
+                                                              int with_bias) {
+  constexpr int NX = (KW + 6) / 4;   // float4 pieces of an input row a 4-pixel unit reads
+  constexpr int KK = KH * KW;
+  extern __shared__ __attribute__((aligned(16))) float c1s[];
+  const int plane = g.XR * g.XW;
+  float* red = c1s + 2 * plane;      // [C1F_T][KK + 1] fold buffer
+  const int t = threadIdx.x;
+  const int co = t / g.TPC, r = t - co * g.TPC;
+  const int hw = g.H * g.W, ohw = g.OH * g.OW, nu = ohw / 4, uq = g.OW / 4;
+  for (int i = t; i < 2 * plane; i += C1F_T) c1s[i] = 0.f;   // zero halos (interiors rewritten per sample)
+  float acc[KK], bacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < KK; ++k) acc[k] = 0.f;
+  const int64_t n0 = (int64_t)blockIdx.x * C1F_SPB, n1 = n0 + C1F_SPB < N ? n0 + C1F_SPB : N;
+  float px[C1F_PX];
+  auto fetch = [&](int64_t n) {   // clamped, unconditional: the loads batch
+#pragma unroll
+    for (int s = 0; s < C1F_PX; ++s) px[s] = x[n * hw + min(t + s * C1F_T, hw - 1)];
+  };
+  auto put = [&](int b) {
+    for (int s = 0; s < C1F_PX; ++s) {
+      const int i = t + s * C1F_T;
+      if (i < hw) {
+        const int ih = i / g.W, iw = i - ih * g.W;
+        c1s[b * plane + (ih + g.pad) * g.XW + iw + g.pad] = binarize ? (float)tsign(px[s]) : px[s];
+      }
+    }
+  };
+  __syncthreads();
+  if (n0 < n1) {
+    fetch(n0);
+    put(0);
+  }
+  for (int64_t n = n0; n < n1; ++n) {
+    const int b = (int)((n - n0) & 1);
+    __syncthreads();   // plane b complete; plane b ^ 1's last reader (sample n - 1) is done
+    if (n + 1 < n1) fetch(n + 1);
+    if (co < g.Co) {
+      const float* xb = c1s + b * plane;
+      const float* dn = dy + (n * g.Co + co) * (int64_t)ohw;
+      for (int u = r; u < nu; u += g.TPC) {
+        const float4 d = *reinterpret_cast<const float4*>(dn + 4 * u);
+        const int oh = u / uq, ow0 = 4 * (u - oh * uq);
+        bacc += (d.x + d.y) + (d.z + d.w);
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh) {
+          float xr[4 * NX];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(xb + (oh + kh) * g.XW + ow0 + 4 * j);
+            xr[4 * j] = v.x, xr[4 * j + 1] = v.y, xr[4 * j + 2] = v.z, xr[4 * j + 3] = v.w;
+          }
+#pragma unroll
+          for (int kw = 0; kw < KW; ++kw) {
+            float a = acc[kh * KW + kw];
+            a = fmaf(d.x, xr[kw], a);
+            a = fmaf(d.y, xr[kw + 1], a);
+            a = fmaf(d.z, xr[kw + 2], a);
+            a = fmaf(d.w, xr[kw + 3], a);
+            acc[kh * KW + kw] = a;
+          }
+        }
+      }
+    }
+    if (n + 1 < n1) put(b ^ 1);
+  }
+  // fixed-order fold of a channel's TPC threads
+#pragma unroll
+  for (int k = 0; k < KK; ++k) red[t * (KK + 1) + k] = acc[k];
+  red[t * (KK + 1) + KK] = bacc;
+  __syncthreads();
+  const int64_t nelem = (int64_t)g.Co * KK + g.Co;
+  float* row = part + (int64_t)blockIdx.x * nelem;
+  for (int e = t; e < g.Co * (KK + 1); e += C1F_T) {
+    const int c = e / (KK + 1), k = e - c * (KK + 1);
+    float s = 0.f;
+    for (int q = 0; q < g.TPC; ++q) s += red[(c * g.TPC + q) * (KK + 1) + k];
+    if (k < KK) row[c * KK + k] = s;
+    else row[(int64_t)g.Co * KK + c] = with_bias ? s : 0.f;
+  }
+}
+
 // ------------------------------------------------------------------ f32-MFMA implicit-GEMM backward
 // Both backward convolutions as implicit GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 products,
 // f32 accumulation: the same numerics class as the fp32 reference's sgemm, at the f32 matrix
@@ -1445,6 +1549,29 @@ using namespace bnn;
 // kernel instead of bf16x3; 0: the VALU LDS-tiled / generic kernels (the parity tests' cross-checks).
 static int g_conv_mfma = 1;
 
+// 1 (default): a one-input-channel layer's filter gradient on the VALU kernel (conv_bwd_filter_c1_k);
+// 0: the MFMA / tiled kernels as for any other layer
+static int g_conv_c1f = 1;
+
+BNN_API int bnn_conv_set_c1_filter(int32_t on) {
+  g_conv_c1f = on != 0;
+  return 0;
+}
+
+inline bool c1_filt_geom(const ConvShape& s, C1Filt* g, int64_t* lds) {
+  if (s.C != 1 || s.groups != 1 || s.stride != 1 || s.dil != 1 || !((s.KH == 5 && s.KW == 5) || (s.KH == 3 && s.KW == 3)) ||
+      s.OW % 4 != 0 || s.Co > 64 || C1F_T % s.Co != 0 || s.pad > s.KH - 1 || s.H * s.W > C1F_PX * C1F_T)
+    return false;
+  const int NX = ((int)s.KW + 6) / 4;
+  const int XW = (int)round_up(std::max<int64_t>(s.W + 2 * s.pad, s.OW - 4 + 4 * NX), 4);
+  const int XR = (int)std::max<int64_t>(s.H + 2 * s.pad, s.OH + s.KH - 1);
+  const int64_t bytes = (2 * (int64_t)XR * XW + (int64_t)C1F_T * (s.KH * s.KW + 1)) * (int64_t)sizeof(float);
+  if (bytes > kMaxTileLds) return false;
+  *g = C1Filt{(int)s.H, (int)s.W, (int)s.OH, (int)s.OW, (int)s.Co, s.pad, XR, XW, (int)(C1F_T / s.Co)};
+  *lds = bytes;
+  return true;
+}
+
 BNN_API int bnn_conv_set_mfma(int32_t mode) {
   g_conv_mfma = mode < 0 ? 1 : (mode > 2 ? 1 : mode);
   return 0;
@@ -1682,7 +1809,10 @@ BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co
   const int64_t mnel = Co * ncombo + Co;
   const int64_t mfma = round_up(mparts * mnel * (int64_t)sizeof(float), 256) +
                        filter_slices(mparts) * mnel * (int64_t)sizeof(double);
-  return std::max(std::max(generic, tiled), mfma);
+  const int64_t cparts = (std::max<int64_t>(N, 1) + C1F_SPB - 1) / C1F_SPB;   // conv_bwd_filter_c1_k
+  const int64_t c1 = round_up(cparts * mnel * (int64_t)sizeof(float), 256) +
+                     filter_slices(cparts) * mnel * (int64_t)sizeof(double);
+  return std::max(std::max(generic, tiled), std::max(mfma, c1));
 }
 
 BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_input, float* dw,
@@ -1698,6 +1828,26 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   const int64_t nw = Co * (C / groups) * KH * KW;
   const int64_t nelem = nw + Co;
   const int64_t nchunks = filter_chunks(std::max<int64_t>(N, 1), nelem);
+  C1Filt cf;
+  int64_t clds = 0;
+  if (N > 0 && g_conv_c1f && g_conv_mfma != 0 && c1_filt_geom(s, &cf, &clds)) {
+    const int64_t nblk = (N + C1F_SPB - 1) / C1F_SPB;
+    const int64_t nel = nw + Co;
+    float* part = reinterpret_cast<float*>(work);
+    const size_t lds = (size_t)clds;
+    if (KH == 5) BNN_TILE_LAUNCH((conv_bwd_filter_c1_k<5, 5>), dim3((unsigned)nblk), dim3(C1F_T), lds, st, dy, x,
+                                 binarize_input, part, N, cf, db != nullptr);
+    else BNN_TILE_LAUNCH((conv_bwd_filter_c1_k<3, 3>), dim3((unsigned)nblk), dim3(C1F_T), lds, st, dy, x,
+                         binarize_input, part, N, cf, db != nullptr);
+    const int64_t nsl = filter_slices(nblk);
+    double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                              round_up(nblk * nel * (int64_t)sizeof(float), 256));
+    hipLaunchKernelGGL(conv_filter_tile_reduce1_k, dim3((unsigned)((nel + 255) / 256), (unsigned)nsl), dim3(256), 0,
+                       st, part, nblk, nel, nsl, slice);
+    hipLaunchKernelGGL(conv_filter_tile_reduce2_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, slice,
+                       nsl, (int)Co, (int)(KH * KW), (int)Co, dw, db);
+    return check_launch("bnn_conv2d_bwd_filter");
+  }
   B3Filt bf;
   int64_t blds = 0;
   if (N > 0 && g_conv_mfma == 1 && b3_filt_geom(s, binarize_input, &bf, &blds)) {

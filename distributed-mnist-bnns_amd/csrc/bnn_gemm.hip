@@ -52,6 +52,11 @@ struct GemmParams {
   // 1: row-major tile order (consecutive tiles along N: concurrent tiles write adjacent segments of
   // the same C rows) instead of the grouped raster
   int raster = 0;
+  // s20 output of the u8-pixel statistics form (bnn_gemm_i8_affine_bnstats_s20): the exact integer
+  // S = sum + off_mul * col_off[n] (integral off_mul, |S| < 2^19: host check) as its low 16 bits
+  // [M][ldc] + high nibbles [M][ldc / 2] instead of fp32 C (XIn XF 2 in bnn_common.h)
+  int16_t* S20lo = nullptr;
+  uint8_t* S20hi = nullptr;
 };
 
 __device__ __forceinline__ double int_offset(const GemmParams& p, int row, int col) {
@@ -729,6 +734,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         const double bs = (p.b_scale && cin) ? (double)p.b_scale[col] : 1.0;
         const bool offs = p.row_off || p.col_off;
         const double coff = (p.col_off && cin) ? (double)p.col_off[col] * p.off_mul : 0.0;
+        const int icoff = (int)coff;   // s20: exact (host check)
 #pragma unroll
         for (int sa = 0; sa < SUB; ++sa) {
           const int ti = t * SUB + sa, ui = u * SUB + sb;
@@ -739,7 +745,10 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
             float f;
             if constexpr (DA == 1 && DB == 1) {
               f = (float)acc[0][ti][ui][i];  // exact: |sum| <= K < 2^24
-              if (offs) {
+              if (p.S20lo != nullptr) {
+                // the integer S travels through the patch as its bit pattern
+                f = __int_as_float((int)acc[0][ti][ui][i] + icoff);
+              } else if (offs) {
                 double v = (double)acc[0][ti][ui][i] + coff;
                 if (p.row_off) v += (double)p.row_off[row] * p.off_mul;
                 f = (float)(v * (p.a_scale ? (double)p.a_scale[row] : 1.0) * bs);
@@ -759,7 +768,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
               }
               f = (float)(v * bs * (p.a_scale ? (double)p.a_scale[row] : 1.0));
             }
-            if (p.bias) f += bb;
+            if (p.bias && p.S20lo == nullptr) f += bb;
             patch[lr * 32 + ((((lc >> 2) ^ (lr & 7)) << 2) | (lc & 3))] = f;
           }
         }
@@ -771,6 +780,19 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         const float4 v = *reinterpret_cast<const float4*>(patch + lr * 32 + ((c4 ^ (lr & 7)) << 2));
         const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
         if (row >= p.M) continue;
+        if (p.S20lo != nullptr) {   // N % 4 == 0, ldc % 4 == 0 (host check): 8 B + 2 B per 4 sums
+          const int64_t o = (int64_t)row * p.ldc + c0;
+          if (c0 < p.N) {
+            const int s0 = __float_as_int(v.x), s1 = __float_as_int(v.y), s2 = __float_as_int(v.z),
+                      s3 = __float_as_int(v.w);
+            *reinterpret_cast<uint2*>(p.S20lo + o) =
+                make_uint2(((uint32_t)s0 & 0xFFFFu) | ((uint32_t)s1 << 16), ((uint32_t)s2 & 0xFFFFu) | ((uint32_t)s3 << 16));
+            *reinterpret_cast<uint16_t*>(p.S20hi + (o >> 1)) =
+                (uint16_t)((((uint32_t)s0 >> 16) & 0xFu) | ((((uint32_t)s1 >> 16) & 0xFu) << 4) |
+                           ((((uint32_t)s2 >> 16) & 0xFu) << 8) | ((((uint32_t)s3 >> 16) & 0xFu) << 12));
+          }
+          continue;
+        }
         if (p.C16 != nullptr) {   // ldc % 4 == 0 (host check): one 8-B store of 4 exact sums
           int16_t* d16 = p.C16 + (int64_t)row * p.ldc + c0;
           if (c0 + 3 < p.N) {
@@ -1008,6 +1030,42 @@ BNN_API int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_
                (int)M, (int)N, (int)K, 0, 0, nullptr, col_off, off_mul};
   p.stat = stat;
   p.stat_rows = stat_rows;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return i8_bnstats_variant(M, N)->id == 2 ? launch_v2<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 0, 0, 1>(p, st)
+                                           : launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 0, 0, 1>(p, st);
+}
+
+// bnn_gemm_i8_affine_bnstats writing the s20 form of z (XIn XF 2): z = fl(fl(S * a) + bias) with
+// S = sum + s0 * col_off[n] read back by the *_s20 BatchNorm entries, bit-identical to the fp32 z.
+// Needs an integral s0 (ToTensor without Normalize) and |S| <= K (128 + |s0|) < 2^19; N % 4 == 0.
+BNN_API int bnn_gemm_i8_s20_ok(int64_t M, int64_t N, int64_t K, int64_t k_true, double s0) {
+  return (N % 4 == 0 && s0 == (double)(int64_t)s0 && k_true > 0 && k_true <= K &&
+          (double)k_true * (128.0 + fabs(s0)) < 524288.0)
+             ? 1
+             : 0;
+}
+
+BNN_API int bnn_gemm_i8_affine_bnstats_s20(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
+                                           const int64_t* col_off, double off_mul, int64_t k_true, int16_t* Slo,
+                                           uint8_t* Shi, int64_t ldc, int64_t M, int64_t N, int64_t K, double* stat,
+                                           int64_t stat_rows, const float* b_scale, const float* bias, void* stream) {
+  const int64_t chunk = M > 0 ? bnn_gemm_i8_bnstats_chunk(M, N) : 1;
+  if (!A || !B || !Slo || !Shi || !col_off || !stat || !i8_bnstats_shape_ok(M, N, K, lda, ldb) || ldc < N ||
+      ldc % 4 != 0 || !aligned16(A) || !aligned16(B) || (reinterpret_cast<uintptr_t>(Slo) & 7) != 0 ||
+      (reinterpret_cast<uintptr_t>(Shi) & 1) != 0 || !bnn_gemm_i8_s20_ok(M, N, K, k_true, off_mul) ||
+      stat_rows != (M + chunk - 1) / chunk) {
+    set_error("bnn_gemm_i8_affine_bnstats_s20: bad arguments (M=%lld N=%lld K=%lld k_true=%lld off_mul=%g "
+              "stat_rows=%lld)", (long long)M, (long long)N, (long long)K, (long long)k_true, off_mul,
+              (long long)stat_rows);
+    return kErrInval;
+  }
+  // b_scale / bias enter only the statistics (the stored S carries neither)
+  GemmParams p{A, B, lda, ldb, 0, 0, nullptr, b_scale, bias, nullptr, ldc,
+               (int)M, (int)N, (int)K, 0, 0, nullptr, col_off, off_mul};
+  p.stat = stat;
+  p.stat_rows = stat_rows;
+  p.S20lo = Slo;
+  p.S20hi = Shi;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return i8_bnstats_variant(M, N)->id == 2 ? launch_v2<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 0, 0, 1>(p, st)
                                            : launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 0, 0, 1>(p, st);

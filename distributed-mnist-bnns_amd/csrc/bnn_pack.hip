@@ -247,7 +247,7 @@ __device__ __forceinline__ void nib_transpose8(uint32_t (&x)[8]) {
   for (int i = 0; i < 8; i += 2) nib_swap(x[i], x[i + 1], 4, 0x0F0F0F0Fu);
 }
 
-template <bool Z16>
+template <int XF>
 __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, int64_t C,
                                                            ColAffine af, uint8_t* __restrict__ q, int64_t ldq,
                                                            uint8_t* __restrict__ qt, int64_t ldqt, int64_t pnks) {
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
   const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
   const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
   const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
-  const float4 xb = xin_bias4<Z16>(xin, cb);
+  const float4 xb = xin_bias4<XF>(xin, cb);
   uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
 #pragma unroll 4
   for (int i = 0; i < AP_T / 4; ++i) {
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
     const int64_t m = m0 + r;
     uint32_t code = 0;
     if (m < M) {
-      const float4 f = xin_load4<Z16>(xin, m * C + cb, xb);
+      const float4 f = xin_load4<XF>(xin, m * C + cb, xb);
       const float v[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) code |= fp4_code(tsign(fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]))) << (4 * j);
@@ -451,13 +451,13 @@ __global__ __launch_bounds__(256) void quant_rows_k(const float* __restrict__ x,
       } else {
         for (int j = 0; j < 4; ++j) v[j] = (k + j < K) ? xr[k + j] : 0.f;
       }
-      Digits d[4];
+      uint32_t d[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] = to_digits(v[j], shift);
+      for (int j = 0; j < 4; ++j) d[j] = digits24(v[j], shift);
       int8_t* o = dg + m * ldq + k;
-      *reinterpret_cast<int*>(o) = pack4(d[0].d0, d[1].d0, d[2].d0, d[3].d0);
-      *reinterpret_cast<int*>(o + plane) = pack4(d[0].d1, d[1].d1, d[2].d1, d[3].d1);
-      *reinterpret_cast<int*>(o + 2 * plane) = pack4(d[0].d2, d[1].d2, d[2].d2, d[3].d2);
+      *reinterpret_cast<uint32_t*>(o) = gather_byte4(d[0], d[1], d[2], d[3], 0);
+      *reinterpret_cast<uint32_t*>(o + plane) = gather_byte4(d[0], d[1], d[2], d[3], 1);
+      *reinterpret_cast<uint32_t*>(o + 2 * plane) = gather_byte4(d[0], d[1], d[2], d[3], 2);
     }
   }
 }
@@ -582,37 +582,35 @@ __device__ __forceinline__ void qct_store_t(const int* tile, int t, int64_t n0, 
                                             int64_t* __restrict__ dsum, long long* acc = nullptr) {
   const int nn = t >> 2, mc = (t & 3) * RPL;
   const int64_t n = n0 + nn;
+  // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22 each,
+  // so 4 * RPL of them fit an int): sum (g ^ 0x808080) - count * 0x808080 (digits24_value); the 4
+  // lanes sharing n are adjacent.  Rows beyond ldqt hold zeros.
+  int part = 0;
   if (n < N && m0 + mc < ldqt) {
-    int g[RPL];
+    uint32_t g[RPL];
 #pragma unroll
-    for (int j = 0; j < RPL; ++j) g[j] = qct_at<LD, SWZ, RPL>(tile, mc + j, nn);
+    for (int j = 0; j < RPL; ++j) g[j] = (uint32_t)qct_at<LD, SWZ, RPL>(tile, mc + j, nn);
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      const int sh8 = 8 * d;
 #pragma unroll
       for (int q = 0; q < RPL / 16; ++q) {
         if (m0 + mc + 16 * q >= ldqt) break;
+        const uint32_t* gq = g + 16 * q;
         v4i w;
-        w.x = pack4(g[16 * q + 0] >> sh8, g[16 * q + 1] >> sh8, g[16 * q + 2] >> sh8, g[16 * q + 3] >> sh8);
-        w.y = pack4(g[16 * q + 4] >> sh8, g[16 * q + 5] >> sh8, g[16 * q + 6] >> sh8, g[16 * q + 7] >> sh8);
-        w.z = pack4(g[16 * q + 8] >> sh8, g[16 * q + 9] >> sh8, g[16 * q + 10] >> sh8, g[16 * q + 11] >> sh8);
-        w.w = pack4(g[16 * q + 12] >> sh8, g[16 * q + 13] >> sh8, g[16 * q + 14] >> sh8, g[16 * q + 15] >> sh8);
+        w.x = (int)gather_byte4(gq[0], gq[1], gq[2], gq[3], d);
+        w.y = (int)gather_byte4(gq[4], gq[5], gq[6], gq[7], d);
+        w.z = (int)gather_byte4(gq[8], gq[9], gq[10], gq[11], d);
+        w.w = (int)gather_byte4(gq[12], gq[13], gq[14], gq[15], d);
         *reinterpret_cast<v4i*>(dt + d * plane + n * ldqt + m0 + mc + 16 * q) = w;
       }
     }
+    if (dsum != nullptr) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) part += (int)(g[j] ^ 0x808080u);
+      part -= RPL * 0x808080;
+    }
   }
   if (dsum != nullptr) {
-    // exact integer sum of the combined digits d2*2^16 + d1*2^8 + d0 of column n (|.| <= 2^22
-    // each, so 4 * RPL of them fit an int); the 4 lanes sharing n are adjacent.  Rows beyond
-    // ldqt hold zeros.
-    int part = 0;
-    if (n < N && m0 + mc < ldqt) {
-#pragma unroll
-      for (int j = 0; j < RPL; ++j) {
-        const int g = qct_at<LD, SWZ, RPL>(tile, mc + j, nn);
-        part += (int)(int8_t)(g & 255) + 256 * (int)(int8_t)((g >> 8) & 255) + 65536 * (int)(int8_t)((g >> 16) & 255);
-      }
-    }
     part += __shfl_xor(part, 1, 64);
     part += __shfl_xor(part, 2, 64);
     if (acc != nullptr)
@@ -654,12 +652,7 @@ __global__ __launch_bounds__(256) void quant_cols_t_k(const float* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int sft = sh[c + j];
-    int packed = 0;
-    if (sft != INT32_MIN) {
-      const Digits d = to_digits(v[j], sft);
-      packed = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
-    }
-    tile[r][c + j] = packed;
+    tile[r][c + j] = sft != INT32_MIN ? (int)digits24(v[j], sft) : 0;
   }
   __syncthreads();
   qct_store(tile, t, n0, m0, N, ldqt, plane, dt, dsum);
@@ -730,7 +723,8 @@ constexpr int QC_RT = 8;
 
 __host__ __device__ inline int64_t qc_strips(int64_t M) { return (M + TILE * QC_RT - 1) / (TILE * QC_RT); }
 
-__global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restrict__ x, const float* __restrict__ dy,
+template <int XF>
+__global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(XIn xin, const float* __restrict__ dy,
                                                             int64_t M, int64_t N, BnCols bc,
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
                                                             int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum,
@@ -751,13 +745,15 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
       sft[j] = (s > 0.f && s == s) ? -ilogbf(s) : INT32_MIN;   // INT32_MIN -> digits 0
     }
   }
-  float4 xv[4], gv[4];
+  XRaw<XF> xv[4];
+  float4 gv[4];
+  const float4 xb = c < N ? xin_bias4<XF>(xin, c) : make_float4(0.f, 0.f, 0.f, 0.f);
   auto load = [&](int64_t m0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t m = m0 + 4 * rg + i;
       if (c < N && m < M) {
-        xv[i] = *reinterpret_cast<const float4*>(x + m * N + c);
+        xv[i] = xin_raw4<XF>(xin, m * N + c);
         gv[i] = *reinterpret_cast<const float4*>(dy + m * N + c);
       }
     }
@@ -772,17 +768,15 @@ __global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(const float* __restr
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t m = m0 + 4 * rg + i;
-      const float xs[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+      const float4 xf = xin_cvt4<XF>(xv[i], xb, xin.scale);
+      const float xs[4] = {xf.x, xf.y, xf.z, xf.w}, gs[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
       int packed[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (c < N && m < M) {
           const float v = bn_dz1(xs[j], gs[j], b.m[j], b.lo[j], b.is[j], b.ga[j], b.be[j], b.a0[j], b.a1[j], bc.hardtanh);
           csum[j] += (double)v;
-          if (sft[j] != INT32_MIN) {
-            const Digits d = to_digits(v, sft[j]);
-            packed[j] = (d.d0 & 255) | ((d.d1 & 255) << 8) | ((d.d2 & 255) << 16);
-          }
+          if (sft[j] != INT32_MIN) packed[j] = (int)digits24(v, sft[j]);
         }
       }
       const int row = (it & 1) * TILE + 4 * rg + i;
@@ -1099,7 +1093,7 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
   const bool fast = fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && C % AP_T == 0 && af.vec && vec &&
                     (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024;
   if (fast) {
-    hipLaunchKernelGGL((bn_apply_pack_fp4_k<false>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+    hipLaunchKernelGGL((bn_apply_pack_fp4_k<0>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                        dim3(256), 0, S(stream), XIn{x, nullptr}, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
                        reinterpret_cast<uint8_t*>(qt), ldqt, qt_fmt == 2 ? ldqt / 32 : (int64_t)0);
     return check_launch("bnn_bn_apply_pack");
@@ -1132,13 +1126,37 @@ BNN_API int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_
               (long long)C, (long long)ldq, (long long)ldqt);
     return kErrInval;
   }
-  hipLaunchKernelGGL((bn_apply_pack_fp4_k<true>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+  hipLaunchKernelGGL((bn_apply_pack_fp4_k<1>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                      dim3(256), 0, S(stream), XIn{x16, xbias}, M, C, af, q, ldq, qt, ldqt, qt_panel ? ldqt / 32 : (int64_t)0);
   return check_launch("bnn_bn_apply_pack_i16");
 }
 
+// bnn_bn_apply_pack for the s20 form of the BatchNorm input (XIn XF 2: x = fl(fl(S * xscale) +
+// xbias) from the u8-pixel layer's 20-bit sums, bnn_gemm_i8_affine_bnstats_s20): FP4 rows + FP4
+// transpose only, C % 256 == 0, any M.
+BNN_API int bnn_bn_apply_pack_s20(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale, int64_t M,
+                                  int64_t C, const float* mean, const float* invstd, const float* mean_lo,
+                                  const float* gamma, const float* beta, uint8_t* q, int64_t ldq, uint8_t* qt,
+                                  int64_t ldqt, int32_t qt_panel, void* stream) {
+  const ColAffine af{mean, mean_lo, invstd, gamma, beta,
+                     aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
+                         (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
+  if (!xlo || (reinterpret_cast<uintptr_t>(xlo) & 7) != 0 || !xhi || (reinterpret_cast<uintptr_t>(xhi) & 1) != 0 ||
+      (xbias && !aligned16(xbias)) || !mean || !invstd || !af.vec || M <= 0 || C <= 0 || C % AP_T != 0 || !q || !qt ||
+      ldq < C / 2 || !aligned16(q) || !qt_ok(reinterpret_cast<const int8_t*>(qt), M, ldqt, 1) ||
+      (M + AP_T - 1) / AP_T > 65535) {
+    set_error("bnn_bn_apply_pack_s20: bad arguments (M=%lld C=%lld ldq=%lld ldqt=%lld; C %% 256 == 0)", (long long)M,
+              (long long)C, (long long)ldq, (long long)ldqt);
+    return kErrInval;
+  }
+  hipLaunchKernelGGL((bn_apply_pack_fp4_k<2>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+                     dim3(256), 0, S(stream), XIn{xlo, xbias, xhi, xscale}, M, C, af, q, ldq, qt, ldqt,
+                     qt_panel ? ldqt / 32 : (int64_t)0);
+  return check_launch("bnn_bn_apply_pack_s20");
+}
+
 namespace bnn {
-int bn_bwd_sums(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+int bn_bwd_sums(XIn xin, int xf, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                 const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                 float* dgamma, float* dbeta, void* work, hipStream_t s, const float** k0_out, const float** k1_out,
                 float* pmx = nullptr, float* scale = nullptr, int64_t* dsum = nullptr);
@@ -1157,12 +1175,15 @@ BNN_API int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C) {
   return round_up(bn_workspace_bytes(M, C), 256) + i8c_pmx_bytes(M, C) + qc_strips(M) * C * (int64_t)sizeof(double);
 }
 
-static int bn_bwd_i8cols_impl(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
+static int bn_bwd_i8cols_impl(XIn xin, int xf, const float* dy, int64_t M, int64_t C, const float* gamma,
                               const float* beta, const float* save_mean, const float* save_invstd,
                               const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
                               int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
                               int64_t* dsum, void* work, void* stream, bool pre) {
-  if (!x || !dy || !digits_t || !scale || !work || M <= 0 || C <= 0 || C % 4 != 0 || !aligned16(x) ||
+  const bool x_ok = xf == 2 ? (xin.p && (reinterpret_cast<uintptr_t>(xin.p) & 7) == 0 && xin.hi &&
+                               (reinterpret_cast<uintptr_t>(xin.hi) & 1) == 0 && (!xin.bias || aligned16(xin.bias)))
+                            : (xf == 0 && xin.p && aligned16(xin.p));
+  if (!x_ok || !dy || !digits_t || !scale || !work || M <= 0 || C <= 0 || C % 4 != 0 ||
       !aligned16(dy) || ldqt % TILE != 0 || ldqt < round_up(M, TILE) || plane < C * ldqt || plane % 16 != 0 ||
       !aligned16(digits_t) || col_chunks(M, C) > 65535 || ldqt / TILE > 65535 || !aligned16(save_mean) ||
       !aligned16(save_invstd) || (save_mean_lo && !aligned16(save_mean_lo)) || (gamma && !aligned16(gamma)) ||
@@ -1181,13 +1202,18 @@ static int bn_bwd_i8cols_impl(const float* x, const float* dy, int64_t M, int64_
   if (pre) {
     bn_stat_slots(work, M, C, &k0, &k1);
   } else {
-    const int rc = bn_bwd_sums(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
+    const int rc = bn_bwd_sums(xin, xf, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
                                work, s, &k0, &k1, pmx, scale, dsum);
     if (rc) return rc;
   }
   const BnCols bc{save_mean, save_mean_lo, save_invstd, gamma, beta, k0, k1, 1.f / (float)M, hardtanh};
-  hipLaunchKernelGGL(bn_dz_quant_cols_t_k, dim3((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT)),
-                     dim3(256), 0, s, x, dy, M, C, bc, scale, digits_t, ldqt, plane, dsum, colsum ? part : nullptr);
+  const dim3 qg((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT));
+  if (xf == 2)
+    hipLaunchKernelGGL(bn_dz_quant_cols_t_k<2>, qg, dim3(256), 0, s, xin, dy, M, C, bc, scale, digits_t, ldqt, plane,
+                       dsum, colsum ? part : nullptr);
+  else
+    hipLaunchKernelGGL(bn_dz_quant_cols_t_k<0>, qg, dim3(256), 0, s, xin, dy, M, C, bc, scale, digits_t, ldqt, plane,
+                       dsum, colsum ? part : nullptr);
   if (colsum)
     hipLaunchKernelGGL(bn_dz_colsum_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, qc_strips(M), C, colsum);
   return check_launch("bnn_bn_bwd_i8cols");
@@ -1198,8 +1224,8 @@ BNN_API int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_
                               const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
                               int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
                               int64_t* dsum, void* work, void* stream) {
-  return bn_bwd_i8cols_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
-                            digits_t, ldqt, plane, scale, colsum, dsum, work, stream, false);
+  return bn_bwd_i8cols_impl(XIn{x, nullptr}, 0, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                            dgamma, dbeta, digits_t, ldqt, plane, scale, colsum, dsum, work, stream, false);
 }
 
 // bnn_bn_bwd_i8cols after bnn_bn_bwd_stats_pre (mode 2): the statistics, the digit scale and the
@@ -1209,6 +1235,29 @@ BNN_API int bnn_bn_bwd_i8cols_pre(const float* x, const float* dy, int64_t M, in
                                   const float* save_mean_lo, int32_t hardtanh, float* dgamma, float* dbeta,
                                   int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
                                   int64_t* dsum, void* work, void* stream) {
-  return bn_bwd_i8cols_impl(x, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh, dgamma, dbeta,
-                            digits_t, ldqt, plane, scale, colsum, dsum, work, stream, true);
+  return bn_bwd_i8cols_impl(XIn{x, nullptr}, 0, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
+                            dgamma, dbeta, digits_t, ldqt, plane, scale, colsum, dsum, work, stream, true);
+}
+
+// bnn_bn_bwd_i8cols[_pre] for the s20 form of the BatchNorm input (the u8-pixel layer's 20-bit sums
+// from bnn_gemm_i8_affine_bnstats_s20: x = fl(fl(S * scale) + xbias)); same outputs, bit for bit
+BNN_API int bnn_bn_bwd_i8cols_s20(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale,
+                                  const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                                  const float* save_mean, const float* save_invstd, const float* save_mean_lo,
+                                  int32_t hardtanh, float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt,
+                                  int64_t plane, float* scale, float* colsum, int64_t* dsum, void* work, void* stream) {
+  return bn_bwd_i8cols_impl(XIn{xlo, xbias, xhi, xscale}, 2, dy, M, C, gamma, beta, save_mean, save_invstd,
+                            save_mean_lo, hardtanh, dgamma, dbeta, digits_t, ldqt, plane, scale, colsum, dsum, work,
+                            stream, false);
+}
+
+BNN_API int bnn_bn_bwd_i8cols_s20_pre(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale,
+                                      const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                                      const float* save_mean, const float* save_invstd, const float* save_mean_lo,
+                                      int32_t hardtanh, float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt,
+                                      int64_t plane, float* scale, float* colsum, int64_t* dsum, void* work,
+                                      void* stream) {
+  return bn_bwd_i8cols_impl(XIn{xlo, xbias, xhi, xscale}, 2, dy, M, C, gamma, beta, save_mean, save_invstd,
+                            save_mean_lo, hardtanh, dgamma, dbeta, digits_t, ldqt, plane, scale, colsum, dsum, work,
+                            stream, true);
 }

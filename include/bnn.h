@@ -147,6 +147,20 @@ int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, in
  * the statistics pass. */
 int bnn_gemm_i8_bnstats_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 
+/* The s20 form of fc1's output (compact pre-activation; mnist-dist2.py:64-65 fc1 -> bn1): the
+ * statistics form above writing, instead of fp32 C, the exact integer S = sum + off_mul*col_off[n]
+ * (|S| < 2^19) as 20-bit two's complement -- Slo [M][ldc] int16 (its low 16 bits, 8-B aligned) and
+ * Shi [M][ldc/2] (its high nibbles, column 2j in the low nibble of byte j, 2-B aligned), 2.5 B per
+ * element.  The *_s20 BatchNorm entries read z = fl(fl(S * b_scale) + bias), bit-identical to the
+ * fp32 C of bnn_gemm_i8_affine_bnstats (b_scale a constant vector, its value passed to them as
+ * xscale; bias as xbias).  bnn_gemm_i8_s20_ok: 1 when off_mul (the pixel offset s0) is integral,
+ * N % 4 == 0 and k_true (128 + |s0|) < 2^19 (ToTensor without Normalize; any K <= 2048). */
+int bnn_gemm_i8_s20_ok(int64_t M, int64_t N, int64_t K, int64_t k_true, double s0);
+int bnn_gemm_i8_affine_bnstats_s20(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
+                                   const int64_t* col_off, double off_mul, int64_t k_true, int16_t* Slo,
+                                   uint8_t* Shi, int64_t ldc, int64_t M, int64_t N, int64_t K, double* stat,
+                                   int64_t stat_rows, const float* b_scale, const float* bias, bnn_stream_t stream);
+
 /* ---------------------------------------------------------------- u8 pixels (first layer)
  * Replaces the fp32 pixel tensor the reference's loader builds (ToTensor = u8/255, optionally
  * Normalize; mnist-dist2.py:96-99, mnist-distributed-BNNS2.py:82) as the operand of fc1
@@ -290,6 +304,10 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
  * integer sums); 2 = as 1 but backward data on the f32 MFMA; 0 = the VALU LDS-tiled / generic
  * kernels.  Process-global; for cross-checks and the kernel sweep. */
 int bnn_conv_set_mfma(int32_t mode);
+/* 1 (default, with bnn_conv_set_mfma != 0): the filter gradient of a one-input-channel layer
+ * (stride 1, 3x3 or 5x5, OW % 4 == 0, Co | 256, Co <= 64 -- the BinCNN's conv1) on a VALU kernel
+ * that reads dY once with coalesced 16-B loads; 0: the MFMA kernels as for any layer. */
+int bnn_conv_set_c1_filter(int32_t on);
 
 /* ---------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
  * The layers between the binarized GEMMs in the reference Net (mnist-dist2.py:52-74):
@@ -476,6 +494,29 @@ int bnn_bn_bwd_i8cols(const float* x, const float* dy, int64_t M, int64_t C, con
                       const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                       float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale,
                       float* colsum, int64_t* dsum, void* work, bnn_stream_t stream);
+
+/* The s20 form of the BatchNorm input (the u8-pixel layer's sums from bnn_gemm_i8_affine_bnstats_s20:
+ * xlo / xhi, xbias [C] (16-B aligned, nullable), xscale), read as x = fl(fl(S * xscale) + xbias) --
+ * bit-identical results to the fp32 entries on that x:
+ *   bnn_bn_apply_pack_s20       = bnn_bn_apply_pack_i16 (FP4 rows + transpose, C % 256 == 0)
+ *   bnn_bn_bwd_i8cols_s20[_pre] = bnn_bn_bwd_i8cols[_pre]
+ * replaces: the fp32 z1 = F.linear(x, W_b) + bias of the first BinarizeLinear (binarized_modules.py:
+ * 80-83, input kept at size(1) == 784) the reference materialises for bn1 (mnist-dist2.py:64-65). */
+int bnn_bn_apply_pack_s20(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale, int64_t M,
+                          int64_t C, const float* mean, const float* invstd, const float* mean_lo, const float* gamma,
+                          const float* beta, uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, int32_t qt_panel,
+                          bnn_stream_t stream);
+int bnn_bn_bwd_i8cols_s20(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale, const float* dy,
+                          int64_t M, int64_t C, const float* gamma, const float* beta, const float* save_mean,
+                          const float* save_invstd, const float* save_mean_lo, int32_t hardtanh, float* dgamma,
+                          float* dbeta, int8_t* digits_t, int64_t ldqt, int64_t plane, float* scale, float* colsum,
+                          int64_t* dsum, void* work, bnn_stream_t stream);
+int bnn_bn_bwd_i8cols_s20_pre(const int16_t* xlo, const uint8_t* xhi, const float* xbias, float xscale,
+                              const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                              const float* save_mean, const float* save_invstd, const float* save_mean_lo,
+                              int32_t hardtanh, float* dgamma, float* dbeta, int8_t* digits_t, int64_t ldqt,
+                              int64_t plane, float* scale, float* colsum, int64_t* dsum, void* work,
+                              bnn_stream_t stream);
 
 /* The BatchNorm(+Hardtanh) backward statistics from the FP6 dX GEMM's epilogue instead of their own
  * pass over (x, dy): bnn_gemm_fp6_bnstats (below) writes per-128-row-tile-row partials of sum g,

@@ -90,7 +90,8 @@ def test_net_r3_one_step_vs_oracle(batch, path):
     model = model.cuda().train()
     named = dict(model.named_parameters())
     z1 = {}
-    model.fc1.register_forward_hook(lambda mod, inp, out: z1.__setitem__("z", host(out).astype(np.float32)))
+    model.fc1.register_forward_hook(
+        lambda mod, inp, out: z1.__setitem__("z", host(BF.dense_preact(out)).astype(np.float32)))
     if fused:
         opt = LatentAdam(model.parameters(), lr=LR, clamp_params=nets.binary_params(model))
         x = torch.as_tensor(u8).cuda()

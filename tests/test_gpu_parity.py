@@ -334,6 +334,42 @@ def test_conv_backward_full_batch_vs_float64(F, shape):
         assert err < GRAD_TOL, err
 
 
+@pytest.mark.parametrize("shape", [
+    (5, 1, 28, 28, 16, 5, 2),      # BinCNN conv1, a ragged last workgroup
+    (7, 1, 12, 16, 8, 3, 1),
+    (3, 1, 20, 8, 32, 5, 0),
+    (9, 1, 28, 28, 64, 3, 1),
+    (6, 1, 10, 12, 4, 5, 4),       # pad = K - 1
+])
+def test_conv1_filter_valu_vs_float64(F, shape):
+    """The one-input-channel filter gradient (conv_bwd_filter_c1_k, bnn_conv_set_c1_filter) against
+    float64 torch on the binarised operands and against the MFMA kernel on the same inputs."""
+    from bnn_amd import _lib as L
+    N, C, H, W, Co, K, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + Co)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g)
+    x = torch.where(torch.rand(N, C, H, W, device="cuda", generator=g) < 0.3, torch.zeros_like(x), x)
+    w = torch.rand(Co, C, K, K, device="cuda", generator=g) * 2 - 1
+    b = torch.randn(Co, device="cuda", generator=g)
+    OH, OW = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    dy = torch.randn(N, Co, OH, OW, device="cuda", generator=g)
+    xs, d64 = torch.sign(x).double(), dy.double()
+    dw64 = torch.nn.grad.conv2d_weight(xs, tuple(w.shape), d64, padding=pad)
+    db64 = d64.sum((0, 2, 3))
+    got = []
+    try:
+        for on in (1, 0):
+            L.call("bnn_conv_set_c1_filter", on)
+            wt, bt = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+            F.binary_conv2d(x, wt, bt, True, 1, pad, 1, 1).backward(dy)
+            got.append((wt.grad.double(), bt.grad.double()))
+    finally:
+        L.call("bnn_conv_set_c1_filter", 1)
+    for gw, gb in got:
+        assert float((gw - dw64).norm() / dw64.norm()) < GRAD_TOL
+        assert float((gb - db64).norm() / db64.norm()) < GRAD_TOL
+
+
 def test_hardtanh_backward(F):
     x = torch.tensor([-2.0, -1.0, -0.5, 0.0, 0.5, 1.0, 3.0] * 11, device="cuda")
     g = torch.randn_like(x)

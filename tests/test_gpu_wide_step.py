@@ -70,7 +70,7 @@ def _bench_setup():
 
 def _counters(BF):
     return {k: getattr(BF, k) for k in ("PIX_STATS_USES", "FP4_STATS_USES", "Z16_HANDOFFS", "Q6_HANDOFFS",
-                                         "I8C_HANDOFFS", "HEAD_CALLS")}
+                                         "I8C_HANDOFFS", "HEAD_CALLS", "S20_HANDOFFS")}
 
 
 class _MaskDrop(torch.nn.Module):
@@ -122,7 +122,7 @@ def test_wide_step_config5_vs_float64(monkeypatch):
     draw = BF.dropout_seed
     monkeypatch.setattr(BF, "dropout_seed", lambda: seeds.append(draw()) or seeds[-1])
     z1 = {}
-    hook = model.fc1.register_forward_hook(lambda mod, inp, out: z1.__setitem__("z", out.detach()))
+    hook = model.fc1.register_forward_hook(lambda mod, inp, out: z1.__setitem__("z", BF.dense_preact(out).detach()))
     c0 = _counters(BF)
     for p in model.parameters():
         p.grad = None
@@ -133,7 +133,8 @@ def test_wide_step_config5_vs_float64(monkeypatch):
     c1 = _counters(BF)
     fired = {k: c1[k] - c0[k] for k in c0}
     assert fired == {"PIX_STATS_USES": int(BF.PIX_STATS), "FP4_STATS_USES": int(BF.FP4_STATS), "Z16_HANDOFFS": 2,
-                     "Q6_HANDOFFS": 2, "I8C_HANDOFFS": 1, "HEAD_CALLS": 1}, fired
+                     "Q6_HANDOFFS": 2, "I8C_HANDOFFS": 1, "HEAD_CALLS": 1,
+                     "S20_HANDOFFS": int(BF.S20 and BF.PIX_STATS)}, fired
     assert len(seeds) == 1, seeds
     grads = {k: p.grad.detach().clone() for k, p in named.items()}
     out = out.detach()
