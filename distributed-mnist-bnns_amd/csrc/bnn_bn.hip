@@ -69,6 +69,18 @@ __device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4])
 }
 
 
+// Waves per SIMD the reduction passes are compiled for (they wait on memory: occupancy is their
+// lever; RED_OCC / HRED_OCC = 1 leaves the compiler's choice)
+#ifndef RED_OCC
+#define RED_OCC 1
+#endif
+#ifndef HRED_OCC
+#define HRED_OCC 1
+#endif
+#ifndef RED_RB
+#define RED_RB 8   // rows per load batch of bn_reduce_k (divides 16)
+#endif
+
 // MODE 0: per-chunk (mean, M2), accumulated as deviations from the chunk's first row so the
 //         float partials see deviations rather than raw magnitudes; merged with Chan's formula.
 // MODE 1: per-chunk (sum g, sum g*xhat) with g = dy*mask(y).
@@ -77,7 +89,7 @@ __device__ __forceinline__ void drop4(const Drop& d, uint64_t i0, float (&v)[4])
 //         bnn_bn_bwd_i8cols scales its int8 column digits by (no column-max pass over dz).
 // One thread = 4 adjacent columns (float4), rows walked in 16-row float partials folded to double.
 template <int MODE, int XF = 0>
-__global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, RED_OCC) void bn_reduce_k(XIn xin, const float* __restrict__ dy,
                                                    int64_t M, int64_t C, const float* __restrict__ mean,
                                                    const float* __restrict__ mean_lo,
                                                    const float* __restrict__ invstd,
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_reduce_k(XIn xin, const float* __restr
   }
   // rows in batches of RB whose loads are all issued before any is used (several KiB in flight
   // per wave: the pass is latency-bound otherwise); the arithmetic order is unchanged
-  constexpr int RB = 8;
+  constexpr int RB = RED_RB;
   for (int64_t r = r0; r < r1; r += 16) {
     float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
     const int64_t re = (r + 16 < r1) ? r + 16 : r1;
@@ -865,7 +877,7 @@ __global__ __launch_bounds__(256, Z16 ? 4 : 2) void bn_head_fwd_k(XIn xin, int64
 // Statistics pass of the head's BatchNorm backward (bn_reduce_k MODE 1 with g = dY4 . W4 formed per
 // element) plus the head's weight gradient partials dW4[q][c] over the chunk's rows (fp32 per chunk).
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256) void bn_head_reduce_k(XIn xin, const float* __restrict__ d4,
+__global__ __launch_bounds__(256, HRED_OCC) void bn_head_reduce_k(XIn xin, const float* __restrict__ d4,
                                                         const float* __restrict__ w4, int64_t M, int64_t C,
                                                         const float* __restrict__ mean, const float* __restrict__ mean_lo,
                                                         const float* __restrict__ invstd,

@@ -589,7 +589,7 @@ __global__ __launch_bounds__(256) void conv_filter_tile_reduce2_k(const double* 
 // keeping its channel's KH*KW sums and the bias sum in fp32 registers over the workgroup's samples;
 // the TPC threads of a channel are folded in a fixed order into the workgroup's partial row
 // (conv_filter_tile_reduce{1,2}_k, double).  Deterministic.
-constexpr int C1F_T = 256, C1F_SPB = 4, C1F_PX = 4;
+constexpr int C1F_T = 256, C1F_SPB = 4, C1F_PX = 4, C1F_UB = 8;
 
 struct C1Filt {
   int H, W, OH, OW, Co, pad, XR, XW, TPC;   // XR x XW: the haloed input plane in LDS
@@ -639,26 +639,38 @@ __global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1_k(const float* __res
     if (co < g.Co) {
       const float* xb = c1s + b * plane;
       const float* dn = dy + (n * g.Co + co) * (int64_t)ohw;
-      for (int u = r; u < nu; u += g.TPC) {
-        const float4 d = *reinterpret_cast<const float4*>(dn + 4 * u);
-        const int oh = u / uq, ow0 = 4 * (u - oh * uq);
-        bacc += (d.x + d.y) + (d.z + d.w);
+      // C1F_UB units' dY loads issued together (one HBM latency per batch, not per unit)
+      for (int u0 = r; u0 < nu; u0 += C1F_UB * g.TPC) {
+        float4 dv[C1F_UB];
 #pragma unroll
-        for (int kh = 0; kh < KH; ++kh) {
-          float xr[4 * NX];
+        for (int i = 0; i < C1F_UB; ++i) {
+          const int u = min(u0 + i * g.TPC, nu - 1);   // clamped, unconditional: the loads batch
+          dv[i] = *reinterpret_cast<const float4*>(dn + 4 * u);
+        }
 #pragma unroll
-          for (int j = 0; j < NX; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(xb + (oh + kh) * g.XW + ow0 + 4 * j);
-            xr[4 * j] = v.x, xr[4 * j + 1] = v.y, xr[4 * j + 2] = v.z, xr[4 * j + 3] = v.w;
-          }
+        for (int i = 0; i < C1F_UB; ++i) {
+          const int u = u0 + i * g.TPC;
+          if (u >= nu) break;
+          const float4 d = dv[i];
+          const int oh = u / uq, ow0 = 4 * (u - oh * uq);
+          bacc += (d.x + d.y) + (d.z + d.w);
 #pragma unroll
-          for (int kw = 0; kw < KW; ++kw) {
-            float a = acc[kh * KW + kw];
-            a = fmaf(d.x, xr[kw], a);
-            a = fmaf(d.y, xr[kw + 1], a);
-            a = fmaf(d.z, xr[kw + 2], a);
-            a = fmaf(d.w, xr[kw + 3], a);
-            acc[kh * KW + kw] = a;
+          for (int kh = 0; kh < KH; ++kh) {
+            float xr[4 * NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+              const float4 v = *reinterpret_cast<const float4*>(xb + (oh + kh) * g.XW + ow0 + 4 * j);
+              xr[4 * j] = v.x, xr[4 * j + 1] = v.y, xr[4 * j + 2] = v.z, xr[4 * j + 3] = v.w;
+            }
+#pragma unroll
+            for (int kw = 0; kw < KW; ++kw) {
+              float a = acc[kh * KW + kw];
+              a = fmaf(d.x, xr[kw], a);
+              a = fmaf(d.y, xr[kw + 1], a);
+              a = fmaf(d.z, xr[kw + 2], a);
+              a = fmaf(d.w, xr[kw + 3], a);
+              acc[kh * KW + kw] = a;
+            }
           }
         }
       }

@@ -720,11 +720,14 @@ __global__ __launch_bounds__(256) void bn_dz_colsum_k(const double* __restrict__
 // part != null the strip's column sums of dz (double; rows in a fixed order) go to
 // part[blockIdx.y][N].
 constexpr int QC_RT = 8;
+#ifndef DZQ_OCC
+#define DZQ_OCC 3   // waves per SIMD (<= 168 VGPRs): the pass waits on memory, so occupancy is its lever
+#endif
 
 __host__ __device__ inline int64_t qc_strips(int64_t M) { return (M + TILE * QC_RT - 1) / (TILE * QC_RT); }
 
 template <int XF>
-__global__ __launch_bounds__(256) void bn_dz_quant_cols_t_k(XIn xin, const float* __restrict__ dy,
+__global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, const float* __restrict__ dy,
                                                             int64_t M, int64_t N, BnCols bc,
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
                                                             int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum,
