@@ -66,6 +66,7 @@ SIGNATURES = {
                                     I32, P]),
     "bnn_conv_set_mfma": (I32, [I32]),
     "bnn_conv_set_c1_filter": (I32, [I32]),
+    "bnn_conv_bf3_plan": (I32, [I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_bn_workspace": (I64, [I64, I64]),
     "bnn_bn_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, P, P]),
     "bnn_bn_fwd_final_parts": (I32, [P, I64, I64, I64, I64, P, P, F32, F32, P, P, P, P]),

@@ -12,6 +12,9 @@
 
 #include "bnn_common.h"
 
+#include <cstring>
+#include <vector>
+
 namespace bnn {
 namespace {
 
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1_k(const float* __res
   constexpr int KK = KH * KW;
   extern __shared__ __attribute__((aligned(16))) float c1s[];
   const int plane = g.XR * g.XW;
-  float* red = c1s + 2 * plane;      // [C1F_T][KK + 1] fold buffer
+  float* red = c1s;                  // [C1F_T][KK + 1] fold buffer, aliasing the planes at the end
   const int t = threadIdx.x;
   const int co = t / g.TPC, r = t - co * g.TPC;
   const int hw = g.H * g.W, ohw = g.OH * g.OW, nu = ohw / 4, uq = g.OW / 4;
@@ -678,6 +681,7 @@ __global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1_k(const float* __res
     if (n + 1 < n1) put(b ^ 1);
   }
   // fixed-order fold of a channel's TPC threads
+  __syncthreads();                   // every plane read is done before red overwrites them
 #pragma unroll
   for (int k = 0; k < KK; ++k) red[t * (KK + 1) + k] = acc[k];
   red[t * (KK + 1) + KK] = bacc;
@@ -833,9 +837,11 @@ inline int b3_ipb(int64_t N) { return N >= 16 * 256 ? 16 : MF_IPB; }
 
 struct B3Data {
   int C, H, W, Co, Cop, KH, KW, OH, OW, pad, OHp, OWp, taps, Kp, ntile_pix;
-  int ps;    // halo pixel stride in bf16 elements: Cop + 8 (16-B aligned; 16 consecutive pixels'
-             // 16-B chunks land on 16 distinct 4-bank groups -- conflict-free ds_*_b128)
-  int ws;    // weight row stride: Kp + 8 (same reason for the A reads)
+  int ps;    // halo pixel stride in bf16 elements, = 16 (mod 32): a 16-lane ds_read_b128 group holds
+             // pixels p = 0..15 with chunk c or c + 1 ({0-3, 12-15} vs {4-11}), and 16-B quad
+             // 6p + [4 <= p <= 11] (mod 16) is one-to-one -- conflict-free when a tile is one image row
+  int ws;    // weight row stride: Kp + 16 (the same rule for the A reads)
+  int rowt;  // 1: pixel tiles are image rows (W <= 16, lanes >= W idle); 0: 16 consecutive pixels
 };
 
 __device__ __forceinline__ void bf16x3_split(float y, unsigned short& d1, unsigned short& d2, unsigned short& d3) {
@@ -883,12 +889,26 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
   for (int i = t; i < 3 * plane; i += B3_T) img[i] = 0;   // zero halo (interior rewritten per sample)
   const int hT = g.KH - 1 - g.pad, wT = g.KW - 1 - g.pad;
   const int HW = g.H * g.W, ohw = g.OH * g.OW;
+  // pixel of lane l in tile tt: image row tt, column l & 15 (rowt), or the 16 consecutive pixels
+  // 16 tt + (l & 15); -1 = a padded column (computed at a clamped address, never stored)
+  auto tile_pix = [&](int tt, int col) -> int {
+    if (g.rowt) return (col < g.W && tt < g.H) ? tt * g.W + col : -1;
+    const int p = tt * 16 + col;
+    return p < HW ? p : -1;
+  };
   int hb[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    int pix = (wv + B3_W * m) * 16 + (lane & 15);
-    if (pix >= HW) pix = 0;   // padded column: computed, never stored
-    const int ih = pix / g.W, iw = pix - ih * g.W;
+    const int tt = wv + B3_W * m, col = lane & 15;
+    int ih, iw;
+    if (g.rowt) {
+      ih = min(tt, g.H - 1);
+      iw = min(col, g.W - 1);
+    } else {
+      const int pix = max(tile_pix(tt, col), 0);
+      ih = pix / g.W;
+      iw = pix - ih * g.W;
+    }
     hb[m] = ih * g.OWp + iw;
   }
   const int my_tiles = (g.ntile_pix - wv + B3_W - 1) / B3_W;
@@ -974,8 +994,8 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       if (m >= my_tiles) continue;
-      const int pix = (wv + B3_W * m) * 16 + (lane & 15);
-      if (pix >= HW) continue;
+      const int pix = tile_pix(wv + B3_W * m, lane & 15);
+      if (pix < 0) continue;
 #pragma unroll
       for (int a = 0; a < NT; ++a)
 #pragma unroll
@@ -1005,6 +1025,7 @@ constexpr int B3_UD = 4, B3_PX = 8;
 
 struct B3Filt {
   int C, H, W, Co, KH, KW, OH, OW, pad, Hp, OWq, Kp, Kd, xrow, Co16, NA, ncombo, ntn, WT, KS, Wh;
+  int CS, XL;   // shifted copies: channel stride and copy stride (bf16), padded for conflict-free B reads
 };
 
 template <int NA, int MT>
@@ -1016,7 +1037,7 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
   unsigned short* dyp = reinterpret_cast<unsigned short*>(ldsf);       // 3 x [Co16][Kd]
   const int PL = g.Co16 * g.Kd;
   unsigned short* xs = dyp + 3 * PL;                                    // KW x [C][Hp][xrow]
-  const int XL = g.C * g.Hp * g.xrow;
+  const int XL = g.XL;
   unsigned short* xh = xs + g.KW * XL;                                  // [C][Hp][Wh], zero halo
   const int XH = g.C * g.Hp * g.Wh;
   float* bpart = reinterpret_cast<float*>(xh + ((XH + 7) & ~7));      // [Co16][Kp / 8]
@@ -1041,7 +1062,7 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
     int combo = nt * 16 + (lane & 15);
     if (combo >= g.ncombo) combo = 0;   // padded column: computed, never stored
     const int ci = fdivi(combo, inv_kk), kk = combo - ci * KK, kh = fdivi(kk, inv_kw), kw = kk - kh * g.KW;
-    boff[m] = ((kw * g.C + ci) * g.Hp + kh) * g.xrow;
+    boff[m] = kw * g.XL + ci * g.CS + kh * g.xrow;
   }
   const int my_tiles = (g.ntn - grp + g.WT - 1) / g.WT;
   mf4 acc[NA][MT];
@@ -1130,7 +1151,7 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_filter_bf3_k(const float* __res
       bf8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (short)src[j];
-      *reinterpret_cast<bf8*>(xs + kw * XL + (c * g.Hp + ihh) * g.xrow + 8 * q) = v;
+      *reinterpret_cast<bf8*>(xs + kw * XL + c * g.CS + ihh * g.xrow + 8 * q) = v;
     }
     lds_barrier();
     for (int k0 = k_lo; k0 < k_hi; k0 += 32) {
@@ -1478,14 +1499,88 @@ inline bool b3_data_geom(const ConvShape& s, B3Data* g, int64_t* lds) {
   d.OWp = d.OW + 2 * (d.KW - 1 - d.pad);
   d.taps = d.KH * d.KW;
   d.Kp = (int)round_up((int64_t)d.taps * d.Cop, 32);
-  d.ntile_pix = (d.H * d.W + 15) / 16;
-  d.ps = d.Cop + 8;
-  d.ws = d.Kp + 8;
+  d.rowt = d.W <= 16 ? 1 : 0;
+  d.ntile_pix = d.rowt ? d.H : (d.H * d.W + 15) / 16;
+  d.ps = (int)round_up(d.Cop, 32) + 16;
+  d.ws = d.Kp + 16;
   if ((d.ntile_pix + B3_W - 1) / B3_W > 16 || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
   const int nt = d.C <= 16 ? 1 : 2;
   *lds = (int64_t)16 * nt * d.ws * 2 + (int64_t)3 * d.OHp * d.OWp * d.ps * 2;
   *g = d;
   return *lds <= kMaxTileLds;
+}
+
+// LDS cycles of one wave's ds_read_b128 on gfx950 (MI355X_MICROARCH.md §LDS): four 16-lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32, bank (a/4) mod 64; a group costs the
+// largest number of distinct dword addresses on one bank.
+static int lds_b128_cycles(const int (&addr)[64]) {
+  static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  int tot = 0;
+  for (int gi = 0; gi < 4; ++gi) {
+    int dw[64];
+    for (int i = 0; i < 16; ++i)
+      for (int w = 0; w < 4; ++w) dw[4 * i + w] = addr[grp[gi][i]] / 4 + w;
+    std::sort(dw, dw + 64);
+    const int n = (int)(std::unique(dw, dw + 64) - dw);
+    int cnt[64] = {0}, worst = 1;
+    for (int i = 0; i < n; ++i) worst = std::max(worst, ++cnt[((dw[i] % 64) + 64) % 64]);
+    tot += worst;
+  }
+  return tot;
+}
+
+// The filter kernel's B reads (one 16-combo tile per lane group row, 4 k-chunks) under a copy
+// layout: total LDS cycles over the first k-steps and every combo tile.
+static int b3_filt_b_cycles(const B3Filt& d, int CS, int XL) {
+  int tot = 0;
+  const int ksteps = std::min(d.Kp / 32, 4);
+  for (int ks = 0; ks < ksteps; ++ks)
+    for (int nt = 0; nt < d.ntn; ++nt) {
+      int addr[64];
+      for (int l = 0; l < 64; ++l) {
+        int combo = nt * 16 + (l & 15);
+        if (combo >= d.ncombo) combo = 0;
+        const int ci = combo / (d.KH * d.KW), kk = combo - ci * d.KH * d.KW, kh = kk / d.KW, kw = kk - kh * d.KW;
+        const int kq = 32 * ks + 8 * (l >> 4), ohq = kq / d.OWq, ow0 = kq - ohq * d.OWq;
+        addr[l] = 2 * (kw * XL + ci * CS + kh * d.xrow + std::min(ohq, d.OH - 1) * d.xrow + ow0);
+      }
+      tot += lds_b128_cycles(addr);
+    }
+  return tot;
+}
+
+// Pads of the shifted copies' channel stride (CS = Hp * xrow + cpad) and copy stride
+// (XL = C * CS + xpad), both multiples of 8 bf16 (16-B aligned pieces), chosen by the bank model
+// above: the plain layout put all KW copies of a combo row on the same banks (5-way conflicts on
+// the BinCNN's conv2).  Memoised per shape.
+static void b3_filt_copy_layout(B3Filt* d) {
+  struct Key { int C, Hp, xrow, KH, KW, OH, OWq, Kp; };
+  static std::vector<std::pair<Key, std::pair<int, int>>> memo;
+  const Key key{d->C, d->Hp, d->xrow, d->KH, d->KW, d->OH, d->OWq, d->Kp};
+  for (const auto& e : memo)
+    if (std::memcmp(&e.first, &key, sizeof(Key)) == 0) {
+      d->CS = e.second.first;
+      d->XL = e.second.second;
+      return;
+    }
+  const int ideal = 4 * std::min(d->Kp / 32, 4) * d->ntn;   // every read conflict-free
+  int best = -1, bcs = d->Hp * d->xrow, bxl = d->C * d->Hp * d->xrow;
+  for (int cpad = 0; cpad < 64 && best != ideal; cpad += 8)
+    for (int xpad = 0; xpad < 256 && best != ideal; xpad += 8) {
+      const int CS = d->Hp * d->xrow + cpad, XL = d->C * CS + xpad;
+      const int c = b3_filt_b_cycles(*d, CS, XL);
+      if (best < 0 || c < best) {
+        best = c;
+        bcs = CS;
+        bxl = XL;
+      }
+    }
+  d->CS = bcs;
+  d->XL = bxl;
+  memo.push_back({key, {bcs, bxl}});
 }
 
 // bf16x3 filter kernel: the input must be exact in bf16 -- binarised (the BinCNN's layers both are)
@@ -1505,13 +1600,14 @@ inline bool b3_filt_geom(const ConvShape& s, int binarize, B3Filt* g, int64_t* l
   d.WT = d.ntn >= 8 ? 8 : (d.ntn >= 4 ? 4 : (d.ntn >= 2 ? 2 : 1));
   d.KS = B3_W / d.WT;
   d.Kp = (int)round_up((int64_t)d.OH * d.OWq, 32 * d.KS);
-  d.Kd = d.Kp + 8;
+  d.Kd = d.Kp + 16;   // = 16 (mod 32): conflict-free A reads (as B3Data::ws)
   d.xrow = d.OWq;
   d.Wh = (int)round_up((int64_t)d.OWq + d.KW - 1, 8);   // xh columns read: 8q + kw + j < OWq + KW - 1
   if ((d.ntn + d.WT - 1) / d.WT > 8) return false;
   if ((int64_t)d.C * d.H * d.W >= (1 << 20) || (int64_t)d.Co * d.OH * d.OW >= (1 << 20)) return false;
+  b3_filt_copy_layout(&d);
   // rows read: oh + kh < OH + KH - 1 <= Hp (stride 1, pad <= K-1)
-  *lds = (int64_t)3 * d.Co16 * d.Kd * 2 + (int64_t)d.KW * d.C * d.Hp * d.xrow * 2 +
+  *lds = (int64_t)3 * d.Co16 * d.Kd * 2 + (int64_t)d.KW * d.XL * 2 +
          round_up((int64_t)d.C * d.Hp * d.Wh, 8) * 2 + (int64_t)d.Co16 * (d.Kp / 8) * 4;
   *g = d;
   return *lds <= kMaxTileLds;
@@ -1575,9 +1671,15 @@ inline bool c1_filt_geom(const ConvShape& s, C1Filt* g, int64_t* lds) {
       s.OW % 4 != 0 || s.Co > 64 || C1F_T % s.Co != 0 || s.pad > s.KH - 1 || s.H * s.W > C1F_PX * C1F_T)
     return false;
   const int NX = ((int)s.KW + 6) / 4;
-  const int XW = (int)round_up(std::max<int64_t>(s.W + 2 * s.pad, s.OW - 4 + 4 * NX), 4);
+  // row pitch: XW / 4 = OW / 4 (mod 16), so the 16 consecutive units a ds_read_b128 lane group reads
+  // (~2.3 rows of OW / 4 units) land on 16 distinct 4-bank quads -- conflict-free (a 32-float pitch
+  // put rows 0 and 2 on the same banks)
+  const int base4 = (int)(round_up(std::max<int64_t>(s.W + 2 * s.pad, s.OW - 4 + 4 * NX), 4) / 4);
+  const int uq = (int)(s.OW / 4) % 16;
+  const int XW = 4 * (uq + 16 * ((base4 - uq + 15) / 16));
   const int XR = (int)std::max<int64_t>(s.H + 2 * s.pad, s.OH + s.KH - 1);
-  const int64_t bytes = (2 * (int64_t)XR * XW + (int64_t)C1F_T * (s.KH * s.KW + 1)) * (int64_t)sizeof(float);
+  const int64_t bytes = std::max<int64_t>(2 * (int64_t)XR * XW, (int64_t)C1F_T * (s.KH * s.KW + 1)) *
+                        (int64_t)sizeof(float);
   if (bytes > kMaxTileLds) return false;
   *g = C1Filt{(int)s.H, (int)s.W, (int)s.OH, (int)s.OW, (int)s.Co, s.pad, XR, XW, (int)(C1F_T / s.Co)};
   *lds = bytes;
@@ -1802,6 +1904,37 @@ BNN_API int bnn_conv2d_bwd_data(const float* dy, const float* w_latent, float* d
   }
   hipLaunchKernelGGL(conv_bwd_data_k, dim3(grid_for(total)), dim3(256), 0, st, dy, w_latent, dx, s);
   return check_launch("bnn_conv2d_bwd_data");
+}
+
+// Host-only plan query (no GPU): the bf16x3 backward kernels' LDS layouts for a shape --
+// out[0..3] = data kernel (ps, ws, rowt, lds bytes) or -1s, out[4..8] = filter kernel (Kd, CS, XL,
+// lds bytes, modelled LDS cycles of its B reads per ds_read_b128 x 100; 400 = conflict-free) or -1s.
+BNN_API int bnn_conv_bf3_plan(int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                              int32_t stride, int32_t pad, int32_t dil, int32_t groups, int64_t* out) {
+  ConvShape s;
+  if (!out || !make_shape(std::max<int64_t>(N, 1), C, H, W, Co, KH, KW, stride, pad, dil, groups, &s)) {
+    set_error("bnn_conv_bf3_plan: bad arguments");
+    return kErrInval;
+  }
+  for (int i = 0; i < 9; ++i) out[i] = -1;
+  B3Data bd;
+  int64_t lds = 0;
+  if (b3_data_geom(s, &bd, &lds)) {
+    out[0] = bd.ps;
+    out[1] = bd.ws;
+    out[2] = bd.rowt;
+    out[3] = lds;
+  }
+  B3Filt bf;
+  if (b3_filt_geom(s, 1, &bf, &lds)) {
+    out[4] = bf.Kd;
+    out[5] = bf.CS;
+    out[6] = bf.XL;
+    out[7] = lds;
+    const int reads = std::min(bf.Kp / 32, 4) * bf.ntn;
+    out[8] = 100 * (int64_t)b3_filt_b_cycles(bf, bf.CS, bf.XL) / reads;
+  }
+  return 0;
 }
 
 BNN_API int64_t bnn_conv2d_bwd_filter_workspace(int64_t N, int64_t C, int64_t Co, int64_t KH,

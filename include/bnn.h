@@ -308,6 +308,12 @@ int bnn_conv_set_mfma(int32_t mode);
  * (stride 1, 3x3 or 5x5, OW % 4 == 0, Co | 256, Co <= 64 -- the BinCNN's conv1) on a VALU kernel
  * that reads dY once with coalesced 16-B loads; 0: the MFMA kernels as for any layer. */
 int bnn_conv_set_c1_filter(int32_t on);
+/* Host-only plan query (needs no GPU): the bf16x3 backward kernels' LDS layouts for a shape.
+ * out[9]: data kernel (pixel pitch ps, weight pitch ws, row tiles, LDS bytes), then filter kernel
+ * (dY pitch Kd, copy channel stride CS, copy stride XL, LDS bytes, modelled cycles x 100 of its B
+ * fragment ds_read_b128, 400 = conflict-free); -1 where the kernel does not take the shape. */
+int bnn_conv_bf3_plan(int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                      int32_t stride, int32_t pad, int32_t dil, int32_t groups, int64_t* out);
 
 /* ---------------------------------------------------------------- BatchNorm1d (+ Hardtanh)
  * The layers between the binarized GEMMs in the reference Net (mnist-dist2.py:52-74):

@@ -66,3 +66,19 @@ def test_ops_refuse_cpu_tensors():
         F.sign(torch.zeros(4))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         F.binary_linear(torch.zeros(2, 8), torch.zeros(3, 8))
+
+
+def test_conv_bf3_plans_are_bank_conflict_free(L):
+    """The bf16x3 conv backward kernels' LDS layouts for the BinCNN's conv2 (host-only plan query):
+    the data kernel's pixel / weight pitches are 16 (mod 32) bf16 with one image row per pixel
+    tile, the filter kernel's dY pitch likewise, and its shifted input copies are padded so the
+    modelled B-fragment ds_read_b128 is conflict-free (4 LDS cycles; the plain layout put all five
+    kw copies of a combo row on the same banks)."""
+    out = (ctypes.c_int64 * 9)()
+    assert L.bnn_conv_bf3_plan(4096, 16, 14, 14, 32, 5, 5, 1, 2, 1, 1, out) == 0
+    ps, ws, rowt, lds_d, kd, cs, xl, lds_f, cyc = list(out)
+    assert ps % 32 == 16 and ws % 32 == 16 and rowt == 1 and lds_d <= 160 * 1024
+    assert kd % 32 == 16 and cs % 8 == 0 and xl % 8 == 0 and lds_f <= 160 * 1024
+    assert cyc == 400
+    # shapes neither kernel takes report -1
+    assert L.bnn_conv_bf3_plan(4, 8, 9, 9, 8, 3, 3, 2, 1, 1, 1, out) == 0 and out[0] == -1 and out[4] == -1
