@@ -1027,6 +1027,27 @@ def _pair_same(v, what):
     return int(v)
 
 
+# conv1 -> BatchNorm2d backward hand-off (c1bn): when the BinCNN's first conv (one input channel,
+# its input needing no gradient) emits its compact output into the fused BatchNorm2d + Hardtanh +
+# MaxPool2d op, that op's backward computes only its statistics (bnn_bn2d_bwd_stats_q) and hands the
+# conv the pooled gradient and those statistics; the conv's weight gradient then forms dY itself
+# (bnn_conv2d_bwd_filter_bn) -- the fp32 dY of the layer is never written.
+C1BN = os.environ.get("BNN_C1BN", "1") != "0"
+_C1BN_WANT = "_bnn_c1bn_consumer"
+_C1BN_ATTR = "_bnn_c1bn"
+C1BN_HANDOFFS = 0
+
+
+def _c1bn_take(dy):
+    ent = getattr(dy, _C1BN_ATTR, None)
+    if ent is None:
+        return None
+    delattr(dy, _C1BN_ATTR)
+    if ent[0] != _q6_key(dy):
+        raise RuntimeError("stale conv1 / BatchNorm2d hand-off")
+    return ent[1:]
+
+
 # BNN_CONV_C1F=1 / 0: the one-input-channel VALU filter-gradient kernel on / off (A/B timing);
 # unset: the library's default
 _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
@@ -1090,6 +1111,10 @@ class BinaryConv2dFunction(torch.autograd.Function):
             ph = torch.zeros((1,), dtype=torch.float32, device=x.device).as_strided((N, Co, OH, OW), (0, 0, 0, 0))
             # the bias as it is now: the optimizer updates the Parameter in place after backward
             setattr(ph, _ZQ_ATTR, (yq, b.clone() if b is not None else None, zf))
+            if (C1BN and C == 1 and binarize_input and not ctx.needs_input_grad[0]
+                    and L.lib().bnn_conv2d_bwd_filter_bn_ok(N, C, H, W, Co, KH, KW, stride, padding, dilation,
+                                                            groups)):
+                setattr(ph, _C1BN_WANT, True)
             return ph
         y = torch.empty((N, Co, OH, OW), dtype=torch.float32, device=x.device)
         if ctx.empty:             # empty batch: F.conv2d returns [0, Co, OH, OW]
@@ -1110,7 +1135,9 @@ class BinaryConv2dFunction(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         binarize_input, stride, padding, dilation, groups = ctx.conf
-        dy = _c2d(dy)
+        bn = _c1bn_take(dy)      # the BatchNorm2d backward's pooled gradient and statistics, if handed over
+        if bn is None:
+            dy = _c2d(dy)
         N, C, H, W = x.shape
         Co, _, KH, KW = w.shape
         if ctx.empty:
@@ -1120,6 +1147,21 @@ class BinaryConv2dFunction(torch.autograd.Function):
                     if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None, None, None)
         dx = dw = db = None
         macs = dy.numel() * (C // groups) * KH * KW
+        if bn is not None:
+            global C1BN_HANDOFFS
+            need_db = ctx.has_bias and ctx.needs_input_grad[2]
+            dw = torch.empty_like(w)
+            db = torch.empty((Co,), dtype=torch.float32, device=x.device) if need_db else None
+            ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
+                             dtype=torch.uint8, device=x.device)
+            zq, zb, zf, dyp, mean, invstd, gw, gb, sg, sgx, inv_n, ht = bn
+            with _timed("conv2d_bwd_filter_bn", 2 * macs, zq.numel() * zq.element_size() + 4 * dyp.numel()):
+                L.call("bnn_conv2d_bwd_filter_bn", L.ptr(zq), L.ptr(zb), zf, L.ptr(dyp), L.ptr(mean), L.ptr(invstd),
+                       L.ptr(gw), L.ptr(gb), L.ptr(sg), L.ptr(sgx), float(inv_n), int(ht), L.ptr(x),
+                       int(binarize_input), L.ptr(dw), L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride,
+                       padding, dilation, groups, L.stream())
+            C1BN_HANDOFFS += 1
+            return (None, dw if ctx.needs_input_grad[1] else None, db, None, None, None, None, None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             with _timed("conv2d_bwd_data", 2 * macs, 4 * (dy.numel() + dx.numel() + w.numel())):
@@ -1668,6 +1710,7 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
         else:
             ctx.save_for_backward(zq[0], w, b, mean, invstd, zq[1], None)
         ctx.zq_fmt = 0 if zq is None else zq[2]
+        ctx.c1bn = (zq is not None and training and pool == 2 and bool(getattr(x, _C1BN_WANT, False)))
         ctx.shape = (N, C, H, W)
         ctx.hardtanh, ctx.pool = hardtanh, pool
         ctx.training = training
@@ -1684,6 +1727,19 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
         ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=dy.device)
         nel = N * C * H * W
         xb = 4 if ctx.zq_fmt == 0 else x.element_size()
+        if ctx.c1bn and ctx.needs_input_grad[0]:
+            # statistics only; the conv's filter gradient forms dx from them (bnn_conv2d_bwd_filter_bn)
+            sg = torch.empty((C,), dtype=torch.float32, device=dy.device)
+            sgx = torch.empty_like(sg)
+            with _timed("bn2d_bwd_stats", 0, xb * nel + 4 * dy.numel()):
+                L.call("bnn_bn2d_bwd_stats_q", L.ptr(x), L.ptr(xbias), ctx.zq_fmt, L.ptr(dy), N, C, H, W, L.ptr(w),
+                       L.ptr(b), L.ptr(mean), L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dw), L.ptr(db),
+                       L.ptr(sg), L.ptr(sgx), L.ptr(ws), L.stream())
+            dx = torch.zeros((1,), dtype=torch.float32, device=dy.device).as_strided((N, C, H, W), (0, 0, 0, 0))
+            setattr(dx, _C1BN_ATTR, (_q6_key(dx), x, xbias, ctx.zq_fmt, dy, mean, invstd, w, b, sg, sgx,
+                                     1.0 / (N * H * W), int(ctx.hardtanh)))
+            return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                    None, None, None, None, None, None, None)
         with _timed("bn2d_bwd", 0, (2 * xb + 4) * nel + 8 * dy.numel()):
             if ctx.zq_fmt:
                 L.call("bnn_bn2d_bwd_q", L.ptr(x), L.ptr(xbias), ctx.zq_fmt, L.ptr(dy), N, C, H, W, L.ptr(w), L.ptr(b),

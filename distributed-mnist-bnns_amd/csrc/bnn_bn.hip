@@ -20,6 +20,7 @@
 
 #include "bnn_common.h"
 #include "bnn_fp6.h"
+#include "bnn_bn2d.h"
 
 namespace bnn {
 const int64_t* g_seed_ctr = nullptr;   // bnn_set_seed_counter (declared in bnn_common.h)
@@ -1084,94 +1085,6 @@ __device__ __forceinline__ void block_sum2(double& a, double& b) {
   }
 }
 
-struct Bn2Chan {   // per-channel affine of the normalisation
-  float mu, is, ga, be;
-};
-
-__device__ __forceinline__ Bn2Chan bn2_chan(int64_t c, const float* mean, const float* invstd, const float* gamma,
-                                            const float* beta) {
-  return Bn2Chan{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f};
-}
-
-// One 2x2 pooling window: pre-activation y (before the clamp) of its 4 elements in torch scan
-// order (h, w), the max-pool output and the argmax slot.
-struct Win {
-  float xh[4], y[4];
-  float out;
-  int arg;
-};
-
-__device__ __forceinline__ Win bn2_window(float2 top, float2 bot, const Bn2Chan& k, int hardtanh) {
-  Win w;
-  const float xs[4] = {top.x, top.y, bot.x, bot.y};
-  float best = -__builtin_inff();
-  int arg = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    w.xh[j] = (xs[j] - k.mu) * k.is;
-    w.y[j] = fmaf(w.xh[j], k.ga, k.be);
-    const float v = hardtanh ? fminf(fmaxf(w.y[j], -1.f), 1.f) : w.y[j];
-    if (v > best || v != v) {
-      best = v;
-      arg = j;
-    }
-  }
-  w.out = best;
-  w.arg = arg;
-  return w;
-}
-
-// The NCHW input of a BatchNorm2d pass: fp32 (XF 0), or (XF 1 / 2) the int8 / int16 exact sums I of
-// the binary convolution that produced it (bnn_conv2d_fwd_q) plus its per-channel bias, read as
-// x = fl(I + bias[c]) -- the value the conv's fp32 epilogue stores, so every result is bit-identical,
-// at 1/4 (conv1: |I| <= 25) or 1/2 the bytes of every pass.
-struct X2 {
-  const void* p;
-  const float* bias;
-};
-
-template <int XF>
-__device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
-  return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
-}
-
-// 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
-template <int XF>
-__device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
-  if constexpr (XF == 0) {
-    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
-  } else if constexpr (XF == 1) {
-    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
-    return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
-                       (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
-  } else {
-    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(x.p) + idx);
-    return make_float4((float)(int16_t)(u.x & 0xFFFF) + b, (float)(int16_t)(u.x >> 16) + b,
-                       (float)(int16_t)(u.y & 0xFFFF) + b, (float)(int16_t)(u.y >> 16) + b);
-  }
-}
-
-// 2 consecutive elements (idx even)
-template <int XF>
-__device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
-  if constexpr (XF == 0) {
-    return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
-  } else if constexpr (XF == 1) {
-    const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
-    return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
-  } else {
-    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int16_t*>(x.p) + idx);
-    return make_float2((float)(int16_t)(u & 0xFFFF) + b, (float)(int16_t)(u >> 16) + b);
-  }
-}
-
-template <int XF>
-__device__ __forceinline__ float x2_ld1(const X2& x, int64_t idx, float b) {
-  if constexpr (XF == 0) return reinterpret_cast<const float*>(x.p)[idx];
-  else if constexpr (XF == 1) return (float)reinterpret_cast<const int8_t*>(x.p)[idx] + b;
-  else return (float)reinterpret_cast<const int16_t*>(x.p)[idx] + b;
-}
-
 // MODE 0: chunk (mean, M2) of x.  MODE 1: chunk (sum g, sum g*xhat), g = masked full-resolution
 // gradient (POOL: routed to the window argmax from the pooled dy).
 template <int MODE, int POOL, int XF = 0>
@@ -1281,6 +1194,131 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(X2 x, const float* __rest
   }
 }
 
+// Backward statistics of a 2x2-pooled BatchNorm2d (bn2d_reduce_k<1, 2>'s sums) with thread =
+// (image, pooled row): the PW windows' loads -- two x rows and one dy row -- are all issued before
+// any is used (3 PW independent loads per thread; the window-per-trip loop waited on memory ~60 %
+// of its cycles: profiles/r04_pmc_sq_cnn.txt).  Same per-window arithmetic; the fp32 partial of a
+// row is folded into the double sums per row.
+template <int PW, int XF>
+__global__ __launch_bounds__(BN2_T) void bn2d_bwd_stats_rows_k(X2 x, const float* __restrict__ dy, int64_t N,
+                                                               int64_t C, int H, int64_t CR,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, int hardtanh,
+                                                               double* __restrict__ p0, double* __restrict__ p1) {
+  constexpr int W = 2 * PW;
+  const int64_t c = blockIdx.x, r = blockIdx.y;
+  const int64_t n0 = r * CR, n1 = (n0 + CR < N) ? n0 + CR : N;
+  const int PH = H / 2;
+  const int64_t HW = (int64_t)H * W, pp = (int64_t)PH * PW;
+  const float xb = x2_bias<XF>(x, c);
+  const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+  double a = 0.0, b = 0.0;
+  const int64_t pairs = (n1 - n0) * PH;
+  for (int64_t i = threadIdx.x; i < pairs; i += BN2_T) {
+    const int64_t q0 = i / PH;
+    const int ph = (int)(i - q0 * PH);
+    const int64_t plane = (n0 + q0) * C + c;
+    const int64_t xo = plane * HW + (int64_t)(2 * ph) * W, yo = plane * pp + (int64_t)ph * PW;
+    float2 top[PW], bot[PW];
+    float g[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
+      bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
+      g[q] = dy[yo + q];
+    }
+    float fa = 0.f, fb = 0.f;
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const Win w = bn2_window(top[q], bot[q], k, hardtanh);
+      const float yv = w.y[w.arg];
+      const float gg = (!hardtanh || (yv > -1.f && yv < 1.f)) ? g[q] : 0.f;
+      fa += gg;
+      fb = fmaf(gg, w.xh[w.arg], fb);
+    }
+    a += (double)fa;
+    b += (double)fb;
+  }
+  block_sum2(a, b);
+  if (threadIdx.x == 0) {
+    p0[r * C + c] = a;
+    p1[r * C + c] = b;
+  }
+}
+
+// The pooled forward / backward apply passes with thread = (plane, pooled row): one index split per
+// row of PW windows (the window-per-thread forms split a 64-bit flat index three times per window)
+// and all of a row's loads issued before use.  Per-window arithmetic identical to bn2d_apply_k /
+// bn2d_bwd_apply_k<2> (bit-identical outputs).
+template <int PW, int XF>
+__global__ __launch_bounds__(256) void bn2d_apply_rows_k(X2 x, int64_t N, int64_t C, int H,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, int hardtanh,
+                                                         float* __restrict__ y) {
+  constexpr int W = 2 * PW;
+  const int PH = H / 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C * PH) return;
+  const int64_t plane = i / PH;
+  const int ph = (int)(i - plane * PH);
+  const int64_t c = plane % C;
+  const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+  const float xb = x2_bias<XF>(x, c);
+  const int64_t xo = plane * ((int64_t)H * W) + (int64_t)(2 * ph) * W;
+  float2 top[PW], bot[PW];
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
+    bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
+  }
+  float* yr = y + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
+#pragma unroll
+  for (int q = 0; q < PW; ++q) yr[q] = bn2_window(top[q], bot[q], k, hardtanh).out;
+}
+
+template <int PW, int XF>
+__global__ __launch_bounds__(256) void bn2d_bwd_apply_rows_k(X2 x, const float* __restrict__ dy, int64_t N,
+                                                             int64_t C, int H, const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int hardtanh,
+                                                             const float* __restrict__ sg,
+                                                             const float* __restrict__ sgx, float inv_n,
+                                                             float* __restrict__ dx) {
+  constexpr int W = 2 * PW;
+  const int PH = H / 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C * PH) return;
+  const int64_t plane = i / PH;
+  const int ph = (int)(i - plane * PH);
+  const int64_t c = plane % C;
+  const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
+  const float m0 = sg[c] * inv_n, m1 = sgx[c] * inv_n, sc = k.ga * k.is;
+  const float xb = x2_bias<XF>(x, c);
+  const int64_t xo = plane * ((int64_t)H * W) + (int64_t)(2 * ph) * W;
+  const float* dr = dy + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
+  float2 top[PW], bot[PW];
+  float gp[PW];
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
+    bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
+    gp[q] = dr[q];
+  }
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const Win w = bn2_window(top[q], bot[q], k, hardtanh);
+    float o[4];
+    bn2_window_dz(w, gp[q], m0, m1, sc, hardtanh, o);
+    *reinterpret_cast<float2*>(dx + xo + 2 * q) = make_float2(o[0], o[1]);
+    *reinterpret_cast<float2*>(dx + xo + W + 2 * q) = make_float2(o[2], o[3]);
+  }
+}
+
 // Forward apply: y = clamp((x-mean)*invstd*gamma+beta) (POOL: max over each 2x2 window).
 template <int POOL, int XF = 0>
 __global__ __launch_bounds__(256) void bn2d_apply_k(X2 x, int64_t N, int64_t C, int H, int W,
@@ -1345,13 +1383,8 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_k(X2 x, const float* __res
       const int64_t off = plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
       const float xb = x2_bias<XF>(x, c);
       const Win w = bn2_window(x2_ld2<XF>(x, off, xb), x2_ld2<XF>(x, off + W, xb), k, hardtanh);
-      const float gp = dy[i];
       float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float g = (j == w.arg && (!hardtanh || (w.y[j] > -1.f && w.y[j] < 1.f))) ? gp : 0.f;
-        o[j] = sc * (g - m0 - w.xh[j] * m1);
-      }
+      bn2_window_dz(w, dy[i], m0, m1, sc, hardtanh, o);
       *reinterpret_cast<float2*>(dx + off) = make_float2(o[0], o[1]);
       *reinterpret_cast<float2*>(dx + off + W) = make_float2(o[2], o[3]);
     }
@@ -1868,6 +1901,15 @@ BNN_API int64_t bnn_bn2d_workspace(int64_t N, int64_t C) {
     else { constexpr int XFV = 0; __VA_ARGS__; }                             \
   } while (0)
 
+// 1 (default): the pooled statistics and forward apply of 28- / 14-wide planes on the row kernels
+// (bn2d_*_rows_k); 2: also the backward apply (slower: A/B only); 0: the window-per-thread kernels
+static int g_bn2_rows = 1;
+
+BNN_API int bnn_bn2d_set_rows(int32_t on) {
+  g_bn2_rows = on < 0 ? 1 : (on > 2 ? 1 : on);
+  return 0;
+}
+
 static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, int64_t W, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, float momentum,
                                float eps, float* save_mean, float* save_invstd, float* y, int32_t hardtanh,
@@ -1889,9 +1931,19 @@ static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, in
   hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
-  BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_apply_k<P, XFV>), dim3(grid_for(outs)), dim3(256),
-                                                               0, s, x, N, C, (int)H, (int)W, save_mean, save_invstd,
-                                                               gamma, beta, hardtanh, y)));
+  if (pool && g_bn2_rows && (W == 28 || W == 14)) {   // the BinCNN's pooled layers: one row per thread
+    const dim3 rg((unsigned)((N * C * (H / 2) + 255) / 256));
+    if (W == 28)
+      BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_apply_rows_k<14, XFV>), rg, dim3(256), 0, s, x, N, C, (int)H,
+                                           save_mean, save_invstd, gamma, beta, hardtanh, y));
+    else
+      BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_apply_rows_k<7, XFV>), rg, dim3(256), 0, s, x, N, C, (int)H,
+                                           save_mean, save_invstd, gamma, beta, hardtanh, y));
+  } else {
+    BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_apply_k<P, XFV>), dim3(grid_for(outs)), dim3(256),
+                                                                 0, s, x, N, C, (int)H, (int)W, save_mean, save_invstd,
+                                                                 gamma, beta, hardtanh, y)));
+  }
   return check_launch("bnn_bn2d_fwd_train");
 }
 
@@ -1934,7 +1986,7 @@ BNN_API int bnn_bn2d_fwd_eval(const float* x, int64_t N, int64_t C, int64_t H, i
 static int bn2d_bwd_impl(X2 x, int xf, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,
                          const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                          int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
-                         void* stream, bool batch_stats) {
+                         void* stream, bool batch_stats, float* k0_out = nullptr, float* k1_out = nullptr) {
   if (!bn2_args_ok(reinterpret_cast<const float*>(x.p), N, C, H, W, pool) || !dy || !save_mean || !save_invstd ||
       !work || (dx && !aligned16(dx)) || (!pool && !aligned16(dy)) || xf < 0 || xf > 2 || (xf == 0 && x.bias) ||
       (x.bias && !aligned16(x.bias))) {
@@ -1945,20 +1997,44 @@ static int bn2d_bwd_impl(X2 x, int xf, const float* dy, int64_t N, int64_t C, in
   const int64_t CR = bn2_chunk_images(N, C), R = (N + CR - 1) / CR;
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
-  float* k0 = reinterpret_cast<float*>(p1 + R * C);
-  float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
-  BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P, XFV>), dim3((unsigned)C, (unsigned)R),
-                                                               dim3(BN2_T), 0, s, x, dy, N, C, (int)H, (int)W, CR,
-                                                               save_mean, save_invstd, gamma, beta, hardtanh, p0, p1)));
+  float* k0 = k0_out ? k0_out : reinterpret_cast<float*>(p1 + R * C);
+  float* k1 = k1_out ? k1_out : reinterpret_cast<float*>(reinterpret_cast<char*>(p1 + R * C) + round_up(C * 4, 256));
+  if (pool && g_bn2_rows && (W == 28 || W == 14)) {   // the BinCNN's pooled layers: row-batched loads
+    if (W == 28)
+      BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_bwd_stats_rows_k<14, XFV>), dim3((unsigned)C, (unsigned)R),
+                                           dim3(BN2_T), 0, s, x, dy, N, C, (int)H, CR, save_mean, save_invstd, gamma,
+                                           beta, hardtanh, p0, p1));
+    else
+      BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_bwd_stats_rows_k<7, XFV>), dim3((unsigned)C, (unsigned)R),
+                                           dim3(BN2_T), 0, s, x, dy, N, C, (int)H, CR, save_mean, save_invstd, gamma,
+                                           beta, hardtanh, p0, p1));
+  } else {
+    BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_reduce_k<1, P, XFV>), dim3((unsigned)C, (unsigned)R),
+                                                                 dim3(BN2_T), 0, s, x, dy, N, C, (int)H, (int)W, CR,
+                                                                 save_mean, save_invstd, gamma, beta, hardtanh, p0, p1)));
+  }
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma,
                      dbeta, k0, k1);
   if (dx) {
     const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;
     const float inv_n = batch_stats ? (float)(1.0 / ((double)N * (double)(H * W))) : 0.f;
-    BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_bwd_apply_k<P, XFV>), dim3(grid_for(outs)),
-                                                                 dim3(256), 0, s, x, dy, N, C, (int)H, (int)W,
-                                                                 save_mean, save_invstd, gamma, beta, hardtanh, k0, k1,
-                                                                 inv_n, dx)));
+    // (the row form, bn2d_bwd_apply_rows_k, is built for A/B only -- g_bn2_rows == 2: its two
+    // full-resolution output rows per thread write 8-B pieces 224 B apart, 186 vs 70 us on the
+    // BinCNN's first layer, profiles/r04_cnn_bn2d_rows.log)
+    if (pool && g_bn2_rows == 2 && (W == 28 || W == 14)) {
+      const dim3 rg((unsigned)((N * C * (H / 2) + 255) / 256));
+      if (W == 28)
+        BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_bwd_apply_rows_k<14, XFV>), rg, dim3(256), 0, s, x, dy, N, C,
+                                             (int)H, save_mean, save_invstd, gamma, beta, hardtanh, k0, k1, inv_n, dx));
+      else
+        BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_bwd_apply_rows_k<7, XFV>), rg, dim3(256), 0, s, x, dy, N, C,
+                                             (int)H, save_mean, save_invstd, gamma, beta, hardtanh, k0, k1, inv_n, dx));
+    } else {
+      BN2_XF_SWITCH(xf, BN2_POOL_SWITCH(pool, hipLaunchKernelGGL((bn2d_bwd_apply_k<P, XFV>), dim3(grid_for(outs)),
+                                                                   dim3(256), 0, s, x, dy, N, C, (int)H, (int)W,
+                                                                   save_mean, save_invstd, gamma, beta, hardtanh, k0,
+                                                                   k1, inv_n, dx)));
+    }
   }
   return check_launch("bnn_bn2d_bwd");
 }
@@ -1981,6 +2057,20 @@ BNN_API int bnn_bn2d_bwd_q(const void* xq, const float* xbias, int32_t xfmt, con
   }
   return bn2d_bwd_impl(X2{xq, xbias}, xfmt, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool, dx,
                        dgamma, dbeta, work, stream, true);
+}
+
+// The backward statistics only (no dx): dgamma, dbeta and sum g / sum g*xhat into sg / sgx (C
+// floats each) -- for a consumer that forms dx itself (bnn_conv2d_bwd_filter_bn)
+BNN_API int bnn_bn2d_bwd_stats_q(const void* xq, const float* xbias, int32_t xfmt, const float* dy, int64_t N,
+                                 int64_t C, int64_t H, int64_t W, const float* gamma, const float* beta,
+                                 const float* save_mean, const float* save_invstd, int32_t hardtanh, int32_t pool,
+                                 float* dgamma, float* dbeta, float* sg, float* sgx, void* work, void* stream) {
+  if ((xfmt != 1 && xfmt != 2) || !sg || !sgx) {
+    set_error("bnn_bn2d_bwd_stats_q: xfmt must be 1 (int8) or 2 (int16); sg, sgx required");
+    return kErrInval;
+  }
+  return bn2d_bwd_impl(X2{xq, xbias}, xfmt, dy, N, C, H, W, gamma, beta, save_mean, save_invstd, hardtanh, pool,
+                       nullptr, dgamma, dbeta, work, stream, true, sg, sgx);
 }
 
 BNN_API int bnn_bn2d_bwd_eval(const float* x, const float* dy, int64_t N, int64_t C, int64_t H, int64_t W,

@@ -1,0 +1,108 @@
+// BatchNorm2d(+Hardtanh)(+MaxPool2d(2)) element helpers shared by the BatchNorm2d passes
+// (bnn_bn.hip) and the conv filter gradient that forms its dY from them (bnn_conv.hip).
+#pragma once
+#include "bnn_common.h"
+
+namespace bnn {
+
+struct Bn2Chan {   // per-channel affine of the normalisation
+  float mu, is, ga, be;
+};
+
+__device__ __forceinline__ Bn2Chan bn2_chan(int64_t c, const float* mean, const float* invstd, const float* gamma,
+                                            const float* beta) {
+  return Bn2Chan{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f};
+}
+
+// One 2x2 pooling window: pre-activation y (before the clamp) of its 4 elements in torch scan
+// order (h, w), the max-pool output and the argmax slot.
+struct Win {
+  float xh[4], y[4];
+  float out;
+  int arg;
+};
+
+__device__ __forceinline__ Win bn2_window(float2 top, float2 bot, const Bn2Chan& k, int hardtanh) {
+  Win w;
+  const float xs[4] = {top.x, top.y, bot.x, bot.y};
+  float best = -__builtin_inff();
+  int arg = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w.xh[j] = (xs[j] - k.mu) * k.is;
+    w.y[j] = fmaf(w.xh[j], k.ga, k.be);
+    const float v = hardtanh ? fminf(fmaxf(w.y[j], -1.f), 1.f) : w.y[j];
+    if (v > best || v != v) {
+      best = v;
+      arg = j;
+    }
+  }
+  w.out = best;
+  w.arg = arg;
+  return w;
+}
+
+// The NCHW input of a BatchNorm2d pass: fp32 (XF 0), or (XF 1 / 2) the int8 / int16 exact sums I of
+// the binary convolution that produced it (bnn_conv2d_fwd_q) plus its per-channel bias, read as
+// x = fl(I + bias[c]) -- the value the conv's fp32 epilogue stores, so every result is bit-identical,
+// at 1/4 (conv1: |I| <= 25) or 1/2 the bytes of every pass.
+struct X2 {
+  const void* p;
+  const float* bias;
+};
+
+template <int XF>
+__device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
+  return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
+}
+
+// 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
+template <int XF>
+__device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
+  } else if constexpr (XF == 1) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
+                       (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    return make_float4((float)(int16_t)(u.x & 0xFFFF) + b, (float)(int16_t)(u.x >> 16) + b,
+                       (float)(int16_t)(u.y & 0xFFFF) + b, (float)(int16_t)(u.y >> 16) + b);
+  }
+}
+
+// 2 consecutive elements (idx even)
+template <int XF>
+__device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) {
+    return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
+  } else if constexpr (XF == 1) {
+    const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
+  } else {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    return make_float2((float)(int16_t)(u & 0xFFFF) + b, (float)(int16_t)(u >> 16) + b);
+  }
+}
+
+template <int XF>
+__device__ __forceinline__ float x2_ld1(const X2& x, int64_t idx, float b) {
+  if constexpr (XF == 0) return reinterpret_cast<const float*>(x.p)[idx];
+  else if constexpr (XF == 1) return (float)reinterpret_cast<const int8_t*>(x.p)[idx] + b;
+  else return (float)reinterpret_cast<const int16_t*>(x.p)[idx] + b;
+}
+
+// The backward of one 2x2 window (bn2d_bwd_apply_k): dz of its 4 elements (torch scan order) from
+// the pooled gradient gp routed to the argmax and masked by the Hardtanh, m0 = sum g / n,
+// m1 = sum g xhat / n and sc = gamma * invstd.
+__device__ __forceinline__ void bn2_window_dz(const Win& w, float gp, float m0, float m1, float sc, int hardtanh,
+                                              float (&o)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float g = (j == w.arg && (!hardtanh || (w.y[j] > -1.f && w.y[j] < 1.f))) ? gp : 0.f;
+    o[j] = sc * (g - m0 - w.xh[j] * m1);
+  }
+}
+
+}  // namespace bnn

@@ -11,6 +11,7 @@
 #include <type_traits>
 
 #include "bnn_common.h"
+#include "bnn_bn2d.h"
 
 #include <cstring>
 #include <vector>
@@ -693,6 +694,134 @@ __global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1_k(const float* __res
     float s = 0.f;
     for (int q = 0; q < g.TPC; ++q) s += red[(c * g.TPC + q) * (KK + 1) + k];
     if (k < KK) row[c * KK + k] = s;
+    else row[(int64_t)g.Co * KK + c] = with_bias ? s : 0.f;
+  }
+}
+
+// conv1's filter gradient straight from its BatchNorm2d + Hardtanh + MaxPool2d(2) backward (the
+// BinCNN's first layer, mnist-dist.py:31-51 template): dY is formed per 2x2 window from the conv's
+// compact output z (its exact int8 / int16 sums + bias), the pooled gradient and the batch
+// statistics -- bn2_window + bn2_window_dz, the arithmetic of bn2d_bwd_apply_k -- and multiplied
+// straight into the filter sums, so the fp32 dY (205 MB at B = 4096) is neither written by a
+// BatchNorm pass nor re-read here.  Unit = (pooled row, 4 output columns): two output rows, two
+// windows; its KH + 1 input rows are read once for both.  Otherwise as conv_bwd_filter_c1_k.
+constexpr int C1BN_UB = 4;   // units per load batch (8 would leave 2 waves per SIMD: 178 VGPRs)
+
+struct C1Bn {
+  X2 z;
+  const float* dyp;                                  // pooled gradient [N][Co][OH/2][OW/2]
+  const float *mean, *invstd, *gamma, *beta, *sg, *sgx;
+  float inv_n;
+  int hardtanh;
+};
+
+template <int KH, int KW, int XF>
+__global__ __launch_bounds__(C1F_T) void conv_bwd_filter_c1bn_k(C1Bn bn, const float* __restrict__ x, int binarize,
+                                                                float* __restrict__ part, int64_t N, C1Filt g,
+                                                                int with_bias) {
+  constexpr int NX = (KW + 6) / 4;
+  constexpr int KK = KH * KW;
+  extern __shared__ __attribute__((aligned(16))) float c1s[];
+  const int plane = g.XR * g.XW;
+  float* red = c1s;
+  const int t = threadIdx.x;
+  const int co = t / g.TPC, r = t - co * g.TPC;
+  const int hw = g.H * g.W, ohw = g.OH * g.OW, uq = g.OW / 4, nu = (g.OH / 2) * uq, pw = g.OW / 2;
+  for (int i = t; i < 2 * plane; i += C1F_T) c1s[i] = 0.f;
+  float acc[KK], bacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < KK; ++k) acc[k] = 0.f;
+  // this thread's channel: the normalisation and the statistics terms of its backward
+  const int cc = co < g.Co ? co : 0;
+  const Bn2Chan k = bn2_chan(cc, bn.mean, bn.invstd, bn.gamma, bn.beta);
+  const float m0 = bn.sg[cc] * bn.inv_n, m1 = bn.sgx[cc] * bn.inv_n, sc = k.ga * k.is;
+  const float zb = x2_bias<XF>(bn.z, cc);
+  const int64_t n0 = (int64_t)blockIdx.x * C1F_SPB, n1 = n0 + C1F_SPB < N ? n0 + C1F_SPB : N;
+  float px[C1F_PX];
+  auto fetch = [&](int64_t n) {
+#pragma unroll
+    for (int s = 0; s < C1F_PX; ++s) px[s] = x[n * hw + min(t + s * C1F_T, hw - 1)];
+  };
+  auto put = [&](int b) {
+    for (int s = 0; s < C1F_PX; ++s) {
+      const int i = t + s * C1F_T;
+      if (i < hw) {
+        const int ih = i / g.W, iw = i - ih * g.W;
+        c1s[b * plane + (ih + g.pad) * g.XW + iw + g.pad] = binarize ? (float)tsign(px[s]) : px[s];
+      }
+    }
+  };
+  __syncthreads();
+  if (n0 < n1) {
+    fetch(n0);
+    put(0);
+  }
+  for (int64_t n = n0; n < n1; ++n) {
+    const int b = (int)((n - n0) & 1);
+    __syncthreads();
+    if (n + 1 < n1) fetch(n + 1);
+    if (co < g.Co) {
+      const float* xb = c1s + b * plane;
+      const int64_t zo = (n * g.Co + co) * (int64_t)ohw, po = (n * g.Co + co) * (int64_t)(ohw / 4);
+      for (int u0 = r; u0 < nu; u0 += C1BN_UB * g.TPC) {
+        float4 zt[C1BN_UB], zbt[C1BN_UB];
+        float2 gp[C1BN_UB];
+#pragma unroll
+        for (int i = 0; i < C1BN_UB; ++i) {   // clamped, unconditional: the loads batch
+          const int u = min(u0 + i * g.TPC, nu - 1);
+          const int pr = u / uq, ow0 = 4 * (u - pr * uq);
+          zt[i] = x2_ld4<XF>(bn.z, zo + (int64_t)(2 * pr) * g.OW + ow0, zb);
+          zbt[i] = x2_ld4<XF>(bn.z, zo + (int64_t)(2 * pr + 1) * g.OW + ow0, zb);
+          gp[i] = *reinterpret_cast<const float2*>(bn.dyp + po + (int64_t)pr * pw + ow0 / 2);
+        }
+#pragma unroll
+        for (int i = 0; i < C1BN_UB; ++i) {
+          const int u = u0 + i * g.TPC;
+          if (u >= nu) break;
+          const int pr = u / uq, ow0 = 4 * (u - pr * uq);
+          float o0[4], o1[4];
+          bn2_window_dz(bn2_window(make_float2(zt[i].x, zt[i].y), make_float2(zbt[i].x, zbt[i].y), k, bn.hardtanh),
+                        gp[i].x, m0, m1, sc, bn.hardtanh, o0);
+          bn2_window_dz(bn2_window(make_float2(zt[i].z, zt[i].w), make_float2(zbt[i].z, zbt[i].w), k, bn.hardtanh),
+                        gp[i].y, m0, m1, sc, bn.hardtanh, o1);
+          const float dt[4] = {o0[0], o0[1], o1[0], o1[1]}, db[4] = {o0[2], o0[3], o1[2], o1[3]};
+          bacc += ((dt[0] + dt[1]) + (dt[2] + dt[3])) + ((db[0] + db[1]) + (db[2] + db[3]));
+          float xr[KH + 1][4 * NX];
+#pragma unroll
+          for (int rr = 0; rr <= KH; ++rr)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+              const float4 v = *reinterpret_cast<const float4*>(xb + (2 * pr + rr) * g.XW + ow0 + 4 * j);
+              xr[rr][4 * j] = v.x, xr[rr][4 * j + 1] = v.y, xr[rr][4 * j + 2] = v.z, xr[rr][4 * j + 3] = v.w;
+            }
+#pragma unroll
+          for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < KW; ++kw) {
+              float a = acc[kh * KW + kw];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) a = fmaf(dt[j], xr[kh][kw + j], a);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) a = fmaf(db[j], xr[kh + 1][kw + j], a);
+              acc[kh * KW + kw] = a;
+            }
+        }
+      }
+    }
+    if (n + 1 < n1) put(b ^ 1);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) red[t * (KK + 1) + kk] = acc[kk];
+  red[t * (KK + 1) + KK] = bacc;
+  __syncthreads();
+  const int64_t nelem = (int64_t)g.Co * KK + g.Co;
+  float* row = part + (int64_t)blockIdx.x * nelem;
+  for (int e = t; e < g.Co * (KK + 1); e += C1F_T) {
+    const int c = e / (KK + 1), kk = e - c * (KK + 1);
+    float s = 0.f;
+    for (int q = 0; q < g.TPC; ++q) s += red[(c * g.TPC + q) * (KK + 1) + kk];
+    if (kk < KK) row[c * KK + kk] = s;
     else row[(int64_t)g.Co * KK + c] = with_bias ? s : 0.f;
   }
 }
@@ -2075,4 +2204,61 @@ BNN_API int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binar
   hipLaunchKernelGGL(conv_bwd_filter_reduce_k, dim3((unsigned)((nelem + 255) / 256)), dim3(256), 0, st,
                      part, nelem, nchunks, nw, dw, db);
   return check_launch("bnn_conv2d_bwd_filter");
+}
+
+// 1 when bnn_conv2d_bwd_filter_bn takes the shape: the one-input-channel filter kernel's geometry
+// (bnn_conv_set_c1_filter on, the MFMA engines on) with an even OH and OW % 4 == 0
+BNN_API int bnn_conv2d_bwd_filter_bn_ok(int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH,
+                                        int64_t KW, int32_t stride, int32_t pad, int32_t dil, int32_t groups) {
+  ConvShape s;
+  C1Filt cf;
+  int64_t lds = 0;
+  return (N > 0 && g_conv_c1f && g_conv_mfma != 0 && make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s) &&
+          c1_filt_geom(s, &cf, &lds) && s.OH % 2 == 0 && s.OW % 4 == 0)
+             ? 1
+             : 0;
+}
+
+// bnn_conv2d_bwd_filter with dY = the BatchNorm2d(+Hardtanh)+MaxPool2d(2) backward of the pooled
+// gradient dyp (bnn_bn2d_bwd_q's dx, never written): z = the conv's compact output (zfmt 1 int8 /
+// 2 int16 sums, zbias [Co]), mean / invstd / gamma / beta its BatchNorm's, sg / sgx the sums from
+// bnn_bn2d_bwd_stats_q, inv_n = 1 / (N OH OW).  Same shapes as bnn_conv2d_bwd_filter_bn_ok.
+BNN_API int bnn_conv2d_bwd_filter_bn(const void* zq, const float* zbias, int32_t zfmt, const float* dyp,
+                                     const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                     const float* sg, const float* sgx, float inv_n, int32_t hardtanh, const float* x,
+                                     int32_t binarize_input, float* dw, float* db, void* work, int64_t N, int64_t C,
+                                     int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int32_t stride,
+                                     int32_t pad, int32_t dil, int32_t groups, void* stream) {
+  ConvShape s;
+  C1Filt cf;
+  int64_t clds = 0;
+  if (!zq || !dyp || !mean || !invstd || !sg || !sgx || !x || !dw || !work || (zfmt != 1 && zfmt != 2) ||
+      !bnn_conv2d_bwd_filter_bn_ok(N, C, H, W, Co, KH, KW, stride, pad, dil, groups) ||
+      !make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s) || !c1_filt_geom(s, &cf, &clds) ||
+      (reinterpret_cast<uintptr_t>(dyp) & 7) != 0 || (reinterpret_cast<uintptr_t>(zq) & 7) != 0) {
+    set_error("bnn_conv2d_bwd_filter_bn: bad arguments");
+    return kErrInval;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nblk = (N + C1F_SPB - 1) / C1F_SPB;
+  const int64_t nw = Co * KH * KW, nel = nw + Co;
+  float* part = reinterpret_cast<float*>(work);
+  const size_t lds = (size_t)clds;
+  const C1Bn bn{X2{zq, zbias}, dyp, mean, invstd, gamma, beta, sg, sgx, inv_n, hardtanh};
+#define BNN_C1BN(KH_, XF_) BNN_TILE_LAUNCH((conv_bwd_filter_c1bn_k<KH_, KH_, XF_>), dim3((unsigned)nblk), dim3(C1F_T), \
+                                           lds, st, bn, x, binarize_input, part, N, cf, db != nullptr)
+  if (KH == 5) {
+    if (zfmt == 1) BNN_C1BN(5, 1); else BNN_C1BN(5, 2);
+  } else {
+    if (zfmt == 1) BNN_C1BN(3, 1); else BNN_C1BN(3, 2);
+  }
+#undef BNN_C1BN
+  const int64_t nsl = filter_slices(nblk);
+  double* slice = reinterpret_cast<double*>(reinterpret_cast<char*>(work) +
+                                            round_up(nblk * nel * (int64_t)sizeof(float), 256));
+  hipLaunchKernelGGL(conv_filter_tile_reduce1_k, dim3((unsigned)((nel + 255) / 256), (unsigned)nsl), dim3(256), 0,
+                     st, part, nblk, nel, nsl, slice);
+  hipLaunchKernelGGL(conv_filter_tile_reduce2_k, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, st, slice, nsl,
+                     (int)Co, (int)(KH * KW), (int)Co, dw, db);
+  return check_launch("bnn_conv2d_bwd_filter_bn");
 }

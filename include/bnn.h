@@ -297,6 +297,22 @@ int bnn_conv2d_bwd_filter(const float* dy, const float* x, int32_t binarize_inpu
                           int64_t Co, int64_t KH, int64_t KW, int32_t stride, int32_t pad,
                           int32_t dil, int32_t groups, bnn_stream_t stream);
 
+/* The first BinarizeConv2d's weight gradient fused with its BatchNorm2d + Hardtanh + MaxPool2d(2)
+ * backward (mnist-dist.py:31-51 template, binarized_modules.py:100-107): bnn_conv2d_bwd_filter with
+ * dY = the BatchNorm2d backward of the pooled gradient dyp, formed per 2x2 window from the conv's
+ * compact output zq (zfmt 1 int8 / 2 int16 sums + zbias, bnn_conv2d_fwd_q), the BatchNorm's
+ * mean / invstd / gamma / beta and sg / sgx from bnn_bn2d_bwd_stats_q (inv_n = 1 / (N OH OW)) -- the
+ * arithmetic of bnn_bn2d_bwd_q's dx, which is never written.  One input channel, stride 1, 3x3 or
+ * 5x5, even OH, OW % 4 == 0 (bnn_conv2d_bwd_filter_bn_ok); work as bnn_conv2d_bwd_filter's. */
+int bnn_conv2d_bwd_filter_bn_ok(int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                                int32_t stride, int32_t pad, int32_t dil, int32_t groups);
+int bnn_conv2d_bwd_filter_bn(const void* zq, const float* zbias, int32_t zfmt, const float* dyp, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, const float* sg,
+                             const float* sgx, float inv_n, int32_t hardtanh, const float* x, int32_t binarize_input,
+                             float* dw, float* db, void* work, int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co,
+                             int64_t KH, int64_t KW, int32_t stride, int32_t pad, int32_t dil, int32_t groups,
+                             bnn_stream_t stream);
+
 /* Convolution engine switch: 1 (default) = MFMA implicit-GEMM kernels for stride-1 ungrouped
  * shapes -- backward data on v_mfma_f32_16x16x32_bf16 with dY split exactly into three bf16
  * terms (exact products, fp32 accumulation), backward filter on v_mfma_f32_16x16x4_f32 (exact f32
@@ -308,6 +324,11 @@ int bnn_conv_set_mfma(int32_t mode);
  * (stride 1, 3x3 or 5x5, OW % 4 == 0, Co | 256, Co <= 64 -- the BinCNN's conv1) on a VALU kernel
  * that reads dY once with coalesced 16-B loads; 0: the MFMA kernels as for any layer. */
 int bnn_conv_set_c1_filter(int32_t on);
+/* 1 (default): the 2x2-pooled BatchNorm2d backward statistics and forward apply over 28- / 14-wide
+ * planes (the BinCNN's layers) on the row kernels (one thread per pooled row, every load of the row
+ * issued up front); 2: the backward apply too (slower; A/B); 0: the window-per-thread kernels.
+ * Same per-element arithmetic (the backward statistics summed per row). */
+int bnn_bn2d_set_rows(int32_t on);
 /* Host-only plan query (needs no GPU): the bf16x3 backward kernels' LDS layouts for a shape.
  * out[9]: data kernel (pixel pitch ps, weight pitch ws, row tiles, LDS bytes), then filter kernel
  * (dY pitch Kd, copy channel stride CS, copy stride XL, LDS bytes, modelled cycles x 100 of its B
@@ -391,6 +412,12 @@ int bnn_bn2d_bwd_q(const void* xq, const float* xbias, int32_t xfmt, const float
                    int64_t W, const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                    int32_t hardtanh, int32_t pool, float* dx, float* dgamma, float* dbeta, void* work,
                    bnn_stream_t stream);
+/* bnn_bn2d_bwd_q's statistics only (no dx): dgamma, dbeta and the column sums sum g, sum g*xhat into
+ * sg / sgx (C floats each), for bnn_conv2d_bwd_filter_bn. */
+int bnn_bn2d_bwd_stats_q(const void* xq, const float* xbias, int32_t xfmt, const float* dy, int64_t N, int64_t C,
+                         int64_t H, int64_t W, const float* gamma, const float* beta, const float* save_mean,
+                         const float* save_invstd, int32_t hardtanh, int32_t pool, float* dgamma, float* dbeta,
+                         float* sg, float* sgx, void* work, bnn_stream_t stream);
 
 /* nn.Dropout(p) fused in front of BatchNorm1d (+ Hardtanh) (mnist-dist2.py:69-70: fc3 -> drop ->
  * bn3): x is the pre-dropout input; the keep mask is a counter-based hash of (seed, row*C + col)

@@ -508,6 +508,70 @@ def test_batchnorm2d_hardtanh_pool_vs_oracle(F, N, C, H, W, pool):
     assert rel_err(host(ye), host(ref)) < 1e-6
 
 
+def test_bn2d_row_kernels_match_window_kernels(F):
+    """The row forms of the pooled BatchNorm2d passes (bnn_bn2d_set_rows) in a fused BinCNN step on
+    compact conv outputs, against the window-per-thread kernels: forward output and loss
+    bit-identical (same statistics, same per-window arithmetic), every gradient within 1e-6 (the
+    backward statistics are summed per row instead of per window group)."""
+    from bnn_amd import _lib as L
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    x, y = synthetic_mnist(512, seed=3)
+    x, y = x.cuda(), y.cuda()
+    res = []
+    try:
+        for on in (1, 0):
+            L.call("bnn_bn2d_set_rows", on)
+            torch.manual_seed(11)
+            m = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+            out = m(x)
+            loss = torch.nn.functional.nll_loss(out, y)
+            loss.backward()
+            res.append((host(out), float(loss), {k: host(p.grad) for k, p in m.named_parameters()}))
+    finally:
+        L.call("bnn_bn2d_set_rows", 1)
+    (o1, l1, g1), (o0, l0, g0) = res
+    assert np.array_equal(o1, o0) and l1 == l0
+    for k in g0:
+        # a conv bias ahead of a BatchNorm has an analytically zero gradient (~1e-8 of summation
+        # noise here): compared absolutely
+        assert rel_err(g1[k], g0[k]) <= 1e-6 or np.abs(g1[k] - g0[k]).max() <= 1e-7, k
+
+
+def test_conv1_bn2d_handoff_matches_unfused(F):
+    """The BinCNN's conv1 weight gradient formed straight from its BatchNorm2d + Hardtanh + MaxPool2d
+    backward (functional.C1BN: bnn_bn2d_bwd_stats_q + bnn_conv2d_bwd_filter_bn, the layer's fp32 dY
+    never written) against the unfused path (bnn_bn2d_bwd_q's dx into bnn_conv2d_bwd_filter): the
+    hand-off fires once per step; loss, layer 2 and the classifier bit-identical; layer 1's BatchNorm
+    gradients identical (same statistics pass); conv1's weight gradient within 1e-6 (another
+    summation order), its bias gradient (analytically zero ahead of a BatchNorm) within 1e-7."""
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    x, y = synthetic_mnist(1024, seed=5)
+    res = []
+    for on in (True, False):
+        F.C1BN = on
+        try:
+            torch.manual_seed(17)
+            m = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+            n0 = F.C1BN_HANDOFFS
+            loss = torch.nn.functional.nll_loss(m(x.cuda()), y.cuda())
+            loss.backward()
+            res.append((float(loss), {k: host(p.grad) for k, p in m.named_parameters()}, F.C1BN_HANDOFFS - n0))
+        finally:
+            F.C1BN = True
+    (l1, g1, h1), (l0, g0, h0) = res
+    assert h1 == 1 and h0 == 0
+    assert l1 == l0
+    for k in g0:
+        if k == "layer1.0.weight":
+            assert rel_err(g1[k], g0[k]) <= 1e-6, k
+        elif k == "layer1.0.bias":
+            assert np.abs(g1[k] - g0[k]).max() <= 1e-7, k
+        else:
+            assert np.array_equal(g1[k], g0[k]), k
+
+
 def test_fused_cnn_step_matches_torch_modules(F):
     """BinCNN with the fused BatchNorm2d+Hardtanh+MaxPool2d op against the same net through torch's
     BatchNorm2d / Hardtanh / MaxPool2d modules (integer-valued conv outputs: pooling ties resolved
@@ -564,6 +628,7 @@ def test_fused_cnn_compact_outputs_bit_identical(F):
     b.load_state_dict(a.state_dict())
     x, y = synthetic_mnist(200, seed=9, device="cuda")
     try:
+        F.C1BN = False            # conv1's BatchNorm hand-off sums in another order (its own test)
         F.ZQ = False
         la = torch.nn.functional.cross_entropy(a(x), y)
         la.backward()
@@ -574,6 +639,7 @@ def test_fused_cnn_compact_outputs_bit_identical(F):
         assert F.ZQ_HANDOFFS - n0 == 2
     finally:
         F.ZQ = True
+        F.C1BN = True
     assert la.item() == lb.item()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         assert torch.equal(pa.grad, pb.grad), n
