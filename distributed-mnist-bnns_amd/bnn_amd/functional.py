@@ -450,10 +450,26 @@ def z16_ok(M, N, K):
 Z16_HANDOFFS = 0          # z16 placeholders produced (tests check the hand-off actually ran)
 
 
+_ZERO1 = {}
+
+
+def _placeholder(shape, device):
+    """A stride-0 fp32 tensor of `shape` (the carrier of a hand-off attribute) viewing one cached zero
+    per device: no fill kernel per placeholder.  In-place writes through it are refused by torch
+    (every element aliases one location)."""
+    key = str(device)
+    z = _ZERO1.get(key)
+    if z is None:
+        z = torch.zeros((1,), dtype=torch.float32, device=device)
+        if not torch.cuda.is_current_stream_capturing():
+            _ZERO1[key] = z
+    return z.as_strided(tuple(shape), (0,) * len(shape))
+
+
 def _z16_carrier(y16, bias):
     global Z16_HANDOFFS
     Z16_HANDOFFS += 1
-    ph = torch.zeros((1,), dtype=torch.float32, device=y16.device).as_strided(tuple(y16.shape), (0, 0))
+    ph = _placeholder(y16.shape, y16.device)
     setattr(ph, _Z16_ATTR, (y16, bias))
     return ph
 
@@ -807,7 +823,7 @@ S20_HANDOFFS = 0          # s20 placeholders produced (tests check the hand-off 
 def _s20_carrier(lo, hi, bias, scale):
     global S20_HANDOFFS
     S20_HANDOFFS += 1
-    ph = torch.zeros((1,), dtype=torch.float32, device=lo.device).as_strided(tuple(lo.shape), (0, 0))
+    ph = _placeholder(lo.shape, lo.device)
     setattr(ph, _S20_ATTR, (lo, hi, bias, float(scale)))
     return ph
 
@@ -846,8 +862,9 @@ def _pixels_fwd_s20(q, wq, M, N, K, a, bias, R, s0):
     hi = torch.empty((M, N // 2), dtype=torch.uint8, device=dev)
     Kp = q.shape[1]
     assert wq.shape[1] == Kp and Kp % ALIGN == 0
-    # a snapshot of the bias: the optimizer updates the Parameter in place after this step's backward
-    bs = bias.clone() if bias is not None else None
+    # the bias itself (a detached view sharing the Parameter's version counter): the consumer saves it
+    # for backward, so torch refuses a backward after an in-place update of it -- no snapshot copy
+    bs = bias
     name = f"{gemm_kernel_name(1, 1, M, N, Kp)} [pixels s20]" if _TIMER is not None else ""
     with _timed(name, 2.0 * M * N * K, M * Kp + N * Kp + 2.5 * M * N):
         L.call("bnn_gemm_i8_affine_bnstats_s20", L.ptr(q), Kp, L.ptr(wq), Kp, L.ptr(R), float(s0), K, L.ptr(lo),
@@ -1108,9 +1125,10 @@ class BinaryConv2dFunction(torch.autograd.Function):
             ctx.conf = (binarize_input, stride, padding, dilation, groups)
             ctx.has_bias = bias is not None
             ZQ_HANDOFFS += 1
-            ph = torch.zeros((1,), dtype=torch.float32, device=x.device).as_strided((N, Co, OH, OW), (0, 0, 0, 0))
-            # the bias as it is now: the optimizer updates the Parameter in place after backward
-            setattr(ph, _ZQ_ATTR, (yq, b.clone() if b is not None else None, zf))
+            ph = _placeholder((N, Co, OH, OW), x.device)
+            # the bias as a detached view (its consumer saves it for backward: an in-place update
+            # before this step's backward is refused by torch's saved-tensor check, no copy needed)
+            setattr(ph, _ZQ_ATTR, (yq, b, zf))
             if (C1BN and C == 1 and binarize_input and not ctx.needs_input_grad[0]
                     and L.lib().bnn_conv2d_bwd_filter_bn_ok(N, C, H, W, Co, KH, KW, stride, padding, dilation,
                                                             groups)):
@@ -1308,7 +1326,7 @@ def _dz_placeholder(M, C, device):
     """The gradient of a z16 pre-activation: its only reader is the producing linear's backward,
     which takes the FP6 digits handed to it, so dz itself is never written (a stride-0 tensor of
     the right shape carries the hand-off)."""
-    return torch.zeros((1,), dtype=torch.float32, device=device).as_strided((M, C), (0, 0))
+    return _placeholder((M, C), device)
 
 
 def _q6_take_required(dy):
@@ -1735,7 +1753,7 @@ class BatchNorm2dHardtanhPoolFunction(torch.autograd.Function):
                 L.call("bnn_bn2d_bwd_stats_q", L.ptr(x), L.ptr(xbias), ctx.zq_fmt, L.ptr(dy), N, C, H, W, L.ptr(w),
                        L.ptr(b), L.ptr(mean), L.ptr(invstd), int(ctx.hardtanh), int(ctx.pool), L.ptr(dw), L.ptr(db),
                        L.ptr(sg), L.ptr(sgx), L.ptr(ws), L.stream())
-            dx = torch.zeros((1,), dtype=torch.float32, device=dy.device).as_strided((N, C, H, W), (0, 0, 0, 0))
+            dx = _placeholder((N, C, H, W), dy.device)
             setattr(dx, _C1BN_ATTR, (_q6_key(dx), x, xbias, ctx.zq_fmt, dy, mean, invstd, w, b, sg, sgx,
                                      1.0 / (N * H * W), int(ctx.hardtanh)))
             return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
@@ -1852,9 +1870,10 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                  if emit_stats and FP4_STATS and fp4 and M > 0 and N % 4 == 0 else 0)
         drop = tuple(emit_stats) if isinstance(emit_stats, tuple) else (0.0, 0)   # (p, seed) of a fused dropout
         if emit_z16 and fp4 and training:
-            # the next BatchNorm reads z = fl(I + bias) from int16 I: a snapshot of the bias (the
-            # optimizer updates the Parameter in place after this step's backward)
-            bs = b.clone() if b is not None else None
+            # the next BatchNorm reads z = fl(I + bias) from int16 I and the bias (a detached view of
+            # the Parameter: its consumer saves it for backward, so torch refuses a backward after an
+            # in-place update of it)
+            bs = b
             if chunk:
                 y16, fst = _fp4_fwd_with_stats(q, wq, M, N, C, None, bs, chunk, True, drop)
                 y = _z16_carrier(y16, bs)

@@ -1194,6 +1194,49 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(X2 x, const float* __rest
   }
 }
 
+// Forward statistics (bn2d_reduce_k<0>'s chunk sum and M2 about the chunk's first element) with the
+// chunk's (image, 4-element group) pairs flattened over the workgroup (no idle lanes when a plane
+// has fewer than 256 groups: conv1's 196) and 4 groups' loads issued together; 32-bit index split.
+template <int XF>
+__global__ __launch_bounds__(BN2_T) void bn2d_fwd_stats_flat_k(X2 x, int64_t N, int64_t C, int HW, int64_t CR,
+                                                               double* __restrict__ p0, double* __restrict__ p1) {
+  constexpr int B = 4;
+  const int64_t c = blockIdx.x, r = blockIdx.y;
+  const int64_t n0 = r * CR, n1 = (n0 + CR < N) ? n0 + CR : N;
+  const float xb = x2_bias<XF>(x, c);
+  const float shift = x2_ld1<XF>(x, (n0 * C + c) * HW, xb);
+  const int hw4 = HW / 4, total = (int)((n1 - n0) * hw4);
+  double a = 0.0, b = 0.0;
+  for (int i0 = threadIdx.x; i0 < total; i0 += B * BN2_T) {
+    float4 v[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int i = min(i0 + q * BN2_T, total - 1);   // clamped, unconditional: the loads batch
+      const int im = i / hw4, gi = i - im * hw4;
+      v[q] = x2_ld4<XF>(x, ((n0 + im) * C + c) * (int64_t)HW + 4 * gi, xb);
+    }
+    float fa = 0.f, fb = 0.f;
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (i0 + q * BN2_T >= total) break;
+      const float d[4] = {v[q].x - shift, v[q].y - shift, v[q].z - shift, v[q].w - shift};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fa += d[e];
+        fb = fmaf(d[e], d[e], fb);
+      }
+    }
+    a += (double)fa;
+    b += (double)fb;
+  }
+  block_sum2(a, b);
+  if (threadIdx.x == 0) {
+    const double nb = (double)((n1 - n0) * HW), dm = a / nb;
+    p0[r * C + c] = (double)shift * nb + a;   // chunk sum
+    p1[r * C + c] = b - a * dm;
+  }
+}
+
 // Backward statistics of a 2x2-pooled BatchNorm2d (bn2d_reduce_k<1, 2>'s sums) with thread =
 // (image, pooled row): the PW windows' loads -- two x rows and one dy row -- are all issued before
 // any is used (3 PW independent loads per thread; the window-per-trip loop waited on memory ~60 %
@@ -1925,9 +1968,14 @@ static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, in
   const int64_t CR = bn2_chunk_images(N, C), R = (N + CR - 1) / CR;
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
-  BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_reduce_k<0, 0, XFV>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0, s,
-                                       x, nullptr, N, C, (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr, 0, p0,
-                                       p1));
+  if (g_bn2_rows && (H * W) % 4 == 0 && CR * (H * W / 4) < (1LL << 30)) {   // flattened, batched loads
+    BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_fwd_stats_flat_k<XFV>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
+                                         s, x, N, C, (int)(H * W), CR, p0, p1));
+  } else {
+    BN2_XF_SWITCH(xf, hipLaunchKernelGGL((bn2d_reduce_k<0, 0, XFV>), dim3((unsigned)C, (unsigned)R), dim3(BN2_T), 0,
+                                         s, x, nullptr, N, C, (int)H, (int)W, CR, nullptr, nullptr, nullptr, nullptr,
+                                         0, p0, p1));
+  }
   hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, N, C, R,
                      momentum, eps, running_mean, running_var, save_mean, save_invstd, nullptr, CR, H * W);
   const int64_t outs = pool ? N * C * (H / 2) * (W / 2) : N * C * H * W / 4;

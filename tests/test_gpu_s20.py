@@ -168,3 +168,21 @@ def test_mlp_step_with_s20_equals_fp32(F):
     assert la == lb
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_compact_bias_is_guarded_not_copied(F):
+    """The compact carriers hold the producing layer's bias itself (no per-step snapshot copy): an
+    in-place update of it between forward and backward is refused by torch's saved-tensor check."""
+    from bnn_amd import nets
+    M, W = 4096, 1024
+    g = torch.Generator(device="cuda").manual_seed(8)
+    u = torch.randint(0, 256, (M, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    y = torch.randint(0, 10, (M,), generator=g, device="cuda")
+    m = nets.MLP(W, W, W, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+    n0 = F.S20_HANDOFFS
+    loss = torch.nn.CrossEntropyLoss()(m(u), y)
+    assert F.S20_HANDOFFS - n0 == 1
+    with torch.no_grad():
+        m.fc1.bias.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()
