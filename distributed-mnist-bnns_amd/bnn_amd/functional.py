@@ -954,7 +954,7 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
         dw = db = None
         if M == 0:
             return (None, torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
-                    torch.zeros((N,), dtype=torch.float32, device=dev) if need_db else None, None, None, None)
+                    torch.zeros((N,), dtype=torch.float32, device=dev) if need_db else None, None, None, None, None)
         pre = _i8c_take(dy)          # the digits straight from the BatchNorm backward, if it made them
         if pre is None:
             dy = _c2d(dy)
