@@ -932,7 +932,10 @@ class BinaryLinearPixelsFunction(torch.autograd.Function):
         bvec = bias.detach() if bias is not None else None
         stats_ok = (PIX_STATS and need_dw and K <= q.shape[1]
                     and L.lib().bnn_gemm_i8_bnstats_ok(M, N, q.shape[1], q.shape[1], wq.shape[1]))
+        # (small grids keep the fp32 z1: the s20 apply-pack is the 256x256-tile kernel, slower than
+        # the small-batch pass below Z16_MIN_TILES tiles -- config 3: 37.7 vs 20 us)
         if (stats_ok and emit_s20 and S20 and I8C_HANDOFF and N % 256 == 0
+                and (N // 256) * ((M + 255) // 256) >= Z16_MIN_TILES
                 and L.lib().bnn_gemm_i8_s20_ok(M, N, q.shape[1], K, float(s0))):
             y = _pixels_fwd_s20(q, wq, M, N, K, a, bvec, R, s0)
         elif stats_ok:

@@ -134,7 +134,7 @@ def test_mlp_step_with_s20_equals_fp32(F):
     from bnn_amd import nets
     from bnn_amd.nets import binary_params
     from bnn_amd.optim import LatentAdam
-    M, W = 8192, 2048
+    M, W = 16384, 2048            # >= Z16_MIN_TILES 256x256 tiles: the hand-off fires
     g = torch.Generator(device="cuda").manual_seed(5)
     u = torch.randint(0, 256, (M, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
     y = torch.randint(0, 10, (M,), generator=g, device="cuda")
@@ -174,7 +174,7 @@ def test_compact_bias_is_guarded_not_copied(F):
     """The compact carriers hold the producing layer's bias itself (no per-step snapshot copy): an
     in-place update of it between forward and backward is refused by torch's saved-tensor check."""
     from bnn_amd import nets
-    M, W = 4096, 1024
+    M, W = 16384, 2048
     g = torch.Generator(device="cuda").manual_seed(8)
     u = torch.randint(0, 256, (M, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
     y = torch.randint(0, 10, (M,), generator=g, device="cuda")
