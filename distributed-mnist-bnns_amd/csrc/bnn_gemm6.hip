@@ -349,6 +349,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
     if (wave == 0)   // a whole 1-KiB piece (512 rows): the scale array has 512 rows of tail padding
       glds16_6(sc_base + (int64_t)kt * p.asc_rows * 2 + lane * 16, base + LO_ST + HI_ST);
   };
+  // piece i (compile-time after unrolling) of stage(kt, buf): lo, hi, B, then wave 0's scale piece
+  constexpr int NPIECE = P_LO + P_HI + P_B + 1;
+  auto stage_piece = [&](int kt, int buf, int i) __attribute__((always_inline)) {
+    char* base = smem + buf * ST;
+    if (i < P_LO) {
+      glds16_6s(lo_base + (int64_t)kt * 128, off_lo[i], base + (wave + i * NW) * 1024);
+    } else if (i < P_LO + P_HI) {
+      const int ii = i - P_LO;
+      glds16_6s(hi_base + (int64_t)kt * 64, off_hi[ii], base + LO_ST + (wave + ii * NW) * 1024);
+    } else if (i < P_LO + P_HI + P_B) {
+      const int ii = i - P_LO - P_HI;
+      glds16_6s(b_base + (int64_t)kt * b_step, off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
+    } else if (wave == 0) {   // asm form: the compiler must not order LDS reads behind it
+      glds16_6s(sc_base + (int64_t)kt * p.asc_rows * 2, (uint32_t)lane * 16u, base + LO_ST + HI_ST);
+    }
+  };
 
   v16f acc[WM][WN];
 #pragma unroll
@@ -586,6 +602,80 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       if (kt + 1 < nk) BNN_FP6_STEP(kt + 1, b1, f1, b0, f0)
     }
 #undef BNN_FP6_STEP
+  } else if constexpr (PP == 4) {
+    // Interleaved form (2 stages): after the barrier each wave reads ALL of this step's fragments
+    // (B, A tile 0, A tile 1) at once -- tile 1's arrive while tile 0's MFMAs run -- and issues the
+    // next stage's LDS-DMA pieces one at a time between its MFMA column groups (4 MFMAs each), so
+    // neither the reads nor the DMA issue sit between the barrier and the first MFMA of the step
+    // (the plain loop issues every piece, then the reads, then waits for them all).
+    static_assert((STAGES == 2 || STAGES == 3) && WM == 2 && DIAG == 0 && NPIECE <= 9,
+                  "interleaved form: 2 or 3 stages, 2 tile rows");
+    // a tile's fragment as loaded: the 4 planes' lo chunks, the 2 hi chunks, the scale byte
+    v4i al[2][4], ah[2][2];
+    int asb[2];
+    auto read_raw = [&](const char* base, int t) __attribute__((always_inline)) {
+      const int lrow = wm * WM * 32 + t * 32 + r;
+      const char* sLo = base + lrow * 128;
+      const char* sHi = base + LO_ST + lrow * 64;
+      const int sw = (lrow >> 1) & 7, sh = (lrow >> 2) & 3;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) al[t][q] = *reinterpret_cast<const v4i*>(sLo + 16 * ((h * 4 + q) ^ sw));
+#pragma unroll
+      for (int q = 0; q < 2; ++q) ah[t][q] = *reinterpret_cast<const v4i*>(sHi + 16 * ((h * 2 + q) ^ sh));
+    };
+    // both tiles' scale bytes: read first, so the scale arithmetic the compiler places early waits
+    // only for them, not for the operand reads behind them
+    auto read_sb = [&](const char* base) __attribute__((always_inline)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        asb[t] = reinterpret_cast<const uint8_t*>(base + LO_ST + HI_ST)[(wm * WM * 32 + t * 32 + r) * 2 + h];
+    };
+    // STAGES - 1 stages ahead; every step issues one stage (near the end a re-load of the last one
+    // into a slot nobody reads): no branch between the MFMA groups -- a conditional piece let the
+    // compiler sink every MFMA below it -- and a constant count of pieces in flight
+    if (nk > 0) {
+      stage(0, 0);
+      if constexpr (STAGES == 3) stage(min(1, nk - 1), 1);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      if constexpr (STAGES == 3) {   // stage kt landed; stage kt + 1 may still be in flight
+        if (mine == PER_WAVE) wait_vmcnt6<PER_WAVE>(); else wait_vmcnt6<PER_WAVE - 1>();
+      } else {
+        wait_vmcnt6<0>();
+      }
+      barrier6();
+      const char* base = smem + (kt % STAGES) * ST;
+      const int kn = min(kt + STAGES - 1, nk - 1);
+      const int nb = (kt + STAGES - 1) % STAGES;
+      if (wave == 0) stage_piece(kn, nb, NPIECE - 1);   // the scale piece (a branch: before the block)
+      v4i bf[WN];
+      read_sb(base);
+      __builtin_amdgcn_sched_barrier(0);
+      read_b(base, bf);
+      read_raw(base, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_raw(base, 1);
+      // group g = one plane of one tile against the WN columns (independent accumulators)
+      auto mma_plane = [&](int t, int j, v16f (&ac)[WN]) __attribute__((always_inline)) {
+        const v4i l = al[t][j], hh = ah[t][j >> 1];
+        const v8i a = (j & 1) ? v8i{l.x, l.y, l.z, l.w, hh.z, hh.w, 0, 0} : v8i{l.x, l.y, l.z, l.w, hh.x, hh.y, 0, 0};
+        const int sj = asb[t] == 255 ? 255 : asb[t] + 5 * j;
+#pragma unroll
+        for (int u = 0; u < WN; ++u) {
+          const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+          ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, ac[u], 2, 4, 0, sj, 0, 127);
+        }
+      };
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {           // tile g / 4, plane 3 - g % 4 (mma_tile's order)
+        __builtin_amdgcn_sched_barrier(0);
+        if (g < 4) mma_plane(0, 3 - g, acc[0]);
+        else mma_plane(1, 7 - g, acc[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g < NPIECE - 1) stage_piece(kn, nb, g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   } else if constexpr (DIAG == 3 || DIAG == 4) {
     // timing-only: fragments read once from stage 0 and reused by every k-step -- the MFMA
     // stream alone (3: with the per-k-step barrier, 4: without)
@@ -859,6 +949,10 @@ const Variant6 kVariants6[] = {
     // (equal to variant 7 within 1% on the wide shapes: the MFMA-busy fraction stays ~0.6 --
     // profiles/r02_fp6_pingpong.txt)
     {16, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 3>", launch6<2, 4, 2, 4, 3, 0, 2, 3>, 128, 512},
+    // interleaved form: all fragment reads right after the barrier, the next stage's DMA pieces
+    // spread between the MFMA column groups
+    {17, "gemm_fp6_k<2, 4, 2, 4, 2, 0, 2, 4>", launch6<2, 4, 2, 4, 2, 0, 2, 4>, 128, 512},
+    {18, "gemm_fp6_k<2, 4, 2, 4, 3, 0, 2, 4>", launch6<2, 4, 2, 4, 3, 0, 2, 4>, 128, 512},
     // timing-only diagnostics of variant 5 (wrong results; never picked by default)
     {91, "diag: v5 without global->LDS staging", launch6<2, 4, 2, 4, 3, 1>, 128, 512},
     {92, "diag: v5 without LDS fragment reads", launch6<2, 4, 2, 4, 3, 2>, 128, 512},

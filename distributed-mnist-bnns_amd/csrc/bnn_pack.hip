@@ -901,11 +901,15 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
   return check_launch("bnn_sign_pack_fp4");
 }
 
-// tuning hook (bnn_adam_pack_set_tile256): 0 forces the 64 x 64 tile kernel (A/B timing)
+// tuning hook (bnn_adam_pack_set_tile256): 1 (default) = the 256 x 256-tile kernel for grids of at
+// least ADAM_T256_MIN_TILES whole tiles (the wide step's 8192 x 8192 weights: 1024), the 64 x 64
+// kernel below, whose 16x finer grid keeps every CU busy on small weights (a 2048 x 2048 weight is
+// 64 big tiles for 256 CUs); 2 = the big tile whenever the shape allows it (tests); 0 = never
 static int ADAM_TILE256 = 1;
+constexpr int64_t ADAM_T256_MIN_TILES = 512;
 
 BNN_API int bnn_adam_pack_set_tile256(int32_t on) {
-  ADAM_TILE256 = on != 0;
+  ADAM_TILE256 = on < 0 ? 0 : (on > 2 ? 2 : on);
   return 0;
 }
 
@@ -938,7 +942,8 @@ static int adam_clamp_pack_impl(float* p, const AdamArgs& a, int64_t N, int64_t 
   }
   const int vec = aligned16(p) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq) && (K % 4 == 0);
   if (fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && vec && N % AP_T == 0 && K % AP_T == 0 &&
-      2 * ldq == K && 2 * ldqt == N && ADAM_TILE256) {
+      2 * ldq == K && 2 * ldqt == N &&
+      (ADAM_TILE256 == 2 || (ADAM_TILE256 == 1 && (K / AP_T) * (N / AP_T) >= ADAM_T256_MIN_TILES))) {
     // whole 256 x 256 tiles, no padding: the 1-KiB-run form
     hipLaunchKernelGGL(adam_pack_fp4_k, dim3((unsigned)(K / AP_T), (unsigned)(N / AP_T)), dim3(256), 0, S(stream), p,
                        a, N, K, reinterpret_cast<uint8_t*>(q), ldq, reinterpret_cast<uint8_t*>(qt), ldqt,

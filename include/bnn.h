@@ -599,7 +599,8 @@ int bnn_hardtanh_bwd(const float* x, const float* g, float* out, int64_t n, bnn_
  * p <- Adam(p, grad*grad_scale) with torch's bias-corrected formula, then, if clamp != 0,
  * p <- clamp(p, -1, 1).  step = 1-based Adam step count after this update. */
 /* Tuning hook: 0 makes bnn_adam_clamp_pack use its 64 x 64-tile kernel even for whole 256 x 256
- * tiles (A/B timing and the equality test); 1 (default) the 1-KiB-run form. */
+ * tiles (A/B timing and the equality test); 1 (default) the 1-KiB-run form for grids of >= 512 whole
+ * tiles; 2 the 1-KiB-run form at every whole-tile shape. */
 int bnn_adam_pack_set_tile256(int32_t on);
 int bnn_adam_clamp(float* p, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale,

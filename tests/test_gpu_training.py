@@ -316,7 +316,7 @@ def test_adam_pack_tile256_equals_tile64(nets, N, K, qt_fmt):
     v0 = torch.rand_like(p0) * 0.01
     outs = []
     try:
-        for tile256 in (1, 0):
+        for tile256 in (2, 0):                # 2: the big tile at any whole-tile shape
             L.call("bnn_adam_pack_set_tile256", tile256)
             b = [p0.clone(), m0.clone(), v0.clone()]
             q = torch.full((N, K // 2), 0x77, dtype=torch.uint8, device="cuda")
