@@ -675,6 +675,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     }
   };
   load_sub(mbase);
+  // the digit records of sub-tile s are stored one phase late -- after sub-tile s+1's dz phase, just
+  // before its loads for s+2 are issued -- so they drain while s+1 is quantised: the vector-memory
+  // counter retires in issue order, and loads issued behind a sub-tile's stores had to wait for those
+  // stores first (the records stored at once cost 0.4-0.7 ms per wide-step pass: timing-only builds
+  // without stores, profiles/r04_q6_diag.log)
+  int64_t m_prev = -1;
   for (int sub = 0; sub < rows_wg / Q6T_SUB; ++sub) {
     const int64_t m0 = mbase + sub * Q6T_SUB;
     if (m0 >= mp) break;                       // block-uniform
@@ -734,6 +740,10 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       atomicMax(&cmax[i >> 1][cq + 3], a3b);
     }
     __syncthreads();
+    // whole-line stores of the PREVIOUS sub-tile: per row (column) its two adjacent blocks' records
+    // are 128 (lo) + 64 (hi) contiguous bytes, its two scale bytes adjacent to the next row's
+    if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
+    __syncthreads();                           // the staged records are read before they are rewritten
     load_sub(m0 + Q6T_SUB);
     // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
     const int b = wave & 1;
@@ -754,11 +764,9 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       }
     }
     __syncthreads();
-    // whole-line stores: per row (column) of the sub-tile its two adjacent blocks' records are 128
-    // (lo) + 64 (hi) contiguous bytes, its two scale bytes adjacent to the next row's
-    q6_stage_store(st, o, t, m0, M, c0, nblk_c);
-    __syncthreads();
+    m_prev = m0;
   }
+  if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
   if (o.part != nullptr) {
     // fixed-order fold of the two column waves' sums: deterministic
     __shared__ double cs[Q6T_COLS];
