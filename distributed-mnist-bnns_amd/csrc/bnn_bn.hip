@@ -760,7 +760,11 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
         // column block (column c0 + lane, rows m0 + 32 b ..): rows beyond M are zeros; its
         // elements are added to the column sum in row order while they are quantised
         Q6StageSink sink{st.clo[lane], st.chi[lane], &st.csc[lane][b], lane, b};
+#ifdef Q6_DIAG_NOCSUM     // timing-only build: the column sums not formed
+        q6_block_pre<Q6T_LD, false>(tile + QB * b * Q6T_LD + lane, am, sink, csum);
+#else
         q6_block_pre<Q6T_LD, true>(tile + QB * b * Q6T_LD + lane, am, sink, csum);
+#endif
       }
     }
     __syncthreads();
