@@ -284,7 +284,8 @@ def main():
     opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model), device_step=dstep)
     as_u8 = args.config != "cnn" and not args.fp32_input
     x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev, as_u8=as_u8)
-    crit = torch.nn.CrossEntropyLoss()
+    from bnn_amd.nn import CrossEntropyLoss
+    crit = CrossEntropyLoss()     # nn.CrossEntropyLoss() on libbnn (mnist-dist2.py's criterion)
 
     def step():
         if exchange is not None:

@@ -1038,6 +1038,50 @@ def linear_nsmall(x, weight, bias=None):
     return LinearNSmallFunction.apply(x, weight, bias)
 
 
+# ----------------------------------------------------------------------------- loss
+class CrossEntropyFunction(torch.autograd.Function):
+    """torch.nn.CrossEntropyLoss() (reduction 'mean') on [M, C] fp32 rows with int64 targets
+    (bnn_cross_entropy_*): the training loop's criterion applied to the nets' LogSoftmax output
+    (mnist-dist2.py:118-137).  Two launches forward (row losses, fixed-order fold), one backward;
+    the loss and its incoming gradient stay on the device (no host synchronisation)."""
+
+    @staticmethod
+    def forward(ctx, p, target):
+        _check(p)
+        p = p.contiguous()
+        target = target.contiguous()
+        M, C = p.shape
+        loss = torch.empty((), dtype=torch.float32, device=p.device)
+        work = torch.empty((int(L.lib().bnn_cross_entropy_workspace(M)),), dtype=torch.uint8, device=p.device)
+        with _timed("cross_entropy_fwd", 0, 4 * M * C + 8 * M):
+            L.call("bnn_cross_entropy_fwd", L.ptr(p), L.ptr(target), M, C, L.ptr(loss), L.ptr(work), work.numel(),
+                   L.stream())
+        ctx.save_for_backward(p, target, work)
+        return loss
+
+    @staticmethod
+    def backward(ctx, go):
+        p, target, work = ctx.saved_tensors
+        M, C = p.shape
+        dp = torch.empty_like(p)
+        go = go.to(torch.float32).contiguous()
+        with _timed("cross_entropy_bwd", 0, 8 * M * C + 8 * M):
+            L.call("bnn_cross_entropy_bwd", L.ptr(p), L.ptr(target), M, C, L.ptr(go), L.ptr(work), L.ptr(dp),
+                   L.stream())
+        return dp, None
+
+
+def cross_entropy_ok(p, target):
+    return (p.is_cuda and p.dim() == 2 and p.dtype == torch.float32 and p.shape[0] > 0
+            and bool(L.lib().bnn_cross_entropy_ok(p.shape[1])) and target.dim() == 1
+            and target.dtype == torch.int64 and target.shape[0] == p.shape[0] and target.device == p.device)
+
+
+def cross_entropy(p, target):
+    """Mean cross-entropy of the rows of p against target (torch.nn.CrossEntropyLoss() semantics)."""
+    return CrossEntropyFunction.apply(p, target)
+
+
 # ----------------------------------------------------------------------------- conv2d
 def _pair_same(v, what):
     if isinstance(v, (tuple, list)):

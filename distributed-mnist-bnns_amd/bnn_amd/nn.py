@@ -10,6 +10,8 @@ Names, constructor signatures and side effects follow the reference:
 * ``BinarizeLinear(*kargs, **kwargs)`` (an ``nn.Linear``)   -- :68-85
 * ``BinarizeConv2d(*kargs, **kwargs)`` (an ``nn.Conv2d``)   -- :87-107
 
+and the training loop's criterion, ``CrossEntropyLoss`` (mnist-dist2.py:118-137), on libbnn.
+
 Side effects kept (the caller loop of mnist-dist2.py:131-137 depends on them):
   ``weight.org`` is created once on the first forward from ``weight.data`` (:77-78),
   ``weight.data`` is replaced by ``sign(weight.org)`` every forward (:79),
@@ -32,7 +34,7 @@ import torch.nn as nn
 from . import functional as BF
 
 __all__ = ["Binarize", "HingeLoss", "SqrtHingeLossFunction", "Quantize", "BinarizeLinear",
-           "BinarizeConv2d"]
+           "BinarizeConv2d", "CrossEntropyLoss"]
 
 
 def Binarize(tensor, quant_mode="det"):
@@ -59,6 +61,20 @@ class HingeLoss(nn.Module):
 
     def forward(self, input, target):
         return self.hinge_loss(input, target)
+
+
+class CrossEntropyLoss(nn.CrossEntropyLoss):
+    """The training loop's criterion (mnist-dist2.py:118-137: ``nn.CrossEntropyLoss()`` on the nets'
+    LogSoftmax output) on libbnn (functional.cross_entropy: one row-loss + one fold launch forward,
+    one backward, no host synchronisation) for CUDA fp32 [M, C] rows with C in {2, 10, 16, 32, 64},
+    int64 targets and the default arguments; anything else goes to torch.  Targets must lie in
+    [0, C): an ignore_index (-100) target makes the libbnn loss NaN instead of being skipped."""
+
+    def forward(self, input, target):
+        if (self.weight is None and self.reduction == "mean" and self.label_smoothing == 0.0
+                and BF.cross_entropy_ok(input, target)):
+            return BF.cross_entropy(input, target)
+        return super().forward(input, target)
 
 
 class SqrtHingeLossFunction(torch.autograd.Function):
