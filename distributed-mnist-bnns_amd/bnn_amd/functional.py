@@ -528,7 +528,11 @@ def _fp6_buffers(rows, Kp, device):
     nb = Kp // 32
     lo = torch.empty((rows, nb * 64), dtype=torch.uint8, device=device)
     hi = torch.empty((rows, nb * 32), dtype=torch.uint8, device=device)
-    sc = torch.zeros((Kp // 64, L.lib().bnn_quant6_scale_rows(rows), 2), dtype=torch.uint8, device=device)
+    # every producer writes the scale bytes of all `rows` rows; the slab's padding rows are read only
+    # by the GEMM's 512-row scale pieces and scale only accumulator rows >= rows, which are never
+    # stored or reduced (gemm_fp6_k clamps its digit rows, the split-K fold and the statistics
+    # epilogue stop at M): left unwritten (a zero fill cost ~5-7 us per operand on the wide step)
+    sc = torch.empty((Kp // 64, L.lib().bnn_quant6_scale_rows(rows), 2), dtype=torch.uint8, device=device)
     return lo, hi, sc
 
 
