@@ -1710,11 +1710,38 @@ def dropout_batch_norm_hardtanh(x, p, bn, seed=None):
     return DropoutBatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, factor, bn.eps, float(p), seed)
 
 
+_BN_DEFER = None   # while a bn_counter_batch is open: the num_batches_tracked buffers to increment
+
+
+class bn_counter_batch:
+    """Inside it, the fused BatchNorm ops defer torch's per-module ``num_batches_tracked += 1``
+    (_BatchNorm.forward) and issue all of them as one multi-tensor launch on exit -- the nets'
+    forward opens one (one launch instead of one per BatchNorm).  Modules with momentum=None
+    (the cumulative average reads the counter) still increment at once."""
+
+    def __enter__(self):
+        global _BN_DEFER
+        self._prev, _BN_DEFER = _BN_DEFER, []
+        return self
+
+    def __exit__(self, *exc):
+        global _BN_DEFER
+        todo, _BN_DEFER = _BN_DEFER, self._prev
+        if len(todo) == 1:
+            todo[0].add_(1)
+        elif todo:
+            torch._foreach_add_(todo, 1)
+        return False
+
+
 def _bn_module_args(bn):
     """torch _BatchNorm.forward bookkeeping: (running_mean, running_var, use_batch_stats, factor)."""
     factor = 0.0 if bn.momentum is None else bn.momentum
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+        if bn.momentum is not None and _BN_DEFER is not None:
+            _BN_DEFER.append(bn.num_batches_tracked)
+        else:
+            bn.num_batches_tracked.add_(1)
         if bn.momentum is None:               # cumulative moving average (host sync, rare)
             factor = 1.0 / float(bn.num_batches_tracked)
     bn_training = bn.training or (bn.running_mean is None and bn.running_var is None)

@@ -91,6 +91,10 @@ class MLP(nn.Module):
                 and not self.fc2.org_protocol and self.fc1.out_features % 256 == 0)
 
     def forward(self, x):
+        with BF.bn_counter_batch():          # the BatchNorms' num_batches_tracked += 1 in one launch
+            return self._forward(x)
+
+    def _forward(self, x):
         x = x.view(-1, 28 * 28)
         z1 = self.fc1(x, emit_compact=True) if self._s20(x) else self.fc1(x)
         M = z1.shape[0]
@@ -163,6 +167,10 @@ class BinCNN(nn.Module):
         return pool(ht(bn(z)))
 
     def forward(self, x):
+        with BF.bn_counter_batch():          # the BatchNorms' num_batches_tracked += 1 in one launch
+            return self._forward(x)
+
+    def _forward(self, x):
         out = self._layer(self.layer2, self._layer(self.layer1, x))
         out = out.reshape(out.size(0), -1)
         if self.fused_bn and BF.linear_nsmall_ok(out, self.fc.weight):
