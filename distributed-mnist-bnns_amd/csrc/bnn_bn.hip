@@ -998,11 +998,15 @@ __global__ __launch_bounds__(256, HRED_OCC) void bn_head_reduce_k(XIn xin, const
 
 // dW4[q][c] = sum over chunks of the partials: FF_COLS elements x FF_GROUPS chunk groups per
 // workgroup, groups folded in a fixed order (double, deterministic)
-__global__ __launch_bounds__(256) void head_dw_final_k(const float* __restrict__ pw, int64_t R, int64_t nq, int64_t C,
-                                                       float* __restrict__ dw4) {
-  __shared__ double sa[FF_GROUPS][FF_COLS];
-  const int lc = threadIdx.x & (FF_COLS - 1), grp = threadIdx.x / FF_COLS;
-  const int64_t e = (int64_t)blockIdx.x * FF_COLS + lc, ne = nq * C;
+// HD_FF_COLS fp32 partials per chunk row = one 128-B line (FF_COLS = 16 read half lines); each
+// element's sum order (chunks grp, grp + FF_GROUPS, ..., then the groups in order) is unchanged
+constexpr int HD_FF_COLS = 32;
+__global__ __launch_bounds__(HD_FF_COLS * FF_GROUPS) void head_dw_final_k(const float* __restrict__ pw, int64_t R,
+                                                                          int64_t nq, int64_t C,
+                                                                          float* __restrict__ dw4) {
+  __shared__ double sa[FF_GROUPS][HD_FF_COLS];
+  const int lc = threadIdx.x & (HD_FF_COLS - 1), grp = threadIdx.x / HD_FF_COLS;
+  const int64_t e = (int64_t)blockIdx.x * HD_FF_COLS + lc, ne = nq * C;
   double s = 0.0;
   if (e < ne)
 #pragma unroll 16
@@ -1878,7 +1882,8 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
     hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
                        save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
-  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + FF_COLS - 1) / FF_COLS)), dim3(256), 0, s, pw, R,
+  hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + HD_FF_COLS - 1) / HD_FF_COLS)),
+                     dim3(HD_FF_COLS * FF_GROUPS), 0, s, pw, R,
                      (int64_t)nout, C, dw4);
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
