@@ -498,6 +498,22 @@ constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4
 #ifndef Q6_HEAD_OCC
 #define Q6_HEAD_OCC 3          // waves per SIMD of the fused head's quantising backward (z16 input)
 #endif
+// Q6_DIAG_STAMPS (diagnostic build): wave 0 of each workgroup of the q6 passes records s_memtime
+// at its phase boundaries (per sub-tile: start, after the dz phase's barrier, after the record
+// stores + barrier, after the quantisation + barrier) into g_q6_stamps, a device buffer no output
+// reads; bnn_q6_stamps_copy hands them to the host (tools/q6_stamps.py).
+#if defined(Q6_DIAG_STAMPS)
+constexpr int Q6_ST_WG = 4096, Q6_ST_PH = 4, Q6_ST_SUB = 8;
+__device__ unsigned long long g_q6_stamps[2][Q6_ST_WG][Q6_ST_SUB][Q6_ST_PH];
+#define Q6_STAMP(sub, ph)                                                                                   \
+  do {                                                                                                     \
+    const unsigned wgid = blockIdx.y * gridDim.x + blockIdx.x;                                             \
+    if (threadIdx.x == 0 && wgid < Q6_ST_WG && (sub) < Q6_ST_SUB)                                          \
+      g_q6_stamps[NOUT > 0 ? 1 : 0][wgid][sub][ph] = __builtin_amdgcn_s_memtime();                         \
+  } while (0)
+#else
+#define Q6_STAMP(sub, ph) do { } while (0)
+#endif
 #if defined(Q6_DIAG_NOQUANT)
 constexpr bool Q6_DIAG_NOQUANT_ON = true;
 #else
@@ -684,6 +700,7 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   for (int sub = 0; sub < rows_wg / Q6T_SUB; ++sub) {
     const int64_t m0 = mbase + sub * Q6T_SUB;
     if (m0 >= mp) break;                       // block-uniform
+    Q6_STAMP(sub, 0);
     if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows
       for (int i = t; i < Q6T_SUB * D4LD; i += 256) {
         const int rr = i / D4LD, q = i - rr * D4LD;
@@ -740,10 +757,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       atomicMax(&cmax[i >> 1][cq + 3], a3b);
     }
     __syncthreads();
+    Q6_STAMP(sub, 1);
     // whole-line stores of the PREVIOUS sub-tile: per row (column) its two adjacent blocks' records
     // are 128 (lo) + 64 (hi) contiguous bytes, its two scale bytes adjacent to the next row's
     if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
     __syncthreads();                           // the staged records are read before they are rewritten
+    Q6_STAMP(sub, 2);
     load_sub(m0 + Q6T_SUB);
     // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
     const int b = wave & 1;
@@ -768,6 +787,7 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       }
     }
     __syncthreads();
+    Q6_STAMP(sub, 3);
     m_prev = m0;
   }
   if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
@@ -1748,6 +1768,14 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
     hipLaunchKernelGGL(q6_colsum_final_k, ffin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_bwd_q6");
 }
+
+#if defined(Q6_DIAG_STAMPS)
+BNN_API int bnn_q6_stamps_copy(void* dst, int64_t bytes) {
+  if (bytes < (int64_t)sizeof(g_q6_stamps)) return kErrInval;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_q6_stamps), sizeof(g_q6_stamps), 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : kErrInval;
+}
+#endif
 
 BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,

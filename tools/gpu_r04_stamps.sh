@@ -1,0 +1,5 @@
+# Round 4: q6 pass phase timing from the Q6_DIAG_STAMPS build (tools/q6_stamps.py).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out
+BNN_LIB=$R/ab/stamps/libbnn.so timeout -k 10 300 python tools/q6_stamps.py > gpurun_out/r04_q6_stamps.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/r04_q6_stamps.log | tail -20; exit $rc
