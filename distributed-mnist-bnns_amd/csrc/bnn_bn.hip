@@ -487,13 +487,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const float* __restrict__ 
 // The apply pass of the BatchNorm backward whose output dz is the upstream gradient dY of the
 // BinarizeLinear that produced z (mnist-dist2.py:66-71: fc -> bn -> htanh -> fc).  That layer's
 // backward multiplies dY twice on the FP6 MFMA (dX = dY.W_b, dW = dY^T.X_b, bnn_gemm6.hip), so
-// this pass writes, besides dz itself (optional), both FP6 digit forms of dz straight from
-// registers -- the rows (blocks of 32 columns) and the transpose (blocks of 32 rows, through an
-// LDS tile) -- and the per-256-row partial column sums of dz (the bias gradient): dz is never
-// re-read.  Bit-identical digits to bnn_quant6_rows / bnn_quant6_cols_t of the same dz.
-// Workgroup: 256 rows x 64 columns, walked as 4 sub-tiles of 64 rows; C % 64 == 0.  Per sub-tile
-// all 256 threads compute dz (float4 per thread and row) into an LDS tile, then waves 0-1 quantise
-// the 128 row blocks (one 32-element block per lane) and waves 2-3 the 128 column blocks.
+// this pass writes, besides dz itself (optional), both FP6 digit forms of dz from an LDS tile --
+// the rows (blocks of 32 columns) and the transpose (blocks of 32 rows) -- and the per-workgroup
+// partial column sums of dz (the bias gradient): dz is never re-read.  Bit-identical digits to
+// bnn_quant6_rows / bnn_quant6_cols_t of the same dz.
+// Workgroup: Q6T_ROWS (512, or 64 on small batches: q6_rows) rows x 64 columns, walked as sub-tiles
+// of 64 rows; C % 64 == 0.  Per sub-tile all 256 threads compute dz (float4 per thread and row)
+// into the LDS tile, then waves 0-1 quantise the 128 row blocks (one 32-element block per lane)
+// and waves 2-3 the 128 column blocks, their digit records staged in LDS for whole-line stores.
 constexpr int Q6T_ROWS = 512, Q6T_SUB = 64, Q6T_COLS = 64, Q6T_LD = Q6T_COLS + 4;
 #ifndef Q6_HEAD_OCC
 #define Q6_HEAD_OCC 3          // waves per SIMD of the fused head's quantising backward (z16 input)
@@ -558,7 +559,7 @@ struct Q6Out {
   int64_t rsc_rows;
   uint8_t *clo, *chi, *csc;        // dz^T: [C][Mp/32][64], [C][Mp/32][32], [Mp/64][csc_rows][2]
   int64_t csc_rows, nblk_m;        // nblk_m = Mp / 32
-  double* part;                    // [M/256 chunks][C] partial column sums, or null
+  double* part;                    // [workgroup rows of the grid][C] partial column sums, or null
 };
 
 // One sub-tile's digit records staged in LDS: rows (64 rows x 2 blocks of 32 columns) and columns
