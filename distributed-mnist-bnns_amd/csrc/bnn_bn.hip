@@ -820,7 +820,10 @@ constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
 template <int NOUT, bool Z16 = false>
-__global__ __launch_bounds__(256, Z16 ? 4 : 2) void bn_head_fwd_k(XIn xin, int64_t M, int64_t C,
+#ifndef HFWD_OCC
+#define HFWD_OCC 4             // waves per SIMD of the fused head's forward (z16 input)
+#endif
+__global__ __launch_bounds__(256, Z16 ? HFWD_OCC : 2) void bn_head_fwd_k(XIn xin, int64_t M, int64_t C,
                                                      const float* __restrict__ mean, const float* __restrict__ mean_lo,
                                                      const float* __restrict__ invstd, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, const float* __restrict__ w4,
