@@ -1,6 +1,6 @@
 # Round 4: the head's statistics pass (bn_head_reduce_k) at 2 columns per thread (-DHR_CW=2: 142
 # VGPRs, 3 waves per SIMD; c2o4 also forced to 4 waves) -- the head tests on c2, then kernel stats
-# of the bench step, O (HEAD: 4 columns per thread, 214 VGPRs, 2 waves) vs c2 vs c2o4.
+# of the bench step, O (HEAD: 4 columns per thread, 214 VGPRs, 2 waves) vs c2 vs c2o4. (The variant was a patch over HEAD, reverted after this run; its source is not in the tree.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
