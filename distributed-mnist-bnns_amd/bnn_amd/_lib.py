@@ -52,8 +52,8 @@ SIGNATURES = {
     "bnn_linear_nsmall_bwd": (I32, [P, P, P, I64, I64, I64, P, P, P, P, I64, P]),
     "bnn_cross_entropy_ok": (I32, [I64]),
     "bnn_cross_entropy_workspace": (I64, [I64]),
-    "bnn_cross_entropy_fwd": (I32, [P, P, I64, I64, P, P, I64, P]),
-    "bnn_cross_entropy_bwd": (I32, [P, P, I64, I64, P, P, P, P]),
+    "bnn_cross_entropy_fwd": (I32, [P, P, I64, I64, I64, P, P, I64, P]),
+    "bnn_cross_entropy_bwd": (I32, [P, P, I64, I64, I64, P, P, P, P]),
     "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),

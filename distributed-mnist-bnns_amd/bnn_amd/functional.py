@@ -341,7 +341,8 @@ def adam_clamp_pack_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.
             L.call("bnn_adam_clamp_pack", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), N, K,
                    float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale),
                    int(bool(clamp)), *tail)
-    ent["key"] = _pack_key(p)
+    _bump(p)
+    ent["key"] = _pack_key(p)           # the operands just written match the bumped version
     return True
 
 
@@ -1047,10 +1048,11 @@ class CrossEntropyFunction(torch.autograd.Function):
     """torch.nn.CrossEntropyLoss() (reduction 'mean') on [M, C] fp32 rows with int64 targets
     (bnn_cross_entropy_*): the training loop's criterion applied to the nets' LogSoftmax output
     (mnist-dist2.py:118-137).  Two launches forward (row losses, fixed-order fold), one backward;
-    the loss and its incoming gradient stay on the device (no host synchronisation)."""
+    the loss and its incoming gradient stay on the device (no host synchronisation).  Rows whose
+    target equals ``ignore_index`` are skipped as torch skips them."""
 
     @staticmethod
-    def forward(ctx, p, target):
+    def forward(ctx, p, target, ignore_index=-100):
         _check(p)
         p = p.contiguous()
         target = target.contiguous()
@@ -1058,9 +1060,10 @@ class CrossEntropyFunction(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=p.device)
         work = torch.empty((int(L.lib().bnn_cross_entropy_workspace(M)),), dtype=torch.uint8, device=p.device)
         with _timed("cross_entropy_fwd", 0, 4 * M * C + 8 * M):
-            L.call("bnn_cross_entropy_fwd", L.ptr(p), L.ptr(target), M, C, L.ptr(loss), L.ptr(work), work.numel(),
-                   L.stream())
+            L.call("bnn_cross_entropy_fwd", L.ptr(p), L.ptr(target), M, C, int(ignore_index), L.ptr(loss),
+                   L.ptr(work), work.numel(), L.stream())
         ctx.save_for_backward(p, target, work)
+        ctx.ignore_index = int(ignore_index)
         return loss
 
     @staticmethod
@@ -1070,9 +1073,9 @@ class CrossEntropyFunction(torch.autograd.Function):
         dp = torch.empty_like(p)
         go = go.to(torch.float32).contiguous()
         with _timed("cross_entropy_bwd", 0, 8 * M * C + 8 * M):
-            L.call("bnn_cross_entropy_bwd", L.ptr(p), L.ptr(target), M, C, L.ptr(go), L.ptr(work), L.ptr(dp),
-                   L.stream())
-        return dp, None
+            L.call("bnn_cross_entropy_bwd", L.ptr(p), L.ptr(target), M, C, ctx.ignore_index, L.ptr(go),
+                   L.ptr(work), L.ptr(dp), L.stream())
+        return dp, None, None
 
 
 def cross_entropy_ok(p, target):
@@ -1081,9 +1084,10 @@ def cross_entropy_ok(p, target):
             and target.dtype == torch.int64 and target.shape[0] == p.shape[0] and target.device == p.device)
 
 
-def cross_entropy(p, target):
-    """Mean cross-entropy of the rows of p against target (torch.nn.CrossEntropyLoss() semantics)."""
-    return CrossEntropyFunction.apply(p, target)
+def cross_entropy(p, target, ignore_index=-100):
+    """Mean cross-entropy of the rows of p against target (torch.nn.CrossEntropyLoss() semantics,
+    ignore_index included)."""
+    return CrossEntropyFunction.apply(p, target, int(ignore_index))
 
 
 # ----------------------------------------------------------------------------- conv2d
@@ -1117,8 +1121,15 @@ def _c1bn_take(dy):
 
 
 # BNN_CONV_C1F=1 / 0: the one-input-channel VALU filter-gradient kernel on / off (A/B timing);
-# unset: the library's default
+# unset: the library's default.  Applied once, before the first conv forward (the forward decides
+# whether conv1 takes the BatchNorm2d hand-off, whose kernel depends on the same switch).
 _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
+
+
+def _conv_env():
+    if _CONV_C1F[0] is not None:
+        L.call("bnn_conv_set_c1_filter", int(_CONV_C1F[0] != "0"))
+        _CONV_C1F[0] = None
 
 
 # Compact conv outputs (zq): a binary-input BinarizeConv2d computes exact integer sums I (|I| <=
@@ -1157,6 +1168,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
     def forward(ctx, x, weight, bias, binarize_input, stride, padding, dilation, groups, emit_compact=False):
         global ZQ_HANDOFFS
         _check(x, weight, bias)
+        _conv_env()
         x = _c2d(x)
         w = _c2d(weight.detach())
         N, C, H, W = x.shape
@@ -1215,6 +1227,12 @@ class BinaryConv2dFunction(torch.autograd.Function):
                     torch.zeros((Co,), dtype=torch.float32, device=x.device)
                     if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None, None, None)
         dx = dw = db = None
+        if bn is not None and not L.lib().bnn_conv2d_bwd_filter_bn_ok(N, C, H, W, Co, KH, KW, stride, padding,
+                                                                      dilation, groups):
+            # the fused kernel was switched off since the forward (bnn_conv_set_c1_filter /
+            # bnn_conv_set_mfma): form dy with the BatchNorm2d backward and take the regular path
+            dy = _bn2d_dy_of_handoff(bn, dy.shape)
+            bn = None
         macs = dy.numel() * (C // groups) * KH * KW
         if bn is not None:
             global C1BN_HANDOFFS
@@ -1243,15 +1261,27 @@ class BinaryConv2dFunction(torch.autograd.Function):
             ws = torch.empty((L.lib().bnn_conv2d_bwd_filter_workspace(N, C, Co, KH, KW, groups),),
                              dtype=torch.uint8, device=x.device)
             with _timed("conv2d_bwd_filter", 2 * macs, 4 * (dy.numel() + x.numel() + w.numel())):
-                if _CONV_C1F[0] is not None:
-                    L.call("bnn_conv_set_c1_filter", int(_CONV_C1F[0] != "0"))
-                    _CONV_C1F[0] = None
                 L.call("bnn_conv2d_bwd_filter", L.ptr(dy), L.ptr(x), int(binarize_input), L.ptr(dw),
                        L.ptr(db), L.ptr(ws), N, C, H, W, Co, KH, KW, stride, padding, dilation, groups,
                        L.stream())
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None, None, None
+
+
+def _bn2d_dy_of_handoff(bn, shape):
+    """The fp32 gradient of the conv output a conv1 / BatchNorm2d hand-off stands for: the pooled
+    BatchNorm2d(+Hardtanh) backward written out by bnn_bn2d_bwd_q (its dgamma / dbeta, already
+    delivered by the BatchNorm's own backward, go to scratch)."""
+    zq, zb, zf, dyp, mean, invstd, gw, gb, sg, sgx, inv_n, ht = bn
+    N, C, H, W = shape
+    dev = dyp.device
+    dz = torch.empty((N, C, H, W), dtype=torch.float32, device=dev)
+    scratch = torch.empty((2, C), dtype=torch.float32, device=dev)
+    ws = torch.empty((L.lib().bnn_bn2d_workspace(N, C),), dtype=torch.uint8, device=dev)
+    L.call("bnn_bn2d_bwd_q", L.ptr(zq), L.ptr(zb), zf, L.ptr(dyp), N, C, H, W, L.ptr(gw), L.ptr(gb), L.ptr(mean),
+           L.ptr(invstd), int(ht), 2, L.ptr(dz), L.ptr(scratch[0]), L.ptr(scratch[1]), L.ptr(ws), L.stream())
+    return dz
 
 
 def binary_conv2d(x, weight, bias=None, binarize_input=True, stride=1, padding=0, dilation=1, groups=1,
@@ -1272,6 +1302,13 @@ def hardtanh_backward(x, g):
     return out
 
 
+def _bump(p):
+    """A raw in-place write through the data pointer: bump the tensor's version as a torch in-place
+    op would, so a backward that saved it (the z16 / s20 / conv bias carriers) refuses to run on
+    the updated value instead of silently using it."""
+    torch.autograd.graph.increment_version(p)
+
+
 def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
                 grad_scale=1.0, clamp=True, sched=None, ctr=None):
     """In-place fused Adam (torch formula) + clamp to [-1, 1] on a latent weight."""
@@ -1280,6 +1317,7 @@ def adam_clamp_(p, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, 
     for t in (p, grad, exp_avg, exp_avg_sq):
         if not t.is_contiguous():
             raise ValueError("adam_clamp_: tensors must be contiguous")
+    _bump(p)
     if sched is not None:
         L.call("bnn_adam_clamp_sched", L.ptr(p), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), p.numel(),
                float(beta1), float(beta2), float(eps), L.ptr(sched), L.ptr(ctr), float(grad_scale),
@@ -1305,6 +1343,7 @@ def adam_clamp_multi_(items, lr, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.
             for t in (p, g, m, v):
                 if not t.is_contiguous():
                     raise ValueError("adam_clamp_multi_: tensors must be contiguous")
+            _bump(p)
         k = len(chunk)
         arr = [(ctypes.c_void_p * k)(*[it[j].data_ptr() for it in chunk]) for j in range(4)]
         nn_ = (ctypes.c_int64 * k)(*[it[0].numel() for it in chunk])
@@ -1320,9 +1359,15 @@ def _bn_ws(M, C, device):
     return torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device=device)
 
 
+STATS_TAP = None   # tests: a list that receives the [3, C] (save_mean, save_invstd, save_mean_lo) of
+                   # every training-mode BatchNorm1d forward, in call order
+
+
 def _bn_stat_buffers(C, device):
     """save_mean, save_invstd, save_mean_lo of a training-mode BatchNorm forward (bnn.h)."""
     st = torch.empty((3, C), dtype=torch.float32, device=device)
+    if STATS_TAP is not None:
+        STATS_TAP.append(st)
     return st[0], st[1], st[2]
 
 

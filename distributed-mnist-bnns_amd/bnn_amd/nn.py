@@ -67,13 +67,14 @@ class CrossEntropyLoss(nn.CrossEntropyLoss):
     """The training loop's criterion (mnist-dist2.py:118-137: ``nn.CrossEntropyLoss()`` on the nets'
     LogSoftmax output) on libbnn (functional.cross_entropy: one row-loss + one fold launch forward,
     one backward, no host synchronisation) for CUDA fp32 [M, C] rows with C in {2, 10, 16, 32, 64},
-    int64 targets and the default arguments; anything else goes to torch.  Targets must lie in
-    [0, C): an ignore_index (-100) target makes the libbnn loss NaN instead of being skipped."""
+    int64 class-index targets, no class weights, reduction 'mean' and no label smoothing; anything
+    else goes to torch.  Rows whose target is ``ignore_index`` are skipped on the device as torch
+    skips them (the mean is over the other rows)."""
 
     def forward(self, input, target):
         if (self.weight is None and self.reduction == "mean" and self.label_smoothing == 0.0
                 and BF.cross_entropy_ok(input, target)):
-            return BF.cross_entropy(input, target)
+            return BF.cross_entropy(input, target, self.ignore_index)
         return super().forward(input, target)
 
 

@@ -3,8 +3,12 @@
 // criterion = nn.CrossEntropyLoss(), mnist-dist2.py:118-137), forward and backward, for the narrow
 // class dimension of the MNIST heads (C <= 64, here 10).
 //
-//   fwd: lse_i = max_i + log(sum_j exp(p_ij - max_i)),  l_i = lse_i - p[i][y_i],  loss = sum_i l_i / M
-//   bwd: dp[i][j] = go / M * (exp(p_ij - lse_i) - [j == y_i])
+//   fwd: lse_i = max_i + log(sum_j exp(p_ij - max_i)),  l_i = lse_i - p[i][y_i],  loss = sum_i l_i / n
+//   bwd: dp[i][j] = go / n * (exp(p_ij - lse_i) - [j == y_i])
+//
+// with torch's ignore_index: a row whose target equals it contributes neither a loss term nor a
+// gradient (dp row = 0), and n = the number of the other rows (all rows ignored: loss NaN, as
+// torch's 0 / 0).  n is formed on the device and kept in the workspace for the backward.
 //
 // torch runs this as log_softmax + nll_loss (+ their two backward kernels and a zero fill); the
 // nll_loss forward reduction is a single workgroup (63 us at M = 65536).  Here: one thread per row,
@@ -33,52 +37,86 @@ __device__ __forceinline__ float row_lse(const float* __restrict__ pr, float (&v
   return mx + logf(s);
 }
 
+// one row's loss term and count (0, 0 for an ignored row)
+template <int C>
+__device__ __forceinline__ void row_loss(const float* __restrict__ p, const int64_t* __restrict__ y, int64_t i,
+                                         int64_t ignore, float* __restrict__ lse, double& l, int& n) {
+  float v[C];
+  const float ls = row_lse<C>(p + i * C, v);
+  lse[i] = ls;
+  const int64_t yi = y[i];
+  if (yi == ignore) return;
+  float py = __builtin_nanf("");   // a target outside [0, C) makes the loss NaN
+#pragma unroll
+  for (int j = 0; j < C; ++j) py = (j == yi) ? v[j] : py;
+  l += (double)(ls - py);
+  n += 1;
+}
+
 template <int C>
 __global__ __launch_bounds__(CE_T) void ce_fwd_k(const float* __restrict__ p, const int64_t* __restrict__ y,
-                                                int64_t M, float* __restrict__ lse, double* __restrict__ part) {
+                                                int64_t M, int64_t ignore, float* __restrict__ lse,
+                                                double* __restrict__ part) {
   const int t = threadIdx.x;
   const int64_t i = (int64_t)blockIdx.x * CE_T + t;
   double l = 0.0;
-  if (i < M) {
-    float v[C];
-    const float ls = row_lse<C>(p + i * C, v);
-    lse[i] = ls;
-    const int64_t yi = y[i];
-    float py = __builtin_nanf("");   // a target outside [0, C) makes the loss NaN
-#pragma unroll
-    for (int j = 0; j < C; ++j) py = (j == yi) ? v[j] : py;
-    l = (double)(ls - py);
-  }
+  int n = 0;
+  if (i < M) row_loss<C>(p, y, i, ignore, lse, l, n);
   // block sum in row order: a fixed shuffle tree per wave, then the 4 waves in order
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) l += __shfl_xor(l, o, 64);
+  for (int o = 1; o < 64; o <<= 1) {
+    l += __shfl_xor(l, o, 64);
+    n += __shfl_xor(n, o, 64);
+  }
   __shared__ double ws[CE_T / 64];
-  if ((t & 63) == 0) ws[t >> 6] = l;
+  __shared__ int wn[CE_T / 64];
+  if ((t & 63) == 0) {
+    ws[t >> 6] = l;
+    wn[t >> 6] = n;
+  }
   __syncthreads();
   if (t == 0) {
     double s = 0.0;
+    int c = 0;
 #pragma unroll
-    for (int w = 0; w < CE_T / 64; ++w) s += ws[w];
-    part[blockIdx.x] = s;
+    for (int w = 0; w < CE_T / 64; ++w) {
+      s += ws[w];
+      c += wn[w];
+    }
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = (double)c;
   }
 }
 
-__global__ __launch_bounds__(CE_T) void ce_fold_k(const double* __restrict__ part, int64_t nb, int64_t M,
-                                                 float* __restrict__ loss) {
+__global__ __launch_bounds__(CE_T) void ce_fold_k(const double* __restrict__ part, int64_t nb, float* __restrict__ loss,
+                                                 float* __restrict__ cnt) {
   // one workgroup: thread t sums blocks t, t + 256, ... in order, then a fixed tree over threads
   const int t = threadIdx.x;
-  double s = 0.0;
-  for (int64_t b = t; b < nb; b += CE_T) s += part[b];
+  double s = 0.0, c = 0.0;
+  for (int64_t b = t; b < nb; b += CE_T) {
+    s += part[2 * b];
+    c += part[2 * b + 1];
+  }
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
-  __shared__ double ws[CE_T / 64];
-  if ((t & 63) == 0) ws[t >> 6] = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    s += __shfl_xor(s, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  __shared__ double ws[CE_T / 64], wc[CE_T / 64];
+  if ((t & 63) == 0) {
+    ws[t >> 6] = s;
+    wc[t >> 6] = c;
+  }
   __syncthreads();
   if (t == 0) {
-    double a = 0.0;
+    double a = 0.0, n = 0.0;
 #pragma unroll
-    for (int w = 0; w < CE_T / 64; ++w) a += ws[w];
-    loss[0] = (float)(a / (double)M);
+    for (int w = 0; w < CE_T / 64; ++w) {
+      a += ws[w];
+      n += wc[w];
+    }
+    loss[0] = (float)(a / n);
+    cnt[0] = (float)n;
   }
 }
 
@@ -89,45 +127,52 @@ constexpr int64_t CE_ONE_MAX = 16384;
 
 template <int C>
 __global__ __launch_bounds__(CE_T1) void ce_fwd1_k(const float* __restrict__ p, const int64_t* __restrict__ y,
-                                                  int64_t M, float* __restrict__ lse, float* __restrict__ loss) {
+                                                  int64_t M, int64_t ignore, float* __restrict__ lse,
+                                                  float* __restrict__ loss, float* __restrict__ cnt) {
   const int t = threadIdx.x;
   double l = 0.0;
-  for (int64_t i = t; i < M; i += CE_T1) {
-    float v[C];
-    const float ls = row_lse<C>(p + i * C, v);
-    lse[i] = ls;
-    const int64_t yi = y[i];
-    float py = __builtin_nanf("");
+  int n = 0;
+  for (int64_t i = t; i < M; i += CE_T1) row_loss<C>(p, y, i, ignore, lse, l, n);
 #pragma unroll
-    for (int j = 0; j < C; ++j) py = (j == yi) ? v[j] : py;
-    l += (double)(ls - py);
+  for (int o = 1; o < 64; o <<= 1) {
+    l += __shfl_xor(l, o, 64);
+    n += __shfl_xor(n, o, 64);
   }
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) l += __shfl_xor(l, o, 64);
   __shared__ double ws[CE_T1 / 64];
-  if ((t & 63) == 0) ws[t >> 6] = l;
+  __shared__ int wn[CE_T1 / 64];
+  if ((t & 63) == 0) {
+    ws[t >> 6] = l;
+    wn[t >> 6] = n;
+  }
   __syncthreads();
   if (t == 0) {
     double a = 0.0;
+    int c = 0;
 #pragma unroll
-    for (int w = 0; w < CE_T1 / 64; ++w) a += ws[w];
-    loss[0] = (float)(a / (double)M);
+    for (int w = 0; w < CE_T1 / 64; ++w) {
+      a += ws[w];
+      c += wn[w];
+    }
+    loss[0] = (float)(a / (double)c);
+    cnt[0] = (float)c;
   }
 }
 
 template <int C>
 __global__ __launch_bounds__(CE_T) void ce_bwd_k(const float* __restrict__ p, const int64_t* __restrict__ y,
-                                                const float* __restrict__ lse, const float* __restrict__ go,
-                                                int64_t M, float* __restrict__ dp) {
+                                                const float* __restrict__ lse, const float* __restrict__ cnt,
+                                                const float* __restrict__ go, int64_t M, int64_t ignore,
+                                                float* __restrict__ dp) {
   const int64_t i = (int64_t)blockIdx.x * CE_T + threadIdx.x;
   if (i >= M) return;
-  const float g = go[0] / (float)M;
+  const float g = go[0] / cnt[0];
   const float ls = lse[i];
   const int64_t yi = y[i];
   const float* pr = p + i * C;
   float* dr = dp + i * C;
+  const bool ign = yi == ignore;
 #pragma unroll
-  for (int j = 0; j < C; ++j) dr[j] = g * (expf(pr[j] - ls) - (j == yi ? 1.f : 0.f));
+  for (int j = 0; j < C; ++j) dr[j] = ign ? 0.f : g * (expf(pr[j] - ls) - (j == yi ? 1.f : 0.f));
 }
 
 }  // namespace
@@ -147,14 +192,16 @@ using namespace bnn;
 
 BNN_API int bnn_cross_entropy_ok(int64_t C) { return C == 2 || C == 10 || C == 16 || C == 32 || C == 64; }
 
+// workspace: lse per row (fp32), the kept-row count (fp32, 16 B), two doubles per 256-row block
+static int64_t ce_lse_bytes(int64_t M) { return (M * (int64_t)sizeof(float) + 15) / 16 * 16; }
+
 BNN_API int64_t bnn_cross_entropy_workspace(int64_t M) {
-  // lse per row (fp32) + one double per 256-row block
   if (M <= 0) return 0;
-  return (M * (int64_t)sizeof(float) + 15) / 16 * 16 + ((M + CE_T - 1) / CE_T) * (int64_t)sizeof(double);
+  return ce_lse_bytes(M) + 16 + ((M + CE_T - 1) / CE_T) * 2 * (int64_t)sizeof(double);
 }
 
-BNN_API int bnn_cross_entropy_fwd(const float* p, const int64_t* y, int64_t M, int64_t C, float* loss, void* work,
-                                  int64_t work_bytes, void* stream) {
+BNN_API int bnn_cross_entropy_fwd(const float* p, const int64_t* y, int64_t M, int64_t C, int64_t ignore_index,
+                                  float* loss, void* work, int64_t work_bytes, void* stream) {
   if (M <= 0 || !p || !y || !loss || !work || !bnn_cross_entropy_ok(C) ||
       work_bytes < bnn_cross_entropy_workspace(M)) {
     set_error("bnn_cross_entropy_fwd: bad arguments (M=%lld C=%lld work=%lld; M > 0, C in {2,10,16,32,64}, "
@@ -163,26 +210,30 @@ BNN_API int bnn_cross_entropy_fwd(const float* p, const int64_t* y, int64_t M, i
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* lse = reinterpret_cast<float*>(work);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + (M * (int64_t)sizeof(float) + 15) / 16 * 16);
+  float* cnt = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + ce_lse_bytes(M));
+  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(work) + ce_lse_bytes(M) + 16);
   const int64_t nb = (M + CE_T - 1) / CE_T;
   if (M <= CE_ONE_MAX) {
-    BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_fwd1_k<CV>), dim3(1), dim3(CE_T1), 0, s, p, y, M, lse, loss));
+    BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_fwd1_k<CV>), dim3(1), dim3(CE_T1), 0, s, p, y, M, ignore_index, lse,
+                                              loss, cnt));
     return check_launch("bnn_cross_entropy_fwd");
   }
-  BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_fwd_k<CV>), dim3((unsigned)nb), dim3(CE_T), 0, s, p, y, M, lse, part));
-  hipLaunchKernelGGL(ce_fold_k, dim3(1), dim3(CE_T), 0, s, part, nb, M, loss);
+  BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_fwd_k<CV>), dim3((unsigned)nb), dim3(CE_T), 0, s, p, y, M, ignore_index,
+                                            lse, part));
+  hipLaunchKernelGGL(ce_fold_k, dim3(1), dim3(CE_T), 0, s, part, nb, loss, cnt);
   return check_launch("bnn_cross_entropy_fwd");
 }
 
-BNN_API int bnn_cross_entropy_bwd(const float* p, const int64_t* y, int64_t M, int64_t C, const float* go,
-                                  const void* work, float* dp, void* stream) {
+BNN_API int bnn_cross_entropy_bwd(const float* p, const int64_t* y, int64_t M, int64_t C, int64_t ignore_index,
+                                  const float* go, const void* work, float* dp, void* stream) {
   if (M <= 0 || !p || !y || !go || !work || !dp || !bnn_cross_entropy_ok(C)) {
     set_error("bnn_cross_entropy_bwd: bad arguments (M=%lld C=%lld)", (long long)M, (long long)C);
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* lse = reinterpret_cast<const float*>(work);
+  const float* cnt = reinterpret_cast<const float*>(reinterpret_cast<const char*>(work) + ce_lse_bytes(M));
   BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_bwd_k<CV>), dim3((unsigned)((M + CE_T - 1) / CE_T)), dim3(CE_T), 0, s,
-                                            p, y, lse, go, M, dp));
+                                            p, y, lse, cnt, go, M, ignore_index, dp));
   return check_launch("bnn_cross_entropy_bwd");
 }

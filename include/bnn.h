@@ -594,16 +594,18 @@ int bnn_linear_nsmall_bwd(const float* x, const float* w, const float* dy, int64
 /* The training step's loss (replaces criterion = nn.CrossEntropyLoss() on the nets' LogSoftmax
  * output, mnist-dist2.py:118-137): p [M][C] fp32 rows (C in {2, 10, 16, 32, 64}: the MNIST heads),
  * y [M] int64 targets.  fwd writes the mean loss to loss[0] (device) and keeps each row's
- * log-sum-exp in work (bnn_cross_entropy_workspace(M) bytes) for bwd, which writes
- * dp = go[0] / M * (softmax(p) - onehot(y)) with go read on the device.  fp32 row arithmetic as
- * torch's log_softmax; the row losses summed in double in a fixed order (deterministic); a target
- * outside [0, C) makes the loss NaN. */
+ * log-sum-exp and the kept-row count n in work (bnn_cross_entropy_workspace(M) bytes) for bwd,
+ * which writes dp = go[0] / n * (softmax(p) - onehot(y)) with go read on the device.  Rows whose
+ * target equals ignore_index (torch's default -100) are skipped as torch skips them: no loss term,
+ * a zero gradient row, n counts the others (all ignored: loss NaN, gradient 0).  fp32 row
+ * arithmetic as torch's log_softmax; the row losses summed in double in a fixed order
+ * (deterministic); any other target outside [0, C) makes the loss NaN. */
 int bnn_cross_entropy_ok(int64_t C);
 int64_t bnn_cross_entropy_workspace(int64_t M);
-int bnn_cross_entropy_fwd(const float* p, const int64_t* y, int64_t M, int64_t C, float* loss, void* work,
-                          int64_t work_bytes, bnn_stream_t stream);
-int bnn_cross_entropy_bwd(const float* p, const int64_t* y, int64_t M, int64_t C, const float* go, const void* work,
-                          float* dp, bnn_stream_t stream);
+int bnn_cross_entropy_fwd(const float* p, const int64_t* y, int64_t M, int64_t C, int64_t ignore_index, float* loss,
+                          void* work, int64_t work_bytes, bnn_stream_t stream);
+int bnn_cross_entropy_bwd(const float* p, const int64_t* y, int64_t M, int64_t C, int64_t ignore_index,
+                          const float* go, const void* work, float* dp, bnn_stream_t stream);
 
 /* ---------------------------------------------------------------- (3) STE backward helpers
  * Hardtanh backward: g_out = g_in * (-1 < x < 1) (strict), as nn.Hardtanh (mnist-dist2.py:51). */

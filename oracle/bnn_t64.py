@@ -49,12 +49,20 @@ def rel_err(a, b):
 TAU = 2.0 ** -20
 
 
-def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5, boundary=None):
+def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5, boundary=None, impl_y=None,
+                    anchored=None):
     """nn.BatchNorm1d / 2d in training mode followed by nn.Hardtanh (mnist-dist2.py:52-53): batch
     statistics over ``dims`` (biased variance normalises, the unbiased one feeds the running
     estimate).  Returns (hardtanh output, cache, new running mean, new running var); z is
     consumed (overwritten by x_hat).  ``boundary`` (a list): the per-column count of elements
-    within TAU of the Hardtanh boundary is appended."""
+    within TAU of the Hardtanh boundary is appended.
+
+    ``impl_y``: the BatchNorm output as the implementation under test rounds it (fp32, same shape).
+    Elements within TAU of +-1 then take the backward mask 1[-1 < y < 1] from it -- the Hardtanh
+    decision is anchored on the implementation's rounding there, as BatchNorm near-ties are anchored
+    on its z1 -- and ``anchored`` (a list) receives (window elements whose mask changed, elements
+    OUTSIDE the window whose impl_y mask differs from float64's: 0 unless impl_y is not a rounding
+    of this y)."""
     m = z.numel() // z.shape[1]
     shape = [1] * z.dim()
     shape[1] = -1
@@ -64,8 +72,17 @@ def batchnorm_train(z, gamma, beta, rmean, rvar, dims, momentum=0.1, eps=1e-5, b
     xhat = z.sub_(mu.view(shape)).mul_(inv.view(shape))
     y = xhat * gamma.view(shape) + beta.view(shape)
     mask = (y > -1.0) & (y < 1.0)              # Hardtanh backward: strict
+    win = (y.abs() - 1.0).abs() < TAU
     if boundary is not None:
-        boundary.append(((y.abs() - 1.0).abs() < TAU).sum(dims))
+        boundary.append(win.sum(dims))
+    if impl_y is not None:
+        imask = (impl_y > -1.0) & (impl_y < 1.0)
+        diff = imask != mask
+        if anchored is not None:
+            anchored.append((int((diff & win).sum()), int((diff & ~win).sum())))
+        mask = torch.where(win, imask, mask)
+        del imask, diff
+    del win
     y.clamp_(-1.0, 1.0)
     new_rm = (1 - momentum) * rmean + momentum * mu
     new_rv = (1 - momentum) * rvar + momentum * var * (m / max(m - 1, 1))
@@ -147,9 +164,16 @@ class MLPOracle:
         self.opt = Adam(lr)
         self.org_protocol = org_protocol
 
-    def step(self, x, target, z1=None, drop=None, update=True):
+    def step(self, x, target, z1=None, drop=None, update=True, anchor=None, bwd=None):
+        """``anchor``: callable (layer index i, fp32 BatchNorm input z as float64) -> the
+        implementation's fp32 BatchNorm output, whose Hardtanh decision is taken for elements within
+        TAU of +-1 (batchnorm_train ``impl_y``; ``self.anchored`` records what it changed).
+        ``bwd``: callable (kind "dw" | "dx", layer index i, g, other operand) -> float64 product, to
+        run the backward GEMMs in another arithmetic (calibration runs); default exact float64
+        ``g.T @ x`` / ``g @ W_b``."""
         p = self.p
         self.boundary = []         # per hidden layer: [h_i] counts of elements within TAU of +-1
+        self.anchored = []         # per hidden layer (with anchor): (changed in window, differing outside)
         x = torch.as_tensor(x).to(self.dev)
         target = torch.as_tensor(target).to(self.dev, torch.int64)
         a = x.reshape(x.shape[0], -1).to(F64)
@@ -166,9 +190,11 @@ class MLPOracle:
             if i == 2 and drop is not None:        # nn.Dropout(p) on fc3's fp32 output (:69)
                 z = (z.to(F32) * torch.as_tensor(drop).to(self.dev, F32)).to(F64)
             bn = f"bn{i + 1}"
+            iy = anchor(i, z) if anchor is not None else None
             a, cache, rm, rv = batchnorm_train(z, p[f"{bn}.weight"], p[f"{bn}.bias"],
                                                p[f"{bn}.running_mean"], p[f"{bn}.running_var"], (0,),
-                                               boundary=self.boundary)
+                                               boundary=self.boundary, impl_y=iy, anchored=self.anchored)
+            del iy
             p[f"{bn}.running_mean"], p[f"{bn}.running_var"] = rm, rv
             caches.append((xu, wb, cache))
         logits = a @ p["fc4.weight"].T + p["fc4.bias"]
@@ -184,9 +210,14 @@ class MLPOracle:
             caches[i] = None
             if i == 2 and drop is not None:        # dropout backward: the same scaled mask
                 g.mul_(torch.as_tensor(drop).to(self.dev, F32).to(F64))
-            grads[f"{l}.weight"] = g.T @ (xu if i == 0 else xu.to(F64))
+            xo = xu if i == 0 else xu.to(F64)
+            grads[f"{l}.weight"] = g.T @ xo if bwd is None else bwd("dw", i, g, xo)
+            del xo
             grads[f"{l}.bias"] = g.sum(0)
-            g = g @ wb if i > 0 else None
+            if i > 0:
+                g = g @ wb if bwd is None else bwd("dx", i, g, wb)
+            else:
+                g = None
         if update:
             self._update(grads)
         return loss, out, grads
@@ -239,7 +270,10 @@ class CNNOracle:
         self.org = {f"{l}.0.weight": self.p[f"{l}.0.weight"].clone() for l in CONV}
         self.opt = Adam(lr)
 
-    def step(self, x, target, update=True):
+    def step(self, x, target, update=True, bwd=None):
+        """``bwd``: callable (kind "dw" | "dx", layer index j, gradient [N, Co, H*W], im2col columns
+        [N, C*k*k, H*W] | the binarised weight [Co, C*k*k]) -> the float64 contraction (dW [Co, C*k*k]
+        | dcols [N, C*k*k, H*W]) in another arithmetic (calibration runs); default exact float64."""
         p = self.p
         x = torch.as_tensor(x).to(self.dev)
         target = torch.as_tensor(target).to(self.dev, torch.int64)
@@ -272,10 +306,12 @@ class CNNOracle:
             co, ci, k, _ = wb.shape
             cols = _unfold(xu, k, pad)                             # [N, C*k*k, H*W]
             gf = g.reshape(n, co, -1)
-            grads[f"{l}.0.weight"] = torch.einsum("nol,nkl->ok", gf, cols).reshape(wb.shape)
+            dw = torch.einsum("nol,nkl->ok", gf, cols) if bwd is None else bwd("dw", j, gf, cols)
+            grads[f"{l}.0.weight"] = dw.reshape(wb.shape)
             grads[f"{l}.0.bias"] = g.sum((0, 2, 3))
             if j > 0:                                             # conv1's input needs no gradient
-                dcols = wb.reshape(co, -1).T @ gf                 # [N, C*k*k, H*W]
+                w2 = wb.reshape(co, -1)
+                dcols = w2.T @ gf if bwd is None else bwd("dx", j, gf, w2)   # [N, C*k*k, H*W]
                 g = tF.fold(dcols, xu.shape[-2:], k, padding=pad)
         if update:
             self._update(grads)

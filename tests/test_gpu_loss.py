@@ -60,6 +60,31 @@ def test_cross_entropy_deterministic_and_nan_target(F):
     assert torch.isnan(F.cross_entropy(p, y2)).item()
 
 
+@pytest.mark.parametrize("M", [300, 65536])
+@pytest.mark.parametrize("ignore", [-100, 3])
+def test_cross_entropy_ignore_index_matches_torch(F, M, ignore):
+    """nn.CrossEntropyLoss(ignore_index=...) semantics: ignored rows add no loss term and get a zero
+    gradient row, the mean is over the others (they used to be counted / NaN)."""
+    from bnn_amd.nn import CrossEntropyLoss
+    p, y = _case(M, 10, 11)
+    y = y.clone()
+    y[::7] = ignore
+    a = p.clone().requires_grad_(True)
+    b = p.clone().requires_grad_(True)
+    la = CrossEntropyLoss(ignore_index=ignore)(a, y)
+    lb = torch.nn.functional.cross_entropy(b, y, ignore_index=ignore)
+    la.backward()
+    lb.backward()
+    assert abs(float(la) - float(lb)) <= 1e-6 * max(1.0, abs(float(lb)))
+    assert (a.grad - b.grad).abs().max().item() <= 1e-6 * b.grad.abs().max().item()
+    assert bool((a.grad[::7] == 0).all())
+    yall = torch.full_like(y, ignore)                        # every row ignored: torch's 0 / 0
+    c = p.clone().requires_grad_(True)
+    lc = CrossEntropyLoss(ignore_index=ignore)(c, yall)
+    lc.backward()
+    assert torch.isnan(lc).item() and bool((c.grad == 0).all())
+
+
 def test_module_routes_and_falls_back(F):
     from bnn_amd.nn import CrossEntropyLoss
     p, y = _case(300, 10, 9)

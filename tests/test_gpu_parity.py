@@ -572,6 +572,51 @@ def test_conv1_bn2d_handoff_matches_unfused(F):
             assert np.array_equal(g1[k], g0[k]), k
 
 
+def test_conv1_filter_switch_between_forward_and_backward(F):
+    """The conv1 / BatchNorm2d hand-off is decided in the forward.  Switching the one-channel filter
+    kernel off after it (bnn_conv_set_c1_filter(0) between forward and backward) falls back to the
+    BatchNorm2d dx + the regular filter kernel instead of failing, and the BNN_CONV_C1F=0 knob is
+    applied before the first conv forward (so that forward does not opt into the hand-off): both
+    steps equal the default one (conv1's weight gradient within 1e-6, its bias within 1e-7, the
+    rest bit-identical)."""
+    from bnn_amd import _lib as L
+    from bnn_amd import nets
+    from bnn_amd.data import synthetic_mnist
+    x, y = synthetic_mnist(512, seed=6)
+    x, y = x.cuda(), y.cuda()
+
+    def step(mode):
+        torch.manual_seed(21)
+        m = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True).cuda()
+        n0 = F.C1BN_HANDOFFS
+        if mode == "env":
+            F._CONV_C1F[0] = "0"
+        loss = torch.nn.functional.nll_loss(m(x), y)
+        if mode == "switch":
+            L.call("bnn_conv_set_c1_filter", 0)
+        loss.backward()
+        return float(loss), {k: host(p.grad) for k, p in m.named_parameters()}, F.C1BN_HANDOFFS - n0
+
+    try:
+        ref = step("default")
+        sw = step("switch")
+        L.call("bnn_conv_set_c1_filter", 1)
+        env = step("env")
+    finally:
+        F._CONV_C1F[0] = None
+        L.call("bnn_conv_set_c1_filter", 1)
+    assert ref[2] == 1 and sw[2] == 0 and env[2] == 0, (ref[2], sw[2], env[2])
+    for l, g, _ in (sw, env):
+        assert l == ref[0]
+        for k in g:
+            if k == "layer1.0.weight":
+                assert rel_err(g[k], ref[1][k]) <= 1e-6, k
+            elif k == "layer1.0.bias":
+                assert np.abs(g[k] - ref[1][k]).max() <= 1e-7, k
+            else:
+                assert np.array_equal(g[k], ref[1][k]), k
+
+
 def test_fused_cnn_step_matches_torch_modules(F):
     """BinCNN with the fused BatchNorm2d+Hardtanh+MaxPool2d op against the same net through torch's
     BatchNorm2d / Hardtanh / MaxPool2d modules (integer-valued conv outputs: pooling ties resolved

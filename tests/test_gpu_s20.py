@@ -186,3 +186,26 @@ def test_compact_bias_is_guarded_not_copied(F):
         m.fc1.bias.add_(1.0)
     with pytest.raises(RuntimeError, match="modified by an inplace operation"):
         loss.backward()
+
+
+def test_compact_bias_guard_fires_after_latent_adam(F):
+    """LatentAdam writes the parameters through raw pointers (bnn_adam_clamp_multi / _pack) and bumps
+    their versions as a torch in-place op would: a backward of a forward taken before the update is
+    refused instead of rebuilding z from the updated bias."""
+    from bnn_amd import nets
+    from bnn_amd.optim import LatentAdam
+    M, W = 16384, 2048                     # the s20 carrier's grid (>= 512 tiles), as above
+    g = torch.Generator(device="cuda").manual_seed(9)
+    u = torch.randint(0, 256, (M, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+    y = torch.randint(0, 10, (M,), generator=g, device="cuda")
+    m = nets.MLP(W, W, W, org_protocol=False, mutate_input=False, fused_bn=True).cuda().train()
+    n0 = F.S20_HANDOFFS
+    loss = torch.nn.CrossEntropyLoss()(m(u), y)
+    assert F.S20_HANDOFFS - n0 == 1
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    v0 = m.fc1.bias._version
+    LatentAdam(m.parameters(), lr=0.01, clamp_params=nets.binary_params(m)).step()
+    assert m.fc1.bias._version > v0
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()

@@ -201,3 +201,32 @@ def test_t64_conv_sums_and_grads_vs_torch(shape):
     dx = torch.nn.functional.fold(wb.reshape(co, -1).T @ gy.reshape(n, co, -1), (h, w), 5, padding=2)
     assert torch.allclose(dw, torch.nn.grad.conv2d_weight(xu, wb.shape, gy, padding=2), rtol=0, atol=1e-10)
     assert torch.allclose(dx, torch.nn.grad.conv2d_input(xu.shape, wb, gy, padding=2), rtol=0, atol=1e-10)
+
+
+def test_t64_hardtanh_anchor_and_bwd_hook():
+    """MLPOracle's calibration hooks (used by tests/test_gpu_wide_step.py): ``anchor`` takes the
+    Hardtanh backward mask from an implementation's fp32 BatchNorm output only inside the 2^-20
+    window around +-1 -- an anchor that is a rounding of the float64 output changes nothing outside
+    it -- and ``bwd`` replaces the backward GEMMs (the identity hook reproduces the default step)."""
+    g = load_golden("trace_wide")
+    init = _init(g)
+    x, t = torch.as_tensor(O.to_tensor(g["s0/u8"])), torch.as_tensor(g["s0/target"])
+    base = T.MLPOracle(init, lr=float(g["meta/lr"]))
+    l0, _, g0 = base.step(x, t, update=False)
+    seen = []
+
+    def anchor(i, z):
+        # the float64 BatchNorm output rounded to fp32 (what an fp32 implementation would form)
+        zz = z.clone()
+        mu, var = zz.mean(0), zz.var(0, unbiased=False)
+        y = (zz - mu) / torch.sqrt(var + 1e-5) * base.p[f"bn{i + 1}.weight"] + base.p[f"bn{i + 1}.bias"]
+        seen.append(i)
+        return y.float()
+
+    m = T.MLPOracle(init, lr=float(g["meta/lr"]))
+    l1, _, g1 = m.step(x, t, update=False, anchor=anchor, bwd=lambda kind, i, gg, o: gg.T @ o if kind == "dw" else gg @ o)
+    assert seen == [0, 1, 2]
+    assert all(outside == 0 for _, outside in m.anchored), m.anchored
+    assert abs(l1 - l0) < 1e-12
+    for k in g0:
+        assert rel_err(_np(g1[k]), _np(g0[k])) < 1e-9 or float((g1[k] - g0[k]).abs().max()) < 1e-12, k
