@@ -66,9 +66,9 @@ CPU_BATCH = {"wide": 512, "mlp": 1024, "small": 64, "cnn": 256}
 def digit_pairs(kernel):
     """MFMA passes per algorithmic MAC of a GEMM kernel instance: fp32 operands enter as digit
     planes -- 3 int8 planes on gemm_i8 ((3,1) = 3 passes, (3,3) = 6), 4 FP6 e2m3 planes against
-    an FP4 ternary operand on gemm_fp6 (4 passes)."""
-    if kernel.startswith("gemm_fp6"):
-        return 4
+    an FP4 ternary operand on gemm_fp6 (4 passes; 5 with a dX operand's residual FP4 plane)."""
+    if kernel.startswith("gemm_fp6"):    # + the residual FP4 plane of a dX operand: a fifth pass
+        return 5 if kernel.endswith("+res") else 4
     if kernel.startswith("conv2d_bwd"):   # dY as 3 exact bf16 terms (bf16x3) on the bf16 MFMA
         return 3
     for tag, n in (("<3, 3,", 6), ("<3, 1,", 3)):
@@ -106,7 +106,13 @@ def parse():
                     help="run the gradient-exchange path at N=1 too: flat buckets, hooks and the RCCL "
                          "bucket all-reduces / buffer broadcast on a one-rank group")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the training step as a HIP graph and time replays (1 GPU; bnn_amd.graph)")
+                    help="capture the training step as a HIP graph and time replays (bnn_amd.graph; with the "
+                         "exchange, its collectives are captured too)")
+    ap.add_argument("--dropin", action="store_true",
+                    help="time the unchanged-script path instead: the reference Net through the drop-in "
+                         "models.binarized_modules (.org protocol, torch BatchNorm / Hardtanh / CrossEntropyLoss, "
+                         "torch.optim.Adam + the .org copy loop of mnist-dist2.py:131-137) on fp32 images")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path's secondary timing")
     ap.add_argument("--fp32-input", action="store_true",
                     help="feed fp32 images (u/255) instead of the u8 pixels the MLPs' fc1 consumes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -125,6 +131,64 @@ def build(cfg, backend):
     else:
         model = nets.MODELS[name](org_protocol=False, mutate_input=False, backend=backend, fused_bn=True)
     return model
+
+
+def build_dropin(cfg):
+    """The reference's own call pattern on the drop-in module (mnist-dist2.py:46-76 Net built from
+    models.binarized_modules' BinarizeLinear / BinarizeConv2d with torch's BatchNorm, Hardtanh,
+    Dropout, LogSoftmax): ``org_protocol`` and ``mutate_input`` left at the reference's behaviour."""
+    from bnn_amd import nets
+    name = CONFIGS[cfg][0]
+    return nets.BinCNN() if name == "cnn" else nets.MODELS[name]()
+
+
+def dropin_step_fn(model, x, y, lr):
+    """mnist-dist2.py:118-137 unchanged: zero_grad, forward, nn.CrossEntropyLoss, backward, then the
+    .org restore -> torch.optim.Adam.step -> clamp loop (optim.org_protocol_step)."""
+    from bnn_amd.optim import org_protocol_step
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad()
+        loss = crit(model(x), y)
+        loss.backward()
+        org_protocol_step(model, opt)
+        return loss
+    return step
+
+
+def time_dropin(cfg, batch, dev, lr, steps, warmup):
+    """(ms per step, samples/s) of the drop-in path on this GPU: the same batch shape as fp32 images."""
+    from bnn_amd.data import synthetic_mnist
+    torch.manual_seed(0)
+    model = build_dropin(cfg).to(dev).train()
+    x, y = synthetic_mnist(batch, seed=1234, device=dev, as_u8=False)
+    step = dropin_step_fn(model, x, y, lr)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {"ms_per_step": round(dt * 1e3, 3), "value": round(batch / dt, 2), "unit": "samples/s", "steps": steps,
+           "warmup": warmup, "loss_last_step": round(float(loss.item()), 5),
+           "path": "models.binarized_modules drop-in (.org protocol, torch BatchNorm/Hardtanh/CrossEntropyLoss, "
+                   "torch.optim.Adam + .org copy loop), fp32 images"}
+    del model, x, y, step
+    torch.cuda.empty_cache()
+    return out
+
+
+def _dropin_with_exchange(model, x, y, opt, exchange):
+    from bnn_amd.optim import org_protocol_step
+    loss = torch.nn.CrossEntropyLoss()(model(x), y)
+    loss.backward()
+    exchange.finish()
+    org_protocol_step(model, opt)
+    return loss
 
 
 def host_threads():
@@ -256,8 +320,6 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_exchange = world > 1 or args.exchange
-    if args.graph and use_exchange:
-        raise SystemExit("--graph times one GPU without the gradient exchange")
     if use_exchange:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
@@ -276,34 +338,52 @@ def main():
 
     batch = args.batch or CONFIGS[args.config][1]
     torch.manual_seed(0)
-    model = build(args.config, args.backend).to(dev).train()
+    model = (build_dropin(args.config) if args.dropin else build(args.config, args.backend)).to(dev).train()
     # --exchange at N = 1: a one-rank RCCL group issuing every collective of an N-GPU step
     exchange = (GradExchange(model, bucket_mb=args.bucket_mb, force_collectives=args.exchange)
                 if use_exchange else None)
+    if args.dropin and args.graph:
+        raise SystemExit("--dropin times the reference's eager loop")
     dstep = BF.DeviceStep(dev).activate() if args.graph else None
-    opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model), device_step=dstep)
-    as_u8 = args.config != "cnn" and not args.fp32_input
+    as_u8 = args.config != "cnn" and not args.fp32_input and not args.dropin
     x, y = synthetic_mnist(batch, seed=1234 + rank, device=dev, as_u8=as_u8)
-    from bnn_amd.nn import CrossEntropyLoss
-    crit = CrossEntropyLoss()     # nn.CrossEntropyLoss() on libbnn (mnist-dist2.py's criterion)
+    if args.dropin:
+        # the unchanged reference loop on the drop-in module (its torch.optim.Adam + .org loop);
+        # the exchange's hooks and finish() bracket it as DDP's would
+        inner = dropin_step_fn(model, x, y, args.lr)
 
-    def step():
-        if exchange is not None:
-            exchange.zero_grad()
-        else:
-            for p in model.parameters():
-                p.grad = None
-        loss = crit(model(x), y)
-        loss.backward()
-        if exchange is not None:
-            exchange.finish()
-        opt.step()
-        return loss
+        def step():
+            if exchange is not None:
+                exchange.zero_grad()
+            loss = inner() if exchange is None else _dropin_with_exchange(model, x, y, inner_opt, exchange)
+            return loss
+        inner_opt = torch.optim.Adam(model.parameters(), lr=args.lr) if exchange is not None else None
+    else:
+        opt = LatentAdam(model.parameters(), lr=args.lr, clamp_params=binary_params(model), device_step=dstep)
+        from bnn_amd.nn import CrossEntropyLoss
+        crit = CrossEntropyLoss()     # nn.CrossEntropyLoss() on libbnn (mnist-dist2.py's criterion)
+
+        def step():
+            if exchange is not None:
+                exchange.zero_grad()
+            else:
+                for p in model.parameters():
+                    p.grad = None
+            loss = crit(model(x), y)
+            loss.backward()
+            if exchange is not None:
+                exchange.finish()
+            opt.step()
+            return loss
 
     run = step
+    coll_per_step = None
     if args.graph:
         from bnn_amd.graph import GraphedStep
+        c0 = exchange.collectives if exchange is not None else 0
         run = GraphedStep(step, opt, dstep, warmup=max(1, args.warmup))   # eager warm-up + capture
+        if exchange is not None:    # replays issue what the capture issued: count warm-up + capture
+            coll_per_step = (exchange.collectives - c0) / (max(1, args.warmup) + 1)
     else:
         for _ in range(args.warmup):
             step()
@@ -319,7 +399,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     dist_info = None
-    if world > 1:
+    if use_exchange:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         ranks = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(ranks, t)
@@ -333,7 +413,8 @@ def main():
                      "rccl_version": nccl_v, "devices": world,
                      "rank_ms_per_step_min": round(min(per_rank) / args.steps * 1e3, 3),
                      "rank_ms_per_step_max": round(max(per_rank) / args.steps * 1e3, 3),
-                     "collectives_per_step": (exchange.collectives / max(1, args.warmup + args.steps)
+                     "collectives_per_step": (coll_per_step if coll_per_step is not None else
+                                              exchange.collectives / max(1, args.warmup + args.steps)
                                               if exchange is not None else None)}
     final_loss = float(loss.item())
 
@@ -364,24 +445,33 @@ def main():
         "vs_baseline": (round(samples / elapsed / PUBLISHED_SMALL_SPS, 2)
                         if args.config == "small" and batch == 64 and world == 1 else None),
         "dtype": "fp4/fp6/int8 MFMA (ternary operands as FP4 e2m1, fp32 operands as 4 FP6 e2m3 digit planes "
-                 "with E8M0 block scales (backward) or 3 int8 digit planes (first layer); fp32 accumulate, fp32 I/O)",
+                 "with E8M0 block scales + an FP4 residual plane on the dX operands (backward: within "
+                 "2^-19 / 2^-22 of the block maximum) or 3 int8 digit planes (first layer); fp32 accumulate, "
+                 "fp32 I/O)",
         "data": ("synthetic MNIST-shaped (80.7% zero pixels), resident in HBM as "
                  + ("u8 pixels (fc1 applies ToTensor on the bytes)" if as_u8 else "fp32 u8/255 images")
                  + ", random-init weights"),
-        "config": {"workload": CONFIGS[args.config][2], "model": args.config, "global_batch": batch * world,
+        "config": {"workload": CONFIGS[args.config][2] + (" -- drop-in path (the unchanged reference loop)"
+                                                           if args.dropin else ""),
+                   "model": args.config + ("-dropin" if args.dropin else ""), "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
                    "backend": args.backend, "exchange": bool(use_exchange), "hip_graph": bool(args.graph),
                    "loss_last_step": round(final_loss, 5)},
     }
     if ksum:
         # binary-GEMM TOPS: in-kernel rate of the ternary x ternary forward GEMMs (2*M*N*K) and the
-        # binary convolutions' forward for the CNN
+        # binary convolutions' forward for the CNN; the first layer's u8-pixel x ternary GEMM (any
+        # "[pixels" label: not a binary GEMM) is reported on its own as fc1_tops
         fwd = [v for k, v in ksum.items()
-               if k.startswith("gemm_fp4") or (k.startswith("gemm_i8") and "<1, 1," in k and "[pixels]" not in k) or k == "conv2d_fwd"
-               or k == "gemm_xnor_k"]
+               if "[pixels" not in k and (k.startswith("gemm_fp4") or (k.startswith("gemm_i8") and "<1, 1," in k)
+                                          or k == "conv2d_fwd" or k == "gemm_xnor_k")]
         if fwd:
             ops, ms_ = sum(v["ops"] for v in fwd), sum(v["ms"] for v in fwd)
             result["binary_gemm_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)
+        pix = [v for k, v in ksum.items() if "[pixels" in k and "<1, 1," in k and v["ops"] > 0]   # fc1's forward
+        if pix:
+            ops, ms_ = sum(v["ops"] for v in pix), sum(v["ms"] for v in pix)
+            result["fc1_tops"] = round(ops / (ms_ * 1e-3) / 1e12, 2)
         step_ms = sum(v["ms"] for v in ksum.values()) / tsteps
         result["kernels"] = {k: {"launches_per_step": v["launches"] / tsteps, "avg_us": round(v["avg_ms"] * 1e3, 1),
                                  "share_of_step": round(v["ms"] / tsteps / ms, 4)}
@@ -396,6 +486,13 @@ def main():
     if cpu_main:
         result["cpu_baselines_other"] = cpu_extra
         result["speedup_vs_cpu"] = round(result["value"] / cpu_main["value"], 1)
+    if rank == 0 and world == 1 and not args.dropin and not args.no_dropin and not args.graph:
+        # the unchanged-script path (models.binarized_modules drop-in + the reference's loop) on the
+        # same GPU and batch, timed after the main measurement: what a user of mnist-dist2.py gets
+        try:
+            result["dropin"] = time_dropin(args.config, batch, dev, args.lr, steps=5, warmup=2)
+        except RuntimeError as e:        # e.g. out of memory: report, never fail the bench line
+            result["dropin"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and not args.no_gpu_torch and args.config in CPU_WIDTHS:
         try:
             gb = min(batch, 16384) if args.config == "wide" else batch

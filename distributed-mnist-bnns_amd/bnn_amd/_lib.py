@@ -93,31 +93,25 @@ SIGNATURES = {
     "bnn_conv2d_fwd_q_ok": (I32, [I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32]),
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
-    "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
-                            P, P]),
+    "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
     "bnn_bn_head_workspace": (I64, [I64, I64, I32]),
     "bnn_bn_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
-    "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P,
-                                 P, P]),
+    "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
     "bnn_bn_fwd_train_i16": (I32, [P, P, I64, I64, P, P, P, P, F32, F32, P, P, P, F32, U64, P, P]),
     "bnn_bn_apply_pack_i16": (I32, [P, P, I64, I64, P, P, P, P, P, P, I64, P, I64, I32, P]),
-    "bnn_bn_bwd_q6_i16": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
-                                P, P]),
+    "bnn_bn_bwd_q6_i16": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
-    "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P,
-                                     P, P, P, P]),
+    "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_bn_bwd_i8cols_workspace": (I64, [I64, I64]),
     "bnn_bn_bwd_i8cols": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
     "bnn_bn_bwd_i8cols_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
     "bnn_bn_bwd_stats_pre": (I32, [P, I64, I64, I64, I32, P, P, P, P, P, P, P, P]),
-    "bnn_bn_bwd_q6_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P]),
-    "bnn_bn_bwd_q6_i16_pre": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P,
-                                    P, P]),
+    "bnn_bn_bwd_q6_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "bnn_bn_bwd_q6_i16_pre": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_gemm_fp6_bnstats_rows": (I64, [I64]),
-    "bnn_gemm_fp6_bnstats": (I32, [P, P, P, I64, P, I64, P, I64, I64, I64, I64, P, P, I32, P, P, P, P, P, I32, I32,
-                                   P, P]),
+    "bnn_gemm_fp6_bnstats": (I32, [P, P, P, I64, P, P, I64, P, I64, I64, I64, I64, P, P, I32, P, P, P, P, P, I32, I32, P, P]),
     "bnn_hardtanh_bwd": (I32, [P, P, P, I64, P]),
     "bnn_adam_clamp": (I32, [P, P, P, P, I64, F32, F32, F32, F32, I64, F32, I32, P]),
     "bnn_adam_clamp_pack": (I32, [P, P, P, P, I64, I64, F32, F32, F32, F32, I64, F32, I32, I32, P, I64, P, I64, I32,
@@ -130,15 +124,15 @@ SIGNATURES = {
     "bnn_counter_add": (I32, [P, I64, P]),
     "bnn_set_seed_counter": (I32, [P]),
     "bnn_quant6_scale_rows": (I64, [I64]),
-    "bnn_quant6_rows": (I32, [P, I64, I64, I64, I64, P, P, P, P]),
+    "bnn_quant6_rows": (I32, [P, I64, I64, I64, I64, P, P, P, P, P]),
     "bnn_quant6_cols_workspace": (I64, [I64, I64]),
     "bnn_quant6_cols_t": (I32, [P, I64, I64, I64, I64, P, P, P, P, P, P]),
-    "bnn_gemm_fp6": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
+    "bnn_gemm_fp6": (I32, [P, P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P]),
     "bnn_gemm_fp6_workspace": (I64, [I64, I64, I64]),
-    "bnn_gemm_fp6_ws": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
+    "bnn_gemm_fp6_ws": (I32, [P, P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_fp4_panel_bytes": (I64, [I64, I64]),
     "bnn_fp4_panelize": (I32, [P, I64, I64, I64, P, P]),
-    "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
+    "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_gemm_fp6_kernel": (ctypes.c_char_p, [I64, I64]),
     "bnn_gemm_fp6_kernel_k": (ctypes.c_char_p, [I64, I64, I64]),
     "bnn_gemm_fp6_set_variant": (I32, [I32]),

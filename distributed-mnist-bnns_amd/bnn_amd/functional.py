@@ -13,6 +13,7 @@ Every op here runs on ROCm tensors through libbnn.so; there is no CPU fallback.
 """
 import contextlib
 
+import itertools
 import os
 
 import torch
@@ -454,17 +455,23 @@ Z16_HANDOFFS = 0          # z16 placeholders produced (tests check the hand-off 
 _ZERO1 = {}
 
 
+_TOKENS = itertools.count(1)
+
+
 def _placeholder(shape, device):
     """A stride-0 fp32 tensor of `shape` (the carrier of a hand-off attribute) viewing one cached zero
     per device: no fill kernel per placeholder.  In-place writes through it are refused by torch
-    (every element aliases one location)."""
+    (every element aliases one location).  Placeholders share data_ptr and version counter, so each
+    carries a unique token that _q6_key includes (the hand-offs' staleness checks tell them apart)."""
     key = str(device)
     z = _ZERO1.get(key)
     if z is None:
         z = torch.zeros((1,), dtype=torch.float32, device=device)
-        if not torch.cuda.is_current_stream_capturing():
+        if z.device.type != "cuda" or not torch.cuda.is_current_stream_capturing():
             _ZERO1[key] = z
-    return z.as_strided(tuple(shape), (0,) * len(shape))
+    ph = z.as_strided(tuple(shape), (0,) * len(shape))
+    ph._bnn_token = next(_TOKENS)
+    return ph
 
 
 def _z16_carrier(y16, bias):
@@ -518,11 +525,23 @@ def set_digit_gemm(kind):
 
 
 class Fp6Operand:
-    """4 FP6 digit planes of an fp32 matrix [rows, K] (blocks of 32 along K, padded to Kp)."""
-    __slots__ = ("lo", "hi", "sc", "rows", "Kp")
+    """4 FP6 digit planes of an fp32 matrix [rows, K] (blocks of 32 along K, padded to Kp), and
+    optionally the residual FP4 plane (``res``: 3 more bits, a fifth MFMA pass; bnn.h)."""
+    __slots__ = ("lo", "hi", "sc", "rows", "Kp", "res")
 
-    def __init__(self, lo, hi, sc, rows, Kp):
-        self.lo, self.hi, self.sc, self.rows, self.Kp = lo, hi, sc, rows, Kp
+    def __init__(self, lo, hi, sc, rows, Kp, res=None):
+        self.lo, self.hi, self.sc, self.rows, self.Kp, self.res = lo, hi, sc, rows, Kp, res
+
+
+# The residual plane on the row operands of the dX GEMMs (dY rows): the hidden BatchNorms' bias
+# gradients sum dX over the batch, where it nearly cancels, and need fp32-grade dX (4 planes: 1.5e-5
+# norm-wise on config 5's bn1/bn2 biases, fp32 GEMMs 7e-6 / 4e-6; tests/test_gpu_wide_step.py).
+# BNN_FP6_RES=0 drops it (A/B timing only).
+FP6_RES = os.environ.get("BNN_FP6_RES", "1") != "0"
+
+
+def _res_buffer(rows, Kp, device):
+    return torch.empty((rows, Kp // 32 * 16), dtype=torch.uint8, device=device) if FP6_RES else None
 
 
 def _fp6_buffers(rows, Kp, device):
@@ -544,9 +563,10 @@ def quant6_rows(x):
     M, K = x.shape
     Kp = round_up(K)
     lo, hi, sc = _fp6_buffers(M, Kp, x.device)
-    with _timed("quant6_rows_k", 0, 4 * M * K + 3 * M * Kp + M * Kp // 32):
-        L.call("bnn_quant6_rows", L.ptr(x), M, K, K, Kp, L.ptr(lo), L.ptr(hi), L.ptr(sc), L.stream())
-    return Fp6Operand(lo, hi, sc, M, Kp)
+    res = _res_buffer(M, Kp, x.device)
+    with _timed("quant6_rows_k", 0, 4 * M * K + (3.5 if res is not None else 3) * M * Kp + M * Kp // 32):
+        L.call("bnn_quant6_rows", L.ptr(x), M, K, K, Kp, L.ptr(lo), L.ptr(hi), L.ptr(sc), L.ptr(res), L.stream())
+    return Fp6Operand(lo, hi, sc, M, Kp, res)
 
 
 def quant6_cols_t(x, want_colsum=False):
@@ -598,17 +618,23 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None, panel_ks=N
     k_true = K if k_true is None else k_true
     if panels is None and M * N * K >= PANEL_MIN_MACS:
         panels = fp4_panels(B4, N, K)
-    name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
+    name = _fp6_name(M, N, K, A) if _TIMER is not None else ""
     wsb = L.lib().bnn_gemm_fp6_workspace(M, N, K)    # split-K partials (small grids), else 0
     ws = torch.empty((wsb,), dtype=torch.uint8, device=dev) if wsb > 0 else None
-    with _timed(name, 2.0 * M * N * k_true, 3 * M * K + N * K // 2 + 4 * M * N):
+    with _timed(name, 2.0 * M * N * k_true, (3.5 if A.res is not None else 3) * M * K + N * K // 2 + 4 * M * N):
         if panels is not None:
-            L.call("bnn_gemm_fp6_panel_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(panels),
-                   panel_ks, L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
+            L.call("bnn_gemm_fp6_panel_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(A.res),
+                   L.ptr(panels), panel_ks, L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
         else:
-            L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(B4), B4.shape[1],
-                   L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
+            L.call("bnn_gemm_fp6_ws", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(A.res), L.ptr(B4),
+                   B4.shape[1], L.ptr(bias), L.ptr(C), C.stride(0), M, N, K, L.ptr(ws), wsb, L.stream())
     return C
+
+
+def _fp6_name(M, N, K, A):
+    """Timer name of an FP6 GEMM launch: the library's kernel choice, + " +res" with the residual
+    plane (a fifth MFMA pass: bench.py counts its passes)."""
+    return L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() + (" +res" if A.res is not None else "")
 
 
 # The BatchNorm-backward statistics in the dX GEMM's epilogue (bnn_gemm_fp6_bnstats): the fused
@@ -629,9 +655,10 @@ def gemm_fp6_bnstats(A, panels, panel_ks, N, x, xbias, x_i16, mean, mlo, invstd,
     C = torch.empty((M, N), dtype=torch.float32, device=dev)
     R = L.lib().bnn_gemm_fp6_bnstats_rows(M)
     part = torch.empty(((4 if mode == 2 else 2) * R * N,), dtype=torch.float32, device=dev)
-    name = L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() if _TIMER is not None else ""
+    name = _fp6_name(M, N, K, A) if _TIMER is not None else ""
     with _timed(name, 2.0 * M * N * K, 3 * M * K + N * K // 2 + 4 * M * N + (2 if x_i16 else 4) * M * N):
-        L.call("bnn_gemm_fp6_bnstats", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(panels), panel_ks,
+        L.call("bnn_gemm_fp6_bnstats", L.ptr(A.lo), L.ptr(A.hi), L.ptr(A.sc), A.sc.shape[1], L.ptr(A.res),
+               L.ptr(panels), panel_ks,
                L.ptr(C), N, M, N, K, L.ptr(x), L.ptr(xbias), int(bool(x_i16)), L.ptr(mean), L.ptr(mlo), L.ptr(invstd),
                L.ptr(gamma), L.ptr(beta), 1, int(mode), L.ptr(part), L.stream())
     BN_EPI_USES += 1
@@ -1391,7 +1418,7 @@ _Q6_WANT = "_bnn_q6_consumer"
 
 
 def _q6_key(t):
-    return (t.data_ptr(), t._version, tuple(t.shape))
+    return (t.data_ptr(), t._version, tuple(t.shape), getattr(t, "_bnn_token", None))
 
 
 Q6_HANDOFF = True        # False: every FP6 linear backward quantises its dy itself (cross-checks)
@@ -1440,7 +1467,7 @@ def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, 
     dev = dy.device
     dx = torch.empty((M, C), dtype=torch.float32, device=dev) if z16 is None else _dz_placeholder(M, C, dev)
     dx_ptr = L.ptr(dx) if z16 is None else None
-    rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
+    rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C, _res_buffer(M, C, dev))
     Mp = round_up(M)
     cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
     cs = torch.empty((C,), dtype=torch.float32, device=dev)
@@ -1450,18 +1477,19 @@ def _bn_bwd_q6(x, dy, M, C, w, b, mean, invstd, mlo, hardtanh, p, seed, dw, db, 
         L.call("bnn_bn_bwd_stats_pre", L.ptr(pre[0]), pre[1], M, C, 1, L.ptr(w), L.ptr(invstd), L.ptr(dw), L.ptr(db),
                None, None, L.ptr(ws), L.stream())
     sfx = "_pre" if pre is not None else ""
-    with _timed(name, 0, xb * M * C + (4 if pre is not None else 8) * M * C + dzb * M * C + 3 * M * C + 3 * C * Mp
+    rb = 0.5 if rows.res is not None else 0.0
+    with _timed(name, 0, xb * M * C + (4 if pre is not None else 8) * M * C + dzb * M * C + (3 + rb) * M * C + 3 * C * Mp
                 + M * C // 16):
         if z16 is None:
             L.call("bnn_bn_bwd_q6" + sfx, L.ptr(x), L.ptr(dy), M, C, L.ptr(w), L.ptr(b), L.ptr(mean), L.ptr(invstd),
                    L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw), L.ptr(db), L.ptr(rows.lo),
-                   L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
-                   L.ptr(ws), L.stream())
+                   L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc),
+                   L.ptr(cs), L.ptr(ws), L.stream())
         else:
             L.call("bnn_bn_bwd_q6_i16" + sfx, L.ptr(z16[0]), L.ptr(z16[1]), L.ptr(dy), M, C, L.ptr(w), L.ptr(b),
                    L.ptr(mean), L.ptr(invstd), L.ptr(mlo), int(hardtanh), float(p), int(seed), dx_ptr, L.ptr(dw),
-                   L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi),
-                   L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
+                   L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(rows.res), L.ptr(cols.lo),
+                   L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
     setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
     return dx
 
@@ -1688,7 +1716,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         dgw = torch.empty((C,), dtype=torch.float32, device=dev) if gw is not None else None
         dgb = torch.empty((C,), dtype=torch.float32, device=dev) if gb is not None else None
         dw4 = torch.empty((HEAD_NOUT, C), dtype=torch.float32, device=dev)
-        rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C)
+        rows = Fp6Operand(*_fp6_buffers(M, C, dev), M, C, _res_buffer(M, C, dev))
         Mp = round_up(M)
         cols = Fp6Operand(*_fp6_buffers(C, Mp, dev), C, Mp)
         cs = torch.empty((C,), dtype=torch.float32, device=dev)
@@ -1698,13 +1726,13 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
                 L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw),
                        L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx),
                        L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
-                       L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
+                       L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
             else:
                 L.call("bnn_bn_head_bwd_q6_i16", L.ptr(z), L.ptr(zb), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C,
                        L.ptr(gw), L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed),
                        None, L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
-                       L.ptr(rows.sc), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws),
-                       L.stream())
+                       L.ptr(rows.sc), L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
+                       L.ptr(ws), L.stream())
         if ctx.q6 or ctx.z16:
             setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
         db4 = dy4.sum(0) if ctx.has_b4 and ctx.needs_input_grad[10] else None

@@ -10,8 +10,12 @@ whole step -- forward, loss, backward, the fused latent update -- once and repla
   seed -- come from a ``functional.DeviceStep`` counter that the captured optimizer advances on
   the device (bnn_adam_*_sched, bnn_set_seed_counter), so every replay is a distinct step and
   the sequence equals the same number of eager device-step steps bit for bit;
-* one process, one GPU: the gradient exchange is not captured (data-parallel runs use the eager
-  path, whose collectives overlap backward).
+* data parallel: a step that runs a ``parallel.GradExchange`` is captured with its collectives --
+  the per-forward buffer broadcast and every bucket all-reduce, issued from the backward hooks on
+  RCCL's stream as in the eager step (torch joins that stream into the capture) -- so a replay
+  issues the same collectives in the same order, overlapped with the backward kernels as before
+  (tests/test_gpu_rccl.py::test_rccl_exchange_captured_in_graph: replays equal eager steps bit for
+  bit on a one-rank RCCL group).  Every rank captures and replays the same step.
 """
 import torch
 

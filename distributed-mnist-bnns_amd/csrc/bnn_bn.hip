@@ -560,6 +560,7 @@ struct Q6Out {
   uint8_t *clo, *chi, *csc;        // dz^T: [C][Mp/32][64], [C][Mp/32][32], [Mp/64][csc_rows][2]
   int64_t csc_rows, nblk_m;        // nblk_m = Mp / 32
   double* part;                    // [workgroup rows of the grid][C] partial column sums, or null
+  uint8_t* rres = nullptr;         // the rows' residual FP4 plane [M][C/32][16] (bnn_fp6.h), or null
 };
 
 // One sub-tile's digit records staged in LDS: rows (64 rows x 2 blocks of 32 columns) and columns
@@ -569,6 +570,7 @@ struct Q6Out {
 struct Q6Stage {
   uint8_t rlo[64][128], clo[64][128];
   uint8_t rhi[64][64], chi[64][64];
+  uint8_t rres[64][32];            // the rows' residual planes: block b of row i at chunk b ^ ((i >> 3) & 1)
   uint8_t rsc[64][2], csc[64][2];
 };
 
@@ -584,6 +586,10 @@ struct Q6StageSink {
     *reinterpret_cast<uint2*>(hi + 16 * ((2 * b + (j >> 1)) ^ (i & 3)) + 8 * (j & 1)) = h;
   }
   __device__ __forceinline__ void scale(uint8_t v) { *sc = v; }
+  __device__ __forceinline__ void residual(uint4 r) {   // rows only: res = st.rres[i]
+    *reinterpret_cast<uint4*>(res + 16 * (b ^ ((i >> 3) & 1))) = r;
+  }
+  uint8_t* res = nullptr;
 };
 
 // The staged records of the sub-tile at rows m0.., columns c0.. to HBM, 16 B per thread and store:
@@ -607,6 +613,11 @@ __device__ __forceinline__ void q6_stage_store(const Q6Stage& st, const Q6Out& o
     const uint4 cv = *reinterpret_cast<const uint4*>(&st.chi[i][16 * (q ^ (i & 3))]);
     if (m0 + i < M) *reinterpret_cast<uint4*>(o.rhi + ((m0 + i) * nblk_c + blk0) * 32 + 16 * q) = rv;
     *reinterpret_cast<uint4*>(o.chi + ((c0 + i) * o.nblk_m + mblk0) * 32 + 16 * q) = cv;
+  }
+  if (o.rres != nullptr && t < 128) {         // row residual planes: 32 B per row (blocks blk0, blk0+1)
+    const int i = t >> 1, q = t & 1;
+    const uint4 rv = *reinterpret_cast<const uint4*>(&st.rres[i][16 * (q ^ ((i >> 3) & 1))]);
+    if (m0 + i < M) *reinterpret_cast<uint4*>(o.rres + ((m0 + i) * nblk_c + blk0) * 16 + 16 * q) = rv;
   }
   if (t < 8) {                                // row scales: rows m0 .. m0+63, blocks blk0, blk0+1
     *reinterpret_cast<uint4*>(o.rsc + (blk0 >> 1) * o.rsc_rows * 2 + m0 * 2 + 16 * t) =
@@ -773,9 +784,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     if (!Q6_DIAG_NOQUANT_ON) {
       if (wave < 2) {
         // row block (row m0 + lane, columns c0 + 32 b ..)
-        Q6StageSink sink{st.rlo[lane], st.rhi[lane], &st.rsc[lane][b], lane, b};
+        Q6StageSink sink{st.rlo[lane], st.rhi[lane], &st.rsc[lane][b], lane, b, st.rres[lane]};
         double unused = 0.0;
-        q6_block_pre<1, false>(tile + lane * Q6T_LD + QB * b, am, sink, unused);
+        if (o.rres != nullptr)     // the dX operand's residual plane (block-uniform branch)
+          q6_block_pre<1, false, Q6StageSink, true>(tile + lane * Q6T_LD + QB * b, am, sink, unused);
+        else
+          q6_block_pre<1, false>(tile + lane * Q6T_LD + QB * b, am, sink, unused);
       } else {
         // column block (column c0 + lane, rows m0 + 32 b ..): rows beyond M are zeros; its
         // elements are added to the column sum in row order while they are quantised
@@ -1725,14 +1739,14 @@ BNN_API int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64
 static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,
                           const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
-                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo,
                           uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream, bool pre = false) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % Q6T_COLS != 0 || !dy || !aligned16(dy) ||
       !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) || !vec_ok(beta) ||
       !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !rlo || !rhi || !rsc || !clo ||
       !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) || !aligned16(chi) ||
-      !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
+      (rres && !aligned16(rres)) || !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_bwd_q6: bad arguments (M=%lld C=%lld; C must be a multiple of 64, 0 <= p < 1)", (long long)M,
               (long long)C);
     return kErrInval;
@@ -1760,6 +1774,7 @@ static int bn_bwd_q6_impl(XIn xin, bool z16, const float* dy, int64_t M, int64_t
   // p0 is free once bn_bwd_final_k has folded it: it takes the column-sum partials
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
+  o.rres = rres;
   const int64_t qr = q6_rows(M, C);
   const dim3 g((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr));
   if (z16)
@@ -1784,29 +1799,29 @@ BNN_API int bnn_q6_stamps_copy(void* dst, int64_t bytes) {
 BNN_API int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,
                           const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
-                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo,
                           uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_bwd_q6_impl(XIn{x, nullptr}, false, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
-                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream);
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, rres, clo, chi, csc, colsum, work, stream);
 }
 
 BNN_API int bnn_bn_bwd_q6_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                               const float* beta, const float* save_mean, const float* save_invstd,
                               const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
-                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo,
                               uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_bwd_q6_impl(XIn{x, nullptr}, false, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
-                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream, true);
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, rres, clo, chi, csc, colsum, work, stream, true);
 }
 
 BNN_API int bnn_bn_bwd_q6_i16_pre(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
                                   const float* gamma, const float* beta, const float* save_mean,
                                   const float* save_invstd, const float* save_mean_lo, int32_t hardtanh, float p,
                                   uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
-                                  uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                                  uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                                   void* stream) {
   return bn_bwd_q6_impl(XIn{x16, xbias}, true, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
-                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream, true);
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, rres, clo, chi, csc, colsum, work, stream, true);
 }
 
 // The statistics half of a training-mode BatchNorm(+Hardtanh) backward from the per-tile-row partials
@@ -1835,10 +1850,10 @@ BNN_API int bnn_bn_bwd_stats_pre(const float* part, int64_t R, int64_t M, int64_
 BNN_API int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
                               const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                               const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
-                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                              float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo,
                               uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_bwd_q6_impl(XIn{x16, xbias}, true, dy, M, C, gamma, beta, save_mean, save_invstd, save_mean_lo, hardtanh,
-                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, clo, chi, csc, colsum, work, stream);
+                        p, seed, dx, dgamma, dbeta, rlo, rhi, rsc, rres, clo, chi, csc, colsum, work, stream);
 }
 
 constexpr int HEAD_NOUT = 10;   // the reference head: nn.Linear(C, 10) (mnist-dist2.py:73)
@@ -1888,14 +1903,14 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
                                int64_t C, const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
                                float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
-                               uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                               uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                                void* stream) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % 256 != 0 || !dy4 || !w4 || !dw4 ||
       nout != HEAD_NOUT || !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) ||
       !vec_ok(beta) || !aligned16(save_mean) || !aligned16(save_invstd) || !vec_ok(save_mean_lo) || !aligned16(w4) ||
       !rlo || !rhi || !rsc || !clo || !chi || !csc || !aligned16(rlo) || !aligned16(rhi) || !aligned16(clo) ||
-      !aligned16(chi) || !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
+      !aligned16(chi) || (rres && !aligned16(rres)) || !(p >= 0.f && p < 1.f) || (M + Q6T_SUB - 1) / Q6T_SUB > 65535) {
     set_error("bnn_bn_head_bwd_q6: bad arguments (M=%lld C=%lld nout=%d)", (long long)M, (long long)C, nout);
     return kErrInval;
   }
@@ -1919,6 +1934,7 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
                      (int64_t)nout, C, dw4);
   const int64_t mp = round_up(M, 64);
   Q6Out o{dx, rlo, rhi, rsc, q6_scale_rows(M), clo, chi, csc, q6_scale_rows(C), mp / QB, colsum ? p0 : nullptr};
+  o.rres = rres;
   const int64_t qr = q6_rows(M, C);
   const dim3 g((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr));
   if (z16)
@@ -1936,10 +1952,10 @@ BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4
                                const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
                                float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
-                               uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                               uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                                void* stream) {
   return bn_head_bwd_q6_impl(XIn{x, nullptr}, false, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
-                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, clo, chi, csc, colsum,
+                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
                              work, stream);
 }
 
@@ -1947,10 +1963,10 @@ BNN_API int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const
                                    int32_t nout, int64_t M, int64_t C, const float* gamma, const float* beta,
                                    const float* save_mean, const float* save_invstd, const float* save_mean_lo,
                                    float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, float* dw4,
-                                   uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc,
+                                   uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc,
                                    float* colsum, void* work, void* stream) {
   return bn_head_bwd_q6_impl(XIn{x16, xbias}, true, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
-                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, clo, chi, csc, colsum,
+                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
                              work, stream);
 }
 

@@ -61,6 +61,33 @@ __device__ __forceinline__ void codes4(float x, int shift, uint32_t (&c)[4]) {
   }
 }
 
+// The residual plane of a row operand (the dX GEMMs' dY rows; bnn_gemm.hip header "residual"): three
+// more bits of x below the four digit planes, as ONE FP4 (e2m1) plane.  With v = rint(x 2^shift)
+// (the digit planes' integer) and v8 = rint(x 2^(shift+3)), d = v8 - 8 v lies in [-4, 4]
+// (|8t - 8 rint(t)| <= 4, and the outer rint moves it by at most 1/2); the e2m1 code of d/2 is |d|
+// (0, 0.5, 1, 1.5, 2 are codes 0..4) with the sign in bit 3, and the GEMM scales the plane by
+// 2^(e - 21) (E8M0 byte = plane 0's byte - 5), so the five planes sum rint(x 2^(22-e)) 2^(e-22):
+// |x - q| <= 2^(e-23) <= max|x_block| 2^-22.  A block with a NaN scale or shift > RES_MAX_SHIFT
+// (max|x| < 2^-105, where 2^(shift+3) is no fp32 number) gets a zero residual.
+constexpr int RES_MAX_SHIFT = 124;
+
+// e = d + 4 in [0, 8] from the two magic-fma words: ba = bits of fma(x, 2^shift, MAGIC + DIGIT_BIAS)
+// = 0x4B400000 + v + DIGIT_BIAS, b8 = bits of fma(x, 2^(shift+3), MAGIC) = 0x4B400000 + v8 -- plain
+// modulo-2^32 arithmetic -- then the code min(e - 4, 12 - e) (unsigned: e >= 4 gives e - 4 <= 4,
+// e < 4 wraps above 12 - e = 8 | (4 - e)).
+__device__ __forceinline__ uint32_t res4_code_bits(uint32_t ba, uint32_t b8) {
+  const uint32_t e = b8 - (ba << 3) + (uint32_t)(7u * 0x4B400000u + 8u * (uint32_t)DIGIT_BIAS + 4u);
+  return min(e - 4u, 12u - e);
+}
+
+// The same from x itself (rint twice; the slow path of blocks outside the magic-fma range)
+__device__ __forceinline__ uint32_t res4_code(float x, int shift) {
+  const int v = __float2int_rn(ldexpf(x, shift));
+  const int v8 = __float2int_rn(ldexpf(x, shift + 3));
+  const int d = v8 - 8 * v;
+  return d < 0 ? (8u | (uint32_t)(-d)) : (uint32_t)d;
+}
+
 __device__ __forceinline__ float absmax_nan(float amax, float x) {
   const float a = fabsf(x);
   return (a == a) ? fmaxf(amax, a) : __builtin_inff();
@@ -71,7 +98,7 @@ __device__ __forceinline__ float absmax_nan(float amax, float x) {
 // hi_blk + 8q), lane 4 the plane-0 scale byte.  Every lane of the wave must call it (shuffles);
 // store = false suppresses this group's writes.
 __device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bool store, uint8_t* lo_blk,
-                                               uint8_t* hi_blk, uint8_t* sc_byte) {
+                                               uint8_t* hi_blk, uint8_t* sc_byte, uint8_t* res_blk = nullptr) {
   const int q = lane & 7;
   float amax = 0.f;
 #pragma unroll
@@ -105,6 +132,13 @@ __device__ __forceinline__ void q6_block_store(const float (&v)[4], int lane, bo
     if ((bit & 31) > 8) w[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
   }
   if (!store) return;
+  if (res_blk != nullptr) {   // the residual plane: this lane's 4 elements are nibbles 4q..4q+3
+    const bool rz = sbyte == 255 || shift > RES_MAX_SHIFT;
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r |= (rz ? 0u : res4_code(v[i], shift)) << (4 * i);
+    *reinterpret_cast<uint16_t*>(res_blk + 2 * q) = (uint16_t)r;
+  }
   if (q < 4) {
     *reinterpret_cast<uint4*>(lo_blk + plane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
     *reinterpret_cast<uint2*>(hi_blk + plane * 8) = make_uint2(w[4], w[5]);
@@ -179,14 +213,21 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
 // an fp32 number) take the ldexp path.  CSUM adds the block's elements to csum in element order
 // (the same double sum as a separate loop over them).  The record goes to sink.plane(j, lo 16 B,
 // hi 8 B) for planes j = 0..3 and sink.scale(byte).  Bit-identical to q6_block_store_lds.
-template <int STRIDE, bool CSUM, typename Sink>
+//
+// RES (row operands of the dX GEMMs): also the block's residual FP4 plane (res4_code_bits: one more
+// magic fma per element) to sink.residual(16 B: element i at bits 4i).
+template <int STRIDE, bool CSUM, typename Sink, bool RES = false>
 __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bits, Sink& sink, double& csum) {
   int shift;
   const int sbyte = block_scale(__uint_as_float(amax_bits), &shift);
   uint32_t P[QB / 2], Q[QB / 2];
+  uint32_t R[RES ? 4 : 1] = {0u};
   if (sbyte != 255 && shift <= 126) {
     const float s = __uint_as_float((uint32_t)(shift + 127) << 23);
     constexpr float MAGIC = 12582912.f + (float)DIGIT_BIAS;
+    // 2^(shift+3) (shift <= RES_MAX_SHIFT; else the residual stays zero)
+    const bool rok = RES && shift <= RES_MAX_SHIFT;
+    const float s8 = rok ? __uint_as_float((uint32_t)(shift + 130) << 23) : 0.f;
 #pragma unroll
     for (int k = 0; k < QB / 2; ++k) {
       const float xa = src[(2 * k) * STRIDE], xb = src[(2 * k + 1) * STRIDE];
@@ -198,6 +239,13 @@ __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bit
       const uint32_t bb = __float_as_uint(__builtin_fmaf(xb, s, MAGIC));
       P[k] = __builtin_amdgcn_perm(bb, ba, 0x05040100u);          // low halves of (a, b)
       Q[k] = __builtin_amdgcn_ubfe(ba, 15, 6) | (__builtin_amdgcn_ubfe(bb, 15, 6) << 16);
+      if constexpr (RES) {
+        if (rok) {
+          const uint32_t ca = res4_code_bits(ba, __float_as_uint(__builtin_fmaf(xa, s8, 12582912.f)));
+          const uint32_t cb = res4_code_bits(bb, __float_as_uint(__builtin_fmaf(xb, s8, 12582912.f)));
+          R[k >> 2] |= (ca | (cb << 4)) << (8 * (k & 3));
+        }
+      }
     }
   } else {
 #pragma unroll
@@ -211,8 +259,13 @@ __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bit
       const uint32_t wb = (uint32_t)(__float2int_rn(ldexpf(xb, shift)) + DIGIT_BIAS);
       P[k] = (wa & 0xFFFFu) | (wb << 16);
       Q[k] = (wa >> 15) | ((wb >> 15) << 16);
+      if constexpr (RES) {
+        if (sbyte != 255 && shift <= RES_MAX_SHIFT)
+          R[k >> 2] |= (res4_code(xa, shift) | (res4_code(xb, shift) << 4)) << (8 * (k & 3));
+      }
     }
   }
+  if constexpr (RES) sink.residual(make_uint4(R[0], R[1], R[2], R[3]));
 #pragma unroll 1
   for (int j = 0; j < 4; ++j) {
     q6v16u hv;

@@ -19,12 +19,19 @@
 // one).  Cost: 4 FP6 MFMA passes at the FP4/FP6 rate (2x the int8 rate) = 2 int8-equivalent
 // passes, against 3 for the int8 digit form (bnn_gemm.hip), with one accumulator instead of three.
 //
+// The residual plane (row operands of the dX GEMMs, whose fp32 precision the hidden BatchNorms' bias
+// gradients need: they sum dX over the batch, where it nearly cancels -- tests/test_gpu_wide_step.py's
+// calibration): three more bits of x as ONE FP4 (e2m1) plane, d = rint(x 2^(22-e)) - 8 I in [-4, 4]
+// (bnn_fp6.h res4_code), scaled by 2^(e-21) (E8M0 byte = plane 0's - 5), a fifth MFMA pass into the
+// same accumulator: |x - q| <= 2^(e-23) <= max|x_block| 2^-22.
+//
 // Operand layouts (K = padded reduction length, a multiple of 64; all rows 16-B aligned):
 //   A digits "lo": [rows][K/32][64 B]  -- per block, 16 B per plane: dwords 0..3 of the plane's
 //                                          6-dword MFMA operand (bits 0..127 of the 32 codes)
 //   A digits "hi": [rows][K/32][32 B]  -- per block, 8 B per plane: dwords 4..5 (bits 128..191)
 //   A scales:      [K/64][rows_pad][2] -- E8M0 byte of plane 0 (plane j adds 5j), per block
 //   B ternary:     [rows][ldb bytes]   -- FP4 nibbles, element k in byte k/2 (low nibble even k)
+//   A residual:    [rows][K/32][16 B]  -- per block, the 32 FP4 codes (element i at bits 4i); optional
 // The MFMA operand map (checked by tools/probes/probe_fp6.hip on MI355X): lane l holds row l%32,
 // k-block l/32 of the 64-k step, element j at bits 6j..6j+5; the lane's scale byte scales its 32.
 #include <algorithm>
@@ -43,7 +50,7 @@ namespace {
 __global__ __launch_bounds__(256) void quant6_rows_k(const float* __restrict__ x, int64_t M, int64_t K,
                                                      int64_t ldx, int64_t nblk, uint8_t* __restrict__ lo,
                                                      uint8_t* __restrict__ hi, uint8_t* __restrict__ sc,
-                                                     int64_t sc_rows, int vec) {
+                                                     int64_t sc_rows, int vec, uint8_t* __restrict__ res) {
   const int lane = threadIdx.x & 63, q = lane & 7;
   const int64_t row = blockIdx.x;
   const int64_t blk = ((int64_t)blockIdx.y * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
@@ -59,7 +66,7 @@ __global__ __launch_bounds__(256) void quant6_rows_k(const float* __restrict__ x
     for (int j = 0; j < 4; ++j) v[j] = (k0 + j < K) ? xr[k0 + j] : 0.f;
   }
   q6_block_store(v, lane, true, lo + (row * nblk + blk) * 64, hi + (row * nblk + blk) * 32,
-                 sc + (blk >> 1) * sc_rows * 2 + row * 2 + (blk & 1));
+                 sc + (blk >> 1) * sc_rows * 2 + row * 2 + (blk & 1), res ? res + (row * nblk + blk) * 16 : nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -201,6 +208,7 @@ struct Gemm6Params {
     float* part;
     int z16, hardtanh, mode;
   } bn;
+  const uint8_t* ares = nullptr;   // the residual FP4 plane [M][K/32][16 B] (instances with RES = 1)
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -264,8 +272,10 @@ __device__ __forceinline__ void tile6_of(int bid, int gm, int gn, int G, int& tm
 // set while tile 1's MFMAs run -- no k-step starts with the matrix pipe waiting on LDS.  All three
 // ring slots are in flight: stage kt+1 is waited for at step kt with stage kt+2 still landing
 // (two steps of cover), and stage kt+3 refills the slot stage kt has just left.
+// RES = 1: A carries the residual FP4 plane (header): BM x 32 B more per stage (block c of row i at
+// chunk c ^ ((i >> 3) & 1), as B's), a fifth MFMA per A fragment; the plain two-stage loop only.
 template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0,
-          int BNS = 0>
+          int BNS = 0, int RES = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6Params p) {
   static_assert(PP != 1 || (WM == 2 && STAGES == 3 && DIAG == 0), "pipelined form 1: 2 tile rows, 3 stages");
   static_assert(PP != 2 || (WM == 1 && WN % 2 == 0 && STAGES == 3 && DIAG == 0),
@@ -276,7 +286,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_ST = BM * 2, B_ST = BN * 32;
   constexpr int SC_PAD = (SC_ST + 1023) / 1024 * 1024;
-  constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST;
+  constexpr int R_ST = RES ? BM * 32 : 0;
+  constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST + R_ST;
+  static_assert(!RES || (PP == 0 && DIAG == 0 && STAGES == 2), "the residual plane: the plain two-stage loop");
   constexpr int I_LO = LO_ST / 1024, I_HI = HI_ST / 1024, I_SC = SC_PAD / 1024, I_B = B_ST / 1024;
   constexpr int PER_WAVE = (I_LO + I_HI + I_B) / NW + 1;   // wave 0 also issues the scale piece
   __shared__ __attribute__((aligned(16))) char smem[STAGES * ST];
@@ -334,6 +346,16 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   const uint8_t* b_base = p.bks > 0 ? p.b + ((int64_t)(n0 / FP4_PANEL) * p.bks + ks0) * (FP4_PANEL * 32) + (n0 % FP4_PANEL) * 32
                                     : p.b + (int64_t)n0 * p.ldb + (int64_t)ks0 * 32;
   const int64_t b_step = (DIAG >= 5) ? BN * 32 : (p.bks > 0 ? FP4_PANEL * 32 : 32);
+  // the residual plane: I_R pieces of 32 rows x 32 B, one per wave (waves >= I_R issue none; the
+  // two-stage loop waits for every piece, so the per-wave counts need not match)
+  constexpr int I_R = R_ST / 1024, P_R = (I_R + NW - 1) / NW;
+  uint32_t off_r[P_R > 0 ? P_R : 1];
+#pragma unroll
+  for (int ii = 0; ii < P_R; ++ii) {
+    const int lrow = (wave + ii * NW) * 32 + (lane >> 1), c = lane & 1;
+    off_r[ii] = (uint32_t)min(lrow, p.M - 1 - m0) * (uint32_t)(nblk * 16) + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1));
+  }
+  const uint8_t* r_base = RES ? p.ares + (int64_t)m0 * nblk * 16 + (int64_t)ks0 * 32 : nullptr;
   auto stage = [&](int kt, int buf) __attribute__((always_inline)) {
     if constexpr (DIAG == 1) return;
     char* base = smem + buf * ST;
@@ -348,6 +370,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       glds16_6s(b_base + (int64_t)kt * b_step, off_b[ii], base + LO_ST + HI_ST + SC_PAD + (wave + ii * NW) * 1024);
     if (wave == 0)   // a whole 1-KiB piece (512 rows): the scale array has 512 rows of tail padding
       glds16_6(sc_base + (int64_t)kt * p.asc_rows * 2 + lane * 16, base + LO_ST + HI_ST);
+    if constexpr (RES) {
+#pragma unroll
+      for (int ii = 0; ii < P_R; ++ii)
+        if (wave + ii * NW < I_R)
+          glds16_6s(r_base + (int64_t)kt * 32, off_r[ii], base + LO_ST + HI_ST + SC_PAD + B_ST + (wave + ii * NW) * 1024);
+    }
   };
   // piece i (compile-time after unrolling) of stage(kt, buf): lo, hi, B, then wave 0's scale piece
   constexpr int NPIECE = P_LO + P_HI + P_B + 1;
@@ -380,6 +408,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   struct AFrag {      // the 4 planes' 6-dword MFMA operands (elements 6, 7 unused) + scale byte
     v8i a0, a1, a2, a3;
     int sb;
+    v4i rr;           // RES: the residual plane's 4 dwords
   };
   auto read_a = [&](const char* base, int t, AFrag& f) __attribute__((always_inline)) {
     const int lrow = wm * WM * 32 + t * 32 + r;
@@ -398,6 +427,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
     f.a2 = v8i{l2.x, l2.y, l2.z, l2.w, h23.x, h23.y, 0, 0};
     f.a3 = v8i{l3.x, l3.y, l3.z, l3.w, h23.z, h23.w, 0, 0};
     f.sb = sSc[lrow * 2 + h];
+    if constexpr (RES)
+      f.rr = *reinterpret_cast<const v4i*>(base + LO_ST + HI_ST + SC_PAD + B_ST + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
   };
   // B fragments: row n, 16 B = k-block h
   auto read_b = [&](const char* base, v4i (&bf)[WN]) __attribute__((always_inline)) {
@@ -445,6 +476,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
       ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, ac[u], 2, 4, 0, s2, 0, 127);
       ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, ac[u], 2, 4, 0, s1, 0, 127);
       ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, ac[u], 2, 4, 0, s0, 0, 127);
+      if constexpr (RES) {   // the residual FP4 plane at plane 0's scale / 32 (blocks below 2^-106: zeros)
+        const int sr = sb == 255 ? 255 : (sb >= 5 ? sb - 5 : 0);
+        const v8i ar = {f.rr.x, f.rr.y, f.rr.z, f.rr.w, 0, 0, 0, 0};
+        ac[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ar, bb, ac[u], 4, 4, 0, sr, 0, 127);
+      }
     }
   };
 
@@ -897,7 +933,7 @@ __global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restric
 }
 
 template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int DIAG = 0, int OCC = 2, int PP = 0,
-          int BNS = 0>
+          int BNS = 0, int RES = 0>
 int launch6(Gemm6Params p, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
   p.gm = (p.M + BM - 1) / BM;
@@ -906,7 +942,7 @@ int launch6(Gemm6Params p, hipStream_t s) {
   const int nk = p.K / 64;
   p.kps = (nk + p.ksplit - 1) / p.ksplit;
   p.ksplit = (nk + p.kps - 1) / p.kps;          // no empty split
-  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES, DIAG, OCC, PP, BNS>),
+  hipLaunchKernelGGL((gemm_fp6_k<WAVES_M, WAVES_N, WM, WN, STAGES, DIAG, OCC, PP, BNS, RES>),
                      dim3((unsigned)((int64_t)p.gm * p.gn * p.ksplit)), dim3(64 * WAVES_M * WAVES_N), 0, s, p);
   if (p.ksplit > 1)
     hipLaunchKernelGGL(gemm6_splitk_sum_k, dim3((unsigned)(((int64_t)p.M * p.N / 4 + 255) / 256)), dim3(256), 0, s,
@@ -993,9 +1029,9 @@ using namespace bnn;
 BNN_API int64_t bnn_quant6_scale_rows(int64_t rows) { return q6_scale_rows(rows); }
 
 BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
-                            uint8_t* sc, void* stream) {
+                            uint8_t* sc, uint8_t* res, void* stream) {
   if (!x || !lo || !hi || !sc || M < 0 || K < 0 || ldx < K || Kp < K || Kp % 64 != 0 || Kp == 0 || !aligned16(lo) ||
-      !aligned16(hi) || M > 0x7fffffff || (Kp / QB + 31) / 32 > 65535) {
+      !aligned16(hi) || (res && !aligned16(res)) || M > 0x7fffffff || (Kp / QB + 31) / 32 > 65535) {
     set_error("bnn_quant6_rows: bad arguments (M=%lld K=%lld Kp=%lld)", (long long)M, (long long)K, (long long)Kp);
     return kErrInval;
   }
@@ -1003,7 +1039,7 @@ BNN_API int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, i
   const int64_t nblk = Kp / QB;
   const int vec = aligned16(x) && (ldx % 4 == 0);
   hipLaunchKernelGGL(quant6_rows_k, dim3((unsigned)M, (unsigned)((nblk + 31) / 32)), dim3(256), 0, S6(stream), x, M,
-                     K, ldx, nblk, lo, hi, sc, bnn_quant6_scale_rows(M), vec);
+                     K, ldx, nblk, lo, hi, sc, bnn_quant6_scale_rows(M), vec, res);
   return check_launch("bnn_quant6_rows");
 }
 
@@ -1067,28 +1103,29 @@ BNN_API int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K) {
 }
 
 static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
-                         int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream);
+                         const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream);
 
 BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
-                         int64_t N, int64_t K, void* stream) {
-  return gemm_fp6_impl(alo, ahi, asc, asc_rows, b, ldb, bias, C, ldc, M, N, K, nullptr, 0, stream);
+                         const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, void* stream) {
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, ares, b, ldb, bias, C, ldc, M, N, K, nullptr, 0, stream);
 }
 
 BNN_API int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                            const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
-                            int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
-  return gemm_fp6_impl(alo, ahi, asc, asc_rows, b, ldb, bias, C, ldc, M, N, K, work, work_bytes, stream);
+                            const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C,
+                            int64_t ldc, int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, ares, b, ldb, bias, C, ldc, M, N, K, work, work_bytes, stream);
 }
 
 static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                         const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M,
-                         int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+                         const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
   const bool panel = ldb < 0;   // bnn_gemm_fp6_panel_ws: ldb = -(k-steps per panel)
   if (!alo || !ahi || !asc || !b || !C || M < 0 || N < 0 || K <= 0 || K % 64 != 0 || (!panel && (ldb < K / 2 || ldb % 16 != 0)) ||
       ldc < N || asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
-      !aligned16(asc) || !aligned16(b) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
+      !aligned16(asc) || !aligned16(b) || (ares && !aligned16(ares)) || (ares && g_variant6 >= 0 && g_variant6 != 7) ||
+      M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
     set_error("bnn_gemm_fp6: bad arguments (M=%lld N=%lld K=%lld ldb=%lld asc_rows=%lld; K a positive multiple of "
               "64, asc_rows a multiple of 256 >= bnn_quant6_scale_rows(M))",
               (long long)M, (long long)N, (long long)K, (long long)ldb, (long long)asc_rows);
@@ -1103,6 +1140,10 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
                 split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0, {}};
+  if (ares) {   // the residual plane runs on the default tile (variant 7) with its own instance
+    p.ares = ares;
+    return launch6<2, 4, 2, 4, 2, 0, 2, 0, 0, 1>(p, S6(stream));
+  }
   return pl.v->fn(p, S6(stream));
 }
 
@@ -1124,14 +1165,15 @@ BNN_API int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t K
 }
 
 BNN_API int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                                  const uint8_t* bpanels, int64_t bks, const float* bias, float* C, int64_t ldc,
-                                  int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream) {
+                                  const uint8_t* ares, const uint8_t* bpanels, int64_t bks, const float* bias, float* C,
+                                  int64_t ldc, int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes,
+                                  void* stream) {
   if ((g_variant6 >= 0 && 512 % find6(g_variant6)->bn != 0) || K <= 0 || bks < K / 64) {
     set_error("bnn_gemm_fp6_panel_ws: bad arguments (K=%lld bks=%lld; bks >= K/64, a tile width dividing 512)",
               (long long)K, (long long)bks);
     return kErrInval;
   }
-  return gemm_fp6_impl(alo, ahi, asc, asc_rows, bpanels, -bks, bias, C, ldc, M, N, K, work, work_bytes, stream);
+  return gemm_fp6_impl(alo, ahi, asc, asc_rows, ares, bpanels, -bks, bias, C, ldc, M, N, K, work, work_bytes, stream);
 }
 
 // The panel GEMM with the BatchNorm-backward statistics of C in its epilogue (Gemm6Params::Bn), for
@@ -1140,7 +1182,8 @@ BNN_API int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const 
 BNN_API int64_t bnn_gemm_fp6_bnstats_rows(int64_t M) { return (M + 127) / 128; }
 
 BNN_API int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                                 const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc, int64_t M, int64_t N,
+                                 const uint8_t* ares, const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc,
+                                 int64_t M, int64_t N,
                                  int64_t K, const void* x, const float* xbias, int32_t x_i16, const float* mean,
                                  const float* mean_lo, const float* invstd, const float* gamma, const float* beta,
                                  int32_t hardtanh, int32_t mode, float* part, void* stream) {
@@ -1155,13 +1198,18 @@ BNN_API int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const u
   }
   if (!alo || !ahi || !asc || !bpanels || !C || M <= 0 || N <= 0 || K % 64 != 0 || ldc < N ||
       asc_rows < bnn_quant6_scale_rows(M) || asc_rows % 256 != 0 || !aligned16(alo) || !aligned16(ahi) ||
-      !aligned16(asc) || !aligned16(bpanels) || M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) {
+      !aligned16(asc) || !aligned16(bpanels) || (ares && !aligned16(ares)) || M > 0x7fffffff || N > 0x7fffffff ||
+      K > 0x7fffffff) {
     set_error("bnn_gemm_fp6_bnstats: bad GEMM arguments");
     return kErrInval;
   }
   Gemm6Params p{alo, ahi, asc, bpanels, -bks, asc_rows, nullptr, C, ldc, (int)M, (int)N, (int)K, 0, 0,
                 K >= 32768 ? 8 : 4, 1, 0, nullptr, bks};
   p.bn = Gemm6Params::Bn{x, xbias, mean, mean_lo, invstd, gamma, beta, part, x_i16 ? 1 : 0, hardtanh ? 1 : 0, mode};
+  if (ares) {
+    p.ares = ares;
+    return launch6<2, 4, 2, 4, 2, 0, 2, 0, 1, 1>(p, S6(stream));
+  }
   return launch6<2, 4, 2, 4, 2, 0, 2, 0, 1>(p, S6(stream));
 }
 

@@ -210,31 +210,36 @@ const char* bnn_gemm_i8_kernel(int32_t a_digits, int32_t b_digits, int64_t M, in
  *   hi  [rows][Kp/32][32 B]   per block: dwords 4..5 of planes 0,1,2,3
  *   sc  [Kp/64][bnn_quant6_scale_rows(rows)][2]  E8M0 byte of plane 0 per block (plane j: +5j;
  *       255 = NaN); the row pitch carries 512 rows of tail padding the GEMM may read
+ *   res [rows][Kp/32][16 B]   optional residual plane (row operands of the dX GEMMs): the next 3
+ *       bits, d = rint(x 2^(22-e)) - 8 rint(x 2^(19-e)) in [-4, 4] as FP4 (e2m1) codes of d/2
+ *       (element i at bits 4i), scaled by plane 0's scale / 32: with it |x - x_q| <= max|x_block|
+ *       * 2^-22 -- fp32-grade sums for the hidden BatchNorms' bias gradients
  * replaces: the fp32 GEMMs of BinarizeLinear's autograd (dX = dY.W_b, dW = dY^T.X_b) and the
  * first layer's F.linear(x, W_b) (models/binarized_modules.py:80). */
 int64_t bnn_quant6_scale_rows(int64_t rows);
 /* x [M][K] (row stride ldx) -> digits of its rows, blocks along K (zero digits for K..Kp-1). */
 int bnn_quant6_rows(const float* x, int64_t M, int64_t K, int64_t ldx, int64_t Kp, uint8_t* lo, uint8_t* hi,
-                    uint8_t* sc, bnn_stream_t stream);
+                    uint8_t* sc, uint8_t* res /* nullable */, bnn_stream_t stream);
 /* x [M][N] -> digits of x^T (rows n, blocks along m, zero digits for M..Mp-1), plus colsum[n] =
  * sum_m x[m][n] (nullable; fixed-order double sums, `work` of bnn_quant6_cols_workspace bytes):
  * the bias gradient dB = sum_B dY (binarized_modules.py:81-83). */
 int64_t bnn_quant6_cols_workspace(int64_t M, int64_t N);
 int bnn_quant6_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, int64_t Mp, uint8_t* lo, uint8_t* hi,
                       uint8_t* sc, float* colsum, void* work, bnn_stream_t stream);
-/* C[m][n] = sum_k A[m][k] B[n][k] (+ bias[n]): A as above (asc_rows = the sc row pitch), B FP4
- * nibbles [N][ldb bytes] (ldb multiple of 16, >= K/2; zero nibbles beyond the true length). */
-int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
-                 int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                 bnn_stream_t stream);
+/* C[m][n] = sum_k A[m][k] B[n][k] (+ bias[n]): A as above (asc_rows = the sc row pitch; ares = its
+ * residual plane or NULL: a fifth MFMA pass), B FP4 nibbles [N][ldb bytes] (ldb multiple of 16,
+ * >= K/2; zero nibbles beyond the true length). */
+int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* ares,
+                 const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N,
+                 int64_t K, bnn_stream_t stream);
 /* The same product with split-K when the tile grid is below one round of the chip (small M x N:
  * the MLP's backward GEMMs at batch 4096): `work` of bnn_gemm_fp6_workspace(M, N, K) bytes (0 = no
  * split for this shape) holds the per-split fp32 partials, folded in split order (deterministic,
  * shape-only) with the bias.  A smaller workspace falls back to the unsplit grid. */
 int64_t bnn_gemm_fp6_workspace(int64_t M, int64_t N, int64_t K);
-int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows, const uint8_t* b,
-                    int64_t ldb, const float* bias, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                    void* work, int64_t work_bytes, bnn_stream_t stream);
+int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
+                    const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                    int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
 /* FP4 panels of a B operand: [N][ldb] -> [ceil(N/512)][Kp/64][512][32 B] (rows beyond N zero), so
  * each GEMM stage stages one contiguous run of B instead of 32 B from each of 512 rows (a quarter
  * line per row); bnn_gemm_fp6_panel_ws = bnn_gemm_fp6_ws with B in that layout, bks = the 64-k
@@ -243,8 +248,9 @@ int bnn_gemm_fp6_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, 
 int64_t bnn_fp4_panel_bytes(int64_t N, int64_t Kp);
 int bnn_fp4_panelize(const uint8_t* b, int64_t N, int64_t ldb, int64_t Kp, uint8_t* panels, bnn_stream_t stream);
 int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                          const uint8_t* bpanels, int64_t bks, const float* bias, float* C, int64_t ldc, int64_t M,
-                          int64_t N, int64_t K, void* work, int64_t work_bytes, bnn_stream_t stream);
+                          const uint8_t* ares, const uint8_t* bpanels, int64_t bks, const float* bias, float* C,
+                          int64_t ldc, int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes,
+                          bnn_stream_t stream);
 /* bnn_gemm_fp6_panel_ws (no bias, the unsplit default plan only) with the BatchNorm-backward column
  * statistics of C in its epilogue: C is the dy of a training-mode BatchNorm(+Hardtanh) over x
  * [M][N] (fp32, or int16 + xbias when x_i16) with save_mean / mean_lo / invstd and gamma / beta;
@@ -252,7 +258,8 @@ int bnn_gemm_fp6_panel_ws(const uint8_t* alo, const uint8_t* ahi, const uint8_t*
  * max|g|, max|xhat| per 128-row tile row), folded by bnn_bn_bwd_stats_pre. */
 int64_t bnn_gemm_fp6_bnstats_rows(int64_t M);
 int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
-                         const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                         const uint8_t* ares, const uint8_t* bpanels, int64_t bks, float* C, int64_t ldc, int64_t M,
+                         int64_t N, int64_t K,
                          const void* x, const float* xbias, int32_t x_i16, const float* mean, const float* mean_lo,
                          const float* invstd, const float* gamma, const float* beta, int32_t hardtanh, int32_t mode,
                          float* part, bnn_stream_t stream);
@@ -438,12 +445,13 @@ int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, co
  * bnn_bn_dropout_bwd (p = 0: no dropout) that also writes both FP6 digit forms of dz -- rows
  * (lo/hi/sc as bnn_quant6_rows with Kp = C) and the transpose (as bnn_quant6_cols_t with
  * Mp = round_up(M, 64)) -- and colsum[n] = sum_m dz[m][n] (nullable), in the same pass, so dz is
- * never re-read; dx (the fp32 dz) is optional.  C % 64 == 0; training statistics only.  Digits
+ * never re-read; dx (the fp32 dz) is optional; rres (nullable) also the rows' residual plane
+ * ([M][C/32][16 B], bnn_quant6_rows' res) for the dX GEMM.  C % 64 == 0; training statistics only.  Digits
  * are bit-identical to the standalone quantisers on the same dz. */
 int bnn_bn_bwd_q6(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                   const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                   float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
-                  uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                  uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                   bnn_stream_t stream);
 int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t stream);
 
@@ -464,7 +472,7 @@ int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, con
 int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
                        const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                        const float* save_mean_lo, float p, uint64_t seed, float* dx, float* dgamma, float* dbeta,
-                       float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi,
+                       float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi,
                        uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
 
 /* Fused BatchNorm-apply -> Hardtanh -> sign-pack for the next binarized layer (mnist-dist2.py:
@@ -502,7 +510,7 @@ int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int
 int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
                       const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                       const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx, float* dgamma,
-                      float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo, uint8_t* chi,
+                      float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi,
                       uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
 int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                         const float* invstd, const float* mean_lo, const float* gamma, const float* beta, float p,
@@ -511,7 +519,7 @@ int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64
 int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy4, const float* w4, int32_t nout,
                            int64_t M, int64_t C, const float* gamma, const float* beta, const float* save_mean,
                            const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed, float* dx,
-                           float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc,
+                           float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres,
                            uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                            bnn_stream_t stream);
 
@@ -565,12 +573,12 @@ int bnn_bn_bwd_stats_pre(const float* part, int64_t R, int64_t M, int64_t C, int
 int bnn_bn_bwd_q6_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma, const float* beta,
                       const float* save_mean, const float* save_invstd, const float* save_mean_lo, int32_t hardtanh,
                       float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi,
-                      uint8_t* rsc, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
+                      uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                       bnn_stream_t stream);
 int bnn_bn_bwd_q6_i16_pre(const int16_t* x16, const float* xbias, const float* dy, int64_t M, int64_t C,
                           const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                           const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
-                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* clo,
+                          float* dgamma, float* dbeta, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo,
                           uint8_t* chi, uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
 int bnn_bn_bwd_i8cols_pre(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                           const float* beta, const float* save_mean, const float* save_invstd,

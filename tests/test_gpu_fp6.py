@@ -4,7 +4,9 @@ dW = dY^T.X_b) and the first layer's forward (models/binarized_modules.py:80).
 
 Bars:
 * quantisers: decoded on the host, every element within max|x_block| * 2^-19 of x (the a-priori
-  bound), digits in range, padding zero, column sums to fp32 rounding of the double sum;
+  bound), digits in range, padding zero, column sums to fp32 rounding of the double sum; the row
+  operands' residual FP4 plane (bnn_fp6.h): digits in [-4, 4] and the five planes' value EXACTLY
+  rint(x 2^(22-e)) 2^(e-22) (within max|x_block| * 2^-23 of x);
 * GEMM: against float64 products of the DECODED digits norm-wise <= 2e-6 (fp32 accumulation of
   exact block partial sums), against the float64 product of x itself <= 1e-5 (the gradient bar).
 """
@@ -54,8 +56,19 @@ def _e2m3_digit(c):
     return s * v8
 
 
-def decode(op, rows):
-    """Host decode of an Fp6Operand: [rows, Kp] float64 values and the digits."""
+def residual_digits(op, rows):
+    """[rows, nblk, 32] digits in [-4, 4] of the residual FP4 plane (element i at bits 4i: byte i/2,
+    low nibble for even i; e2m1 code of d/2 = |d|, sign bit 3)."""
+    nblk = op.Kp // 32
+    r = host(op.res).reshape(-1, nblk, 16)[:rows].astype(np.int64)
+    nib = np.stack([r & 15, r >> 4], axis=-1).reshape(rows, nblk, 32)
+    assert np.all((nib & 7) <= 4)
+    return np.where(nib & 8, -(nib & 7), nib & 7)
+
+
+def decode(op, rows, residual=True):
+    """Host decode of an Fp6Operand: [rows, Kp] float64 values and the digits (with the residual
+    plane, scaled by plane 0's scale / 32, when the operand has one)."""
     nblk = op.Kp // 32
     d = _e2m3_digit(_codes(host(op.lo), host(op.hi), rows, nblk))     # [rows, nblk, 4, 32]
     sc = host(op.sc)                                                  # [Kp/64, rows_pad, 2]
@@ -63,10 +76,12 @@ def decode(op, rows):
     val = np.zeros((rows, nblk, 32))
     for j in range(4):
         val += d[:, :, j, :] * np.ldexp(1.0, (E + 5 * j - 130))[..., None]
+    if residual and op.res is not None:
+        val += residual_digits(op, rows) * np.ldexp(1.0, E - 133)[..., None]
     return val.reshape(rows, nblk * 32), d, E
 
 
-def _check_quant(x, val, d, E):
+def _check_quant(x, val, d, E, bits=19):
     rows, K = x.shape
     nblk = val.shape[1] // 32
     assert np.all(np.abs(d[..., :3, :]) <= 16) and np.all(np.abs(d[..., 3, :]) <= 16)
@@ -74,7 +89,7 @@ def _check_quant(x, val, d, E):
     xp = np.zeros((rows, nblk * 32))
     xp[:, :K] = x
     amax = np.abs(xp.reshape(rows, nblk, 32)).max(-1)
-    bound = np.repeat(amax * 2.0 ** -19, 32, axis=1)
+    bound = np.repeat(amax * 2.0 ** -bits, 32, axis=1)
     assert np.all(np.abs(val - xp) <= bound + 1e-300)
     assert not val[:, K:].any()
     nz = amax > 0
@@ -90,8 +105,17 @@ def test_quant6_rows_decodes_within_bound(F, M, K):
     if M > 3:
         x[3] = 0.0
     op = F.quant6_rows(torch.as_tensor(x).cuda())
+    val4, d, E = decode(op, M, residual=False)
+    _check_quant(x.astype(np.float64), val4, d, E)
+    assert op.res is not None                            # the row operands carry the residual plane
     val, d, E = decode(op, M)
-    _check_quant(x.astype(np.float64), val, d, E)
+    _check_quant(x.astype(np.float64), val, d, E, bits=22)
+    # the five planes are rint(x 2^(22-e)) 2^(e-22) exactly (e = E - 111 from the block max)
+    xp = np.zeros((M, op.Kp))
+    xp[:, :K] = x
+    step = np.repeat(np.ldexp(1.0, E - 111 - 22), 32, axis=1)
+    want = np.rint(xp / step) * step
+    assert np.array_equal(val, want)
 
 
 @pytest.mark.parametrize("M,N", [(300, 200), (64, 8192), (1000, 37), (33, 64)])
@@ -114,10 +138,12 @@ def test_gemm_fp6_every_variant(F, M, N, K):
     bias = rng.standard_normal(N).astype(np.float32)
     xt = torch.as_tensor(x).cuda()
     op = F.quant6_rows(xt)
+    op4 = F.Fp6Operand(op.lo, op.hi, op.sc, op.rows, op.Kp)    # the four digit planes alone
     w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
-    val, _, _ = decode(op, M)
+    val, _, _ = decode(op4, M)
     exact_q = val[:, :K] @ w.astype(np.float64).T + bias        # what the MFMA sums (no rounding)
     exact_x = x.astype(np.float64) @ w.astype(np.float64).T + bias
+    bt = torch.as_tensor(bias).cuda()
     names = set()
     try:
         for v in range(0, 16):
@@ -126,12 +152,17 @@ def test_gemm_fp6_every_variant(F, M, N, K):
             if name in names:
                 continue
             names.add(name)
-            C = host(F.gemm_fp6(op, w4, N, bias=torch.as_tensor(bias).cuda()))
+            C = host(F.gemm_fp6(op4, w4, N, bias=bt))
             assert rel_err(C, exact_q) < 2e-6, (name, rel_err(C, exact_q))
             assert rel_err(C, exact_x) < 1e-5, (name, rel_err(C, exact_x))
     finally:
         L.call("bnn_gemm_fp6_set_variant", -1)
     assert len(names) >= 3
+    # the default kernel with the residual plane (a fifth MFMA pass): the five-plane product
+    val5, _, _ = decode(op, M)
+    exact_q5 = val5[:, :K] @ w.astype(np.float64).T + bias
+    C5 = host(F.gemm_fp6(op, w4, N, bias=bt))
+    assert rel_err(C5, exact_q5) < 2e-6 and rel_err(C5, exact_x) < 2e-6, (rel_err(C5, exact_q5), rel_err(C5, exact_x))
 
 
 @pytest.mark.parametrize("M,N,K", [(768, 1536, 4096), (1536, 3072, 4096), (4096, 1536, 768), (200, 132, 8192),
@@ -163,7 +194,8 @@ def test_gemm_fp6_split_k(F, M, N, K):
     F.gemm_fp6(op, w4, N, bias=bt, out=Cv)
     assert np.array_equal(host(Cv), C1)
     C0 = torch.empty(M, N, device="cuda")               # no workspace: the unsplit grid
-    L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(w4), w4.shape[1],
+    L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(op.res), L.ptr(w4),
+           w4.shape[1],
            L.ptr(bt), L.ptr(C0), N, M, N, op.Kp, None, 0, L.stream())
     assert rel_err(host(C0), exact_q) < 2e-6
 
@@ -203,7 +235,8 @@ def test_fp4_panels_and_panel_gemm(F, M, N, K):
         C0 = torch.empty(M, N, device="cuda")
         wsb = L.lib().bnn_gemm_fp6_workspace(M, N, op.Kp)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device="cuda")
-        L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(w4), w4.shape[1],
+        L.call("bnn_gemm_fp6_ws", L.ptr(op.lo), L.ptr(op.hi), L.ptr(op.sc), op.sc.shape[1], L.ptr(op.res), L.ptr(w4),
+           w4.shape[1],
                L.ptr(bt), L.ptr(C0), N, M, N, op.Kp, L.ptr(ws), wsb, L.stream())
         C_rows = host(C0)
     C_pan = host(F.gemm_fp6(op, w4, N, bias=bt, panels=P))

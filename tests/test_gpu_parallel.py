@@ -1,13 +1,21 @@
-"""BASELINE config 2 on the GPU: the build's own fused binarized MLP (libbnn layers, u8 pixels, the
-fused BatchNorm passes, direct bucket writes) trained data-parallel by GradExchange, against torch's
-DistributedDataParallel wrapping an identical copy -- the component the reference wraps around its
-model (mnist-dist2.py:93).  Two ranks share the one GPU of the test box over gloo (RCCL refuses two
-ranks on one device; the 8-GPU RCCL run is the driver's scaling bench).
+"""Data-parallel training on the GPU through GradExchange (libbnn layers, the fused BatchNorm passes,
+direct bucket writes) against torch's DistributedDataParallel wrapping an identical copy -- the
+component the reference wraps around its model (mnist-dist2.py:93, mnist-dist.py:56,66).  Two ranks
+share the one GPU of the test box over gloo (RCCL refuses two ranks on one device; the 8-GPU RCCL
+run is the driver's scaling bench).  Workloads:
 
-* gradients of every parameter equal DDP's bit for bit at every step (gloo sums; a/2 + b/2 and
-  (a + b)/2 round identically);
-* replicas stay identical across ranks (init broadcast + averaged gradients);
-* BatchNorm buffers follow DDP's broadcast_buffers (rank 0's statistics before each forward).
+* ``config2`` -- BASELINE config 2 at its real size: the reference's Net (mnist-dist2.py:46-76,
+  infl_ratio 3: 784-3072-1536-768-10, Dropout 0.3) at batch 100 per rank, world size 2, u8 pixels;
+* ``mlp`` -- a 512-256-256 MLP at batch 512 with small (0.25 MB) buckets, so the 512 x 512 weights
+  span several bucket slices;
+* ``cnn`` -- BASELINE config 4's data-parallel form: the BinCNN (conv5x5 1->16 -> BN2d -> Hardtanh ->
+  MaxPool, conv5x5 16->32 -> ..., Linear(1568, 10)) on fp32 images, batch 256 per rank.
+
+Bars: gradients of every parameter equal DDP's bit for bit at every step (gloo sums; a/2 + b/2 and
+(a + b)/2 round identically); replicas stay identical across ranks (init broadcast + averaged
+gradients); BatchNorm buffers follow DDP's broadcast_buffers (rank 0's statistics before each
+forward).  Dropout masks differ per rank, as the reference's do, and are the same for both copies
+on a rank (the seed drawn from torch's generator, reseeded before each forward).
 """
 import os
 import socket
@@ -32,7 +40,15 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+WORKLOADS = {
+    # kind: (batch per rank, bucket MB, steps)
+    "config2": (100, 25.0, 3),
+    "mlp": (512, 0.25, 2),
+    "cnn": (256, 1.0, 3),
+}
+
+
+def _worker(rank, world, port, q, kind):
     try:
         for p in (ROOT, PKG):
             if p not in sys.path:
@@ -41,43 +57,54 @@ def _worker(rank, world, port, q):
         os.environ["MASTER_PORT"] = str(port)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
+        from bnn_amd import functional as BF
         from bnn_amd import nets
         from bnn_amd.parallel import GradExchange
+        batch, bucket_mb, steps = WORKLOADS[kind]
 
         def make():
             torch.manual_seed(100 + rank)               # different init per rank on purpose
-            return nets.MLP(512, 256, 256, p_drop=0.0, org_protocol=False, mutate_input=False,
-                            fused_bn=True).cuda().train()
+            if kind == "cnn":
+                m = nets.BinCNN(org_protocol=False, mutate_input=False, fused_bn=True)
+            elif kind == "config2":
+                m = nets.Net(org_protocol=False, mutate_input=False, fused_bn=True)     # p_drop 0.3
+            else:
+                m = nets.MLP(512, 256, 256, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True)
+            return m.cuda().train()
 
         ours, ref = make(), make()
-        ex = GradExchange(ours, bucket_mb=0.25)         # the 512x512 weight spans several buckets
+        ex = GradExchange(ours, bucket_mb=bucket_mb)
         ddp = torch.nn.parallel.DistributedDataParallel(ref, device_ids=[0])
         g = torch.Generator(device="cuda").manual_seed(1234 + rank)
-        u = torch.randint(0, 256, (512, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
-        y = torch.randint(0, 10, (512,), generator=g, device="cuda")
         crit = torch.nn.CrossEntropyLoss()
         written = 0
-        for step in range(2):
+        for step in range(steps):
+            u = torch.randint(0, 256, (batch, 1, 28, 28), generator=g, device="cuda").to(torch.uint8)
+            u = torch.where(torch.rand(u.shape, generator=g, device="cuda") < 0.807, torch.zeros_like(u), u)
+            x = u.float().div(255.0) if kind == "cnn" else u
+            y = torch.randint(0, 10, (batch,), generator=g, device="cuda")
             ex.zero_grad()
             ref.zero_grad(set_to_none=True)
-            crit(ours(u), y).backward()
+            torch.manual_seed(1000 + 10 * step + rank)      # this rank's dropout seed, for both copies
+            crit(ours(x), y).backward()
             written += ex.direct_writes
             ex.finish()
-            crit(ddp(u), y).backward()
+            torch.manual_seed(1000 + 10 * step + rank)
+            crit(ddp(x), y).backward()
             for (n, p), q_ in zip(ours.named_parameters(), ref.parameters()):
                 assert torch.equal(p.grad, q_.grad), (step, n, float((p.grad - q_.grad).abs().max()))
             with torch.no_grad():
                 for p, q_ in zip(ours.parameters(), ref.parameters()):
                     p.add_(p.grad, alpha=-0.01)
                     q_.add_(q_.grad, alpha=-0.01)
-            from bnn_amd import functional as BF
             for p, q_ in zip(ours.parameters(), ref.parameters()):   # raw in-place updates
                 BF.invalidate_packed(p)
                 BF.invalidate_packed(q_)
         for a, b in zip(ours.buffers(), ref.buffers()):
             assert torch.equal(a, b)
+        counters = {"ZQ_HANDOFFS": BF.ZQ_HANDOFFS, "HEAD_CALLS": BF.HEAD_CALLS, "Q6_HANDOFFS": BF.Q6_HANDOFFS}
         out = {"params": [p.detach().cpu().numpy() for p in ours.parameters()], "written": written,
-               "nbuckets": len(ex.buckets)}
+               "nbuckets": len(ex.buckets), "counters": counters}
         ex.remove()
         q.put((rank, out))
         dist.destroy_process_group()
@@ -86,13 +113,14 @@ def _worker(rank, world, port, q):
         q.put((rank, "ERR " + traceback.format_exc()))
 
 
-def test_fused_mlp_gradexchange_matches_ddp_two_ranks_on_gpu():
+@pytest.mark.parametrize("kind", ["config2", "mlp", "cnn"])
+def test_gradexchange_matches_ddp_two_ranks_on_gpu(kind):
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, kind)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -104,6 +132,11 @@ def test_fused_mlp_gradexchange_matches_ddp_two_ranks_on_gpu():
                 p.kill()
     for r in range(2):
         assert not isinstance(out[r], str), out[r]
-    assert out[0]["nbuckets"] > 3 and out[0]["written"] > 0
+    if kind == "mlp":
+        assert out[0]["nbuckets"] > 3 and out[0]["written"] > 0
+    if kind == "config2":
+        assert out[0]["written"] > 0 and out[0]["counters"]["HEAD_CALLS"] > 0     # the fused MLP path ran
+    if kind == "cnn":
+        assert out[0]["counters"]["ZQ_HANDOFFS"] > 0                             # the fused BinCNN path ran
     for a, b in zip(out[0]["params"], out[1]["params"]):
         np.testing.assert_array_equal(a, b)

@@ -577,8 +577,9 @@ def test_conv1_filter_switch_between_forward_and_backward(F):
     kernel off after it (bnn_conv_set_c1_filter(0) between forward and backward) falls back to the
     BatchNorm2d dx + the regular filter kernel instead of failing, and the BNN_CONV_C1F=0 knob is
     applied before the first conv forward (so that forward does not opt into the hand-off): both
-    steps equal the default one (conv1's weight gradient within 1e-6, its bias within 1e-7, the
-    rest bit-identical)."""
+    steps equal the default one (conv1's weight gradient -- then from the bf16x3 MFMA filter kernel
+    instead of the VALU one -- within the 1e-5 gradient bar, its bias within 1e-7, the rest
+    bit-identical)."""
     from bnn_amd import _lib as L
     from bnn_amd import nets
     from bnn_amd.data import synthetic_mnist
@@ -610,7 +611,7 @@ def test_conv1_filter_switch_between_forward_and_backward(F):
         assert l == ref[0]
         for k in g:
             if k == "layer1.0.weight":
-                assert rel_err(g[k], ref[1][k]) <= 1e-6, k
+                assert rel_err(g[k], ref[1][k]) <= 1e-5, k
             elif k == "layer1.0.bias":
                 assert np.abs(g[k] - ref[1][k]).max() <= 1e-7, k
             else:

@@ -2,7 +2,8 @@
 autograd hand-off that feeds its digits to the next BinarizeLinear backward
 (functional._bn_bwd_q6 / _q6_take).
 
-Bars: dz, dgamma, dbeta and every digit byte bit-identical to bnn_bn_bwd (/ bnn_bn_dropout_bwd)
+Bars: dz, dgamma, dbeta and every digit byte (the rows' residual plane included: the fused pass forms
+it with magic fmas, bnn_quant6_rows with rint) bit-identical to bnn_bn_bwd (/ bnn_bn_dropout_bwd)
 followed by bnn_quant6_rows and bnn_quant6_cols_t on the same dz; the bias gradient (a double
 column sum, summed in another order) within 1e-6; a whole training step's parameter gradients
 bit-identical with and without the hand-off, bias gradients of the consuming layers within 1e-6.
@@ -60,6 +61,7 @@ def test_bn_bwd_q6_matches_separate_passes(F, M, C, p):
     for a, b in ((rows, rows2), (cols, cols2)):
         assert a.Kp == b.Kp and a.rows == b.rows
         assert torch.equal(a.lo, b.lo) and torch.equal(a.hi, b.hi)
+        assert (a.res is None) == (b.res is None) and (a.res is None or torch.equal(a.res, b.res))
         n = a.rows
         assert torch.equal(a.sc[:, :n], b.sc[:, :n])
     assert rel_err(host(cs2), host(dz).astype(np.float64).sum(0)) <= 1e-6

@@ -106,11 +106,12 @@ def test_apply_pack_i16_bit_identical(F, M, C):
 
 
 def _fp6_bufs(F, M, C):
-    rows = F.Fp6Operand(*F._fp6_buffers(M, C, "cuda"), M, C)
+    rows = F.Fp6Operand(*F._fp6_buffers(M, C, "cuda"), M, C, F._res_buffer(M, C, "cuda"))
     Mp = F.round_up(M)
     cols = F.Fp6Operand(*F._fp6_buffers(C, Mp, "cuda"), C, Mp)
-    for t in (rows.lo, rows.hi, rows.sc, cols.lo, cols.hi, cols.sc):
-        t.fill_(0x5A)
+    for t in (rows.lo, rows.hi, rows.sc, rows.res, cols.lo, cols.hi, cols.sc):
+        if t is not None:
+            t.fill_(0x5A)
     return rows, cols
 
 
@@ -127,13 +128,13 @@ def test_bwd_q6_i16_bit_identical(F, M, C, p):
         rows, cols = _fp6_bufs(F, M, C)
         ws = torch.empty((L.lib().bnn_bn_workspace(M, C),), dtype=torch.uint8, device="cuda")
         common = [M, C, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(lo), 1, float(p), 11, L.ptr(dx),
-                  L.ptr(dg), L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(cols.lo),
-                  L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream()]
+                  L.ptr(dg), L.ptr(db), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc), L.ptr(rows.res),
+                  L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream()]
         if form == "f32":
             L.call("bnn_bn_bwd_q6", L.ptr(z), L.ptr(dy), *common)
         else:
             L.call("bnn_bn_bwd_q6_i16", L.ptr(z16), L.ptr(bias), L.ptr(dy), *common)
-        res.append([dx, dg, db, cs, rows.lo, rows.hi, rows.sc, cols.lo, cols.hi, cols.sc])
+        res.append([dx, dg, db, cs, rows.lo, rows.hi, rows.sc, rows.res, cols.lo, cols.hi, cols.sc])
     for x, y in zip(*res):
         assert eq(x, y)
 
@@ -164,12 +165,12 @@ def test_head_i16_bit_identical(F, M, C):
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, 10),), dtype=torch.uint8, device="cuda")
         common = [L.ptr(dy4), L.ptr(w4), 10, M, C, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(lo), p,
                   seed, L.ptr(dx), L.ptr(dg), L.ptr(db), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
-                  L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream()]
+                  L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream()]
         if form == "f32":
             L.call("bnn_bn_head_bwd_q6", L.ptr(z), *common)
         else:
             L.call("bnn_bn_head_bwd_q6_i16", L.ptr(z16), L.ptr(bias), *common)
-        res.append([y4, dx, dg, db, dw4, cs, rows.lo, rows.hi, rows.sc, cols.lo, cols.hi, cols.sc])
+        res.append([y4, dx, dg, db, dw4, cs, rows.lo, rows.hi, rows.sc, rows.res, cols.lo, cols.hi, cols.sc])
     for x, y in zip(*res):
         assert eq(x, y)
 
