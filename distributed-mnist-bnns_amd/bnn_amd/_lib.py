@@ -70,6 +70,7 @@ SIGNATURES = {
                                     I32, P]),
     "bnn_conv_set_mfma": (I32, [I32]),
     "bnn_conv_set_c1_filter": (I32, [I32]),
+    "bnn_conv_set_popc": (I32, [I32]),
     "bnn_bn2d_set_rows": (I32, [I32]),
     "bnn_bn2d_bwd_stats_q": (I32, [P, P, I32, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P, P]),
     "bnn_conv2d_bwd_filter_bn_ok": (I32, [I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32]),

@@ -1245,6 +1245,8 @@ class BinaryConv2dFunction(torch.autograd.Function):
         binarize_input, stride, padding, dilation, groups = ctx.conf
         bn = _c1bn_take(dy)      # the BatchNorm2d backward's pooled gradient and statistics, if handed over
         if bn is None:
+            if dy.dim() == 4 and dy.numel() > 1 and dy.stride() == (0, 0, 0, 0):
+                raise RuntimeError("a conv gradient placeholder lost its BatchNorm2d hand-off")
             dy = _c2d(dy)
         N, C, H, W = x.shape
         Co, _, KH, KW = w.shape

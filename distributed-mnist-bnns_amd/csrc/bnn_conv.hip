@@ -1781,6 +1781,10 @@ int64_t tile_filter_parts(const ConvShape& s) {
 
 using namespace bnn;
 
+#ifndef BNN_CONV_POPC_DEFAULT
+#define BNN_CONV_POPC_DEFAULT 0
+#endif
+
 // 1 (default): backward data on the bf16x3 MFMA kernel, backward filter / forward on the f32-MFMA
 // and int8-MFMA implicit-GEMM kernels, where the shape allows; 2: the f32-MFMA backward data
 // kernel instead of bf16x3; 0: the VALU LDS-tiled / generic kernels (the parity tests' cross-checks).
@@ -1789,6 +1793,60 @@ static int g_conv_mfma = 1;
 // 1 (default): a one-input-channel layer's filter gradient on the VALU kernel (conv_bwd_filter_c1_k);
 // 0: the MFMA / tiled kernels as for any other layer
 static int g_conv_c1f = 1;
+
+// The binarised-input forward's engine (bnn_conv_popc.hip): 1 = the VALU popcount kernels where their
+// geometry allows (C == 16 or C == 1), 0 = the int8-MFMA / dot4 kernels.  Default: set from the
+// measured times of both on the BinCNN's layers (DESIGN.md §6 "Conv engines").
+static int g_conv_popc = BNN_CONV_POPC_DEFAULT;
+
+namespace bnn {
+bool popc_fwd_ok(int64_t N, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int stride, int pad,
+                 int dil, int groups);
+int64_t popc_wpack_words(int64_t Co, int64_t C, int64_t K);
+int popc_fwd_launch(const float* x, const float* w_latent, const float* bias, void* y, int yfmt, int64_t N, int64_t C,
+                    int64_t H, int64_t W, int64_t Co, int64_t K, int pad, uint32_t* wpk, hipStream_t st);
+}  // namespace bnn
+
+BNN_API int bnn_conv_set_popc(int32_t on) {
+  if (on < 0) return g_conv_popc;      // query
+  g_conv_popc = on != 0;
+  return 0;
+}
+
+// The popcount engine's packed weight words: one device buffer per process and device, grown on
+// demand outside graph capture (the eager warm-up step before a capture sizes it), used in stream
+// order by every popcount launch.
+static uint32_t* popc_wpack_buffer(int64_t words) {
+  static uint32_t* buf[64] = {nullptr};
+  static int64_t cap[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] >= words) return buf[dev];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(nullptr, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
+  if (buf[dev] != nullptr) (void)hipFree(buf[dev]);
+  buf[dev] = nullptr;
+  cap[dev] = 0;
+  const int64_t n = std::max<int64_t>(words, 8192);
+  if (hipMalloc(reinterpret_cast<void**>(&buf[dev]), (size_t)n * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  cap[dev] = n;
+  return buf[dev];
+}
+
+static bool popc_pick(const ConvShape& s, int binarize) {
+  return binarize && g_conv_popc &&
+         popc_fwd_ok(s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.stride, s.pad, s.dil, s.groups);
+}
+
+static int popc_run(const ConvShape& s, const float* x, const float* w, const float* bias, void* y, int yfmt,
+                    hipStream_t st, const char* who) {
+  uint32_t* wpk = popc_wpack_buffer(popc_wpack_words(s.Co, s.C, s.KH));
+  if (wpk == nullptr) {
+    set_error("%s: no popcount weight buffer (first use inside a graph capture, or out of memory)", who);
+    return kErrInval;
+  }
+  return popc_fwd_launch(x, w, bias, y, yfmt, s.N, s.C, s.H, s.W, s.Co, s.KH, s.pad, wpk, st);
+}
 
 BNN_API int bnn_conv_set_c1_filter(int32_t on) {
   g_conv_c1f = on != 0;
@@ -1832,6 +1890,7 @@ BNN_API int bnn_conv2d_fwd(const float* x, int32_t binarize_input, const float* 
   const int64_t total = N * Co * s.OH * s.OW;
   if (total == 0) return 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (popc_pick(s, binarize_input)) return popc_run(s, x, w_latent, bias, y, 0, st, "bnn_conv2d_fwd");
   MfFwd mf;
   int64_t mlds = 0;
   if (binarize_input && g_conv_mfma && mf_fwd_geom(s, &mf, &mlds)) {
@@ -1908,8 +1967,9 @@ static void launch_c1_q(const ConvShape& s, const float* x, const float* w_laten
 }
 
 // Which compact-output kernel bnn_conv2d_fwd_q runs for a shape: 1 = int8 MFMA, 2 = single-channel
-// dot4, 0 = none (the shape is refused).  Shared by the entry and its query so they cannot disagree.
+// dot4, 3 = popcount, 0 = none (the shape is refused).  Shared by the entry and its query so they cannot disagree.
 static int fwd_q_path(const ConvShape& s, MfFwd* mf, int64_t* mlds) {
+  if (popc_pick(s, 1)) return 3;
   if (g_conv_mfma && mf_fwd_geom(s, mf, mlds)) return 1;
   if (g_conv_mfma && s.C == 1 && s.KW <= 8 && tile_geom_ok(s)) return 2;
   return 0;
@@ -1963,6 +2023,7 @@ BNN_API int bnn_conv2d_fwd_q(const float* x, const float* w_latent, void* y, int
     });
     return check_launch("bnn_conv2d_fwd_q");
   }
+  if (path == 3) return popc_run(s, x, w_latent, nullptr, y, yfmt, st, "bnn_conv2d_fwd_q");
   if (path == 2) {
     if (yfmt == 1) launch_c1_q<int8_t>(s, x, w_latent, reinterpret_cast<int8_t*>(y), st);
     else launch_c1_q<int16_t>(s, x, w_latent, reinterpret_cast<int16_t*>(y), st);

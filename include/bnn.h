@@ -331,6 +331,13 @@ int bnn_conv_set_mfma(int32_t mode);
  * (stride 1, 3x3 or 5x5, OW % 4 == 0, Co | 256, Co <= 64 -- the BinCNN's conv1) on a VALU kernel
  * that reads dY once with coalesced 16-B loads; 0: the MFMA kernels as for any layer. */
 int bnn_conv_set_c1_filter(int32_t on);
+/* Binarised-input forward engine (bnn_conv2d_fwd with binarize_input, bnn_conv2d_fwd_q): 1 = the
+ * VALU popcount kernels (sign / nonzero bit planes, and + xor + v_bcnt per 32 taps, exact integer
+ * sums) where they take the shape -- stride 1, dilation 1, one group, square odd K, pad <= K - 1, and
+ * C == 16 (K <= 7) or C == 1 (K*K <= 32, W + 2 pad <= 32, H + 2 pad <= 40); 0 = the int8-MFMA / dot4
+ * kernels.  The two write identical outputs; the default is the faster on the BinCNN's layers
+ * (DESIGN.md §6).  Process-global; on < 0 only returns the current setting (0 / 1). */
+int bnn_conv_set_popc(int32_t on);
 /* 1 (default): the 2x2-pooled BatchNorm2d backward statistics and forward apply over 28- / 14-wide
  * planes (the BinCNN's layers) on the row kernels (one thread per pooled row, every load of the row
  * issued up front); 2: the backward apply too (slower; A/B); 0: the window-per-thread kernels.

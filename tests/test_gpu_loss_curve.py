@@ -22,8 +22,8 @@ first's); training-set accuracy after the 300 steps within 1.5 points of T's.
 
 With dropout on (p = 0.3 before bn3, mnist-dist2.py:69; test_mnist_loss_curve_dropout): L draws
 its keep masks from the build's hash, T from torch's Philox stream, so no two runs
-share a mask; the calibration T2 is T with another dropout seed, and the same windowed bars hold
-with T2 in place of T1 (accuracy measured in eval mode, dropout off).
+share a mask; both are sampled over several dropout seeds and their means compared, the bands set
+by the spread of torch's own seeds (accuracy measured in eval mode, dropout off).
 """
 import os
 
@@ -130,25 +130,39 @@ def test_mnist_loss_curve_matches_reference_semantics():
     assert abs(accL - accT) <= 0.015
 
 
+LIBBNN_SEEDS = (11, 12, 13)
+TORCH_SEEDS = (21, 31, 41, 51)
+
+
 def test_mnist_loss_curve_dropout():
     """p = 0.3 (mnist-dist2.py:69), the bench's dropout: the fused path's hash masks against torch's
-    dropout; the band is the gap between two torch runs that differ only in their dropout seed."""
+    dropout.  No two runs share a mask, so both sides are sampled over several dropout seeds (3 for
+    libbnn, 4 for torch) and their MEANS are compared, the band set by how far torch's own seeds
+    spread: window losses of the mean curves within max(2 x the largest window gap between the mean
+    curves of torch's two seed halves, 0.02); mean accuracy within max(the range of torch's four
+    accuracies, 0.01).  (Round 5: the single-seed form of this check -- one libbnn run against one
+    torch run, bar max(1.5 points, 2 x the gap between two torch runs) -- failed at 1.54 points once
+    the dX GEMMs' residual plane moved libbnn's trajectory: 94.21 % against 95.75 / 95.30 %, a
+    sample of one.)"""
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     from bnn_amd import nets
     torch.manual_seed(5)
     state = {k: v.clone() for k, v in nets.MLP(*WIDTHS, p_drop=0.3).state_dict().items()}
     x, y, order = _data()
-    L, accL = _run_libbnn(state, x, y, order, p_drop=0.3, seed=11)
-    T, accT = _run_torch(state, x, y, order, p_drop=0.3, seed=21)
-    T2, accT2 = _run_torch(state, x, y, order, p_drop=0.3, seed=31)
-    wl, wt, wt2 = _windows(L), _windows(T), _windows(T2)
-    band = max(2 * float(np.abs(wt2 - wt).max()), 0.02)
-    print("\nwindow mean loss, p=0.3  libbnn:", " ".join(f"{v:.3f}" for v in wl))
-    print("window mean loss, p=0.3  torch :", " ".join(f"{v:.3f}" for v in wt))
-    print("window mean loss, p=0.3  torch2:", " ".join(f"{v:.3f}" for v in wt2))
-    print(f"max window gap libbnn {np.abs(wl - wt).max():.4f}, torch2 {np.abs(wt2 - wt).max():.4f} (band {band:.4f}); "
-          f"accuracy libbnn {accL:.4f}, torch {accT:.4f}, torch2 {accT2:.4f}")
+    runs_l = [_run_libbnn(state, x, y, order, p_drop=0.3, seed=s) for s in LIBBNN_SEEDS]
+    runs_t = [_run_torch(state, x, y, order, p_drop=0.3, seed=s) for s in TORCH_SEEDS]
+    wl = np.mean([_windows(r[0]) for r in runs_l], axis=0)
+    wts = [_windows(r[0]) for r in runs_t]
+    wt = np.mean(wts, axis=0)
+    half = np.abs(np.mean(wts[:2], axis=0) - np.mean(wts[2:], axis=0))
+    band = max(2 * float(half.max()), 0.02)
+    acc_l, acc_t = [r[1] for r in runs_l], [r[1] for r in runs_t]
+    abar = max(max(acc_t) - min(acc_t), 0.01)
+    print("\nwindow mean loss, p=0.3  libbnn (mean of 3):", " ".join(f"{v:.3f}" for v in wl))
+    print("window mean loss, p=0.3  torch  (mean of 4):", " ".join(f"{v:.3f}" for v in wt))
+    print(f"max window gap {np.abs(wl - wt).max():.4f} (band {band:.4f}: torch halves {half.max():.4f}); "
+          f"accuracy libbnn {acc_l} mean {np.mean(acc_l):.4f}, torch {acc_t} mean {np.mean(acc_t):.4f} (bar {abar:.4f})")
     assert np.abs(wl - wt).max() <= band
-    assert wl[-1] < 0.5 * wl[0] and wt[-1] < 0.5 * wt[0]
-    assert abs(accL - accT) <= max(0.015, 2 * abs(accT2 - accT))
+    assert all(_windows(r[0])[-1] < 0.5 * _windows(r[0])[0] for r in runs_l + runs_t)
+    assert abs(np.mean(acc_l) - np.mean(acc_t)) <= abar

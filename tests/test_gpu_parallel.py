@@ -11,8 +11,9 @@ run is the driver's scaling bench).  Workloads:
 * ``cnn`` -- BASELINE config 4's data-parallel form: the BinCNN (conv5x5 1->16 -> BN2d -> Hardtanh ->
   MaxPool, conv5x5 16->32 -> ..., Linear(1568, 10)) on fp32 images, batch 256 per rank.
 
-Bars: gradients of every parameter equal DDP's bit for bit at every step (gloo sums; a/2 + b/2 and
-(a + b)/2 round identically); replicas stay identical across ranks (init broadcast + averaged
+Bars: gradients of every parameter equal, bit for bit at every step, both DDP's and the exact
+average of the ranks' own gradients (a third copy per rank without any exchange, all-gathered; gloo
+sums, and a/2 + b/2 and (a + b)/2 round identically); replicas stay identical across ranks (init broadcast + averaged
 gradients); BatchNorm buffers follow DDP's broadcast_buffers (rank 0's statistics before each
 forward).  Dropout masks differ per rank, as the reference's do, and are the same for both copies
 on a rank (the seed drawn from torch's generator, reseeded before each forward).
@@ -72,9 +73,12 @@ def _worker(rank, world, port, q, kind):
                 m = nets.MLP(512, 256, 256, p_drop=0.0, org_protocol=False, mutate_input=False, fused_bn=True)
             return m.cuda().train()
 
-        ours, ref = make(), make()
+        ours, ref, plain = make(), make(), make()
         ex = GradExchange(ours, bucket_mb=bucket_mb)
         ddp = torch.nn.parallel.DistributedDataParallel(ref, device_ids=[0])
+        for p in plain.parameters():              # rank 0's weights, as the exchange / DDP broadcast them
+            dist.broadcast(p.data, src=0)
+            BF.invalidate_packed(p)
         g = torch.Generator(device="cuda").manual_seed(1234 + rank)
         crit = torch.nn.CrossEntropyLoss()
         written = 0
@@ -85,22 +89,29 @@ def _worker(rank, world, port, q, kind):
             y = torch.randint(0, 10, (batch,), generator=g, device="cuda")
             ex.zero_grad()
             ref.zero_grad(set_to_none=True)
-            torch.manual_seed(1000 + 10 * step + rank)      # this rank's dropout seed, for both copies
+            for p in plain.parameters():
+                p.grad = None
+            torch.manual_seed(1000 + 10 * step + rank)      # this rank's dropout seed, for every copy
             crit(ours(x), y).backward()
             written += ex.direct_writes
             ex.finish()
             torch.manual_seed(1000 + 10 * step + rank)
             crit(ddp(x), y).backward()
-            for (n, p), q_ in zip(ours.named_parameters(), ref.parameters()):
-                assert torch.equal(p.grad, q_.grad), (step, n, float((p.grad - q_.grad).abs().max()))
+            torch.manual_seed(1000 + 10 * step + rank)
+            crit(plain(x), y).backward()
+            for (n, p), q_, r_ in zip(ours.named_parameters(), ref.parameters(), plain.parameters()):
+                gs = [torch.empty_like(r_.grad) for _ in range(world)]
+                dist.all_gather(gs, r_.grad.contiguous())
+                avg = sum(gs) / world                       # the exact average of the ranks' gradients
+                assert torch.equal(p.grad, avg), (step, n, "exchange", float((p.grad - avg).abs().max()))
+                assert torch.equal(q_.grad, avg), (step, n, "ddp", float((q_.grad - avg).abs().max()))
+                r_.grad = avg                               # the plain copy follows the same trajectory
             with torch.no_grad():
-                for p, q_ in zip(ours.parameters(), ref.parameters()):
-                    p.add_(p.grad, alpha=-0.01)
-                    q_.add_(q_.grad, alpha=-0.01)
-            for p, q_ in zip(ours.parameters(), ref.parameters()):   # raw in-place updates
-                BF.invalidate_packed(p)
-                BF.invalidate_packed(q_)
-        for a, b in zip(ours.buffers(), ref.buffers()):
+                for m_ in (ours, ref, plain):
+                    for p in m_.parameters():
+                        p.add_(p.grad, alpha=-0.01)
+                        BF.invalidate_packed(p)             # raw in-place updates
+        for a, b, c in zip(ours.buffers(), ref.buffers(), plain.buffers()):
             assert torch.equal(a, b)
         counters = {"ZQ_HANDOFFS": BF.ZQ_HANDOFFS, "HEAD_CALLS": BF.HEAD_CALLS, "Q6_HANDOFFS": BF.Q6_HANDOFFS}
         out = {"params": [p.detach().cpu().numpy() for p in ours.parameters()], "written": written,
