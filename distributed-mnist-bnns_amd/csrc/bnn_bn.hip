@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(BN2_T) void bn2d_reduce_k(X2 x, const float* __rest
       for (int64_t n = n0 + li; n < n1; n += ipi) {
         const int64_t base = (n * C + c) * HW;
         for (int j = j0; j < hw4; j += jstep) {
-          const float4 v = x2_ld4<XF>(x, base + 4 * j, xb);
+          const float4 v = x2_ld4<XF, true>(x, base + 4 * j, xb);
           const float d[4] = {v.x - shift, v.y - shift, v.z - shift, v.w - shift};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(BN2_T) void bn2d_fwd_stats_flat_k(X2 x, int64_t N, 
     for (int q = 0; q < B; ++q) {
       const int i = min(i0 + q * BN2_T, total - 1);   // clamped, unconditional: the loads batch
       const int im = i / hw4, gi = i - im * hw4;
-      v[q] = x2_ld4<XF>(x, ((n0 + im) * C + c) * (int64_t)HW + 4 * gi, xb);
+      v[q] = x2_ld4<XF, true>(x, ((n0 + im) * C + c) * (int64_t)HW + 4 * gi, xb);
     }
     float fa = 0.f, fb = 0.f;
 #pragma unroll
@@ -1369,8 +1369,8 @@ __global__ __launch_bounds__(256) void bn2d_apply_rows_k(X2 x, int64_t N, int64_
   float2 top[PW], bot[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
-    top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
-    bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
+    top[q] = x2_ld2<XF, true>(x, xo + 2 * q, xb);
+    bot[q] = x2_ld2<XF, true>(x, xo + W + 2 * q, xb);
   }
   float* yr = y + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
 #pragma unroll
@@ -1436,7 +1436,7 @@ __global__ __launch_bounds__(256) void bn2d_apply_k(X2 x, int64_t N, int64_t C, 
       const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
       const float xb = x2_bias<XF>(x, c);
       const int64_t xo = plane * HW + (int64_t)(2 * ph) * W + 2 * pw;
-      y[i] = bn2_window(x2_ld2<XF>(x, xo, xb), x2_ld2<XF>(x, xo + W, xb), k, hardtanh).out;
+      y[i] = bn2_window(x2_ld2<XF, true>(x, xo, xb), x2_ld2<XF, true>(x, xo + W, xb), k, hardtanh).out;
     }
     return;
   }
@@ -1444,7 +1444,7 @@ __global__ __launch_bounds__(256) void bn2d_apply_k(X2 x, int64_t N, int64_t C, 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const int64_t c = ((4 * i) / HW) % C;
     const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
-    const float4 xv = x2_ld4<XF>(x, 4 * i, x2_bias<XF>(x, c));
+    const float4 xv = x2_ld4<XF, true>(x, 4 * i, x2_bias<XF>(x, c));
     float v[4] = {fmaf((xv.x - k.mu) * k.is, k.ga, k.be), fmaf((xv.y - k.mu) * k.is, k.ga, k.be),
                   fmaf((xv.z - k.mu) * k.is, k.ga, k.be), fmaf((xv.w - k.mu) * k.is, k.ga, k.be)};
     if (hardtanh) {

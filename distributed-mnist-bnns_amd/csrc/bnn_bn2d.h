@@ -57,7 +57,36 @@ __device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
 }
 
 // 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
-template <int XF>
+// The BatchNorm2d FORWARD passes read the compact (int8 / int16) conv outputs with device-scope loads
+// (COH = true).  With plain loads those passes returned different statistics from run to run --
+// never in one process alone, but in about one step in ten while other processes used the same
+// GPU (the two-rank data-parallel tests run that way) -- although every kernel of the sequence
+// waits for its loads, and a host synchronisation before and between the passes and an eviction of
+// every L2 did not change it; device-scope loads did (0 of 156 steps, plain 11 of 156;
+// tools/race_trace.py, profiles/r05_race_*.log).  The backward passes keep plain loads
+// (every stage after the forward was identical once the forward was).  BN2_PLAIN_LOADS builds the
+// plain form everywhere (A/B only).
+template <bool COH>
+__device__ __forceinline__ uint2 x2_raw8(const void* p) {
+#ifndef BN2_PLAIN_LOADS
+  if constexpr (COH) {
+    const uint64_t v =
+        __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+  }
+#endif
+  return *reinterpret_cast<const uint2*>(p);
+}
+template <bool COH>
+__device__ __forceinline__ uint32_t x2_raw4(const void* p) {
+#ifndef BN2_PLAIN_LOADS
+  if constexpr (COH)
+    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+
+template <int XF, bool COH = false>
 __device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
@@ -66,14 +95,14 @@ __device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
     return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
                        (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
   } else {
-    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    const uint2 u = x2_raw8<COH>(reinterpret_cast<const int16_t*>(x.p) + idx);
     return make_float4((float)(int16_t)(u.x & 0xFFFF) + b, (float)(int16_t)(u.x >> 16) + b,
                        (float)(int16_t)(u.y & 0xFFFF) + b, (float)(int16_t)(u.y >> 16) + b);
   }
 }
 
 // 2 consecutive elements (idx even)
-template <int XF>
+template <int XF, bool COH = false>
 __device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
@@ -81,7 +110,7 @@ __device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
     const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
     return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
   } else {
-    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int16_t*>(x.p) + idx);
+    const uint32_t u = x2_raw4<COH>(reinterpret_cast<const int16_t*>(x.p) + idx);
     return make_float2((float)(int16_t)(u & 0xFFFF) + b, (float)(int16_t)(u >> 16) + b);
   }
 }

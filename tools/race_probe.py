@@ -4,6 +4,8 @@ gradient (and the loss) with its first repetition, bit for bit.  A kernel with a
 barrier, an LDS hazard) that single-process scheduling hides shows up here as differing elements.
 
     python tools/race_probe.py [processes] [repetitions] [kinds...]
+
+RACE_PROBE_FLAGS="C1BN=0,ZQ=0" sets functional's switches of those names before the runs.
 """
 import os
 import sys
@@ -33,6 +35,10 @@ def _worker(rank, reps, kinds, q):
     try:
         sys.path.insert(0, PKG)
         torch.cuda.set_device(0)
+        from bnn_amd import functional as BF
+        for kv in filter(None, os.environ.get("RACE_PROBE_FLAGS", "").split(",")):
+            k, v = kv.split("=")
+            setattr(BF, k, bool(int(v)))
         lines = []
         for kind in kinds:
             batch = KINDS[kind]
