@@ -101,6 +101,7 @@ class GradExchange:
         self._next = 0
         self._handles = []
         self._armed = set()        # weights whose zeroed bucket view a layer may overwrite
+        self._counted = set()      # params already counted toward their buckets this step
         self.direct_write = direct_write
         self.direct_writes = 0     # gradients written straight into their views (tests, logs)
         for p in params:
@@ -220,6 +221,7 @@ class GradExchange:
             b.work = None
         self._next = 0
         self.launch_log = []
+        self._counted = set()
         if self.direct_write:
             self._armed = {id(p) for _, plist, _ in self._flats for p in plist}
 
@@ -234,6 +236,17 @@ class GradExchange:
         """p's gradient was written into its view by the layer (what the accumulate hook reports)."""
         self._armed.discard(id(p))
         self.direct_writes += 1
+        self._count(p)
+
+    def _count(self, p):
+        """p's gradient is complete in its view: count it toward its buckets ONCE per step.  A weight
+        written by its layer gets no gradient from autograd, but torch still runs its post-accumulate
+        hook (with nothing accumulated): counted twice, its bucket would be all-reduced before the
+        parameters after it in backward order had their gradients (config 2's fc1.bias,
+        tools/ddp_config2_diag.py, profiles/r05_ddp_config2_hook_order.log)."""
+        if id(p) in self._counted:
+            return
+        self._counted.add(id(p))
         for bi in self._param_buckets[p]:
             self.buckets[bi].pending -= 1
         self._launch_ready()
@@ -250,9 +263,7 @@ class GradExchange:
     def _make_hook(self, bucket_ids):
         def hook(p):
             self._armed.discard(id(p))
-            for bi in bucket_ids:
-                self.buckets[bi].pending -= 1
-            self._launch_ready()
+            self._count(p)
         return hook
 
     def _launch_ready(self):

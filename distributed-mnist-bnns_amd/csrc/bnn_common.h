@@ -26,6 +26,24 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+
+// GEMM epilogue output stores, non-temporal (the nt bit: streamed, not kept in the caches): the big
+// GEMMs' outputs (1-2 GB per launch) are far beyond the 256 MB MALL, and the streamed stores drain
+// faster -- pixel GEMM 1188 -> 993 us, FP4 2136 -> 2034, FP6 dX 8572 -> 8476, dW 6808 -> 6760 --
+// against +111 us in the pass that reads the pixel GEMM's output next: wide step 47.2 -> 46.6 ms
+// (profiles/r05_z_wide_{default,nt}.log).  BNN_NT_STORES=0 builds the plain stores (A/B).
+#ifndef BNN_NT_STORES
+#define BNN_NT_STORES 1
+#endif
+__device__ __forceinline__ void out_store4f(float* p, float4 v) {
+  if (BNN_NT_STORES) __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
+  else *reinterpret_cast<float4*>(p) = v;
+}
+__device__ __forceinline__ void out_store2u(void* p, uint32_t lo, uint32_t hi) {
+  if (BNN_NT_STORES) __builtin_nontemporal_store(v2u{lo, hi}, reinterpret_cast<v2u*>(p));
+  else *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+}
 
 // Ternary sign as used by the reference (models/binarized_modules.py:13, Tensor.sign()):
 // +1 for x>0, -1 for x<0, 0 for x==0 (NaN maps to 0 here; the reference would propagate NaN).

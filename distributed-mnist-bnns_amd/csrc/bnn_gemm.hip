@@ -785,8 +785,8 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
           if (c0 < p.N) {
             const int s0 = __float_as_int(v.x), s1 = __float_as_int(v.y), s2 = __float_as_int(v.z),
                       s3 = __float_as_int(v.w);
-            *reinterpret_cast<uint2*>(p.S20lo + o) =
-                make_uint2(((uint32_t)s0 & 0xFFFFu) | ((uint32_t)s1 << 16), ((uint32_t)s2 & 0xFFFFu) | ((uint32_t)s3 << 16));
+            out_store2u(p.S20lo + o, ((uint32_t)s0 & 0xFFFFu) | ((uint32_t)s1 << 16),
+                        ((uint32_t)s2 & 0xFFFFu) | ((uint32_t)s3 << 16));
             *reinterpret_cast<uint16_t*>(p.S20hi + (o >> 1)) =
                 (uint16_t)((((uint32_t)s0 >> 16) & 0xFu) | ((((uint32_t)s1 >> 16) & 0xFu) << 4) |
                            ((((uint32_t)s2 >> 16) & 0xFu) << 8) | ((((uint32_t)s3 >> 16) & 0xFu) << 12));
@@ -798,7 +798,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
           if (c0 + 3 < p.N) {
             const uint32_t lo = (uint32_t)(uint16_t)(int16_t)v.x | ((uint32_t)(uint16_t)(int16_t)v.y << 16);
             const uint32_t hi = (uint32_t)(uint16_t)(int16_t)v.z | ((uint32_t)(uint16_t)(int16_t)v.w << 16);
-            *reinterpret_cast<uint2*>(d16) = make_uint2(lo, hi);
+            out_store2u(d16, lo, hi);
           } else {
             const float vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -812,7 +812,7 @@ __device__ __forceinline__ void gemm_v2_body(const GemmParams& p) {
         if (p.M > 0) continue;
 #endif
         if (vec_ok && c0 + 3 < p.N) {
-          *reinterpret_cast<float4*>(dst) = v;
+          out_store4f(dst, v);
         } else {
           const float vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

@@ -838,7 +838,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
         if (row >= p.M) continue;
         float* dst = Cout + (int64_t)row * ldo + c0;
         if (vec_ok && c0 + 3 < p.N) {
-          *reinterpret_cast<float4*>(dst) = v;
+          out_store4f(dst, v);
         } else {
           const float vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

@@ -171,3 +171,80 @@ def test_shard_indices_match_distributed_sampler_golden():
         if n >= 1000:
             got = got[:64]
         np.testing.assert_array_equal(got, want)
+
+
+def _worker_direct_write_count(rank, world, port, q):
+    """A weight whose gradient a layer writes straight into its bucket view (direct_write): torch
+    still runs that weight's post-accumulate hook (nothing accumulated), and the bucket must not be
+    counted complete until every OTHER parameter in it has its gradient -- here the bias used
+    before the layer in forward, i.e. after it in backward."""
+    try:
+        for p in (ROOT, PKG):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from bnn_amd.parallel import GradExchange
+
+        class Net(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.b = torch.nn.Parameter(torch.randn(8))
+                self.w = torch.nn.Parameter(torch.randn(4, 8))
+
+        ex_box = []
+
+        class Written(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, x, w):
+                ctx.save_for_backward(x, w)
+                ctx.w = w
+                return x @ w.t()
+
+            @staticmethod
+            def backward(ctx, g):
+                x, w = ctx.saved_tensors
+                ex = ex_box[0]
+                sink = ex.grad_sink(ctx.w)
+                assert sink is not None
+                sink.copy_(g.t() @ x)
+                ex.grad_written(ctx.w)
+                return g @ w, None
+
+        torch.manual_seed(3)
+        net = Net()
+        seen = []
+        # registered before the exchange's own hooks, so it runs first: the bucket holding b must
+        # not have been launched yet when b's gradient has just been accumulated
+        net.b.register_post_accumulate_grad_hook(lambda p: seen.append(len(ex_box[0].launch_log)))
+        ex = GradExchange(net, bucket_mb=1.0, force_collectives=True)
+        ex_box.append(ex)
+        assert len(ex.buckets) == 1
+        x = torch.randn(5, 8)
+        for step in range(2):
+            ex.zero_grad()
+            Written.apply(x + net.b, net.w).square().sum().backward()
+            ex.finish()
+            g = 2 * ((x + net.b.detach()) @ net.w.detach().t())
+            assert torch.allclose(net.w.grad, g.t() @ (x + net.b.detach()), rtol=1e-5, atol=1e-6), step
+            assert torch.allclose(net.b.grad, (g @ net.w.detach()).sum(0), rtol=1e-5, atol=1e-6), step
+        q.put((rank, {"seen": seen, "writes": ex.direct_writes}))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc()))
+
+
+def test_gradexchange_counts_direct_written_weight_once():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    p = ctx.Process(target=_worker_direct_write_count, args=(0, 1, port, q))
+    p.start()
+    rank, out = q.get(timeout=120)
+    p.join(timeout=60)
+    assert not isinstance(out, str), out
+    assert out["writes"] == 2
+    assert out["seen"] == [0, 0]          # the bucket was launched only after b's gradient
