@@ -474,6 +474,13 @@ def _placeholder(shape, device):
     return ph
 
 
+def _is_placeholder(t):
+    """t views the cached zero every hand-off placeholder is made of (a stride-0 gradient that is
+    NOT a placeholder -- e.g. sum()'s expanded ones -- is a legitimate dense-valued gradient)."""
+    z = _ZERO1.get(str(t.device))
+    return z is not None and t.data_ptr() == z.data_ptr()
+
+
 def _z16_carrier(y16, bias):
     global Z16_HANDOFFS
     Z16_HANDOFFS += 1
@@ -1245,7 +1252,7 @@ class BinaryConv2dFunction(torch.autograd.Function):
         binarize_input, stride, padding, dilation, groups = ctx.conf
         bn = _c1bn_take(dy)      # the BatchNorm2d backward's pooled gradient and statistics, if handed over
         if bn is None:
-            if dy.dim() == 4 and dy.numel() > 1 and dy.stride() == (0, 0, 0, 0):
+            if dy.dim() == 4 and dy.numel() > 1 and dy.stride() == (0, 0, 0, 0) and _is_placeholder(dy):
                 raise RuntimeError("a conv gradient placeholder lost its BatchNorm2d hand-off")
             dy = _c2d(dy)
         N, C, H, W = x.shape
@@ -1456,7 +1463,7 @@ def _dz_placeholder(M, C, device):
 
 def _q6_take_required(dy):
     pre = _q6_take(dy)
-    if pre is None and dy.dim() == 2 and dy.stride() == (0, 0):
+    if pre is None and dy.dim() == 2 and dy.stride() == (0, 0) and _is_placeholder(dy):
         raise RuntimeError("a z16 gradient placeholder lost its FP6 hand-off (was the pre-activation consumed twice?)")
     return pre
 
@@ -1540,7 +1547,7 @@ def _bn_bwd_i8c(x, dy, M, C, w, b, mean, invstd, mlo, dw, db, pre=None, s20=None
 def _i8c_take(dy):
     ent = getattr(dy, _I8C_ATTR, None)
     if ent is None:
-        if dy.dim() == 2 and dy.stride() == (0, 0):
+        if dy.dim() == 2 and dy.stride() == (0, 0) and _is_placeholder(dy):
             raise RuntimeError("a gradient placeholder lost its int8 column-digit hand-off")
         return None
     delattr(dy, _I8C_ATTR)
