@@ -838,6 +838,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
         if (row >= p.M) continue;
         float* dst = Cout + (int64_t)row * ldo + c0;
         if (vec_ok && c0 + 3 < p.N) {
+#ifdef GEMM6_DIAG_NOSTORE     // timing-only build: the epilogue without its global stores
+          if (p.M > 0) continue;
+#endif
           out_store4f(dst, v);
         } else {
           const float vs[4] = {v.x, v.y, v.z, v.w};
@@ -1140,6 +1143,7 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const bool split = need > 0 && work != nullptr && aligned16(work) && work_bytes >= need;
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
                 split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0, {}};
+
   if (ares) {   // the residual plane runs on the default tile (variant 7) with its own instance
     p.ares = ares;
     return launch6<2, 4, 2, 4, 2, 0, 2, 0, 0, 1>(p, S6(stream));
