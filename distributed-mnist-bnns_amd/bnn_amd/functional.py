@@ -1158,6 +1158,10 @@ def _c1bn_take(dy):
 # unset: the library's default.  Applied once, before the first conv forward (the forward decides
 # whether conv1 takes the BatchNorm2d hand-off, whose kernel depends on the same switch).
 _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
+# BNN_FP6_PERS=1 / 0: the FP6 GEMM's persistent default tile on / off (A/B timing); unset: the
+# library's default (on)
+if os.environ.get("BNN_FP6_PERS") is not None:
+    L.call("bnn_gemm_fp6_set_persistent", int(os.environ["BNN_FP6_PERS"] != "0"))
 
 
 def _conv_env():

@@ -35,6 +35,7 @@
 // The MFMA operand map (checked by tools/probes/probe_fp6.hip on MI355X): lane l holds row l%32,
 // k-block l/32 of the 64-k step, element j at bits 6j..6j+5; the lane's scale byte scales its 32.
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 
@@ -914,6 +915,217 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
   }
 }
 
+// Persistent form of the default 128 x 512 tile (variant 7; RES = 1 with the residual plane): one
+// workgroup per CU walks the tiles bid, bid + G, ... in the same XCD / raster order as the one-tile
+// grid, and its fp32 epilogue no longer holds the CU.  The four waves of wave row 1 issue every
+// global store of a tile (their own 32 x 32 patches and, through a separate LDS patch region, their
+// row-0 partners'); the four of wave row 0 never store.  gfx9 counts loads and stores in one
+// in-order vmcnt, so a wave waiting for its stage pieces also waits for every store issued before
+// them: the first S_LD stages of each tile are issued by the row-0 waves alone (and the next tile's
+// first stage during the current tile's last k-step), so the row-1 waves' stores drain under the
+// next tile's first S_LD k-steps; from stage S_LD on all eight waves share the staging again.  Same fragments, MFMAs and accumulation order as gemm_fp6_k<2, 4, 2, 4, 2>:
+// bit-identical C.  No bias, no split-K, no statistics (the host picks this form only then).
+template <int RES>
+__global__ __launch_bounds__(512, 2) void gemm_fp6_pers_k(Gemm6Params p) {
+  constexpr int WAVES_N = 4, WM = 2, WN = 4, NL = 4;     // NL loading waves (wave row 0)
+  constexpr int BM = 128, BN = 512;
+  constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_PAD = 1024, B_ST = BN * 32, R_ST = RES ? BM * 32 : 0;
+  constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST + R_ST;
+  constexpr int P_LO = LO_ST / 1024 / NL, P_HI = HI_ST / 1024 / NL, P_B = B_ST / 1024 / NL, P_R = R_ST / 1024 / NL;
+  static_assert(P_LO * NL * 1024 == LO_ST && P_HI * NL * 1024 == HI_ST && P_B * NL * 1024 == B_ST, "piece split");
+  static_assert(R_ST / 1024 <= NL, "residual pieces: at most one per loading wave");
+  // the first S_LD stages of a tile are issued by the loading waves alone (the storing waves' vmcnt
+  // holds the previous tile's stores); from stage S_LD on every wave issues its one-tile share
+  constexpr int S_LD = 16;
+  using NLt = std::integral_constant<int, NL>;
+  using NWt = std::integral_constant<int, 8>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * ST + 8 * 4096];
+  float* const patches = reinterpret_cast<float*>(smem + 2 * ST);   // one 32 x 32 fp32 patch per wave
+
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const bool loader = wm == 0;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t nblk = p.K / QB;
+  const int nk = p.K / 64, ntiles = p.gm * p.gn, G = (int)gridDim.x;
+  int L = (int)blockIdx.x;
+  if (L >= ntiles) return;
+
+  // Stage issue (loading waves).  The host takes this form only for M % 128 == 0, N % 512 == 0 and B
+  // in the panel layout, so no row is clamped: each piece's per-lane offset (row in tile and the
+  // XOR-swizzled 16-B chunk) is a function of the lane alone, formed at issue from an opaque copy of
+  // the lane index (so it is not hoisted into 11 registers held across the k loop), and the stage
+  // bases are formed from (m0, n0, kt) in scalar registers -- the persistent loop has neither VGPRs
+  // nor SGPRs to spare beside the 128 accumulators.
+  const int64_t b_step = FP4_PANEL * 32;
+  // NI = the number of waves issuing the stage (NL: the loading waves alone; NW: all eight, each a
+  // one-tile share); wi = this wave's index among them
+  auto stage = [&](auto ni_tag, int m0, int n0, int kt, int buf) __attribute__((always_inline)) {
+    constexpr int NI = decltype(ni_tag)::value;
+    constexpr int I_R = R_ST / 1024;
+    constexpr int Q_LO = LO_ST / 1024 / NI, Q_HI = HI_ST / 1024 / NI, Q_B = B_ST / 1024 / NI, Q_R = (I_R + NI - 1) / NI;
+    const int wi = wave;
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    char* base = smem + buf * ST;
+    const uint8_t* lo_b = p.alo + (int64_t)m0 * nblk * 64 + (int64_t)kt * 128;
+    const uint8_t* hi_b = p.ahi + (int64_t)m0 * nblk * 32 + (int64_t)kt * 64;
+    const uint8_t* b_b = p.b + ((int64_t)(n0 / FP4_PANEL) * p.bks + kt) * b_step + (n0 % FP4_PANEL) * 32;
+#pragma unroll
+    for (int ii = 0; ii < Q_LO; ++ii) {
+      const int lrow = (wi + ii * NI) * 8 + (ln >> 3), c = ln & 7;
+      glds16_6s(lo_b, (uint32_t)lrow * (uint32_t)(nblk * 64) + 16u * (uint32_t)(c ^ ((lrow >> 1) & 7)),
+                base + (wi + ii * NI) * 1024);
+    }
+#pragma unroll
+    for (int ii = 0; ii < Q_HI; ++ii) {
+      const int lrow = (wi + ii * NI) * 16 + (ln >> 2), c = ln & 3;
+      glds16_6s(hi_b, (uint32_t)lrow * (uint32_t)(nblk * 32) + 16u * (uint32_t)(c ^ ((lrow >> 2) & 3)),
+                base + LO_ST + (wi + ii * NI) * 1024);
+    }
+#pragma unroll
+    for (int ii = 0; ii < Q_B; ++ii) {
+      const int lrow = (wi + ii * NI) * 32 + (ln >> 1), c = ln & 1;
+      glds16_6s(b_b, (uint32_t)lrow * 32u + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1)),
+                base + LO_ST + HI_ST + SC_PAD + (wi + ii * NI) * 1024);
+    }
+    if (wave == 0) glds16_6(p.asc + (int64_t)m0 * 2 + (int64_t)kt * p.asc_rows * 2 + ln * 16, base + LO_ST + HI_ST);
+    if constexpr (RES) {
+      const uint8_t* r_b = p.ares + (int64_t)m0 * nblk * 16 + (int64_t)kt * 32;
+#pragma unroll
+      for (int ii = 0; ii < Q_R; ++ii) {
+        if (wi + ii * NI >= I_R) continue;   // the residual's pieces: one per wave of the first I_R
+        const int lrow = (wi + ii * NI) * 32 + (ln >> 1), c = ln & 1;
+        glds16_6s(r_b, (uint32_t)lrow * (uint32_t)(nblk * 16) + 16u * (uint32_t)(c ^ ((lrow >> 3) & 1)),
+                  base + LO_ST + HI_ST + SC_PAD + B_ST + (wi + ii * NI) * 1024);
+      }
+    }
+  };
+
+  int tm, tn;
+  tile6_of(L, p.gm, p.gn, p.group, tm, tn);
+  if (loader) stage(NLt{}, tm * BM, tn * BN, 0, 0);
+  int gk = 0;   // k-steps run so far (the ring slot of step kt of this tile is gk & 1)
+  const bool vec_ok = ((p.ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(p.C) & 15) == 0);
+  for (;;) {
+    v16f acc[WM][WN];
+#pragma unroll
+    for (int t = 0; t < WM; ++t)
+#pragma unroll
+      for (int u = 0; u < WN; ++u) acc[t][u] = v16f{0};
+    const int m0 = tm * BM, n0 = tn * BN;
+    int ntm = 0, ntn = 0;
+    const bool more = L + G < ntiles;
+    if (more) tile6_of(L + G, p.gm, p.gn, p.group, ntm, ntn);
+    for (int kt = 0; kt < nk; ++kt, ++gk) {
+      // this wave's pieces of stage kt; a storing wave issues pieces only from stage S_LD on, by when
+      // the previous tile's stores ahead of them in its vmcnt have drained
+      if (loader || kt >= S_LD) wait_vmcnt6<0>();
+      barrier6();
+      const int buf = gk & 1;
+      if (kt + 1 < nk) {
+        if (kt + 1 >= S_LD) stage(NWt{}, m0, n0, kt + 1, buf ^ 1);
+        else if (loader) stage(NLt{}, m0, n0, kt + 1, buf ^ 1);
+      } else if (more && loader) {
+        stage(NLt{}, ntm * BM, ntn * BN, 0, buf ^ 1);   // the next tile's first stage
+      }
+      const char* base = smem + buf * ST;
+      v4i bf[WN];
+      const char* sB = base + LO_ST + HI_ST + SC_PAD;
+#pragma unroll
+      for (int u = 0; u < WN; ++u) {
+        const int lrow = wn * WN * 32 + u * 32 + r;
+        bf[u] = *reinterpret_cast<const v4i*>(sB + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
+      }
+#pragma unroll
+      for (int t = 0; t < WM; ++t) {
+        const int lrow = wm * WM * 32 + t * 32 + r;
+        const char* sLo = base;
+        const char* sHi = base + LO_ST;
+        const uint8_t* sSc = reinterpret_cast<const uint8_t*>(base + LO_ST + HI_ST);
+        const int sw = (lrow >> 1) & 7;
+        const v4i l0 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 0) ^ sw));
+        const v4i l1 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 1) ^ sw));
+        const v4i l2 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 2) ^ sw));
+        const v4i l3 = *reinterpret_cast<const v4i*>(sLo + lrow * 128 + 16 * ((h * 4 + 3) ^ sw));
+        const v4i h01 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2) ^ ((lrow >> 2) & 3)));
+        const v4i h23 = *reinterpret_cast<const v4i*>(sHi + lrow * 64 + 16 * ((h * 2 + 1) ^ ((lrow >> 2) & 3)));
+        const v8i a0 = v8i{l0.x, l0.y, l0.z, l0.w, h01.x, h01.y, 0, 0};
+        const v8i a1 = v8i{l1.x, l1.y, l1.z, l1.w, h01.z, h01.w, 0, 0};
+        const v8i a2 = v8i{l2.x, l2.y, l2.z, l2.w, h23.x, h23.y, 0, 0};
+        const v8i a3 = v8i{l3.x, l3.y, l3.z, l3.w, h23.z, h23.w, 0, 0};
+        const int sb = sSc[lrow * 2 + h];
+        v4i rr = v4i{0, 0, 0, 0};
+        if constexpr (RES)
+          rr = *reinterpret_cast<const v4i*>(base + LO_ST + HI_ST + SC_PAD + B_ST + lrow * 32 + 16 * (h ^ ((lrow >> 3) & 1)));
+        const int s0 = sb, s1 = sb == 255 ? 255 : sb + 5, s2 = sb == 255 ? 255 : sb + 10, s3 = sb == 255 ? 255 : sb + 15;
+        const int sr = sb == 255 ? 255 : (sb >= 5 ? sb - 5 : 0);
+#pragma unroll
+        for (int u = 0; u < WN; ++u) {
+          const v8i bb = {bf[u].x, bf[u].y, bf[u].z, bf[u].w, 0, 0, 0, 0};
+          acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a3, bb, acc[t][u], 2, 4, 0, s3, 0, 127);
+          acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a2, bb, acc[t][u], 2, 4, 0, s2, 0, 127);
+          acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, bb, acc[t][u], 2, 4, 0, s1, 0, 127);
+          acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, bb, acc[t][u], 2, 4, 0, s0, 0, 127);
+          if constexpr (RES) {
+            const v8i ar = {rr.x, rr.y, rr.z, rr.w, 0, 0, 0, 0};
+            acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ar, bb, acc[t][u], 4, 4, 0, sr, 0, 127);
+          }
+        }
+      }
+    }
+    // epilogue: every wave transposes its 32 x 32 patches through its own slot of the patch region
+    // (the ring holds the next tile's first stage); the storing wave of each column group writes its
+    // partner's patch (rows 0..63 of the tile) and its own (rows 64..127) as 16-B row segments
+    float* const mine = patches + wave * 1024;
+    float* const partner = patches + (wave - NL) * 1024;   // storing waves only
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int tcol0 = n0 + wn * WN * 32 + u * 32;
+#pragma unroll
+      for (int t = 0; t < WM; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int lr = (i & 3) + 8 * (i >> 2) + 4 * h;
+          mine[lr * 32 + ((((r >> 2) ^ (lr & 7)) << 2) | (r & 3))] = acc[t][u][i];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier6();
+        if (!loader) {
+          const int c4 = lane & 7;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const float* src = half ? mine : partner;
+            const int trow0 = m0 + half * WM * 32 + t * 32;
+#pragma unroll
+            for (int ps = 0; ps < 4; ++ps) {
+              const int lr = (lane >> 3) + 8 * ps;
+              const float4 v = *reinterpret_cast<const float4*>(src + lr * 32 + ((c4 ^ (lr & 7)) << 2));
+              const int row = trow0 + lr, c0 = tcol0 + 4 * c4;
+              if (row >= p.M) continue;
+              float* dst = p.C + (int64_t)row * p.ldc + c0;
+              if (vec_ok && c0 + 3 < p.N) {
+                out_store4f(dst, v);
+              } else {
+                const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (c0 + j < p.N) dst[j] = vs[j];
+              }
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        barrier6();   // the slots are free for the next patch
+      }
+    }
+    if (!more) break;
+    L += G;
+    tm = ntm;
+    tn = ntn;
+  }
+}
+
 // C = bias + sum over splits of the partials, in split order (deterministic); float4 per thread
 __global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restrict__ part, int S, int64_t M, int64_t N,
                                                           const float* __restrict__ bias, float* __restrict__ C,
@@ -951,6 +1163,21 @@ int launch6(Gemm6Params p, hipStream_t s) {
     hipLaunchKernelGGL(gemm6_splitk_sum_k, dim3((unsigned)(((int64_t)p.M * p.N / 4 + 255) / 256)), dim3(256), 0, s,
                        p.part, p.ksplit, (int64_t)p.M, (int64_t)p.N, p.bias, p.C, p.ldc);
   return check_launch("bnn_gemm_fp6");
+}
+
+// The persistent form (gemm_fp6_pers_k) for grids of at least two rounds, no bias / split-K: measured
+// slower than one workgroup per tile on both backward shapes (dX 8.52 vs 8.60 ms with the row-0
+// waves staging every stage, dW 7.2-7.3 vs 6.85-6.89; sharing the staging again after the first 16
+// k-steps: dX 9.27, dW 7.80 -- profiles/r05_fp6_persistent_ab.log), so off by default (A/B switch).
+int g_fp6_pers = 0;
+
+template <int RES>
+int launch6_pers(Gemm6Params p, int ncu, hipStream_t s) {
+  p.gm = (p.M + 127) / 128;
+  p.gn = (p.N + 511) / 512;
+  const int ntiles = p.gm * p.gn;
+  hipLaunchKernelGGL((gemm_fp6_pers_k<RES>), dim3((unsigned)std::min(ntiles, ncu)), dim3(512), 0, s, p);
+  return check_launch("bnn_gemm_fp6 (persistent)");
 }
 
 struct Variant6 {
@@ -1144,11 +1371,25 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
                 split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0, {}};
 
+  // the persistent form of the default tile: no bias, whole K per tile, at least two rounds of tiles
+  const int64_t tiles = ((M + 127) / 128) * ((N + 511) / 512);
+  const bool pers = g_fp6_pers && bias == nullptr && p.ksplit == 1 && g_variant6 < 0 && tiles >= 2 * device_cus() &&
+                    panel && M % 128 == 0 && N % 512 == 0;
   if (ares) {   // the residual plane runs on the default tile (variant 7) with its own instance
     p.ares = ares;
+    if (pers) return launch6_pers<1>(p, device_cus(), S6(stream));
     return launch6<2, 4, 2, 4, 2, 0, 2, 0, 0, 1>(p, S6(stream));
   }
+  if (pers && pl.v->id == 7) return launch6_pers<0>(p, device_cus(), S6(stream));
   return pl.v->fn(p, S6(stream));
+}
+
+// 1 (default): the FP6 GEMM's default tile runs persistent with split load / store roles on grids
+// of two or more rounds (gemm_fp6_pers_k); 0: one workgroup per tile.  on < 0 queries.
+BNN_API int bnn_gemm_fp6_set_persistent(int32_t on) {
+  if (on < 0) return g_fp6_pers;
+  g_fp6_pers = on != 0;
+  return 0;
 }
 
 BNN_API int64_t bnn_fp4_panel_bytes(int64_t N, int64_t Kp) {
@@ -1222,6 +1463,10 @@ BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, 
 BNN_API const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K) {
   const Fp6Plan pl = plan6(M, N, K);
   static thread_local char buf[96];
+  // the persistent form where the shape takes it (no bias, B in panels: the backward GEMMs)
+  if (pl.ksplit <= 1 && g_fp6_pers && g_variant6 < 0 && M % 128 == 0 && N % 512 == 0 &&
+      (M / 128) * (N / 512) >= 2 * device_cus())
+    return "gemm_fp6_pers_k<2, 4, 2, 4, 2>";
   if (pl.ksplit <= 1) return pl.v->name;
   snprintf(buf, sizeof buf, "%s split-K %d", pl.v->name, pl.ksplit);
   return buf;

@@ -266,6 +266,12 @@ int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
 const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
+/* 1: on grids of >= 2 rounds of 128 x 512 tiles with no bias, M % 128 == 0, N % 512 == 0 and B in
+ * panels (the backward GEMMs), the default tile runs persistent -- one workgroup per CU, the waves
+ * split into loading and storing roles so a tile's fp32 stores drain under the next tile's k loop
+ * (gemm_fp6_pers_k); bit-identical to 0 (one workgroup per tile, the default: measured faster).
+ * on < 0 queries. */
+int bnn_gemm_fp6_set_persistent(int32_t on);
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row

@@ -243,3 +243,41 @@ def test_fp4_panels_and_panel_gemm(F, M, N, K):
     assert np.array_equal(C_pan, C_rows)
     val, _, _ = decode(op, M)
     assert rel_err(C_pan, val[:, :K] @ w.astype(np.float64).T + host(bt)) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 4096, 1024), (16512, 4096, 1088), (8192, 8192, 4096)])
+@pytest.mark.parametrize("res", [True, False])
+def test_fp6_persistent_gemm_bit_identical(F, M, N, K, res):
+    """The persistent form of the default tile (gemm_fp6_pers_k: one workgroup per CU, loading and
+    storing waves split so a tile's stores drain under the next tile's k loop; an A/B switch, off by
+    default) against one workgroup per tile: C bit-identical, with and without the residual plane; grids of
+    4-5 tiles per workgroup, an uneven tile count (129 tile rows) and an odd number of k-steps (17:
+    the two-slot ring's parity carries across tiles), and within 2e-6 of the float64 product of the
+    decoded operand."""
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M + N + K + res)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-3, 3, (M, 1)))).astype(np.float32)
+    w = rng.integers(-1, 2, (N, K)).astype(np.float32)
+    w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
+    P = F.fp4_panels(w4, N, K)
+    op = F.quant6_rows(torch.as_tensor(x).cuda())
+    if not res:
+        op.res = None
+    prev = L.lib().bnn_gemm_fp6_set_persistent(-1)
+    ks = P.numel() // (((N + 511) // 512) * 512 * 32)
+    try:
+        L.call("bnn_gemm_fp6_set_persistent", 1)
+        assert "pers" in L.lib().bnn_gemm_fp6_kernel_k(M, N, op.Kp).decode()
+        C1 = F.gemm_fp6(op, None, N, panels=P, panel_ks=ks)
+        L.call("bnn_gemm_fp6_set_persistent", 0)
+        assert "pers" not in L.lib().bnn_gemm_fp6_kernel_k(M, N, op.Kp).decode()
+        C0 = F.gemm_fp6(op, None, N, panels=P, panel_ks=ks)
+        torch.cuda.synchronize()
+    finally:
+        L.call("bnn_gemm_fp6_set_persistent", prev)
+    assert torch.equal(C0, C1)
+    op_head = F.quant6_rows(torch.as_tensor(x[:2048]).cuda())      # rows quantise independently
+    if not res:
+        op_head.res = None
+    val, _, _ = decode(op_head, 2048, residual=res)
+    assert rel_err(host(C1)[:2048], val[:, :K] @ w.astype(np.float64).T) < 2e-6
