@@ -86,7 +86,9 @@ def op_peak(kernel):
     if kernel.startswith("gemm_fp4"):
         return "mfma", MI355X_FP4_DENSE_TOPS, "ternary GEMM ops 2*M*N*K on the FP4 MFMA"
     if kernel.startswith("gemm_fp6"):   # same f8f6f4 MFMA, FP6 x FP4 issues at the FP4 rate
-        return "mfma", MI355X_FP4_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the FP6 x FP4 MFMA (4 digit planes)"
+        passes = ("4 FP6 digit planes + the FP4 residual plane: 5 MFMA passes" if kernel.endswith(" +res")
+                  else "4 FP6 digit planes: 4 MFMA passes")
+        return "mfma", MI355X_FP4_DENSE_TOPS, f"algorithmic GEMM ops 2*M*N*K on the FP6 x FP4 MFMA ({passes})"
     if kernel.startswith("gemm_xnor"):   # VALU popcount bound with the nonzero-mask plane
         return "valu", MI355X_XNOR_TOPS, "ternary popcount ops 2*M*N*K"
     return "mfma", MI355X_INT8_DENSE_TOPS, "algorithmic GEMM ops 2*M*N*K on the int8 MFMA"
@@ -257,6 +259,10 @@ def pmc_traffic(kernel):
     the call's kernels over the number of calls.  None when no pass covers the kernel."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    # a timer name "<kernel> +res" is the RES = 1 instance of the FP6 GEMM template (last parameter 1)
+    res = kernel.endswith(" +res")
+    if res:
+        kernel = kernel[:-len(" +res")]
     prefix = kernel.rstrip(">")
     for f in reversed(files):
         try:
@@ -275,9 +281,12 @@ def pmc_traffic(kernel):
             if calls:
                 return int(total / calls), os.path.relpath(f, ROOT)
             continue
-        for name, v in ks.items():
-            if name == kernel or (name.startswith(prefix) and name[len(prefix):len(prefix) + 1] in (",", ">")):
-                return v["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+        hits = [(name, v) for name, v in ks.items()
+                if name == kernel or (name.startswith(prefix) and name[len(prefix):len(prefix) + 1] in (",", ">"))]
+        if kernel.startswith("gemm_fp6_k") and len(hits) > 1:   # the instance with / without the residual plane
+            hits = [(n, v) for n, v in hits if n.endswith(", 1>") == res] or hits
+        if hits:
+            return hits[0][1]["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
 
