@@ -92,19 +92,21 @@ SIGNATURES = {
     "bnn_bn2d_bwd_q": (I32, [P, P, I32, P, I64, I64, I64, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "bnn_conv2d_fwd_q": (I32, [P, P, P, I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, P]),
     "bnn_conv2d_fwd_q_ok": (I32, [I32, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32]),
-    "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P]),
+    "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P, P]),
+    "bnn_dropout_keep_bits_bytes": (I64, [I64, I64]),
+    "bnn_bn_set_head_reduce_cols": (I32, [I32]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),
     "bnn_bn_head_workspace": (I64, [I64, I64, I32]),
-    "bnn_bn_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
-    "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "bnn_bn_head_fwd": (I32, [P, I64, I64, P, P, P, P, P, F32, U64, P, P, I32, P, P, P]),
+    "bnn_bn_head_bwd_q6": (I32, [P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_bn_apply_pack": (I32, [P, I64, I64, P, P, P, P, P, I32, P, I64, P, I64, I32, P]),
-    "bnn_bn_fwd_train_i16": (I32, [P, P, I64, I64, P, P, P, P, F32, F32, P, P, P, F32, U64, P, P]),
+    "bnn_bn_fwd_train_i16": (I32, [P, P, I64, I64, P, P, P, P, F32, F32, P, P, P, F32, U64, P, P, P]),
     "bnn_bn_apply_pack_i16": (I32, [P, P, I64, I64, P, P, P, P, P, P, I64, P, I64, I32, P]),
     "bnn_bn_bwd_q6_i16": (I32, [P, P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
-    "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, I32, P, P, P]),
-    "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "bnn_bn_head_fwd_i16": (I32, [P, P, I64, I64, P, P, P, P, P, F32, U64, P, P, I32, P, P, P]),
+    "bnn_bn_head_bwd_q6_i16": (I32, [P, P, P, P, I32, I64, I64, P, P, P, P, P, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_bn_bwd_i8cols_workspace": (I64, [I64, I64]),
     "bnn_bn_bwd_i8cols": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),
     "bnn_bn_bwd_i8cols_pre": (I32, [P, P, I64, I64, P, P, P, P, P, I32, P, P, P, I64, I64, P, P, P, P, P]),

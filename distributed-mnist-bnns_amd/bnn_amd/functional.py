@@ -1158,10 +1158,13 @@ def _c1bn_take(dy):
 # unset: the library's default.  Applied once, before the first conv forward (the forward decides
 # whether conv1 takes the BatchNorm2d hand-off, whose kernel depends on the same switch).
 _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
-# BNN_FP6_PERS=1 / 0: the FP6 GEMM's persistent default tile on / off (A/B timing); unset: the
-# library's default (on)
+# BNN_FP6_PERS=1 / 0: the FP6 GEMM's persistent tile on / off (A/B timing); unset: the library's
+# default (off)
 if os.environ.get("BNN_FP6_PERS") is not None:
     L.call("bnn_gemm_fp6_set_persistent", int(os.environ["BNN_FP6_PERS"] != "0"))
+# BNN_HEAD_RED_COLS=2 / 4: columns per thread of the head's statistics pass (A/B timing)
+if os.environ.get("BNN_HEAD_RED_COLS") is not None:
+    L.call("bnn_bn_set_head_reduce_cols", int(os.environ["BNN_HEAD_RED_COLS"]))
 
 
 def _conv_env():
@@ -1628,7 +1631,8 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
         with _timed("bn_dropout_fwd_train", 0, 12 * M * C):
             L.call("bnn_bn_dropout_fwd_train", L.ptr(x), M, C, L.ptr(w), L.ptr(b), L.ptr(running_mean),
                    L.ptr(running_var), float(momentum if momentum is not None else -1.0), float(eps),
-                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(y), 1, float(p), int(seed), L.ptr(ws), L.stream())
+                   L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(y), 1, float(p), int(seed), None, L.ptr(ws),
+                   L.stream())
         ctx.save_for_backward(x, w, b, mean, invstd, mlo)
         ctx.p, ctx.seed = p, seed
         return y
@@ -1656,7 +1660,10 @@ class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
 
 
 HEAD_NOUT = 10
-HEAD_CALLS = 0            # fused drop->bn->htanh->fc heads run (tests check the path actually ran)
+HEAD_CALLS = 0
+# BNN_KEEP_BITS=0: the head passes evaluate the dropout hash themselves instead of reading the keep-bit
+# plane the statistics pass writes (A/B; identical masks either way)
+_KEEP_BITS = [os.environ.get("BNN_KEEP_BITS", "1") != "0"]            # fused drop->bn->htanh->fc heads run (tests check the path actually ran)
 
 
 class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
@@ -1682,32 +1689,37 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         mean, invstd, mlo = _bn_stat_buffers(C, z.device)
         mom = float(momentum if momentum is not None else -1.0)
         fs = _fstats_of(z, M, C, (float(p), int(seed)))
+        kb = None   # the dropout keep-bit plane: written by the statistics pass, read by the head passes
         if fs is not None and float(p) > 0:
             global FP4_STATS_USES
             FP4_STATS_USES += 1
             L.call("bnn_bn_fwd_final_parts", L.ptr(fs[0]), fs[1], fs[2], M, C, L.ptr(running_mean),
                    L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.stream())
         else:
+            if float(p) > 0 and _KEEP_BITS[0]:
+                kb = torch.empty((int(L.lib().bnn_dropout_keep_bits_bytes(M, C)) // 4,), dtype=torch.int32,
+                                 device=z.device)
             with _timed("bn_dropout_fwd_stats", 0, (4 if zz is None else 2) * M * C):
                 if zz is None:
                     L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(running_mean),
                            L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1,
-                           float(p), int(seed), L.ptr(ws), L.stream())
+                           float(p), int(seed), L.ptr(kb), L.ptr(ws), L.stream())
                 else:
                     L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb),
                            L.ptr(running_mean), L.ptr(running_var), mom, float(eps), L.ptr(mean), L.ptr(invstd),
-                           L.ptr(mlo), float(p), int(seed), L.ptr(ws), L.stream())
+                           L.ptr(mlo), float(p), int(seed), L.ptr(kb), L.ptr(ws), L.stream())
         w4c = w4.detach().contiguous()
         y4 = torch.empty((M, HEAD_NOUT), dtype=torch.float32, device=z.device)
         b4d = b4.detach() if b4 is not None else None
         with _timed("bn_head_fwd", 0, (4 if zz is None else 2) * M * C + 4 * M * HEAD_NOUT):
             if zz is None:
                 L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(mlo), L.ptr(gw),
-                       L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d), L.ptr(y4), L.stream())
+                       L.ptr(gb), float(p), int(seed), L.ptr(kb), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d), L.ptr(y4),
+                       L.stream())
             else:
                 L.call("bnn_bn_head_fwd_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(mean), L.ptr(invstd),
-                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), float(p), int(seed), L.ptr(w4c), HEAD_NOUT, L.ptr(b4d),
-                       L.ptr(y4), L.stream())
+                       L.ptr(mlo), L.ptr(gw), L.ptr(gb), float(p), int(seed), L.ptr(kb), L.ptr(w4c), HEAD_NOUT,
+                       L.ptr(b4d), L.ptr(y4), L.stream())
         if zz is None:
             ctx.save_for_backward(z, gw, gb, mean, invstd, mlo, w4c, None)
         else:
@@ -1715,6 +1727,7 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         ctx.z16 = zz is not None
         ctx.dims = (M, C)
         ctx.p, ctx.seed = p, seed
+        ctx.kb = kb
         ctx.has_b4 = b4 is not None
         return y4
 
@@ -1737,13 +1750,14 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
         with _timed("bn_head_bwd_q6", 0, (8 if ctx.z16 else 16) * M * C + (0 if ctx.z16 else 4) * M * C + 6 * M * C):
             if not ctx.z16:
                 L.call("bnn_bn_head_bwd_q6", L.ptr(z), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C, L.ptr(gw),
-                       L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed), L.ptr(dx),
+                       L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed),
+                       L.ptr(ctx.kb), L.ptr(dx),
                        L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
                        L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream())
             else:
                 L.call("bnn_bn_head_bwd_q6_i16", L.ptr(z), L.ptr(zb), L.ptr(dy4), L.ptr(w4c), HEAD_NOUT, M, C,
                        L.ptr(gw), L.ptr(gb), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), float(ctx.p), int(ctx.seed),
-                       None, L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
+                       L.ptr(ctx.kb), None, L.ptr(dgw), L.ptr(dgb), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi),
                        L.ptr(rows.sc), L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs),
                        L.ptr(ws), L.stream())
         if ctx.q6 or ctx.z16:
@@ -2000,8 +2014,8 @@ class BNHardtanhBinaryLinearFunction(torch.autograd.Function):
                            float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, L.ptr(ws), L.stream())
                 else:
                     L.call("bnn_bn_fwd_train_i16", L.ptr(zz[0]), L.ptr(zz[1]), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm),
-                           L.ptr(rv), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 0.0, 0, L.ptr(ws),
-                           L.stream())
+                           L.ptr(rv), mom, float(eps), L.ptr(mean), L.ptr(invstd), L.ptr(mlo), 0.0, 0, None,
+                           L.ptr(ws), L.stream())
         else:
             mean, mlo = rm.contiguous(), None
             invstd = (rv + eps).rsqrt()

@@ -49,14 +49,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // Drop, drop_hash, drop_resolve, g_seed_ctr: bnn_common.h (the FP4 statistics epilogue evaluates
 // the same mask)
 
-// keep bits of elements i0 .. i0+3 (bit j), evaluated once and applied to both the input and the
-// gradient where a pass needs both
-__device__ __forceinline__ uint32_t drop_bits4(const Drop& d, uint64_t i0) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) m |= (uint32_t)drop_keep(d, i0 + j) << j;
-  return m;
-}
+// drop_bits4 (bnn_common.h): keep bits of elements i0 .. i0+3, evaluated once and applied to both
+// the input and the gradient where a pass needs both
 
 __device__ __forceinline__ void drop4m(const Drop& d, uint32_t m, float (&v)[4]) {
   if (!d.on) return;
@@ -144,13 +138,16 @@ __global__ __launch_bounds__(256, RED_OCC) void bn_reduce_k(XIn xin, const float
       xv8[u] = xin_load4<XF>(xin, rr * C + c, xb);
       if constexpr (BWD) gb[u] = ld4(dy + rr * C + c);
     }
+    uint32_t kw = 0;   // MODE 0: the batch's keep bits (rows past the end stay 0)
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u;
       if (rr >= re) break;
       const float4 xv = xv8[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-      drop4(dp, (uint64_t)(rr * C + c), xs);
+      const uint32_t km = dp.on ? drop_bits4(dp, (uint64_t)(rr * C + c)) : 0u;
+      drop4m(dp, km, xs);
+      kw |= km << (4 * u);
       if (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -177,6 +174,9 @@ __global__ __launch_bounds__(256, RED_OCC) void bn_reduce_k(XIn xin, const float
         }
       }
     }
+    // the keep-bit plane (host: only with 8-row batches starting at multiples of 8)
+    if constexpr (MODE == 0 && RB == 8)
+      if (dp.bits_out != nullptr) dp.bits_out[keep_word(rb, c, C)] = kw;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -598,6 +598,12 @@ struct Q6StageSink {
 // initialised).
 __device__ __forceinline__ void q6_stage_store(const Q6Stage& st, const Q6Out& o, int t, int64_t m0, int64_t M,
                                                int64_t c0, int64_t nblk_c) {
+  // the per-lane store addresses are formed here, per call, from an opaque copy of the thread index:
+  // hoisted out of the sub-tile loop they are ~10 live 64-bit registers, which the head variant
+  // spilled -- and a spill reload waits (vmcnt) behind the next sub-tile's prefetched loads
+#ifndef Q6_STORE_HOIST   // A/B build knob: let the compiler hoist them
+  asm volatile("" : "+v"(t));
+#endif
   const int64_t blk0 = c0 / QB, mblk0 = m0 / QB;
 #pragma unroll
   for (int it = 0; it < 2; ++it) {            // lo: 512 chunks each
@@ -630,7 +636,7 @@ __device__ __forceinline__ void q6_stage_store(const Q6Stage& st, const Q6Out& o
 
 // NOUT > 0 (the fused head, bnn_bn_head_bwd_q6): dy is the head's output gradient dY4 [M][NOUT]
 // and the gradient reaching the BatchNorm is dY4 . W4, formed per element (W4 [NOUT][C]).
-template <int NOUT, bool Z16 = false>
+template <int NOUT, bool Z16 = false, bool KB = false>
 __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_OCC : 3)) void bn_bwd_apply_q6_k(XIn xin, const float* __restrict__ dy,
                                                          int64_t M, int64_t C, const float* __restrict__ mean,
                                                          const float* __restrict__ mean_lo,
@@ -690,12 +696,19 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   // software pipeline: sub-tile s+1's x (and dY) rows are loaded into registers before sub-tile s
   // is quantised, so their HBM latency hides behind the quantiser's VALU work
   constexpr int NI = Q6T_SUB / 16;
+  // a thread's NI rows of a sub-tile: the head's 4 consecutive rows (half of one keep-bit word of the
+  // forward's dropout mask), else rows 16 apart
+  constexpr bool RC4 = NOUT > 0;
+  static_assert(!KB || (RC4 && NI == 4), "keep bits: the head's row mapping (4 rows = half a word)");
+  auto row_of = [&](int i) __attribute__((always_inline)) { return RC4 ? NI * (t >> 4) + i : (t >> 4) + 16 * i; };
   XRaw<Z16> xr[NI];
   float4 gr[NOUT > 0 ? 1 : NI];
+  // KB: the sub-tile's keep-bit words (8-row groups x 16 column groups), staged in LDS with dY4
+  __shared__ uint32_t kbs[KB ? Q6T_SUB / 8 : 1][16];
   auto load_sub = [&](int64_t m0n) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int64_t r = m0n + (t >> 4) + 16 * i;
+      const int64_t r = m0n + row_of(i);
       if (m0n < mp && r < M) {
         xr[i] = xin_raw4<Z16>(xin, r * C + c);
         if constexpr (NOUT == 0) gr[i] = ld4(dy + r * C + c);
@@ -718,6 +731,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
         const int rr = i / D4LD, q = i - rr * D4LD;
         d4s[i] = (m0 + rr < M && q < NOUT) ? dy[(m0 + rr) * NOUT + q] : 0.f;
       }
+      if constexpr (KB) {
+        if (t < Q6T_SUB * 2) {
+          const int64_t r8 = m0 + 8 * (t >> 4);
+          kbs[t >> 4][t & 15] = r8 < M ? dp.bits[keep_word(r8, c0 + 4 * (t & 15), C)] : 0u;
+        }
+      }
       __syncthreads();
     }
     asm volatile("" ::: "memory");   // the table reads stay inside the loop
@@ -728,9 +747,11 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
     const float ga[4] = {gav.x, gav.y, gav.z, gav.w}, be[4] = {bev.x, bev.y, bev.z, bev.w};
     const float a0[4] = {a0v.x, a0v.y, a0v.z, a0v.w}, a1[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
+    // KB: this thread's 4 rows are one half of a keep-bit word
+    const uint32_t kb = KB ? kbs[(NI * (t >> 4)) >> 3][t & 15] >> (16 * ((t >> 4) & 1)) : 0u;
 #pragma unroll
     for (int i = 0; i < Q6T_SUB / 16; ++i) {
-      const int rr = (t >> 4) + 16 * i;
+      const int rr = row_of(i);
       const int64_t r = m0 + rr;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       float wc[NOUT > 0 ? NOUT : 1][4];     // the head's weight columns c..c+3, re-read per row (the
@@ -752,7 +773,9 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
           const float4 gv = gr[i];
           gs[0] = gv.x, gs[1] = gv.y, gs[2] = gv.z, gs[3] = gv.w;
         }
-        const uint32_t km = dp.on ? drop_bits4(dp, (uint64_t)(r * C + c)) : 0u;
+        uint32_t km = 0u;
+        if constexpr (KB) km = (kb >> (4 * i)) & 15u;
+        else if (dp.on) km = drop_bits4(dp, (uint64_t)(r * C + c));
         drop4m(dp, km, xs);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -763,10 +786,10 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
       const uint32_t a0b = abs_bits(v[0]), a1b = abs_bits(v[1]), a2b = abs_bits(v[2]), a3b = abs_bits(v[3]);
       atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
-      atomicMax(&cmax[i >> 1][cq], a0b);
-      atomicMax(&cmax[i >> 1][cq + 1], a1b);
-      atomicMax(&cmax[i >> 1][cq + 2], a2b);
-      atomicMax(&cmax[i >> 1][cq + 3], a3b);
+      atomicMax(&cmax[rr >> 5][cq], a0b);
+      atomicMax(&cmax[rr >> 5][cq + 1], a1b);
+      atomicMax(&cmax[rr >> 5][cq + 2], a2b);
+      atomicMax(&cmax[rr >> 5][cq + 3], a3b);
     }
     __syncthreads();
     Q6_STAMP(sub, 1);
@@ -828,12 +851,14 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
 // group (a pitch of 128 put W4's 10 rows on ONE bank: the head forward spent ~40 % of its time in
 // LDS bank conflicts, profiles/r04_pmc_bn.txt).  h3's stays 132 (float4 stores; 2-way on reads).
 constexpr int HD_ROWS = 64, HD_COLS = 128, HD_LD = HD_COLS + 4, HD_WLD = HD_COLS + 2;
-// elementwise map of a 64 x 128 chunk: thread -> 4 columns 4 (t % 32), rows t / 32 + 8 i
+// elementwise map of a 64 x 128 chunk: thread -> 4 columns 4 (t % 32), rows 8 (t / 32) + i (8
+// consecutive rows: one keep-bit word per chunk)
 constexpr int HD_CG = HD_COLS / 4, HD_RS = 256 / HD_CG, HD_NI = HD_ROWS / HD_RS;
+static_assert(HD_NI == 8, "a thread's rows are one keep-bit word");
 
 typedef float hf4 __attribute__((ext_vector_type(4)));
 
-template <int NOUT, bool Z16 = false>
+template <int NOUT, bool Z16 = false, bool KB = false>
 #ifndef HFWD_OCC
 #define HFWD_OCC 4             // waves per SIMD of the fused head's forward (z16 input)
 #endif
@@ -857,18 +882,22 @@ __global__ __launch_bounds__(256, Z16 ? HFWD_OCC : 2) void bn_head_fwd_k(XIn xin
   // normalised and multiplied (the pass is latency-bound otherwise); W4's columns and the BatchNorm
   // parameters of the chunk (L2-resident) are loaded at its top, ahead of the barrier
   XRaw<Z16> xn[HD_NI];
+  const int64_t rt = r0 + HD_NI * (t / HD_CG);   // this thread's first row
+  uint32_t kn = 0u;                               // its keep-bit word of the fetched chunk
   auto fetch_x = [&](int64_t c0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) {
-      const int64_t r = r0 + t / HD_CG + HD_RS * i;
+      const int64_t r = rt + i;
       if (r < M) xn[i] = xin_raw4<Z16>(xin, r * C + c0 + cq);
     }
+    if (KB && rt < M) kn = dp.bits[keep_word(rt, c0 + cq, C)];
   };
   fetch_x(0);
   for (int64_t c0 = 0; c0 < C; c0 += HD_COLS) {
     XRaw<Z16> xc[HD_NI];
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) xc[i] = xn[i];
+    const uint32_t kc = kn;
     if (c0 + HD_COLS < C) fetch_x(c0 + HD_COLS);
     const int64_t c = c0 + cq;
     const float4 xb = xin_bias4<Z16>(xin, c);
@@ -886,13 +915,14 @@ __global__ __launch_bounds__(256, Z16 ? HFWD_OCC : 2) void bn_head_fwd_k(XIn xin
     __syncthreads();   // the previous chunk's fragment reads are done
 #pragma unroll
     for (int i = 0; i < HD_NI; ++i) {
-      const int rr = t / HD_CG + HD_RS * i;
+      const int rr = HD_NI * (t / HD_CG) + i;
       const int64_t r = r0 + rr;
       float h[4] = {0.f, 0.f, 0.f, 0.f};
       if (r < M) {
         const float4 xv = xin_cvt4<Z16>(xc[i], xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-        drop4(dp, (uint64_t)(r * C + c), xs);
+        if constexpr (KB) drop4m(dp, (kc >> (4 * i)) & 15u, xs);
+        else drop4(dp, (uint64_t)(r * C + c), xs);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           h[j] = fminf(fmaxf(fmaf(((xs[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]), -1.f), 1.f);
@@ -927,7 +957,7 @@ __global__ __launch_bounds__(256, Z16 ? HFWD_OCC : 2) void bn_head_fwd_k(XIn xin
 
 // Statistics pass of the head's BatchNorm backward (bn_reduce_k MODE 1 with g = dY4 . W4 formed per
 // element) plus the head's weight gradient partials dW4[q][c] over the chunk's rows (fp32 per chunk).
-template <int NOUT, bool Z16 = false>
+template <int NOUT, bool Z16 = false, bool KB = false>
 __global__ __launch_bounds__(256, HRED_OCC) void bn_head_reduce_k(XIn xin, const float* __restrict__ d4,
                                                         const float* __restrict__ w4, int64_t M, int64_t C,
                                                         const float* __restrict__ mean, const float* __restrict__ mean_lo,
@@ -979,13 +1009,16 @@ __global__ __launch_bounds__(256, HRED_OCC) void bn_head_reduce_k(XIn xin, const
     float4 xv8[RB];
 #pragma unroll
     for (int u = 0; u < RB; ++u) xv8[u] = xin_load4<Z16>(xin, (rb + u < re ? rb + u : re - 1) * C + c, xbias);
+    // the forward's keep bits of these 8 rows (host: only with 8-row batches at multiples of 8)
+    const uint32_t kw = KB ? dp.bits[keep_word(rb, c, C)] : 0u;
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t rr = rb + u;
       if (rr >= re) break;
       const float4 xv = xv8[u];
       float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-      drop4(dp, (uint64_t)(rr * C + c), xs);
+      if constexpr (KB) drop4m(dp, (kw >> (4 * u)) & 15u, xs);
+      else drop4(dp, (uint64_t)(rr * C + c), xs);
       float dq[NOUT];
 #pragma unroll
       for (int q = 0; q < NOUT; ++q) dq[q] = myd4[(rr - r0) * NOUT + q];
@@ -1032,6 +1065,136 @@ __global__ __launch_bounds__(256, HRED_OCC) void bn_head_reduce_k(XIn xin, const
 #pragma unroll
   for (int q = 0; q < NOUT; ++q)
     *reinterpret_cast<float4*>(pw + (chunk * NOUT + q) * C + c) = make_float4(aw[q][0], aw[q][1], aw[q][2], aw[q][3]);
+}
+
+// bn_head_reduce_k with 2 columns per thread instead of 4: half the per-thread weight columns,
+// dW4 accumulators and BatchNorm parameters (~100 registers: 4 waves per SIMD where the 4-column
+// form holds 2), 4-B row loads.  Every column's sums run over the same rows in the same order as
+// bn_head_reduce_k's: bit-identical partials.
+template <int NOUT, bool Z16 = false, bool KB = false>
+__global__ __launch_bounds__(256, 4) void bn_head_reduce2_k(XIn xin, const float* __restrict__ d4,
+                                                         const float* __restrict__ w4, int64_t M, int64_t C,
+                                                         const float* __restrict__ mean, const float* __restrict__ mean_lo,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         double* __restrict__ p0, double* __restrict__ p1,
+                                                         float* __restrict__ pw, int64_t chunk_rows, Drop dp0) {
+  const Drop dp = drop_resolve(dp0);
+  const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t C2 = C / 2;
+  const int64_t chunk = id / C2;
+  const int64_t c = (id - chunk * C2) * 2;
+  const int64_t r0 = chunk * chunk_rows;
+  const int64_t r1 = (M < r0 + chunk_rows) ? M : r0 + chunk_rows;
+  // C % 256 == 0 (host check): a wave's 64 column pairs share one chunk (its dY4 rows staged once)
+  __shared__ float d4s[4][BN_ROWS * NOUT];
+  float* myd4 = d4s[threadIdx.x >> 6];
+  if (r0 < M)
+    for (int64_t i = threadIdx.x & 63; i < (r1 - r0) * NOUT; i += 64) myd4[i] = d4[r0 * NOUT + i];
+  __syncthreads();     // before any return: every wave of the workgroup reaches it
+  if (r0 >= M) return;
+  float mu[2], lo[2], is[2], ga[2], be[2], xb[2];
+  float wc[NOUT][2], aw[NOUT][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    mu[j] = mean[c + j];
+    lo[j] = mean_lo ? mean_lo[c + j] : 0.f;
+    is[j] = invstd[c + j];
+    ga[j] = gamma ? gamma[c + j] : 1.f;
+    be[j] = beta ? beta[c + j] : 0.f;
+    xb[j] = (Z16 && xin.bias != nullptr) ? xin.bias[c + j] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NOUT; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      wc[q][j] = w4[q * C + c + j];
+      aw[q][j] = 0.f;
+    }
+  double a[2] = {0, 0}, b[2] = {0, 0};
+  const uint32_t ksh = (uint32_t)(c & 3);   // this pair's bits within a row's nibble
+  for (int64_t r = r0; r < r1; r += 16) {
+    float fa[2] = {0, 0}, fb[2] = {0, 0};
+    const int64_t re = (r + 16 < r1) ? r + 16 : r1;
+    constexpr int RB = 8;
+    for (int64_t rb = r; rb < re; rb += RB) {
+      uint32_t xr[Z16 ? RB : 2 * RB];
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int64_t idx = (rb + u < re ? rb + u : re - 1) * C + c;
+        if constexpr (Z16) {
+          xr[u] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int16_t*>(xin.p) + idx);
+        } else {
+          const float2 f = *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(xin.p) + idx);
+          xr[2 * u] = __float_as_uint(f.x);
+          xr[2 * u + 1] = __float_as_uint(f.y);
+        }
+      }
+      const uint32_t kw = KB ? dp.bits[keep_word(rb, c, C)] : 0u;
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int64_t rr = rb + u;
+        if (rr >= re) break;
+        float xs[2];
+        if constexpr (Z16) {
+          xs[0] = (float)(int16_t)(xr[u] & 0xFFFFu) + xb[0];
+          xs[1] = (float)(int16_t)(xr[u] >> 16) + xb[1];
+        } else {
+          xs[0] = __uint_as_float(xr[2 * u]);
+          xs[1] = __uint_as_float(xr[2 * u + 1]);
+        }
+        if (dp.on) {
+          uint32_t km;
+          if constexpr (KB) {
+            km = (kw >> (4 * u + ksh)) & 3u;
+          } else {
+            const uint32_t key = drop_key(dp.seed), h0 = (uint32_t)(rr * C + c) * 0x9E3779B1u;
+            km = (uint32_t)(fmix32(h0 ^ key) < dp.thresh) | ((uint32_t)(fmix32((h0 + 0x9E3779B1u) ^ key) < dp.thresh) << 1);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) xs[j] = ((km >> j) & 1u) ? xs[j] * dp.scale : 0.f;
+        }
+        float dq[NOUT];
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) dq[q] = myd4[(rr - r0) * NOUT + q];
+        pf2 gs2 = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q)   // head_grad4's order
+          gs2 = __builtin_elementwise_fma(pf2{dq[q], dq[q]}, pf2{wc[q][0], wc[q][1]}, gs2);
+        float hh[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float xh = ((xs[e] - mu[e]) - lo[e]) * is[e];
+          const float y = fmaf(xh, ga[e], be[e]);
+          const bool in = y > -1.f && y < 1.f;
+          const float g = in ? (e ? gs2.y : gs2.x) : 0.f;
+          fa[e] += g;
+          fb[e] = fmaf(g, xh, fb[e]);
+          hh[e] = fminf(fmaxf(y, -1.f), 1.f);     // the forward's h3
+        }
+#pragma unroll
+        for (int q = 0; q < NOUT; ++q) {
+          const pf2 a2 = __builtin_elementwise_fma(pf2{dq[q], dq[q]}, pf2{hh[0], hh[1]}, pf2{aw[q][0], aw[q][1]});
+          aw[q][0] = a2.x;
+          aw[q][1] = a2.y;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      a[j] += (double)fa[j];
+      b[j] += (double)fb[j];
+    }
+  }
+  const int64_t o = chunk * C + c;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    p0[o + j] = a[j];
+    p1[o + j] = b[j];
+  }
+#pragma unroll
+  for (int q = 0; q < NOUT; ++q)
+    *reinterpret_cast<float2*>(pw + (chunk * NOUT + q) * C + c) = make_float2(aw[q][0], aw[q][1]);
 }
 
 // dW4[q][c] = sum over chunks of the partials: FF_COLS elements x FF_GROUPS chunk groups per
@@ -1518,6 +1681,27 @@ bool bn2_args_ok(const float* x, int64_t N, int64_t C, int64_t H, int64_t W, int
 
 using namespace bnn;
 
+namespace {
+// The dropout keep-bit plane (Drop::bits, keep_word): the forward statistics pass writes it where
+// its thread's 8-row load batches are whole words (chunks of a multiple of 8 rows), else
+// keep_bits_k does; the statistics pass of the head backward reads it on the same condition.
+inline bool keep_bits_fused(int64_t M, int64_t C) { return RED_RB == 8 && bn_chunk_rows(M, C) % 8 == 0; }
+
+__global__ __launch_bounds__(256) void keep_bits_k(int64_t M, int64_t C, Drop d0, uint32_t* __restrict__ out) {
+  const Drop d = drop_resolve(d0);
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x, C4 = C / 4;
+  if (w >= keep_words(M, C)) return;
+  const int64_t r0 = (w / C4) * 8, c = (w % C4) * 4;
+  uint32_t kw = 0;
+  for (int i = 0; i < 8 && r0 + i < M; ++i) kw |= drop_bits4(d, (uint64_t)((r0 + i) * C + c)) << (4 * i);
+  out[w] = kw;
+}
+}  // namespace
+
+BNN_API int64_t bnn_dropout_keep_bits_bytes(int64_t M, int64_t C) {
+  return (M > 0 && C > 0 && C % 4 == 0) ? keep_words(M, C) * (int64_t)sizeof(uint32_t) : -1;
+}
+
 BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
   // two double partial arrays [R][C] + two float vectors [C]
   return 2 * bn_chunks(M, C) * C * (int64_t)sizeof(double) + 2 * round_up(C * 4, 256);
@@ -1526,7 +1710,7 @@ BNN_API int64_t bnn_bn_workspace(int64_t M, int64_t C) {
 static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* save_mean_lo, float* y,
-                             int32_t hardtanh, void* work, void* stream, Drop dp) {
+                             int32_t hardtanh, void* work, void* stream, Drop dp, uint32_t* keep_bits = nullptr) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || !save_mean || !save_invstd || !work || !vec_ok(y) ||
       !vec_ok(save_mean_lo) || (running_mean == nullptr) != (running_var == nullptr) || !vec_ok(gamma) ||
@@ -1541,12 +1725,20 @@ static int bn_fwd_train_impl(XIn xin, bool z16, int64_t M, int64_t C, const floa
   double* p1 = p0 + R * C;
   // without a caller buffer the lo part of the mean lives in the workspace (the bwd's k0 slot)
   float* lo = save_mean_lo ? save_mean_lo : reinterpret_cast<float*>(p1 + R * C);
+  // the keep-bit plane: written by the statistics pass where its row batches are whole words, else
+  // by its own kernel
+  Drop dps = dp;
+  if (keep_bits != nullptr && dp.on) {
+    if (keep_bits_fused(M, C)) dps.bits_out = keep_bits;
+    else hipLaunchKernelGGL(keep_bits_k, dim3((unsigned)((keep_words(M, C) + 255) / 256)), dim3(256), 0, s, M, C, dp,
+                            keep_bits);
+  }
   if (z16)
     hipLaunchKernelGGL((bn_reduce_k<0, 1>), reduce_grid(M, C), dim3(256), 0, s, xin,
-                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
+                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dps);
   else
     hipLaunchKernelGGL((bn_reduce_k<0, 0>), reduce_grid(M, C), dim3(256), 0, s, xin,
-                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dp);
+                       nullptr, M, C, nullptr, nullptr, nullptr, nullptr, nullptr, 0, p0, p1, bn_chunk_rows(M, C), dps);
   hipLaunchKernelGGL(bn_fwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, M, C, R, momentum, eps, running_mean,
                      running_var, save_mean, save_invstd, lo, bn_chunk_rows(M, C), (int64_t)1);
   if (y != nullptr)   // y == NULL: statistics only (the fused apply+pack path writes no fp32 y)
@@ -1584,25 +1776,28 @@ BNN_API int bnn_bn_fwd_train(const float* x, int64_t M, int64_t C, const float* 
 BNN_API int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                                      float* running_mean, float* running_var, float momentum, float eps,
                                      float* save_mean, float* save_invstd, float* save_mean_lo, float* y,
-                                     int32_t hardtanh, float p, uint64_t seed, void* work, void* stream) {
+                                     int32_t hardtanh, float p, uint64_t seed, uint32_t* keep_bits, void* work,
+                                     void* stream) {
   if (!(p >= 0.f && p < 1.f)) {
     set_error("bnn_bn_dropout_fwd_train: p must be in [0, 1) (got %g)", (double)p);
     return kErrInval;
   }
   return bn_fwd_train_impl(XIn{x, nullptr}, false, M, C, gamma, beta, running_mean, running_var, momentum, eps,
-                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed));
+                           save_mean, save_invstd, save_mean_lo, y, hardtanh, work, stream, make_drop(p, seed),
+                           keep_bits);
 }
 
 BNN_API int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* gamma,
                                  const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                                  float* save_mean, float* save_invstd, float* save_mean_lo, float p, uint64_t seed,
-                                 void* work, void* stream) {
+                                 uint32_t* keep_bits, void* work, void* stream) {
   if (!(p >= 0.f && p < 1.f)) {
     set_error("bnn_bn_fwd_train_i16: p must be in [0, 1) (got %g)", (double)p);
     return kErrInval;
   }
   return bn_fwd_train_impl(XIn{x16, xbias}, true, M, C, gamma, beta, running_mean, running_var, momentum, eps,
-                           save_mean, save_invstd, save_mean_lo, nullptr, 0, work, stream, make_drop(p, seed));
+                           save_mean, save_invstd, save_mean_lo, nullptr, 0, work, stream, make_drop(p, seed),
+                           keep_bits);
 }
 
 BNN_API int bnn_bn_fwd_eval(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -1858,13 +2053,29 @@ BNN_API int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const floa
 
 constexpr int HEAD_NOUT = 10;   // the reference head: nn.Linear(C, 10) (mnist-dist2.py:73)
 
+// columns per thread of the head's statistics pass (bnn_bn_set_head_reduce_cols): 2 (bn_head_reduce2_k,
+// 4 waves per SIMD: 496 vs 527 us on the wide step, profiles/r05_kb2_*) or 4 (bn_head_reduce_k);
+// bit-identical results
+#ifndef BNN_HEAD_RED_COLS_DEFAULT
+#define BNN_HEAD_RED_COLS_DEFAULT 2
+#endif
+static int g_head_red_cols = BNN_HEAD_RED_COLS_DEFAULT;
+
+BNN_API int32_t bnn_bn_set_head_reduce_cols(int32_t cols) {
+  if (cols < 0) return g_head_red_cols;
+  if (cols != 2 && cols != 4) return kErrInval;
+  g_head_red_cols = cols;
+  return 0;
+}
+
 BNN_API int64_t bnn_bn_head_workspace(int64_t M, int64_t C, int32_t nout) {
   return bnn_bn_workspace(M, C) + round_up(bn_chunks(M, C) * (int64_t)nout * C * (int64_t)sizeof(float), 256);
 }
 
 static int bn_head_fwd_impl(XIn xin, bool z16, int64_t M, int64_t C, const float* mean, const float* invstd,
                             const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
-                            const float* w4, int32_t nout, const float* b4, float* y4, void* stream) {
+                            const uint32_t* keep_bits, const float* w4, int32_t nout, const float* b4, float* y4,
+                            void* stream) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % HD_COLS != 0 || !mean || !invstd || !w4 || !y4 ||
       nout != HEAD_NOUT || !aligned16(mean) || !aligned16(invstd) || !vec_ok(mean_lo) || !vec_ok(gamma) ||
@@ -1875,36 +2086,36 @@ static int bn_head_fwd_impl(XIn xin, bool z16, int64_t M, int64_t C, const float
   }
   const dim3 g((unsigned)((M + HD_ROWS - 1) / HD_ROWS));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (z16)
-    hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, true>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
-                       beta, w4, b4, y4, make_drop(p, seed));
-  else
-    hipLaunchKernelGGL((bn_head_fwd_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma,
-                       beta, w4, b4, y4, make_drop(p, seed));
+  Drop dp = make_drop(p, seed);
+  dp.bits = dp.on ? keep_bits : nullptr;
+  auto k = z16 ? (dp.bits ? bn_head_fwd_k<HEAD_NOUT, true, true> : bn_head_fwd_k<HEAD_NOUT, true, false>)
+               : (dp.bits ? bn_head_fwd_k<HEAD_NOUT, false, true> : bn_head_fwd_k<HEAD_NOUT, false, false>);
+  hipLaunchKernelGGL(k, g, dim3(256), 0, s, xin, M, C, mean, mean_lo, invstd, gamma, beta, w4, b4, y4, dp);
   return check_launch("bnn_bn_head_fwd");
 }
 
 BNN_API int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                             const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
-                            const float* w4, int32_t nout, const float* b4, float* y4, void* stream) {
-  return bn_head_fwd_impl(XIn{x, nullptr}, false, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, w4, nout, b4, y4,
-                          stream);
+                            const uint32_t* keep_bits, const float* w4, int32_t nout, const float* b4, float* y4,
+                            void* stream) {
+  return bn_head_fwd_impl(XIn{x, nullptr}, false, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, keep_bits, w4,
+                          nout, b4, y4, stream);
 }
 
 BNN_API int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                                 const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
-                                float p, uint64_t seed, const float* w4, int32_t nout, const float* b4, float* y4,
-                                void* stream) {
-  return bn_head_fwd_impl(XIn{x16, xbias}, true, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, w4, nout, b4, y4,
-                          stream);
+                                float p, uint64_t seed, const uint32_t* keep_bits, const float* w4, int32_t nout,
+                                const float* b4, float* y4, void* stream) {
+  return bn_head_fwd_impl(XIn{x16, xbias}, true, M, C, mean, invstd, mean_lo, gamma, beta, p, seed, keep_bits, w4,
+                          nout, b4, y4, stream);
 }
 
 static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float* w4, int32_t nout, int64_t M,
                                int64_t C, const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
-                               float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
-                               uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
-                               void* stream) {
+                               const uint32_t* keep_bits, float* dx, float* dgamma, float* dbeta, float* dw4,
+                               uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi,
+                               uint8_t* csc, float* colsum, void* work, void* stream) {
   const float* x = reinterpret_cast<const float*>(xin.p);
   if (!(z16 ? bn_args_ok16(xin, M, C) : bn_args_ok(x, M, C)) || C % 256 != 0 || !dy4 || !w4 || !dw4 ||
       nout != HEAD_NOUT || !save_mean || !save_invstd || !work || (dx && !aligned16(dx)) || !vec_ok(gamma) ||
@@ -1915,19 +2126,28 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
     return kErrInval;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Drop dp = make_drop(p, seed);
+  Drop dp = make_drop(p, seed);
+  dp.bits = dp.on ? keep_bits : nullptr;   // the apply pass reads the forward's keep bits in any shape
+  Drop dpr = dp;                           // the statistics pass where its 8-row batches are whole words
+  if (!keep_bits_fused(M, C)) dpr.bits = nullptr;
   const int64_t R = bn_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
   float* k1 = reinterpret_cast<float*>(reinterpret_cast<char*>(k0) + round_up(C * 4, 256));
   float* pw = reinterpret_cast<float*>(reinterpret_cast<char*>(work) + bnn_bn_workspace(M, C));
-  if (z16)
-    hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, true>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
-                       save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
-  else
-    hipLaunchKernelGGL((bn_head_reduce_k<HEAD_NOUT, false>), reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C,
-                       save_mean, save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dp);
+  if (g_head_red_cols == 2) {
+    auto kr = z16 ? (dpr.bits ? bn_head_reduce2_k<HEAD_NOUT, true, true> : bn_head_reduce2_k<HEAD_NOUT, true, false>)
+                  : (dpr.bits ? bn_head_reduce2_k<HEAD_NOUT, false, true> : bn_head_reduce2_k<HEAD_NOUT, false, false>);
+    const dim3 g2((unsigned)(((C / 2) * bn_chunks(M, C) + 255) / 256));
+    hipLaunchKernelGGL(kr, g2, dim3(256), 0, s, xin, dy4, w4, M, C, save_mean, save_mean_lo, save_invstd, gamma,
+                       beta, p0, p1, pw, bn_chunk_rows(M, C), dpr);
+  } else {
+    auto kr = z16 ? (dpr.bits ? bn_head_reduce_k<HEAD_NOUT, true, true> : bn_head_reduce_k<HEAD_NOUT, true, false>)
+                  : (dpr.bits ? bn_head_reduce_k<HEAD_NOUT, false, true> : bn_head_reduce_k<HEAD_NOUT, false, false>);
+    hipLaunchKernelGGL(kr, reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C, save_mean, save_mean_lo,
+                       save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dpr);
+  }
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + HD_FF_COLS - 1) / HD_FF_COLS)),
                      dim3(HD_FF_COLS * FF_GROUPS), 0, s, pw, R,
@@ -1937,12 +2157,10 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
   o.rres = rres;
   const int64_t qr = q6_rows(M, C);
   const dim3 g((unsigned)(C / Q6T_COLS), (unsigned)((M + qr - 1) / qr));
-  if (z16)
-    hipLaunchKernelGGL((bn_bwd_apply_q6_k<HEAD_NOUT, true>), g, dim3(256), 0, s, xin, dy4, M, C, save_mean,
-                       save_mean_lo, save_invstd, gamma, beta, 1, k0, k1, 1.f / (float)M, o, dp, w4, (int)qr);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_q6_k<HEAD_NOUT, false>), g, dim3(256), 0, s, xin, dy4, M, C, save_mean,
-                       save_mean_lo, save_invstd, gamma, beta, 1, k0, k1, 1.f / (float)M, o, dp, w4, (int)qr);
+  auto ka = z16 ? (dp.bits ? bn_bwd_apply_q6_k<HEAD_NOUT, true, true> : bn_bwd_apply_q6_k<HEAD_NOUT, true, false>)
+                : (dp.bits ? bn_bwd_apply_q6_k<HEAD_NOUT, false, true> : bn_bwd_apply_q6_k<HEAD_NOUT, false, false>);
+  hipLaunchKernelGGL(ka, g, dim3(256), 0, s, xin, dy4, M, C, save_mean, save_mean_lo, save_invstd, gamma, beta, 1, k0,
+                     k1, 1.f / (float)M, o, dp, w4, (int)qr);
   if (colsum)
     hipLaunchKernelGGL(q6_colsum_final_k, ffin_grid(C), dim3(256), 0, s, p0, (M + qr - 1) / qr, C, colsum);
   return check_launch("bnn_bn_head_bwd_q6");
@@ -1951,22 +2169,22 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
 BNN_API int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
                                const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
-                               float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi,
-                               uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
-                               void* stream) {
+                               const uint32_t* keep_bits, float* dx, float* dgamma, float* dbeta, float* dw4,
+                               uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi,
+                               uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_head_bwd_q6_impl(XIn{x, nullptr}, false, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
-                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
+                             save_mean_lo, p, seed, keep_bits, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
                              work, stream);
 }
 
 BNN_API int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy4, const float* w4,
                                    int32_t nout, int64_t M, int64_t C, const float* gamma, const float* beta,
                                    const float* save_mean, const float* save_invstd, const float* save_mean_lo,
-                                   float p, uint64_t seed, float* dx, float* dgamma, float* dbeta, float* dw4,
-                                   uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi, uint8_t* csc,
-                                   float* colsum, void* work, void* stream) {
+                                   float p, uint64_t seed, const uint32_t* keep_bits, float* dx, float* dgamma,
+                                   float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres,
+                                   uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work, void* stream) {
   return bn_head_bwd_q6_impl(XIn{x16, xbias}, true, dy4, w4, nout, M, C, gamma, beta, save_mean, save_invstd,
-                             save_mean_lo, p, seed, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
+                             save_mean_lo, p, seed, keep_bits, dx, dgamma, dbeta, dw4, rlo, rhi, rsc, rres, clo, chi, csc, colsum,
                              work, stream);
 }
 

@@ -266,7 +266,19 @@ struct Drop {
   int on;
   float scale;      // 1 / (1 - p)
   const int64_t* ctr = nullptr;   // device step counter folded into the seed (bnn_set_seed_counter)
+  // keep-bit plane (keep_word below): the forward statistics pass writes the mask once (bits_out),
+  // the later passes over the same tensor read it (bits) instead of evaluating the hash again
+  const uint32_t* bits = nullptr;
+  uint32_t* bits_out = nullptr;
 };
+
+// Keep-bit plane of a [M][C] tensor (C % 4 == 0): word (r / 8, c / 4) holds the keep bits of rows
+// (r & ~7) + i, columns (c & ~3) + j at bit 4 i + j -- one dword per 8 rows of a thread's float4
+// column group, one nibble per row.  (M + 7) / 8 * C / 4 words.
+__host__ __device__ __forceinline__ int64_t keep_word(int64_t r, int64_t c, int64_t C) {
+  return (r >> 3) * (C >> 2) + (c >> 2);
+}
+__host__ __device__ __forceinline__ int64_t keep_words(int64_t M, int64_t C) { return (M + 7) / 8 * (C / 4); }
 
 // Process-wide device step counter for graph-captured training steps: dropout launches made
 // while it is set draw their mask from seed + ctr[0] * golden, so one captured graph replays with
@@ -300,6 +312,16 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t i) {
 }
 
 __device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t i) { return drop_hash(d.seed, i) < d.thresh; }
+
+// keep bits of elements i0 .. i0+3 (bit j): the index products (i0 + j) * golden formed by adds
+// from one multiply (the same values mod 2^32; the 32-bit multiply is a quarter-rate instruction)
+__device__ __forceinline__ uint32_t drop_bits4(const Drop& d, uint64_t i0) {
+  const uint32_t key = drop_key(d.seed), h0 = (uint32_t)i0 * 0x9E3779B1u;
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m |= (uint32_t)(fmix32((h0 + (uint32_t)j * 0x9E3779B1u) ^ key) < d.thresh) << j;
+  return m;
+}
 
 
 inline Drop make_drop(float p, uint64_t seed) {

@@ -931,7 +931,7 @@ __global__ __launch_bounds__(512, 2) void gemm_fp6_pers_k(Gemm6Params p) {
   constexpr int BM = 128, BN = 512;
   constexpr int LO_ST = BM * 128, HI_ST = BM * 64, SC_PAD = 1024, B_ST = BN * 32, R_ST = RES ? BM * 32 : 0;
   constexpr int ST = LO_ST + HI_ST + SC_PAD + B_ST + R_ST;
-  constexpr int P_LO = LO_ST / 1024 / NL, P_HI = HI_ST / 1024 / NL, P_B = B_ST / 1024 / NL, P_R = R_ST / 1024 / NL;
+  constexpr int P_LO = LO_ST / 1024 / NL, P_HI = HI_ST / 1024 / NL, P_B = B_ST / 1024 / NL;
   static_assert(P_LO * NL * 1024 == LO_ST && P_HI * NL * 1024 == HI_ST && P_B * NL * 1024 == B_ST, "piece split");
   static_assert(R_ST / 1024 <= NL, "residual pieces: at most one per loading wave");
   // the first S_LD stages of a tile are issued by the loading waves alone (the storing waves' vmcnt

@@ -441,13 +441,19 @@ int bnn_bn2d_bwd_stats_q(const void* xq, const float* xbias, int32_t xfmt, const
 
 /* nn.Dropout(p) fused in front of BatchNorm1d (+ Hardtanh) (mnist-dist2.py:69-70: fc3 -> drop ->
  * bn3): x is the pre-dropout input; the keep mask is a counter-based hash of (seed, row*C + col)
- * regenerated by every pass (never stored), kept values scaled by 1/(1-p) as torch does; the
- * backward's dx is the gradient w.r.t. the pre-dropout input.  p in [0, 1).  bnn_dropout_mask
- * writes the mask the fused passes use (scale or 0 per element, n = M*C) for tests. */
+ * regenerated by every pass, kept values scaled by 1/(1-p) as torch does; the backward's dx is
+ * the gradient w.r.t. the pre-dropout input.  p in [0, 1).  bnn_dropout_mask writes the mask the
+ * fused passes use (scale or 0 per element, n = M*C) for tests.
+ * keep_bits (nullable; p > 0, C % 4 == 0): the forward statistics pass also stores the mask as a
+ * bit plane of bnn_dropout_keep_bits_bytes(M, C) bytes -- word (r/8)*(C/4) + c/4 holds rows
+ * (r & ~7) + i, columns (c & ~3) + j at bit 4i + j -- which bnn_bn_head_fwd / bnn_bn_head_bwd_q6
+ * (and their _i16 forms) then read instead of evaluating the hash (same mask, bit-identical
+ * results).  bnn_dropout_keep_bits_bytes returns -1 for M <= 0 or C % 4 != 0. */
+int64_t bnn_dropout_keep_bits_bytes(int64_t M, int64_t C);
 int bnn_bn_dropout_fwd_train(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta,
                              float* running_mean, float* running_var, float momentum, float eps,
                              float* save_mean, float* save_invstd, float* save_mean_lo, float* y, int32_t hardtanh,
-                             float p, uint64_t seed, void* work, bnn_stream_t stream);
+                             float p, uint64_t seed, uint32_t* keep_bits, void* work, bnn_stream_t stream);
 int bnn_bn_dropout_bwd(const float* x, const float* dy, int64_t M, int64_t C, const float* gamma,
                        const float* beta, const float* save_mean, const float* save_invstd,
                        const float* save_mean_lo, int32_t hardtanh, float p, uint64_t seed, float* dx,
@@ -477,14 +483,21 @@ int bnn_dropout_mask(int64_t n, float p, uint64_t seed, float* out, bnn_stream_t
  * bnn_bn_head_bwd_q6: given dY4 [M][nout], the BatchNorm(+dropout) backward with the incoming
  *   gradient dh3 = dY4 . W4 formed per element, as bnn_bn_bwd_q6 (dx optional, both FP6 digit
  *   forms of dx, colsum of dx), plus dW4 = dY4^T . h3 [nout][C] (h3 recomputed from x).
- *   work: bnn_bn_head_workspace(M, C, nout) bytes.  The head's bias gradient is sum_m dY4. */
+ *   work: bnn_bn_head_workspace(M, C, nout) bytes.  The head's bias gradient is sum_m dY4.
+ * keep_bits (nullable): the mask plane the statistics pass stored (bnn_bn_dropout_fwd_train), read
+ *   instead of the hash; it must come from the same (M, C, p, seed) forward. */
 int64_t bnn_bn_head_workspace(int64_t M, int64_t C, int32_t nout);
+/* Columns per thread of bnn_bn_head_bwd_q6's statistics pass: 2 (default: half the registers, twice
+ * the threads) or 4; identical results.  cols < 0 returns the current setting. */
+int bnn_bn_set_head_reduce_cols(int32_t cols);
 int bnn_bn_head_fwd(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                     const float* mean_lo, const float* gamma, const float* beta, float p, uint64_t seed,
-                    const float* w4, int32_t nout, const float* b4, float* y4, bnn_stream_t stream);
+                    const uint32_t* keep_bits, const float* w4, int32_t nout, const float* b4, float* y4,
+                    bnn_stream_t stream);
 int bnn_bn_head_bwd_q6(const float* x, const float* dy4, const float* w4, int32_t nout, int64_t M, int64_t C,
                        const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
-                       const float* save_mean_lo, float p, uint64_t seed, float* dx, float* dgamma, float* dbeta,
+                       const float* save_mean_lo, float p, uint64_t seed, const uint32_t* keep_bits, float* dx,
+                       float* dgamma, float* dbeta,
                        float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres, uint8_t* clo, uint8_t* chi,
                        uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
 
@@ -515,7 +528,7 @@ int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, c
 int bnn_bn_fwd_train_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* gamma,
                          const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                          float* save_mean, float* save_invstd, float* save_mean_lo, float p, uint64_t seed,
-                         void* work, bnn_stream_t stream);
+                         uint32_t* keep_bits, void* work, bnn_stream_t stream);
 int bnn_bn_apply_pack_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                           const float* invstd, const float* mean_lo, const float* gamma, const float* beta,
                           uint8_t* q, int64_t ldq, uint8_t* qt, int64_t ldqt, int32_t qt_panel,
@@ -527,12 +540,12 @@ int bnn_bn_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy, i
                       uint8_t* csc, float* colsum, void* work, bnn_stream_t stream);
 int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t M, int64_t C, const float* mean,
                         const float* invstd, const float* mean_lo, const float* gamma, const float* beta, float p,
-                        uint64_t seed, const float* w4, int32_t nout, const float* b4, float* y4,
-                        bnn_stream_t stream);
+                        uint64_t seed, const uint32_t* keep_bits, const float* w4, int32_t nout, const float* b4,
+                        float* y4, bnn_stream_t stream);
 int bnn_bn_head_bwd_q6_i16(const int16_t* x16, const float* xbias, const float* dy4, const float* w4, int32_t nout,
                            int64_t M, int64_t C, const float* gamma, const float* beta, const float* save_mean,
-                           const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed, float* dx,
-                           float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres,
+                           const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
+                           const uint32_t* keep_bits, float* dx, float* dgamma, float* dbeta, float* dw4, uint8_t* rlo, uint8_t* rhi, uint8_t* rsc, uint8_t* rres,
                            uint8_t* clo, uint8_t* chi, uint8_t* csc, float* colsum, void* work,
                            bnn_stream_t stream);
 

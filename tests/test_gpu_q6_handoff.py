@@ -44,7 +44,7 @@ def test_bn_bwd_q6_matches_separate_passes(F, M, C, p):
     ws = F._bn_ws(M, C, "cuda")
     seed = 1234
     L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gw), L.ptr(gb), L.ptr(rm), L.ptr(rv), 0.1, 1e-5,
-           L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p), seed, L.ptr(ws), L.stream())
+           L.ptr(mean), L.ptr(invstd), L.ptr(mlo), None, 1, float(p), seed, None, L.ptr(ws), L.stream())
     # reference: the separate passes
     dz = torch.empty_like(z)
     dgw, dgb = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")

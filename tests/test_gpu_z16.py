@@ -69,11 +69,12 @@ def _stats(F, z, z16, bias, M, C, p=0.0, seed=0):
         bet = torch.linspace(-0.2, 0.2, C, device="cuda")
         if form == "f32":
             L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, C, L.ptr(gam), L.ptr(bet), L.ptr(rm), L.ptr(rv), 0.1,
-                   1e-5, L.ptr(mean), L.ptr(invstd), L.ptr(lo), None, 1, float(p), int(seed), L.ptr(ws), L.stream())
+                   1e-5, L.ptr(mean), L.ptr(invstd), L.ptr(lo), None, 1, float(p), int(seed), None, L.ptr(ws),
+                   L.stream())
         else:
             L.call("bnn_bn_fwd_train_i16", L.ptr(z16), L.ptr(bias), M, C, L.ptr(gam), L.ptr(bet), L.ptr(rm),
-                   L.ptr(rv), 0.1, 1e-5, L.ptr(mean), L.ptr(invstd), L.ptr(lo), float(p), int(seed), L.ptr(ws),
-                   L.stream())
+                   L.ptr(rv), 0.1, 1e-5, L.ptr(mean), L.ptr(invstd), L.ptr(lo), float(p), int(seed), None,
+                   L.ptr(ws), L.stream())
         outs.append((mean, invstd, lo, rm, rv, gam, bet))
     return outs
 
@@ -154,17 +155,17 @@ def test_head_i16_bit_identical(F, M, C):
         y4 = torch.empty(M, 10, device="cuda")
         if form == "f32":
             L.call("bnn_bn_head_fwd", L.ptr(z), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo), L.ptr(gam), L.ptr(bet),
-                   p, seed, L.ptr(w4), 10, L.ptr(b4), L.ptr(y4), L.stream())
+                   p, seed, None, L.ptr(w4), 10, L.ptr(b4), L.ptr(y4), L.stream())
         else:
             L.call("bnn_bn_head_fwd_i16", L.ptr(z16), L.ptr(bias), M, C, L.ptr(mean), L.ptr(invstd), L.ptr(lo),
-                   L.ptr(gam), L.ptr(bet), p, seed, L.ptr(w4), 10, L.ptr(b4), L.ptr(y4), L.stream())
+                   L.ptr(gam), L.ptr(bet), p, seed, None, L.ptr(w4), 10, L.ptr(b4), L.ptr(y4), L.stream())
         dx = torch.empty(M, C, device="cuda")
         dg, db, cs = (torch.empty(C, device="cuda") for _ in range(3))
         dw4 = torch.empty(10, C, device="cuda")
         rows, cols = _fp6_bufs(F, M, C)
         ws = torch.empty((L.lib().bnn_bn_head_workspace(M, C, 10),), dtype=torch.uint8, device="cuda")
         common = [L.ptr(dy4), L.ptr(w4), 10, M, C, L.ptr(gam), L.ptr(bet), L.ptr(mean), L.ptr(invstd), L.ptr(lo), p,
-                  seed, L.ptr(dx), L.ptr(dg), L.ptr(db), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
+                  seed, None, L.ptr(dx), L.ptr(dg), L.ptr(db), L.ptr(dw4), L.ptr(rows.lo), L.ptr(rows.hi), L.ptr(rows.sc),
                   L.ptr(rows.res), L.ptr(cols.lo), L.ptr(cols.hi), L.ptr(cols.sc), L.ptr(cs), L.ptr(ws), L.stream()]
         if form == "f32":
             L.call("bnn_bn_head_bwd_q6", L.ptr(z), *common)
@@ -323,7 +324,7 @@ def test_gemm_fp4_bnstats_dropout(F, i16):
     mean0, istd0, lo0 = F._bn_stat_buffers(N, "cuda")
     rm0, rv0 = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
     L.call("bnn_bn_dropout_fwd_train", L.ptr(z), M, N, None, None, L.ptr(rm0), L.ptr(rv0), 0.1, 1e-5, L.ptr(mean0),
-           L.ptr(istd0), L.ptr(lo0), None, 1, p, seed, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
+           L.ptr(istd0), L.ptr(lo0), None, 1, p, seed, None, L.ptr(F._bn_ws(M, N, "cuda")), L.stream())
     mean1, istd1, lo1, rm1, rv1 = res[0]
     assert torch.equal(mean0, mean1) and torch.equal(lo0, lo1)
     assert rel_err(host(istd1), host(istd0)) <= 1e-6
