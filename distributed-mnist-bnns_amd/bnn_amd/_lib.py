@@ -95,6 +95,7 @@ SIGNATURES = {
     "bnn_bn_dropout_fwd_train": (I32, [P, I64, I64, P, P, P, P, F32, F32, P, P, P, P, I32, F32, U64, P, P, P]),
     "bnn_dropout_keep_bits_bytes": (I64, [I64, I64]),
     "bnn_bn_set_head_reduce_cols": (I32, [I32]),
+    "bnn_gemm_i8_bnstats_set_tile": (I32, [I32]),
     "bnn_bn_dropout_bwd": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P]),
     "bnn_bn_bwd_q6": (I32, [P, P, I64, I64, P, P, P, P, P, I32, F32, U64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "bnn_dropout_mask": (I32, [I64, F32, U64, P, P]),

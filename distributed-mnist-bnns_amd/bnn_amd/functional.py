@@ -1162,6 +1162,9 @@ _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
 # default (off)
 if os.environ.get("BNN_FP6_PERS") is not None:
     L.call("bnn_gemm_fp6_set_persistent", int(os.environ["BNN_FP6_PERS"] != "0"))
+# BNN_PIX_TILE=1 / 2: the u8-pixel statistics GEMM's tile, 128 x 128 / 256 x 256 (A/B timing)
+if os.environ.get("BNN_PIX_TILE") is not None:
+    L.call("bnn_gemm_i8_bnstats_set_tile", int(os.environ["BNN_PIX_TILE"]))
 # BNN_HEAD_RED_COLS=2 / 4: columns per thread of the head's statistics pass (A/B timing)
 if os.environ.get("BNN_HEAD_RED_COLS") is not None:
     L.call("bnn_bn_set_head_reduce_cols", int(os.environ["BNN_HEAD_RED_COLS"]))

@@ -705,6 +705,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   float4 gr[NOUT > 0 ? 1 : NI];
   // KB: the sub-tile's keep-bit words (8-row groups x 16 column groups), staged in LDS with dY4
   __shared__ uint32_t kbs[KB ? Q6T_SUB / 8 : 1][16];
+  // the head's dY4 rows (and keep words) of the next sub-tile ride in registers with its x loads
+  // (3 floats + 1 word per thread), written to LDS at the sub-tile's top: a load issued there had
+  // the dz phase wait on its full HBM latency once per sub-tile
+  constexpr int ND4 = NOUT > 0 ? (Q6T_SUB * D4LD + 255) / 256 : 1;
+  float d4r[ND4];
+  uint32_t kbr = 0u;
   auto load_sub = [&](int64_t m0n) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -712,6 +718,17 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       if (m0n < mp && r < M) {
         xr[i] = xin_raw4<Z16>(xin, r * C + c);
         if constexpr (NOUT == 0) gr[i] = ld4(dy + r * C + c);
+      }
+    }
+    if constexpr (NOUT > 0) {
+#pragma unroll
+      for (int u = 0; u < ND4; ++u) {
+        const int i = t + 256 * u, rr = i / D4LD, q = i - rr * D4LD;
+        d4r[u] = (m0n < mp && i < Q6T_SUB * D4LD && m0n + rr < M && q < NOUT) ? dy[(m0n + rr) * NOUT + q] : 0.f;
+      }
+      if constexpr (KB) {
+        const int64_t r8 = m0n + 8 * (t >> 4);
+        kbr = (m0n < mp && t < Q6T_SUB * 2 && r8 < M) ? dp.bits[keep_word(r8, c0 + 4 * (t & 15), C)] : 0u;
       }
     }
   };
@@ -726,16 +743,12 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     const int64_t m0 = mbase + sub * Q6T_SUB;
     if (m0 >= mp) break;                       // block-uniform
     Q6_STAMP(sub, 0);
-    if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows
-      for (int i = t; i < Q6T_SUB * D4LD; i += 256) {
-        const int rr = i / D4LD, q = i - rr * D4LD;
-        d4s[i] = (m0 + rr < M && q < NOUT) ? dy[(m0 + rr) * NOUT + q] : 0.f;
-      }
+    if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows (prefetched)
+#pragma unroll
+      for (int u = 0; u < ND4; ++u)
+        if (t + 256 * u < Q6T_SUB * D4LD) d4s[t + 256 * u] = d4r[u];
       if constexpr (KB) {
-        if (t < Q6T_SUB * 2) {
-          const int64_t r8 = m0 + 8 * (t >> 4);
-          kbs[t >> 4][t & 15] = r8 < M ? dp.bits[keep_word(r8, c0 + 4 * (t & 15), C)] : 0u;
-        }
+        if (t < Q6T_SUB * 2) kbs[t >> 4][t & 15] = kbr;
       }
       __syncthreads();
     }

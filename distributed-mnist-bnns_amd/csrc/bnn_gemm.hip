@@ -993,9 +993,21 @@ BNN_API int bnn_gemm_i8_affine(const int8_t* A, int64_t lda, int64_t a_plane, in
 
 // The statistics form runs the 32x32 (1,1) kernels only: 128x128 tiles (64-row chunks) on grids
 // below 512 of the 256x256 tiles (128-row chunks), as pick_kernel's BK=64 choices
+// bnn_gemm_i8_bnstats_set_tile: 0 = by grid size (above), 1 = always the 128 x 128 tile, 2 = always
+// 256 x 256 (A/B hook; the chunk query and the launch read the same setting)
+static int g_i8_bnstats_tile = 0;
+
 static const Variant* i8_bnstats_variant(int64_t M, int64_t N) {
   const bool big = ((M + 255) / 256) * ((N + 255) / 256) >= 512;
+  if (g_i8_bnstats_tile != 0) return find_variant(g_i8_bnstats_tile == 2 ? 2 : 1);
   return find_variant(big ? 2 : 1);
+}
+
+BNN_API int32_t bnn_gemm_i8_bnstats_set_tile(int32_t tile) {
+  if (tile < 0) return g_i8_bnstats_tile;
+  if (tile > 2) return kErrInval;
+  g_i8_bnstats_tile = tile;
+  return 0;
 }
 
 BNN_API int64_t bnn_gemm_i8_bnstats_chunk(int64_t M, int64_t N) {

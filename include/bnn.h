@@ -138,6 +138,10 @@ int64_t bnn_gemm_fp4_bnstats_chunk(int64_t M, int64_t N, int64_t K);
 int bnn_gemm_fp4_bnstats(const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb, const float* bias,
                          float* C, int16_t* C16, int64_t ldc, const float* zbias, int64_t M, int64_t N, int64_t K,
                          float drop_p, uint64_t drop_seed, double* stat, int64_t stat_rows, bnn_stream_t stream);
+/* Tile of the u8-pixel statistics GEMM (bnn_gemm_i8_affine_bnstats[_s20] and its chunk query):
+ * 0 = by grid size (default), 1 = 128 x 128, 2 = 256 x 256; tile < 0 returns the setting.  Set it
+ * before the chunk query of a launch (both read it). */
+int bnn_gemm_i8_bnstats_set_tile(int32_t tile);
 int bnn_gemm_i8_affine_bnstats(const int8_t* A, int64_t lda, const int8_t* B, int64_t ldb,
                                const float* b_scale, const float* bias, const int64_t* col_off,
                                double off_mul, float* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
