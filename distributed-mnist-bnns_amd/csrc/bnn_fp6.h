@@ -61,31 +61,34 @@ __device__ __forceinline__ void codes4(float x, int shift, uint32_t (&c)[4]) {
   }
 }
 
-// The residual plane of a row operand (the dX GEMMs' dY rows; bnn_gemm.hip header "residual"): three
+// The residual plane of a row operand (the dX GEMMs' dY rows; bnn_gemm6.hip header "residual"): three
 // more bits of x below the four digit planes, as ONE FP4 (e2m1) plane.  With v = rint(x 2^shift)
-// (the digit planes' integer) and v8 = rint(x 2^(shift+3)), d = v8 - 8 v lies in [-4, 4]
-// (|8t - 8 rint(t)| <= 4, and the outer rint moves it by at most 1/2); the e2m1 code of d/2 is |d|
-// (0, 0.5, 1, 1.5, 2 are codes 0..4) with the sign in bit 3, and the GEMM scales the plane by
+// (the digit planes' integer), 4r = x 2^(shift+2) - 4v is exact in fp32 (|4r| <= 2), and the digit
+// d = rint(8r) in [-4, 4] is stored as the e2m1 code of d/2: the conversion unit's round-to-nearest-
+// even of 4r onto {0, 0.5, 1, 1.5, 2} (v_cvt_scalef32_pk_fp4_f32, scale 1 -- ties go to the even code
+// exactly as rint's; a negative 4r that rounds to zero gives -0, code 8, the same value;
+// tools/probes/probe_cvt_fp4.hip, profiles/r05_probe_cvt_fp4.log).  The GEMM scales the plane by
 // 2^(e - 21) (E8M0 byte = plane 0's byte - 5), so the five planes sum rint(x 2^(22-e)) 2^(e-22):
 // |x - q| <= 2^(e-23) <= max|x_block| 2^-22.  A block with a NaN scale or shift > RES_MAX_SHIFT
-// (max|x| < 2^-105, where 2^(shift+3) is no fp32 number) gets a zero residual.
+// (max|x| < 2^-105, where 2^(shift+2) is no fp32 number) gets a zero residual.
 constexpr int RES_MAX_SHIFT = 124;
 
-// e = d + 4 in [0, 8] from the two magic-fma words: ba = bits of fma(x, 2^shift, MAGIC + DIGIT_BIAS)
-// = 0x4B400000 + v + DIGIT_BIAS, b8 = bits of fma(x, 2^(shift+3), MAGIC) = 0x4B400000 + v8 -- plain
-// modulo-2^32 arithmetic -- then the code min(e - 4, 12 - e) (unsigned: e >= 4 gives e - 4 <= 4,
-// e < 4 wraps above 12 - e = 8 | (4 - e)).
-__device__ __forceinline__ uint32_t res4_code_bits(uint32_t ba, uint32_t b8) {
-  const uint32_t e = b8 - (ba << 3) + (uint32_t)(7u * 0x4B400000u + 8u * (uint32_t)DIGIT_BIAS + 4u);
-  return min(e - 4u, 12u - e);
+// the pair's two codes into byte `idx` (compile-time after unrolling) of `old`
+__device__ __forceinline__ uint32_t res4_pack2(uint32_t old, float r4a, float r4b, int idx) {
+  switch (idx & 3) {
+    case 0: return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(old, r4a, r4b, 1.f, 0);
+    case 1: return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(old, r4a, r4b, 1.f, 1);
+    case 2: return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(old, r4a, r4b, 1.f, 2);
+    default: return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(old, r4a, r4b, 1.f, 3);
+  }
 }
 
-// The same from x itself (rint twice; the slow path of blocks outside the magic-fma range)
+// one element's code from x itself (ldexp: any shift up to RES_MAX_SHIFT; the slow path of blocks
+// outside the magic-fma range, and the lane-per-element quantiser)
 __device__ __forceinline__ uint32_t res4_code(float x, int shift) {
-  const int v = __float2int_rn(ldexpf(x, shift));
-  const int v8 = __float2int_rn(ldexpf(x, shift + 3));
-  const int d = v8 - 8 * v;
-  return d < 0 ? (8u | (uint32_t)(-d)) : (uint32_t)d;
+  const float v = rintf(ldexpf(x, shift));
+  const float r4 = ldexpf(x, shift + 2) - 4.f * v;   // exact
+  return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, r4, 0.f, 1.f, 0) & 15u;
 }
 
 __device__ __forceinline__ float absmax_nan(float amax, float x) {
@@ -214,8 +217,8 @@ __device__ __forceinline__ void q6_block_store_lds(const float* src, bool store,
 // (the same double sum as a separate loop over them).  The record goes to sink.plane(j, lo 16 B,
 // hi 8 B) for planes j = 0..3 and sink.scale(byte).  Bit-identical to q6_block_store_lds.
 //
-// RES (row operands of the dX GEMMs): also the block's residual FP4 plane (res4_code_bits: one more
-// magic fma per element) to sink.residual(16 B: element i at bits 4i).
+// RES (row operands of the dX GEMMs): also the block's residual FP4 plane (two fmas and half a
+// conversion per element) to sink.residual(16 B: element i at bits 4i).
 template <int STRIDE, bool CSUM, typename Sink, bool RES = false>
 __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bits, Sink& sink, double& csum) {
   int shift;
@@ -225,9 +228,9 @@ __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bit
   if (sbyte != 255 && shift <= 126) {
     const float s = __uint_as_float((uint32_t)(shift + 127) << 23);
     constexpr float MAGIC = 12582912.f + (float)DIGIT_BIAS;
-    // 2^(shift+3) (shift <= RES_MAX_SHIFT; else the residual stays zero)
+    // 2^(shift+2) (shift <= RES_MAX_SHIFT; else the residual stays zero)
     const bool rok = RES && shift <= RES_MAX_SHIFT;
-    const float s8 = rok ? __uint_as_float((uint32_t)(shift + 130) << 23) : 0.f;
+    const float s4 = rok ? __uint_as_float((uint32_t)(shift + 129) << 23) : 0.f;
 #pragma unroll
     for (int k = 0; k < QB / 2; ++k) {
       const float xa = src[(2 * k) * STRIDE], xb = src[(2 * k + 1) * STRIDE];
@@ -241,9 +244,11 @@ __device__ __forceinline__ void q6_block_pre(const float* src, uint32_t amax_bit
       Q[k] = __builtin_amdgcn_ubfe(ba, 15, 6) | (__builtin_amdgcn_ubfe(bb, 15, 6) << 16);
       if constexpr (RES) {
         if (rok) {
-          const uint32_t ca = res4_code_bits(ba, __float_as_uint(__builtin_fmaf(xa, s8, 12582912.f)));
-          const uint32_t cb = res4_code_bits(bb, __float_as_uint(__builtin_fmaf(xb, s8, 12582912.f)));
-          R[k >> 2] |= (ca | (cb << 4)) << (8 * (k & 3));
+          // -4v = fl(ba) * -4 + 4 MAGIC and 4r = x 2^(shift+2) - 4v, both exact: two fmas and one
+          // conversion per pair (the integer route took ~17 VALU per pair on the critical row waves)
+          const float ra = __builtin_fmaf(xa, s4, __builtin_fmaf(__uint_as_float(ba), -4.f, 4.f * MAGIC));
+          const float rb = __builtin_fmaf(xb, s4, __builtin_fmaf(__uint_as_float(bb), -4.f, 4.f * MAGIC));
+          R[k >> 2] = res4_pack2(R[k >> 2], ra, rb, k);
         }
       }
     }

@@ -230,8 +230,8 @@ BNN_API int bnn_linear_nsmall_bwd(const float* x, const float* w, const float* d
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (M == 0) {
-    if (dw) hipMemsetAsync(dw, 0, N * K * sizeof(float), s);
-    if (db) hipMemsetAsync(db, 0, N * sizeof(float), s);
+    if (dw) (void)hipMemsetAsync(dw, 0, N * K * sizeof(float), s);
+    if (db) (void)hipMemsetAsync(db, 0, N * sizeof(float), s);
     return check_launch("bnn_linear_nsmall_bwd");
   }
   const int64_t rpb = ls_rows_per_block(M), G = (M + rpb - 1) / rpb;
