@@ -762,6 +762,11 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     const float a0[4] = {a0v.x, a0v.y, a0v.z, a0v.w}, a1[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
     // KB: this thread's 4 rows are one half of a keep-bit word
     const uint32_t kb = KB ? kbs[(NI * (t >> 4)) >> 3][t & 15] >> (16 * ((t >> 4) & 1)) : 0u;
+    // column-block maxima of this thread's 4 columns per 32-row block (CPR: pre-reduced in registers
+    // and across the wave's lane groups, one atomic per column and wave; the head form, at its
+    // register limit, keeps one atomic per element)
+    constexpr bool CPR = NOUT == 0;
+    uint32_t cmx[2][4] = {};
 #pragma unroll
     for (int i = 0; i < Q6T_SUB / 16; ++i) {
       const int rr = row_of(i);
@@ -798,11 +803,38 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
       }
       *reinterpret_cast<float4*>(tile + rr * Q6T_LD + cq) = make_float4(v[0], v[1], v[2], v[3]);
       const uint32_t a0b = abs_bits(v[0]), a1b = abs_bits(v[1]), a2b = abs_bits(v[2]), a3b = abs_bits(v[3]);
-      atomicMax(&rmax[(t & 15) >> 3][rr], max(max(a0b, a1b), max(a2b, a3b)));
-      atomicMax(&cmax[rr >> 5][cq], a0b);
-      atomicMax(&cmax[rr >> 5][cq + 1], a1b);
-      atomicMax(&cmax[rr >> 5][cq + 2], a2b);
-      atomicMax(&cmax[rr >> 5][cq + 3], a3b);
+      // the row block's maximum over its 8 lanes (quad swaps, then the half-row mirror: DPP, no LDS
+      // traffic) -- one lane writes it; the 8 lanes are the whole 32-column block, so no atomic
+      uint32_t rm = max(max(a0b, a1b), max(a2b, a3b));
+      rm = max(rm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rm, 0xB1, 0xF, 0xF, false));
+      rm = max(rm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rm, 0x4E, 0xF, 0xF, false));
+      rm = max(rm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rm, 0x141, 0xF, 0xF, false));
+      if ((t & 7) == 0) rmax[(t & 15) >> 3][rr] = rm;
+      if constexpr (CPR) {   // rows 16 apart: blocks i / 2
+        const int cb = i >> 1;
+        cmx[cb][0] = max(cmx[cb][0], a0b);
+        cmx[cb][1] = max(cmx[cb][1], a1b);
+        cmx[cb][2] = max(cmx[cb][2], a2b);
+        cmx[cb][3] = max(cmx[cb][3], a3b);
+      } else {
+        atomicMax(&cmax[rr >> 5][cq], a0b);
+        atomicMax(&cmax[rr >> 5][cq + 1], a1b);
+        atomicMax(&cmax[rr >> 5][cq + 2], a2b);
+        atomicMax(&cmax[rr >> 5][cq + 3], a3b);
+      }
+    }
+    if constexpr (CPR) {
+      // across the wave's 4 lane groups (the same columns, rows of the same blocks), then one atomic
+      // per column, block and wave (the other waves merge into it)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t m = cmx[cb][j];
+          m = max(m, (uint32_t)__shfl_xor((int)m, 16, 64));
+          m = max(m, (uint32_t)__shfl_xor((int)m, 32, 64));
+          if (lane < 16) atomicMax(&cmax[cb][cq + j], m);
+        }
     }
     __syncthreads();
     Q6_STAMP(sub, 1);
