@@ -292,3 +292,97 @@ def test_wide_bench_loss_vs_reference_semantics():
           f"step 0: {L[0]:.5f} / {T1[0]:.5f} / {T2[0]:.5f}")
     assert abs(L[0] - T1[0]) <= 0.01 and abs(T1[0] - T2[0]) <= 0.01    # same init, masks differ
     assert abs(tail(L) - tail(T1)) <= band
+
+
+def test_wide_bench_loss_same_masks():
+    """The bench workload against the reference semantics (torch fp32 RefMLP, the reference's .org
+    protocol) driven by libbnn's OWN dropout masks: the seeds the fused head draws are recorded and
+    the reference's dropout multiplies by bnn_dropout_mask of the same seed, so the runs differ only
+    in arithmetic (FP6 digit planes and fixed-order sums against torch's fp32 GEMMs and BatchNorm).
+    Calibration: the same reference run on the batch in another row order (masks permuted with it)
+    -- the same math in another fp32 summation order.  Bars: step 0 within 1e-4; steps 1-2 (before
+    the Adam steps at lr 0.01 have inflated the logits -- mnist-dist2.py's own dynamics, after which
+    fp32 rounding differences grow chaotically) within 2e-3 relative; the mean of the last 10 steps
+    within max(3 x the calibration's gap, 5 %) -- against ~0.9 for differing masks
+    (test_wide_bench_loss_vs_reference_semantics)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import _lib as L
+    from bnn_amd import functional as BF
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    from oracle.bnn_torch import RefMLP, train_step
+    model, x, y = _bench_setup()
+    state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    seeds = []
+    orig = BF.dropout_seed
+
+    def recording_seed():
+        s = orig()
+        seeds.append(int(s))
+        return s
+
+    BF.dropout_seed = recording_seed
+    try:
+        opt = LatentAdam(model.parameters(), lr=LR, clamp_params=binary_params(model))
+        crit = torch.nn.CrossEntropyLoss()
+        Lb = []
+        for _ in range(STEPS):
+            for p in model.parameters():
+                p.grad = None
+            loss = crit(model(x), y)
+            loss.backward()
+            opt.step()
+            Lb.append(loss.detach())
+    finally:
+        BF.dropout_seed = orig
+    Lb = np.array([float(v) for v in Lb])
+    assert len(seeds) == STEPS, "the fused head drew one dropout seed per step"
+    p_drop = model.drop.p
+    del model, opt
+    torch.cuda.empty_cache()
+
+    class SeedDrop(torch.nn.Module):
+        """x * bnn_dropout_mask(seed) (kept values x / (1 - p), as torch), rows in `order`."""
+
+        def __init__(self, order):
+            super().__init__()
+            self.i, self.order = 0, order
+
+        def forward(self, z):
+            m = torch.empty(z.numel(), device=z.device)
+            L.call("bnn_dropout_mask", z.numel(), float(p_drop), seeds[self.i], L.ptr(m), L.stream())
+            self.i += 1
+            m = m.view_as(z)
+            return z * (m if self.order is None else m[self.order])
+
+    def reference(order):
+        ref = RefMLP(8192, 8192, 8192, p_drop=p_drop)
+        ref.load_state_dict(state)
+        ref = ref.cuda().train()
+        ref.drop = SeedDrop(order)
+        ropt = torch.optim.Adam(ref.parameters(), lr=LR)
+        xf = x.float().div(255.0)
+        yy = y
+        if order is not None:
+            xf, yy = xf[order], y[order]
+        out = np.array([train_step(ref, ropt, xf.clone(), yy, True) for _ in range(STEPS)])
+        del ref, ropt
+        torch.cuda.empty_cache()
+        return out
+
+    T = reference(None)
+    Tp = reference(torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(5)).cuda())
+    tail = lambda a: float(a[-10:].mean())   # noqa: E731
+    rel = np.abs(Lb - T) / np.abs(T)
+    calib = abs(tail(T) - tail(Tp))
+    bar = max(3 * calib, 0.05 * tail(T))
+    print("\nwide bench workload, same dropout masks: libbnn", " ".join(f"{v:.4f}" for v in Lb))
+    print("reference semantics torch fp32, libbnn's masks  ", " ".join(f"{v:.4f}" for v in T))
+    print("the same, batch rows permuted (calibration)     ", " ".join(f"{v:.4f}" for v in Tp))
+    print(f"relative gap per step: {' '.join(f'{v:.1e}' for v in rel)}")
+    print(f"tail means: libbnn {tail(Lb):.4f}, torch {tail(T):.4f}, permuted {tail(Tp):.4f}; "
+          f"|libbnn - torch| {abs(tail(Lb) - tail(T)):.4f} against bar {bar:.4f} (calibration gap {calib:.4f})")
+    assert abs(Lb[0] - T[0]) <= 1e-4
+    assert np.all(rel[1:3] <= 2e-3)
+    assert abs(tail(Lb) - tail(T)) <= bar
