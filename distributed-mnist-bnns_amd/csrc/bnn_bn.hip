@@ -701,8 +701,20 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   constexpr bool RC4 = NOUT > 0;
   static_assert(!KB || (RC4 && NI == 4), "keep bits: the head's row mapping (4 rows = half a word)");
   auto row_of = [&](int i) __attribute__((always_inline)) { return RC4 ? NI * (t >> 4) + i : (t >> 4) + 16 * i; };
-  XRaw<Z16> xr[NI];
-  float4 gr[NOUT > 0 ? 1 : NI];
+  // prefetch depth: the bn2 form on z16 (int16 x + fp32 dY rows, 6 B per element in) loads two
+  // sub-tiles ahead -- one quantise phase did not cover its loads' latency under the record-store
+  // stream (phase stamps, profiles/r05_q6_stamps.log); the head form and the fp32-x form, at their
+  // register limits (a second fp32 x set spills), one
+#ifdef Q6_PREFETCH1
+  constexpr int PD = 1;                         // timing-only A/B builds
+#else
+  constexpr int PD = (NOUT == 0 && Z16) ? 2 : 1;
+#endif
+  XRaw<Z16> xr[PD][NI];
+  float4 gr[PD][NOUT > 0 ? 1 : NI];
+  // this workgroup's rows end here: the prefetch past its last sub-tile loads nothing (it read the
+  // next workgroup's rows -- 1/8 of the pass's input -- and threw them away)
+  const int64_t mend = min(mp, mbase + (int64_t)rows_wg);
   // KB: the sub-tile's keep-bit words (8-row groups x 16 column groups), staged in LDS with dY4
   __shared__ uint32_t kbs[KB ? Q6T_SUB / 8 : 1][16];
   // the head's dY4 rows (and keep words) of the next sub-tile ride in registers with its x loads
@@ -711,37 +723,42 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
   constexpr int ND4 = NOUT > 0 ? (Q6T_SUB * D4LD + 255) / 256 : 1;
   float d4r[ND4];
   uint32_t kbr = 0u;
-  auto load_sub = [&](int64_t m0n) __attribute__((always_inline)) {
+  auto load_sub = [&](int64_t m0n, auto slot_c) __attribute__((always_inline)) {
+    constexpr int S = decltype(slot_c)::value;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int64_t r = m0n + row_of(i);
-      if (m0n < mp && r < M) {
-        xr[i] = xin_raw4<Z16>(xin, r * C + c);
-        if constexpr (NOUT == 0) gr[i] = ld4(dy + r * C + c);
+      if (m0n < mend && r < M) {
+        xr[S][i] = xin_raw4<Z16>(xin, r * C + c);
+        if constexpr (NOUT == 0) gr[S][i] = ld4(dy + r * C + c);
       }
     }
     if constexpr (NOUT > 0) {
 #pragma unroll
       for (int u = 0; u < ND4; ++u) {
         const int i = t + 256 * u, rr = i / D4LD, q = i - rr * D4LD;
-        d4r[u] = (m0n < mp && i < Q6T_SUB * D4LD && m0n + rr < M && q < NOUT) ? dy[(m0n + rr) * NOUT + q] : 0.f;
+        d4r[u] = (m0n < mend && i < Q6T_SUB * D4LD && m0n + rr < M && q < NOUT) ? dy[(m0n + rr) * NOUT + q] : 0.f;
       }
       if constexpr (KB) {
         const int64_t r8 = m0n + 8 * (t >> 4);
-        kbr = (m0n < mp && t < Q6T_SUB * 2 && r8 < M) ? dp.bits[keep_word(r8, c0 + 4 * (t & 15), C)] : 0u;
+        kbr = (m0n < mend && t < Q6T_SUB * 2 && r8 < M) ? dp.bits[keep_word(r8, c0 + 4 * (t & 15), C)] : 0u;
       }
     }
   };
-  load_sub(mbase);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, PD - 1>;
+  load_sub(mbase, S0{});
+  if constexpr (PD == 2) load_sub(mbase + Q6T_SUB, S1{});
   // the digit records of sub-tile s are stored one phase late -- after sub-tile s+1's dz phase, just
   // before its loads for s+2 are issued -- so they drain while s+1 is quantised: the vector-memory
   // counter retires in issue order, and loads issued behind a sub-tile's stores had to wait for those
   // stores first (the records stored at once cost 0.4-0.7 ms per wide-step pass: timing-only builds
   // without stores, profiles/r04_q6_diag.log)
   int64_t m_prev = -1;
-  for (int sub = 0; sub < rows_wg / Q6T_SUB; ++sub) {
+  // one sub-tile; slot_c = its prefetch register set (compile-time: the loop runs PD sub-tiles per trip)
+  auto sub_tile = [&](int sub, auto slot_c) __attribute__((always_inline)) {
+    constexpr int S = decltype(slot_c)::value;
     const int64_t m0 = mbase + sub * Q6T_SUB;
-    if (m0 >= mp) break;                       // block-uniform
     Q6_STAMP(sub, 0);
     if constexpr (NOUT > 0) {   // this sub-tile's dY4 rows, padded to float4 rows (prefetched)
 #pragma unroll
@@ -782,13 +799,13 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
         }
       }
       if (r < M) {
-        const float4 xv = xin_cvt4<Z16>(xr[i], xb);
+        const float4 xv = xin_cvt4<Z16>(xr[S][i], xb);
         float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         float gs[4];
         if constexpr (NOUT > 0) {
           head_grad4<NOUT>(d4s + rr * D4LD, wc, gs);
         } else {
-          const float4 gv = gr[i];
+          const float4 gv = gr[S][i];
           gs[0] = gv.x, gs[1] = gv.y, gs[2] = gv.z, gs[3] = gv.w;
         }
         uint32_t km = 0u;
@@ -843,7 +860,7 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
     __syncthreads();                           // the staged records are read before they are rewritten
     Q6_STAMP(sub, 2);
-    load_sub(m0 + Q6T_SUB);
+    load_sub(m0 + PD * Q6T_SUB, slot_c);
     // this lane's block maximum (waves 0-1: row blocks, 2-3: column blocks), reset for the next sub-tile
     const int b = wave & 1;
     uint32_t* amp = wave < 2 ? &rmax[b][lane] : &cmax[b][lane];
@@ -872,6 +889,14 @@ __global__ __launch_bounds__(256, (NOUT > 0 && !Z16) ? 2 : (NOUT > 0 ? Q6_HEAD_O
     __syncthreads();
     Q6_STAMP(sub, 3);
     m_prev = m0;
+  };
+  for (int sub = 0; sub < rows_wg / Q6T_SUB; sub += PD) {
+    if (mbase + sub * Q6T_SUB >= mp) break;     // block-uniform
+    sub_tile(sub, S0{});
+    if constexpr (PD == 2) {
+      if (sub + 1 >= rows_wg / Q6T_SUB || mbase + (sub + 1) * Q6T_SUB >= mp) break;
+      sub_tile(sub + 1, S1{});
+    }
   }
   if (m_prev >= 0) q6_stage_store(st, o, t, m_prev, M, c0, nblk_c);
   if (o.part != nullptr) {
