@@ -735,7 +735,15 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
   constexpr int TM = 2 * TILE;                                       // rows per store tile
   __shared__ __attribute__((aligned(16))) int tile[TM * TILE];       // swizzled (qct_at<TILE, true, 32>)
   double csum[4] = {0.0, 0.0, 0.0, 0.0};
-  const int64_t n0 = (int64_t)blockIdx.x * TILE;
+  // bijective XCD remap (workgroups b and b+8 share an XCD under round-robin dispatch): an XCD takes
+  // a contiguous run of (strip, row-block) tiles, so the four strips whose s20 nibbles share one
+  // 128-B line (64 columns = 32 B of nibbles per row) read it through one L2 -- spread over four
+  // XCDs each L2 fetched the whole line (PMC: 8.5 B fetched per element against 6.5 algorithmic)
+  const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+  const int xcd = bid & 7, xq = nwg >> 3, xr = nwg & 7;
+  const int L = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (bid >> 3);
+  const int bx = L % (int)gridDim.x, by = L / (int)gridDim.x;
+  const int64_t n0 = (int64_t)bx * TILE;
   const int t = threadIdx.x, cg = t & 15, rg = t >> 4;
   const int64_t c = n0 + 4 * cg;
   Bn4 b;
@@ -761,7 +769,7 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
       }
     }
   };
-  const int64_t mb = (int64_t)blockIdx.y * QC_RT * TILE;
+  const int64_t mb = (int64_t)by * QC_RT * TILE;
   long long dacc = 0;   // this thread's column (n0 + t/4) digit sum over the strip
   load(mb);
   for (int it = 0; it < QC_RT; ++it) {
@@ -802,7 +810,7 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
   }
   if (dsum != nullptr && (t & 3) == 0 && n0 + (t >> 2) < N && dacc != 0)
     atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n0 + (t >> 2)), (unsigned long long)dacc);
-  if (part != nullptr && blockIdx.y < qc_strips(M)) {
+  if (part != nullptr && by < qc_strips(M)) {
     // fixed-order fold of the 16 row groups' sums (the tile is free: every qct_store read is done)
     __syncthreads();
     double* ps = reinterpret_cast<double*>(tile);   // [16][64] doubles = 8 KiB <= 32 KiB
@@ -813,7 +821,7 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
       double s = 0.0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) s += ps[r * TILE + t];
-      part[(int64_t)blockIdx.y * N + n0 + t] = s;
+      part[(int64_t)by * N + n0 + t] = s;
     }
   }
 }
