@@ -141,6 +141,7 @@ SIGNATURES = {
     "bnn_gemm_fp6_kernel_k": (ctypes.c_char_p, [I64, I64, I64]),
     "bnn_gemm_fp6_set_variant": (I32, [I32]),
     "bnn_gemm_fp6_set_persistent": (I32, [I32]),
+    "bnn_gemm_fp6_set_half": (I32, [I32, ctypes.c_double]),
 }
 
 _lib = None

@@ -469,16 +469,22 @@ def _placeholder(shape, device):
         z = torch.zeros((1,), dtype=torch.float32, device=device)
         if z.device.type != "cuda" or not torch.cuda.is_current_stream_capturing():
             _ZERO1[key] = z
+        _ZERO_PTRS.add(z.data_ptr())          # capture-time zeros too: the graph's pool keeps them
     ph = z.as_strided(tuple(shape), (0,) * len(shape))
     ph._bnn_token = next(_TOKENS)
     return ph
 
 
+_ZERO_PTRS = set()
+
+
 def _is_placeholder(t):
-    """t views the cached zero every hand-off placeholder is made of (a stride-0 gradient that is
-    NOT a placeholder -- e.g. sum()'s expanded ones -- is a legitimate dense-valued gradient)."""
-    z = _ZERO1.get(str(t.device))
-    return z is not None and t.data_ptr() == z.data_ptr()
+    """t is a hand-off placeholder: it carries a placeholder token, or (an object torch re-wrapped
+    without the Python attributes) views one of the zeros placeholders are made of -- in graph
+    capture each placeholder gets a fresh zero from the graph's pool, so the cached one is not
+    enough.  A stride-0 gradient that is NOT a placeholder (e.g. sum()'s expanded ones) is a
+    legitimate dense-valued gradient."""
+    return getattr(t, "_bnn_token", None) is not None or t.data_ptr() in _ZERO_PTRS
 
 
 def _z16_carrier(y16, bias):

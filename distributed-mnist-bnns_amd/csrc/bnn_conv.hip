@@ -11,6 +11,10 @@
 #include <type_traits>
 
 #include "bnn_common.h"
+
+#include <map>
+#include <mutex>
+#include <vector>
 #include "bnn_bn2d.h"
 
 #include <cstring>
@@ -1813,24 +1817,31 @@ BNN_API int bnn_conv_set_popc(int32_t on) {
   return 0;
 }
 
-// The popcount engine's packed weight words: one device buffer per process and device, grown on
-// demand outside graph capture (the eager warm-up step before a capture sizes it), used in stream
-// order by every popcount launch.
-static uint32_t* popc_wpack_buffer(int64_t words) {
-  static uint32_t* buf[64] = {nullptr};
-  static int64_t cap[64] = {0};
+// The popcount engine's packed weight words: one device buffer per (device, stream), so launches on
+// different streams never share one.  A buffer only grows outside graph capture (the eager warm-up
+// step before a capture sizes it), and a buffer that was outgrown is retired, never freed: a HIP
+// graph captured earlier may still hold its pointer and write it on replay.
+static uint32_t* popc_wpack_buffer(int64_t words, hipStream_t st) {
+  struct Buf {
+    uint32_t* p;
+    int64_t cap;
+  };
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, Buf> bufs;
+  static std::vector<uint32_t*> retired;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (cap[dev] >= words) return buf[dev];
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  Buf& b = bufs[{dev, st}];
+  if (b.cap >= words) return b.p;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(nullptr, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
-  if (buf[dev] != nullptr) (void)hipFree(buf[dev]);
-  buf[dev] = nullptr;
-  cap[dev] = 0;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
   const int64_t n = std::max<int64_t>(words, 8192);
-  if (hipMalloc(reinterpret_cast<void**>(&buf[dev]), (size_t)n * sizeof(uint32_t)) != hipSuccess) return nullptr;
-  cap[dev] = n;
-  return buf[dev];
+  uint32_t* p = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)n * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (b.p != nullptr) retired.push_back(b.p);
+  b = Buf{p, n};
+  return p;
 }
 
 static bool popc_pick(const ConvShape& s, int binarize) {
@@ -1840,7 +1851,7 @@ static bool popc_pick(const ConvShape& s, int binarize) {
 
 static int popc_run(const ConvShape& s, const float* x, const float* w, const float* bias, void* y, int yfmt,
                     hipStream_t st, const char* who) {
-  uint32_t* wpk = popc_wpack_buffer(popc_wpack_words(s.Co, s.C, s.KH));
+  uint32_t* wpk = popc_wpack_buffer(popc_wpack_words(s.Co, s.C, s.KH), st);
   if (wpk == nullptr) {
     set_error("%s: no popcount weight buffer (first use inside a graph capture, or out of memory)", who);
     return kErrInval;

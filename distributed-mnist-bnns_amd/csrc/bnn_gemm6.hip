@@ -210,6 +210,11 @@ struct Gemm6Params {
     int z16, hardtanh, mode;
   } bn;
   const uint8_t* ares = nullptr;   // the residual FP4 plane [M][K/32][16 B] (instances with RES = 1)
+  // first-round stagger (bnn_gemm_fp6_set_half): workgroups stg_lo <= bid < stg_hi wait stg_ticks of
+  // the 100 MHz realtime clock before their k loop, so the two workgroups sharing a CU run half a
+  // tile apart and one's epilogue stores drain while the other's MFMAs run
+  int stg_lo = 0, stg_hi = 0;
+  int64_t stg_ticks = 0;
 };
 
 __device__ __forceinline__ void glds16_6(const void* g, void* l) {
@@ -296,6 +301,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void gemm_fp6_k(Gemm6P
 
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  if (p.stg_ticks > 0 && (int)blockIdx.x >= p.stg_lo && (int)blockIdx.x < p.stg_hi) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < p.stg_ticks) __builtin_amdgcn_s_sleep(32);
+  }
   int tm, tn;
   const int split = p.ksplit > 1 ? (int)(blockIdx.x % p.ksplit) : 0;
   tile6_of(p.ksplit > 1 ? (int)(blockIdx.x / p.ksplit) : (int)blockIdx.x, p.gm, p.gn, p.group, tm, tn);
@@ -1232,6 +1241,11 @@ const Variant6 kVariants6[] = {
 };
 
 int g_variant6 = -1;
+// bnn_gemm_fp6_set_half: 0 = the 128 x 512 tile, one workgroup per CU (default); 1 = the dX
+// launches (residual plane) on 64 x 512 tiles, two 4-wave workgroups per CU; 2 = the dW launches
+// (4 planes) too.  g_half_ticks: the first-round stagger of the second workgroup on each CU.
+int g_fp6_half = 0;
+int64_t g_half_ticks = 0;
 
 const Variant6* find6(int id) {
   for (const Variant6& v : kVariants6)
@@ -1336,6 +1350,14 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
                          const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
                          int64_t M, int64_t N, int64_t K, void* work, int64_t work_bytes, void* stream);
 
+// Whether a launch takes the persistent form of the default tile (gemm_fp6_pers_k, selected by
+// bnn_gemm_fp6_set_persistent): no bias, B in panels, whole K per tile, a 128 x 512-tiled shape of at
+// least two rounds of tiles.  One predicate for gemm_fp6_impl and the name bnn_gemm_fp6_kernel_k reports.
+static bool fp6_pers_applies(int64_t M, int64_t N, int ksplit, bool has_bias, bool panel) {
+  return g_fp6_pers && !has_bias && panel && ksplit <= 1 && g_variant6 < 0 && M % 128 == 0 && N % 512 == 0 &&
+         (M / 128) * (N / 512) >= 2 * device_cus();
+}
+
 BNN_API int bnn_gemm_fp6(const uint8_t* alo, const uint8_t* ahi, const uint8_t* asc, int64_t asc_rows,
                          const uint8_t* ares, const uint8_t* b, int64_t ldb, const float* bias, float* C, int64_t ldc,
                          int64_t M, int64_t N, int64_t K, void* stream) {
@@ -1371,24 +1393,43 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   Gemm6Params p{alo, ahi, asc, b, ldb, asc_rows, bias, C, ldc, (int)M, (int)N, (int)K, 0, 0, K >= 32768 ? 8 : 4,
                 split ? pl.ksplit : 1, 0, split ? reinterpret_cast<float*>(work) : nullptr, panel ? -ldb : 0, {}};
 
-  // the persistent form of the default tile: no bias, whole K per tile, at least two rounds of tiles
-  const int64_t tiles = ((M + 127) / 128) * ((N + 511) / 512);
-  const bool pers = g_fp6_pers && bias == nullptr && p.ksplit == 1 && g_variant6 < 0 && tiles >= 2 * device_cus() &&
-                    panel && M % 128 == 0 && N % 512 == 0;
+  const bool pers = fp6_pers_applies(M, N, p.ksplit, bias != nullptr, panel);
+  // the half-tile form: 64 x 512 tiles, two workgroups per CU, the second resident of each CU in the
+  // first round (blocks [CUs, 2 CUs): tools/probes/probe_wg_placement.hip) held back g_half_ticks
+  const bool half = g_fp6_half > 0 && bias == nullptr && p.ksplit == 1 && g_variant6 < 0 && !pers &&
+                    (ares ? true : g_fp6_half > 1) && M % 64 == 0 && N % 512 == 0 &&
+                    (M / 64) * (N / 512) >= 4 * device_cus();
+  if (half) {
+    p.stg_lo = device_cus();
+    p.stg_hi = 2 * device_cus();
+    p.stg_ticks = g_half_ticks;
+  }
   if (ares) {   // the residual plane runs on the default tile (variant 7) with its own instance
     p.ares = ares;
     if (pers) return launch6_pers<1>(p, device_cus(), S6(stream));
+    if (half) return launch6<1, 4, 2, 4, 2, 0, 2, 0, 0, 1>(p, S6(stream));
     return launch6<2, 4, 2, 4, 2, 0, 2, 0, 0, 1>(p, S6(stream));
   }
+  if (half) return launch6<1, 4, 2, 4, 2>(p, S6(stream));
   if (pers && pl.v->id == 7) return launch6_pers<0>(p, device_cus(), S6(stream));
   return pl.v->fn(p, S6(stream));
 }
 
-// 1 (default): the FP6 GEMM's default tile runs persistent with split load / store roles on grids
-// of two or more rounds (gemm_fp6_pers_k); 0: one workgroup per tile.  on < 0 queries.
+// 0 (default): one workgroup per tile.  1: the default tile runs persistent with split load / store
+// roles on grids of two or more rounds (gemm_fp6_pers_k; measured slower on both backward shapes,
+// DESIGN.md §5 -- kept for A/B).  on < 0 queries.
 BNN_API int bnn_gemm_fp6_set_persistent(int32_t on) {
   if (on < 0) return g_fp6_pers;
   g_fp6_pers = on != 0;
+  return 0;
+}
+
+// The FP6 GEMM's half-tile form (g_fp6_half above): mode 0 / 1 / 2, stagger in microseconds (the
+// first-round wait of the second workgroup on each CU); mode < 0 queries the mode.
+BNN_API int bnn_gemm_fp6_set_half(int32_t mode, double stagger_us) {
+  if (mode < 0) return g_fp6_half;
+  g_fp6_half = mode;
+  g_half_ticks = (int64_t)(stagger_us * 100.0);
   return 0;
 }
 
@@ -1463,10 +1504,10 @@ BNN_API const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N) { return pick6(M, 
 BNN_API const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K) {
   const Fp6Plan pl = plan6(M, N, K);
   static thread_local char buf[96];
-  // the persistent form where the shape takes it (no bias, B in panels: the backward GEMMs)
-  if (pl.ksplit <= 1 && g_fp6_pers && g_variant6 < 0 && M % 128 == 0 && N % 512 == 0 &&
-      (M / 128) * (N / 512) >= 2 * device_cus())
-    return "gemm_fp6_pers_k<2, 4, 2, 4, 2>";
+  // the name of what the backward GEMMs (no bias, B in panels) launch on this shape: the persistent
+  // form where gemm_fp6_impl's predicate takes it; a residual-plane launch runs the default tile's
+  // RES instance, which is variant 7 = the plan's choice on every unsplit shape of the wide step
+  if (fp6_pers_applies(M, N, pl.ksplit, false, true)) return "gemm_fp6_pers_k<2, 4, 2, 4, 2>";
   if (pl.ksplit <= 1) return pl.v->name;
   snprintf(buf, sizeof buf, "%s split-K %d", pl.v->name, pl.ksplit);
   return buf;

@@ -276,6 +276,12 @@ int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) *
  * (gemm_fp6_pers_k); bit-identical to 0 (one workgroup per tile, the default: measured faster).
  * on < 0 queries. */
 int bnn_gemm_fp6_set_persistent(int32_t on);
+/* Half-tile form of the backward GEMMs: mode 1 runs the dX launches (residual plane) on 64 x 512
+ * tiles, two 4-wave workgroups per CU, the second resident of each CU held back stagger_us in the
+ * first round so one workgroup's fp32 epilogue drains while the other's MFMAs run; mode 2 also the
+ * dW launches; 0 = the 128 x 512 tile (default).  Same fragments and accumulation order per output
+ * element: bit-identical C.  mode < 0 queries. */
+int bnn_gemm_fp6_set_half(int32_t mode, double stagger_us);
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row

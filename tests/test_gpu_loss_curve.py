@@ -130,20 +130,22 @@ def test_mnist_loss_curve_matches_reference_semantics():
     assert abs(accL - accT) <= 0.015
 
 
-LIBBNN_SEEDS = (11, 12, 13)
-TORCH_SEEDS = (21, 31, 41, 51)
+LIBBNN_SEEDS = tuple(range(100, 108))
+TORCH_SEEDS = tuple(range(200, 208))
 
 
 def test_mnist_loss_curve_dropout():
     """p = 0.3 (mnist-dist2.py:69), the bench's dropout: the fused path's hash masks against torch's
-    dropout.  No two runs share a mask, so both sides are sampled over several dropout seeds (3 for
-    libbnn, 4 for torch) and their MEANS are compared, the band set by how far torch's own seeds
-    spread: window losses of the mean curves within max(2 x the largest window gap between the mean
-    curves of torch's two seed halves, 0.02); mean accuracy within max(the range of torch's four
-    accuracies, 0.01).  (Round 5: the single-seed form of this check -- one libbnn run against one
-    torch run, bar max(1.5 points, 2 x the gap between two torch runs) -- failed at 1.54 points once
-    the dX GEMMs' residual plane moved libbnn's trajectory: 94.21 % against 95.75 / 95.30 %, a
-    sample of one.)"""
+    dropout.  No two runs share a mask, so both sides are sampled over 8 dropout seeds each and
+    their MEANS are compared: window losses of the mean curves within max(2 x the largest window gap
+    between the mean curves of torch's two seed halves, 0.02); mean training accuracy within 3
+    standard errors of the difference of the two means (the seed-to-seed spread, estimated from all
+    16 runs, so one outlying seed cannot set the bar), at least 0.5 points.
+    History: round 5's single-seed form failed once at 1.54 points (94.21 % against 95.75 / 95.30 %,
+    a sample of one), and its replacement's bar -- the range of 4 torch seeds -- let one outlier set
+    it.  With 8 seeds per side (profiles/r06_a_dropout_spread.log): libbnn 95.13 % +- 0.29 (s.e.),
+    BNN_FP6_RES=0 95.35 +- 0.32, BNN_KEEP_BITS=0 95.13 (bit-identical masks), torch 94.57 +- 0.45:
+    neither round-5 change moved the accuracy beyond seed noise."""
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     from bnn_amd import nets
@@ -155,14 +157,18 @@ def test_mnist_loss_curve_dropout():
     wl = np.mean([_windows(r[0]) for r in runs_l], axis=0)
     wts = [_windows(r[0]) for r in runs_t]
     wt = np.mean(wts, axis=0)
-    half = np.abs(np.mean(wts[:2], axis=0) - np.mean(wts[2:], axis=0))
+    h = len(wts) // 2
+    half = np.abs(np.mean(wts[:h], axis=0) - np.mean(wts[h:], axis=0))
     band = max(2 * float(half.max()), 0.02)
-    acc_l, acc_t = [r[1] for r in runs_l], [r[1] for r in runs_t]
-    abar = max(max(acc_t) - min(acc_t), 0.01)
-    print("\nwindow mean loss, p=0.3  libbnn (mean of 3):", " ".join(f"{v:.3f}" for v in wl))
-    print("window mean loss, p=0.3  torch  (mean of 4):", " ".join(f"{v:.3f}" for v in wt))
+    acc_l, acc_t = np.array([r[1] for r in runs_l]), np.array([r[1] for r in runs_t])
+    se = float(np.hypot(acc_l.std(ddof=1) / np.sqrt(len(acc_l)), acc_t.std(ddof=1) / np.sqrt(len(acc_t))))
+    abar = max(3 * se, 0.005)
+    print("\nwindow mean loss, p=0.3  libbnn (mean of 8):", " ".join(f"{v:.3f}" for v in wl))
+    print("window mean loss, p=0.3  torch  (mean of 8):", " ".join(f"{v:.3f}" for v in wt))
     print(f"max window gap {np.abs(wl - wt).max():.4f} (band {band:.4f}: torch halves {half.max():.4f}); "
-          f"accuracy libbnn {acc_l} mean {np.mean(acc_l):.4f}, torch {acc_t} mean {np.mean(acc_t):.4f} (bar {abar:.4f})")
+          f"accuracy libbnn {np.round(acc_l, 4).tolist()} mean {acc_l.mean():.4f}, torch {np.round(acc_t, 4).tolist()} "
+          f"mean {acc_t.mean():.4f}; |difference| {abs(acc_l.mean() - acc_t.mean()):.4f} against 3 s.e. = {3 * se:.4f} "
+          f"(bar {abar:.4f})")
     assert np.abs(wl - wt).max() <= band
     assert all(_windows(r[0])[-1] < 0.5 * _windows(r[0])[0] for r in runs_l + runs_t)
-    assert abs(np.mean(acc_l) - np.mean(acc_t)) <= abar
+    assert abs(acc_l.mean() - acc_t.mean()) <= abar

@@ -37,11 +37,11 @@ float64 oracle (oracle/bnn_t64.py, pinned to the reference's traces on the CPU) 
 * the update: every parameter after LatentAdam equals torch's Adam (float64) + the clamp on the
   GPU's own gradient, elementwise <= 1e-7.
 
-test_wide_bench_loss_vs_reference_semantics records the loss of the bench's first 25 steps (its
-batch, seed, lr and dropout) beside the reference semantics on torch fp32 on the same GPU
-(oracle/bnn_torch.py RefMLP + the .org protocol, torch's dropout) run twice with different
-dropout seeds: the spread of those two is the band the fused path is held to (mean of the last 10
-steps), and the curves are printed (why the loss of this workload sits above ln 10).
+test_wide_bench_loss_same_masks records the loss of the bench's first 25 steps (its batch, seed,
+lr and dropout) beside the reference semantics on torch fp32 on the same GPU (oracle/bnn_torch.py
+RefMLP + the .org protocol) driven by libbnn's own dropout masks, so the two differ only in
+arithmetic; the band is the spread of the reference run under row permutations of the batch, and
+the curves are printed (why the loss of this workload sits above ln 10).
 """
 import numpy as np
 import pytest
@@ -250,50 +250,6 @@ def test_wide_step_config5_vs_float64(monkeypatch):
 STEPS = 25
 
 
-def test_wide_bench_loss_vs_reference_semantics():
-    if not torch.cuda.is_available():
-        pytest.skip("needs a ROCm GPU")
-    from bnn_amd.nets import binary_params
-    from bnn_amd.optim import LatentAdam
-    from oracle.bnn_torch import RefMLP, train_step
-    model, x, y = _bench_setup()
-    state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    opt = LatentAdam(model.parameters(), lr=LR, clamp_params=binary_params(model))
-    crit = torch.nn.CrossEntropyLoss()
-    L = []
-    for _ in range(STEPS):                                # bench.main's step()
-        for p in model.parameters():
-            p.grad = None
-        loss = crit(model(x), y)
-        loss.backward()
-        opt.step()
-        L.append(loss.detach())
-    L = np.array([float(v) for v in L])
-    del model, opt
-    torch.cuda.empty_cache()
-    xf = x.float().div(255.0)
-    curves = []
-    for seed in (100, 200):
-        torch.manual_seed(seed)                           # torch's dropout masks (Philox)
-        ref = RefMLP(8192, 8192, 8192, p_drop=0.3)
-        ref.load_state_dict(state)
-        ref = ref.cuda().train()
-        ropt = torch.optim.Adam(ref.parameters(), lr=LR)
-        curves.append(np.array([train_step(ref, ropt, xf.clone(), y, True) for _ in range(STEPS)]))
-        del ref, ropt
-        torch.cuda.empty_cache()
-    T1, T2 = curves
-    tail = lambda a: float(a[-10:].mean())   # noqa: E731
-    band = max(2 * abs(tail(T1) - tail(T2)), 0.05 * tail(T1))
-    print("\nwide bench workload, loss per step (libbnn fused, hash dropout):", " ".join(f"{v:.3f}" for v in L))
-    print("reference semantics torch fp32, dropout seed 100             :", " ".join(f"{v:.3f}" for v in T1))
-    print("reference semantics torch fp32, dropout seed 200             :", " ".join(f"{v:.3f}" for v in T2))
-    print(f"mean of the last 10 steps: libbnn {tail(L):.4f}, torch {tail(T1):.4f} / {tail(T2):.4f} (band {band:.4f}); "
-          f"step 0: {L[0]:.5f} / {T1[0]:.5f} / {T2[0]:.5f}")
-    assert abs(L[0] - T1[0]) <= 0.01 and abs(T1[0] - T2[0]) <= 0.01    # same init, masks differ
-    assert abs(tail(L) - tail(T1)) <= band
-
-
 def test_wide_bench_loss_same_masks():
     """The bench workload against the reference semantics (torch fp32 RefMLP, the reference's .org
     protocol) driven by libbnn's OWN dropout masks: the seeds the fused head draws are recorded and
@@ -303,8 +259,9 @@ def test_wide_bench_loss_same_masks():
     -- the same math in another fp32 summation order.  Bars: step 0 within 1e-4; steps 1-2 (before
     the Adam steps at lr 0.01 have inflated the logits -- mnist-dist2.py's own dynamics, after which
     fp32 rounding differences grow chaotically) within 2e-3 relative; the mean of the last 10 steps
-    within max(3 x the calibration's gap, 5 %) -- against ~0.9 for differing masks
-    (test_wide_bench_loss_vs_reference_semantics)."""
+    within 1.5 x the calibration spread -- the largest gap between the tail means of the reference
+    run and two row-permuted copies of it (three arithmetic orders of the same math).  (Round 5 held
+    it to 3 x one permutation's gap; the differing-mask comparison this test superseded allowed 28 %.)"""
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     from bnn_amd import _lib as L
@@ -373,16 +330,18 @@ def test_wide_bench_loss_same_masks():
 
     T = reference(None)
     Tp = reference(torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(5)).cuda())
+    Tq = reference(torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(6)).cuda())
     tail = lambda a: float(a[-10:].mean())   # noqa: E731
     rel = np.abs(Lb - T) / np.abs(T)
-    calib = abs(tail(T) - tail(Tp))
-    bar = max(3 * calib, 0.05 * tail(T))
+    calib = max(abs(tail(T) - tail(Tp)), abs(tail(T) - tail(Tq)), abs(tail(Tp) - tail(Tq)))
+    bar = 1.5 * calib
     print("\nwide bench workload, same dropout masks: libbnn", " ".join(f"{v:.4f}" for v in Lb))
     print("reference semantics torch fp32, libbnn's masks  ", " ".join(f"{v:.4f}" for v in T))
     print("the same, batch rows permuted (calibration)     ", " ".join(f"{v:.4f}" for v in Tp))
+    print("the same, another row permutation (calibration) ", " ".join(f"{v:.4f}" for v in Tq))
     print(f"relative gap per step: {' '.join(f'{v:.1e}' for v in rel)}")
-    print(f"tail means: libbnn {tail(Lb):.4f}, torch {tail(T):.4f}, permuted {tail(Tp):.4f}; "
-          f"|libbnn - torch| {abs(tail(Lb) - tail(T)):.4f} against bar {bar:.4f} (calibration gap {calib:.4f})")
+    print(f"tail means: libbnn {tail(Lb):.4f}, torch {tail(T):.4f}, permuted {tail(Tp):.4f} / {tail(Tq):.4f}; "
+          f"|libbnn - torch| {abs(tail(Lb) - tail(T)):.4f} against bar {bar:.4f} (calibration spread {calib:.4f})")
     assert abs(Lb[0] - T[0]) <= 1e-4
     assert np.all(rel[1:3] <= 2e-3)
     assert abs(tail(Lb) - tail(T)) <= bar
