@@ -23,6 +23,7 @@ SIGNATURES = {
     "bnn_last_error": (ctypes.c_char_p, []),
     "bnn_sign_pack_i8": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_sign_pack_fp4": (I32, [P, I64, I64, I64, P, I64, P, I64, I32, P]),
+    "bnn_sign_pack_fp4_out": (I32, [P, I64, I64, P, I64, P, I64, I32, P, P]),
     "bnn_sign_f32": (I32, [P, P, I64, P]),
     "bnn_sign_pack_bits": (I32, [P, I64, I64, I64, P, P, I64, P]),
     "bnn_quant_rows": (I32, [P, I64, I64, I64, P, I64, I64, P, P]),
@@ -54,6 +55,7 @@ SIGNATURES = {
     "bnn_cross_entropy_workspace": (I64, [I64]),
     "bnn_cross_entropy_fwd": (I32, [P, P, I64, I64, I64, P, P, I64, P]),
     "bnn_cross_entropy_bwd": (I32, [P, P, I64, I64, I64, P, P, P, P]),
+    "bnn_unit_to_pixels": (I32, [P, I64, P, P, P]),
     "bnn_pixels_pack": (I32, [P, I64, I64, I64, P, I64, P, I64, P]),
     "bnn_row_sums": (I32, [P, I64, I64, I64, P, P]),
     "bnn_gemm_fp4": (I32, [P, I64, P, I64, P, P, I64, I64, I64, I64, P]),
@@ -139,9 +141,11 @@ SIGNATURES = {
     "bnn_gemm_fp6_panel_ws": (I32, [P, P, P, I64, P, P, I64, P, P, I64, I64, I64, I64, P, I64, P]),
     "bnn_gemm_fp6_kernel": (ctypes.c_char_p, [I64, I64]),
     "bnn_gemm_fp6_kernel_k": (ctypes.c_char_p, [I64, I64, I64]),
+    "bnn_gemm_fp6_kernel_kr": (ctypes.c_char_p, [I64, I64, I64, I32]),
     "bnn_gemm_fp6_set_variant": (I32, [I32]),
     "bnn_gemm_fp6_set_persistent": (I32, [I32]),
     "bnn_gemm_fp6_set_half": (I32, [I32, ctypes.c_double]),
+    "bnn_gemm_fp6_set_half_group": (I32, [I32]),
 }
 
 _lib = None

@@ -179,6 +179,27 @@ def sign_pack_fp4(x, want_qt=False, qt_fmt="i8", want_q=True):
     return q4, qt
 
 
+def sign_pack_fp4_writeback(x, want_qt=False):
+    """The drop-in BinarizeLinear's input side effect and its GEMM operands from one read of x:
+    (sign(x) fp32 -- the new ``input.data`` of binarized_modules.py:76 -- FP4 rows, FP4 transpose in
+    the FP6 GEMM's panel layout or None)."""
+    _check(x)
+    x = _c2d(x)
+    M, K = x.shape
+    s = torch.empty_like(x)
+    q4 = torch.empty((M, round_up(K, 256) // 2), dtype=torch.uint8, device=x.device)
+    qt = _qt_buffer(K, M, "fp4p", x.device) if want_qt else None
+    if M == 0:
+        return s, q4, qt
+    if qt is None:
+        sign(x, out=s)
+        return (s,) + sign_pack_fp4(s, want_qt=False)[:1] + (None,)
+    with _timed("sign_pack_fp4_out", 0, 8 * M * K + q4.numel() + qt.numel()):
+        L.call("bnn_sign_pack_fp4_out", L.ptr(x), M, K, L.ptr(q4), q4.shape[1], L.ptr(qt), qt.shape[1],
+               _QT_CODE["fp4p"], L.ptr(s), L.stream())
+    return s, q4, qt
+
+
 def sign_pack_bits(x, words=None):
     """fp32 [M,K] -> (sign bits, nonzero bits) int32 [M, words], words >= ceil(K/32)."""
     _check(x)
@@ -551,10 +572,17 @@ class Fp6Operand:
 # norm-wise on config 5's bn1/bn2 biases, fp32 GEMMs 7e-6 / 4e-6; tests/test_gpu_wide_step.py).
 # BNN_FP6_RES=0 drops it (A/B timing only).
 FP6_RES = os.environ.get("BNN_FP6_RES", "1") != "0"
+# ... on operands of at least this many rows.  dbeta sums dX over the batch, and the 4-plane
+# operand's rounding there grows with it (~sqrt(rows) against a sum that cancels): at B = 65,536
+# the 4-plane dX put bn1/bn2's bias gradients at 1.6e-5 / 1.5e-5 (profiles/r05_d_wide_step_parity_
+# residual.log), at B = 4,096 (config 3) every gradient stays <= 1e-5 without the fifth pass
+# (tests/test_gpu_net_configs.py, profiles/r06_*), so the smaller batches skip its MFMA pass and stores.
+FP6_RES_MIN_ROWS = int(os.environ.get("BNN_FP6_RES_MIN_ROWS", "8192"))
 
 
 def _res_buffer(rows, Kp, device):
-    return torch.empty((rows, Kp // 32 * 16), dtype=torch.uint8, device=device) if FP6_RES else None
+    return (torch.empty((rows, Kp // 32 * 16), dtype=torch.uint8, device=device)
+            if FP6_RES and rows >= FP6_RES_MIN_ROWS else None)
 
 
 def _fp6_buffers(rows, Kp, device):
@@ -647,7 +675,8 @@ def gemm_fp6(A, B4, N, bias=None, k_true=None, out=None, panels=None, panel_ks=N
 def _fp6_name(M, N, K, A):
     """Timer name of an FP6 GEMM launch: the library's kernel choice, + " +res" with the residual
     plane (a fifth MFMA pass: bench.py counts its passes)."""
-    return L.lib().bnn_gemm_fp6_kernel_k(M, N, K).decode() + (" +res" if A.res is not None else "")
+    res = A.res is not None
+    return L.lib().bnn_gemm_fp6_kernel_kr(M, N, K, int(res)).decode() + (" +res" if res else "")
 
 
 # The BatchNorm-backward statistics in the dX GEMM's epilogue (bnn_gemm_fp6_bnstats): the fused
@@ -688,7 +717,9 @@ class BinaryLinearFunction(torch.autograd.Function):
     """y = F.linear(bin(x), sign(w)) + b with the reference's STE backward (see module doc)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, binarize_input, backend="fp4", cache=False):
+    def forward(ctx, x, weight, bias, binarize_input, backend="fp4", cache=False, xpack=None):
+        # xpack: (FP4 rows, FP4 panel transpose or None) of sign(x), made with the input write-back
+        # (sign_pack_fp4_writeback); used instead of packing x again
         _check(x, weight, bias)
         M, K = x.shape
         N = weight.shape[0]
@@ -705,8 +736,14 @@ class BinaryLinearFunction(torch.autograd.Function):
         # keeps the 24-bit int8 digit form (forward bar 1e-6)
         ctx.fp6 = backend == "fp4" and DIGIT_GEMM == "fp6" and binarize_input
         qf = "fp4" if ctx.fp6 else "i8"
+        ctx.x_panels = False
         if binarize_input:
-            if backend == "fp4":
+            if backend == "fp4" and xpack is not None and ctx.fp6 and (xpack[1] is not None or not need_dw):
+                x4, xqt = xpack
+                ctx.x_panels = xqt is not None
+                w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache, qt_fmt=qf)
+                y = gemm_fp4(x4, w4, M, N, bias=b, k_true=K)
+            elif backend == "fp4":
                 x4, xqt = sign_pack_fp4(x, want_qt=need_dw, qt_fmt=qf)
                 w4, wqt = packed_weight(weight, "fp4", True, need_dx, cache, qt_fmt=qf)
                 y = gemm_fp4(x4, w4, M, N, bias=b, k_true=K)
@@ -737,7 +774,7 @@ class BinaryLinearFunction(torch.autograd.Function):
             return (torch.empty((0, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None,
                     torch.zeros((N, K), dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None,
                     torch.zeros((N,), dtype=torch.float32, device=dev)
-                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None)
+                    if ctx.has_bias and ctx.needs_input_grad[2] else None, None, None, None, None)
         xs, wqt = ctx.saved_tensors
         dy = _c2d(dy)
         dx = dw = db = None
@@ -749,9 +786,12 @@ class BinaryLinearFunction(torch.autograd.Function):
             if ctx.needs_input_grad[1] or need_db:
                 dt, cs = (pre[1], pre[2]) if pre is not None else quant6_cols_t(dy, want_colsum=need_db)
                 if ctx.needs_input_grad[1]:
-                    dw = gemm_fp6(dt, xs, K, k_true=M)                         # dY^T . X_b
+                    if ctx.x_panels:                                           # dY^T . X_b
+                        dw = gemm_fp6(dt, None, K, k_true=M, panels=xs, panel_ks=xs.shape[1] // 32)
+                    else:
+                        dw = gemm_fp6(dt, xs, K, k_true=M)
                 db = cs if need_db else None
-            return dx, dw, db, None, None, None
+            return dx, dw, db, None, None, None, None
         if ctx.needs_input_grad[0]:
             d, s = quant_rows(dy)                                   # [3, M, ldN]
             dx = gemm_i8(d, 3, wqt, 1, M, K, a_scale=s, k_true=N)   # dY . W_b
@@ -764,14 +804,14 @@ class BinaryLinearFunction(torch.autograd.Function):
                     xt, sxc, _ = quant_cols_t(xs)
                     dw = gemm_i8(dt, 3, xt, 3, N, K, a_scale=sc, b_scale=sxc, k_true=M)
             db = cs
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4", cache=False):
+def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4", cache=False, xpack=None):
     """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened).  ``cache``: the
     weight is a latent weight whose packed operands are cached on it (packed_weight)."""
     lead = x.shape[:-1]
-    y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend, cache)
+    y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend, cache, xpack)
     return y.reshape(*lead, weight.shape[0])
 
 
@@ -793,6 +833,28 @@ def pixels_to_float(u, normalize=None):
     if normalize is not None:
         x = (x - normalize[0]) / normalize[1]
     return x
+
+
+UNIT_PIXELS = 0          # fp32 ToTensor images recognised as bytes (tests check the path ran)
+
+
+def unit_to_pixels(x):
+    """fp32 images [.., K] that are exactly ToTensor's fl(u / 255) -> their bytes u (uint8, same
+    shape), else None.  One pass (bnn_unit_to_pixels) and one host read of its mismatch flag; None
+    during graph capture (the flag cannot be read there)."""
+    global UNIT_PIXELS
+    _check(x)
+    if x.numel() == 0 or (x.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return None
+    x = x if x.is_contiguous() else x.contiguous()
+    u = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    bad = torch.zeros((1,), dtype=torch.int32, device=x.device)
+    with _timed("unit_to_pixels_k", 0, 5 * x.numel()):
+        L.call("bnn_unit_to_pixels", L.ptr(x), x.numel(), L.ptr(u), L.ptr(bad), L.stream())
+    if int(bad.item()) != 0:
+        return None
+    UNIT_PIXELS += 1
+    return u
 
 
 def pixels_pack(u, want_q=True, want_qt=False):

@@ -114,6 +114,9 @@ class BinarizeLinear(nn.Linear):
         super().__init__(*kargs, **kwargs)
 
     pixel_normalize = None   # (mean, std) of a Normalize after ToTensor, for uint8 inputs
+    # the 784-input layer recognises fp32 ToTensor images (exact multiples fl(u / 255) of bytes) and
+    # runs its u8-pixel GEMMs on them (BF.unit_to_pixels); False keeps the fp32-digit GEMMs
+    detect_pixels = True
 
     def forward(self, input, emit_compact=False):
         # emit_compact (the build's fused MLP only): a u8-pixel layer's output may travel as its
@@ -128,14 +131,35 @@ class BinarizeLinear(nn.Linear):
                     self.bias.org = self.bias.data.clone()
             return BF.binary_linear_pixels(input, self.weight, self.bias, self.pixel_normalize,
                                            cache=not self.org_protocol, emit_compact=emit_compact)
+        if (not binarize and self.detect_pixels and self.pixel_normalize is None and input.dtype == torch.float32
+                and input.dim() == 2 and input.is_cuda and not input.requires_grad):
+            # fp32 images straight from ToTensor (mnist-dist2.py:96-99): exactly fl(u / 255) for bytes
+            # u, so fc1 runs on the bytes -- the same F.linear value within fp32 rounding (the u8
+            # path's integer sums are exact), one int8 pass instead of three digit planes each way
+            u = BF.unit_to_pixels(input)
+            if u is not None:
+                if self.org_protocol:
+                    _apply_org_protocol(self.weight)
+                    if self.bias is not None:
+                        self.bias.org = self.bias.data.clone()
+                return BF.binary_linear_pixels(u, self.weight, self.bias, None, cache=not self.org_protocol)
+        xpack = None
         if binarize and self.mutate_input:
-            input.data = BF.sign(input.data)                    # :76
+            if (self.backend == "fp4" and BF.DIGIT_GEMM == "fp6" and input.dim() == 2 and input.dtype == torch.float32
+                    and input.is_cuda):
+                # the write-back and the GEMM operands of sign(input) from one read of the input
+                need_dw = self.weight.requires_grad and torch.is_grad_enabled()
+                s, x4, xqt = BF.sign_pack_fp4_writeback(input.data, want_qt=need_dw)
+                input.data = s                                  # :76
+                xpack = (x4, xqt)
+            else:
+                input.data = BF.sign(input.data)                # :76
         if self.org_protocol:
             _apply_org_protocol(self.weight)                    # :77-79
             if self.bias is not None:
                 self.bias.org = self.bias.data.clone()          # :82
         return BF.binary_linear(input, self.weight, self.bias, binarize, self.backend,
-                                cache=not self.org_protocol)
+                                cache=not self.org_protocol, xpack=xpack)
 
 
 class BinarizeConv2d(nn.Conv2d):

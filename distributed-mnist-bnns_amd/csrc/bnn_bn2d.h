@@ -3,6 +3,8 @@
 #pragma once
 #include "bnn_common.h"
 
+#include <type_traits>
+
 namespace bnn {
 
 struct Bn2Chan {   // per-channel affine of the normalisation
@@ -56,42 +58,58 @@ __device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
   return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
 }
 
-// 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
-// The BatchNorm2d FORWARD passes read the compact (int8 / int16) conv outputs with device-scope loads
-// (COH = true).  With plain loads those passes returned different statistics from run to run --
-// never in one process alone, but in about one step in ten while other processes used the same
-// GPU (the two-rank data-parallel tests run that way) -- although every kernel of the sequence
-// waits for its loads, and a host synchronisation before and between the passes and an eviction of
-// every L2 did not change it; device-scope loads did (0 of 156 steps, plain 11 of 156;
-// tools/race_trace.py, profiles/r05_race_*.log).  The backward passes keep plain loads
-// (every stage after the forward was identical once the forward was).  BN2_PLAIN_LOADS builds the
-// plain form everywhere (A/B only).
+// Every read of the compact (int8 / int16) conv outputs goes around the reading CU's vector L1
+// (BN2_LOADS 1: nt loads, which the compiler still merges into 16-B instructions).  With plain
+// loads the BatchNorm2d forward passes returned different statistics from run to run -- never in
+// one process alone, in about one step in ten while other processes used the same GPU (the
+// two-rank data-parallel tests run that way) -- although the conv sums in memory were identical
+// every time; host synchronisations before and between the passes and a 512 MB L2 eviction left it
+// so, loads that bypass L1 (agent-scope sc1, round 5) removed it (0 of 156 steps, plain 11 of 156;
+// tools/race_trace.py, profiles/r05_race_*.log).  sc1 and nt loads are served by L2 and skip L1
+// alone (MI355X_MICROARCH.md, visibility table), so the stale bytes came from the consumer CU's L1:
+// the fix belongs to every consumer of freshly written compact data, the forward and backward
+// BatchNorm2d passes and conv1's fused filter gradient alike.  BN2_LOADS 0 / 2
+// build the plain / sc1-atomic forms (A/B only).
+#ifndef BN2_LOADS
+#define BN2_LOADS 1
+#endif
 template <bool COH>
 __device__ __forceinline__ uint2 x2_raw8(const void* p) {
-#ifndef BN2_PLAIN_LOADS
-  if constexpr (COH) {
+  if constexpr (COH && BN2_LOADS == 2) {
     const uint64_t v =
         __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+  } else if constexpr (COH && BN2_LOADS == 1) {
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+    return make_uint2(v.x, v.y);
   }
-#endif
   return *reinterpret_cast<const uint2*>(p);
 }
 template <bool COH>
 __device__ __forceinline__ uint32_t x2_raw4(const void* p) {
-#ifndef BN2_PLAIN_LOADS
-  if constexpr (COH)
+  if constexpr (COH && BN2_LOADS == 2)
     return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+  else if constexpr (COH && BN2_LOADS == 1)
+    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
   return *reinterpret_cast<const uint32_t*>(p);
 }
+template <bool COH, typename T>
+__device__ __forceinline__ T x2_raw_small(const T* p) {   // 1 or 2 bytes
+  if constexpr (COH && BN2_LOADS == 2)
+    return (T)__hip_atomic_load(reinterpret_cast<const typename std::make_unsigned<T>::type*>(p), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+  else if constexpr (COH && BN2_LOADS == 1)
+    return __builtin_nontemporal_load(p);
+  return *p;
+}
 
-template <int XF, bool COH = false>
+// 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
+template <int XF, bool COH = true>
 __device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
   } else if constexpr (XF == 1) {
-    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    const uint32_t u = x2_raw4<COH>(reinterpret_cast<const int8_t*>(x.p) + idx);
     return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
                        (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
   } else {
@@ -102,12 +120,12 @@ __device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
 }
 
 // 2 consecutive elements (idx even)
-template <int XF, bool COH = false>
+template <int XF, bool COH = true>
 __device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
   } else if constexpr (XF == 1) {
-    const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    const uint16_t u = (uint16_t)x2_raw_small<COH>(reinterpret_cast<const int16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx));
     return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
   } else {
     const uint32_t u = x2_raw4<COH>(reinterpret_cast<const int16_t*>(x.p) + idx);
@@ -115,11 +133,11 @@ __device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
   }
 }
 
-template <int XF>
+template <int XF, bool COH = true>
 __device__ __forceinline__ float x2_ld1(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) return reinterpret_cast<const float*>(x.p)[idx];
-  else if constexpr (XF == 1) return (float)reinterpret_cast<const int8_t*>(x.p)[idx] + b;
-  else return (float)reinterpret_cast<const int16_t*>(x.p)[idx] + b;
+  else if constexpr (XF == 1) return (float)x2_raw_small<COH>(reinterpret_cast<const int8_t*>(x.p) + idx) + b;
+  else return (float)x2_raw_small<COH>(reinterpret_cast<const int16_t*>(x.p) + idx) + b;
 }
 
 // The backward of one 2x2 window (bn2d_bwd_apply_k): dz of its 4 elements (torch scan order) from

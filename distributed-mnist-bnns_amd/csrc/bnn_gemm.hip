@@ -838,6 +838,24 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp4_k(GemmParams 
   gemm_v2_body<1, 1, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, 0, 1, S16, BST>(p);
 }
 
+// The FP4 form held to <= 256 registers per lane (two waves per SIMD): 4-wave tiles small enough
+// in LDS for two workgroups per CU, so one's epilogue stores drain beside the other's k loop
+// (as the FP6 GEMM's half-tile form, bnn_gemm6.hip).
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0, int S16 = 0, int BST = 0>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void gemm_fp4_h_k(GemmParams p) {
+  gemm_v2_body<1, 1, WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, 0, 1, S16, BST>(p);
+}
+
+template <int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0, int S16 = 0, int BST = 0>
+int launch_fp4h(GemmParams p, hipStream_t s) {
+  constexpr int BM = WAVES_M * WM * 32, BN = WAVES_N * WN * 32;
+  p.gm = (p.M + BM - 1) / BM;
+  p.gn = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_fp4_h_k<WAVES_M, WAVES_N, WM, WN, STAGES, BKT, IL, S16, BST>),
+                     dim3((unsigned)((int64_t)p.gm * p.gn)), dim3(64 * WAVES_M * WAVES_N), 0, s, p);
+  return check_launch("bnn_gemm_fp4");
+}
+
 template <int DA, int DB, int WAVES_M, int WAVES_N, int WM, int WN, int STAGES, int BKT, int IL = 0,
           int DIAG = 0, int F4 = 0, int S16 = 0, int BST = 0>
 int launch_v2(GemmParams p, hipStream_t s) {
@@ -916,6 +934,11 @@ const Variant kVariants[] = {
     {31, "gemm_fp4_k<2, 2, 2, 2, 3, 64, 0, 0>", launch_v2<1, 1, 2, 2, 2, 2, 3, 64, 0, 0, 1>, 64},
     {32, "gemm_fp4_k<2, 4, 4, 2, 3, 64, 0, 0>", launch_v2<1, 1, 2, 4, 4, 2, 3, 64, 0, 0, 1>, 64},
     {33, "gemm_fp4_k<2, 4, 4, 2, 2, 128, 0, 0>", launch_v2<1, 1, 2, 4, 4, 2, 2, 128, 0, 0, 1>, 128},
+    // two workgroups per CU (A/B sweep, tools/fp4_half_ab.py): 128 x 256 tiles with BK 64 (3 / 2
+    // stages), 128 x 128 tiles of 2 waves with BK 128 + 16x16 MFMAs
+    {37, "gemm_fp4_h_k<1, 4, 4, 2, 3, 64, 0, 0>", launch_fp4h<1, 4, 4, 2, 3, 64, 0, 0>, 64},
+    {38, "gemm_fp4_h_k<1, 4, 4, 2, 2, 64, 0, 0>", launch_fp4h<1, 4, 4, 2, 2, 64, 0, 0>, 64},
+    {39, "gemm_fp4_h_k<1, 2, 4, 2, 2, 128, 2, 1>", launch_fp4h<1, 2, 4, 2, 2, 128, 2, 1>, 128},
     {21, "gemm_i8_v2_k<3, 3, 2, 2, 2, 1, 2, 64, 0, 0, 0>", launch_v2<3, 3, 2, 2, 2, 1, 2, 64>, 64},
     {22, "gemm_i8_v2_k<3, 3, 2, 4, 2, 1, 2, 64, 0, 0, 0>", launch_v2<3, 3, 2, 4, 2, 1, 2, 64>, 64},
 };

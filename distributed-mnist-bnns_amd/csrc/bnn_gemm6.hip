@@ -1241,11 +1241,17 @@ const Variant6 kVariants6[] = {
 };
 
 int g_variant6 = -1;
-// bnn_gemm_fp6_set_half: 0 = the 128 x 512 tile, one workgroup per CU (default); 1 = the dX
+// bnn_gemm_fp6_set_half: 0 = the 128 x 512 tile, one workgroup per CU; 1 (default) = the dX
 // launches (residual plane) on 64 x 512 tiles, two 4-wave workgroups per CU; 2 = the dW launches
 // (4 planes) too.  g_half_ticks: the first-round stagger of the second workgroup on each CU.
-int g_fp6_half = 0;
+// Measured on the wide step's shapes (profiles/r06_b_fp6_half.log, one box, interleaved): dX + res
+// 8.83 -> 8.31 ms with no stagger (40-200 us: 8.32-8.35), dW 7.12 -> 7.30-7.37 (kept on the 128 x
+// 512 tile).  The two residents of a CU (blocks b and b + 256 in the first round,
+// tools/probes/probe_wg_placement.hip) drift apart by themselves once their tiles' epilogues and
+// barrier waits differ, so one's fp32 stores drain beside the other's MFMAs.
+int g_fp6_half = 1;
 int64_t g_half_ticks = 0;
+int g_half_group = 0;   // raster group rows of the half-tile form (0: as the 128 x 512 tile's, 4 / 8)
 
 const Variant6* find6(int id) {
   for (const Variant6& v : kVariants6)
@@ -1353,6 +1359,14 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
 // Whether a launch takes the persistent form of the default tile (gemm_fp6_pers_k, selected by
 // bnn_gemm_fp6_set_persistent): no bias, B in panels, whole K per tile, a 128 x 512-tiled shape of at
 // least two rounds of tiles.  One predicate for gemm_fp6_impl and the name bnn_gemm_fp6_kernel_k reports.
+// Whether a launch takes the half-tile form (bnn_gemm_fp6_set_half): mode 1 the residual-plane (dX)
+// launches, mode 2 every launch; no bias, whole K per tile, 64 x 512-tiled shapes of >= 2 rounds of
+// two workgroups per CU.
+static bool fp6_half_applies(int64_t M, int64_t N, int ksplit, bool has_bias, bool res) {
+  return g_fp6_half > 0 && (res || g_fp6_half > 1) && !has_bias && ksplit <= 1 && g_variant6 < 0 && M % 64 == 0 &&
+         N % 512 == 0 && (M / 64) * (N / 512) >= 4 * device_cus();
+}
+
 static bool fp6_pers_applies(int64_t M, int64_t N, int ksplit, bool has_bias, bool panel) {
   return g_fp6_pers && !has_bias && panel && ksplit <= 1 && g_variant6 < 0 && M % 128 == 0 && N % 512 == 0 &&
          (M / 128) * (N / 512) >= 2 * device_cus();
@@ -1396,13 +1410,12 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
   const bool pers = fp6_pers_applies(M, N, p.ksplit, bias != nullptr, panel);
   // the half-tile form: 64 x 512 tiles, two workgroups per CU, the second resident of each CU in the
   // first round (blocks [CUs, 2 CUs): tools/probes/probe_wg_placement.hip) held back g_half_ticks
-  const bool half = g_fp6_half > 0 && bias == nullptr && p.ksplit == 1 && g_variant6 < 0 && !pers &&
-                    (ares ? true : g_fp6_half > 1) && M % 64 == 0 && N % 512 == 0 &&
-                    (M / 64) * (N / 512) >= 4 * device_cus();
+  const bool half = !pers && fp6_half_applies(M, N, p.ksplit, bias != nullptr, ares != nullptr);
   if (half) {
     p.stg_lo = device_cus();
     p.stg_hi = 2 * device_cus();
     p.stg_ticks = g_half_ticks;
+    if (g_half_group > 0) p.group = g_half_group;
   }
   if (ares) {   // the residual plane runs on the default tile (variant 7) with its own instance
     p.ares = ares;
@@ -1430,6 +1443,12 @@ BNN_API int bnn_gemm_fp6_set_half(int32_t mode, double stagger_us) {
   if (mode < 0) return g_fp6_half;
   g_fp6_half = mode;
   g_half_ticks = (int64_t)(stagger_us * 100.0);
+  return 0;
+}
+
+// Tuning hook: raster group (tile rows per group, tile6_of) of the half-tile form; 0 = default.
+BNN_API int bnn_gemm_fp6_set_half_group(int32_t g) {
+  g_half_group = g < 0 ? 0 : g;
   return 0;
 }
 
@@ -1511,6 +1530,14 @@ BNN_API const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K) {
   if (pl.ksplit <= 1) return pl.v->name;
   snprintf(buf, sizeof buf, "%s split-K %d", pl.v->name, pl.ksplit);
   return buf;
+}
+
+// As bnn_gemm_fp6_kernel_k for a launch with (res != 0) or without the residual plane.
+BNN_API const char* bnn_gemm_fp6_kernel_kr(int64_t M, int64_t N, int64_t K, int32_t res) {
+  const Fp6Plan pl = plan6(M, N, K);
+  if (!fp6_pers_applies(M, N, pl.ksplit, false, true) && fp6_half_applies(M, N, pl.ksplit, false, res != 0))
+    return "gemm_fp6_k<1, 4, 2, 4, 2>";
+  return bnn_gemm_fp6_kernel_k(M, N, K);
 }
 
 BNN_API int bnn_gemm_fp6_set_variant(int32_t v) {

@@ -247,22 +247,32 @@ __device__ __forceinline__ void nib_transpose8(uint32_t (&x)[8]) {
   for (int i = 0; i < 8; i += 2) nib_swap(x[i], x[i + 1], 4, 0x0F0F0F0Fu);
 }
 
-template <int XF>
+// IDN = 1: no BatchNorm (y = x: the plain sign-pack of bnn_sign_pack_fp4 on 256 x 256 tiles), and
+// sout (nullable) also receives sign(x) as fp32 -- the drop-in's `input.data = sign(input)` write-back
+// (binarized_modules.py:76) from the same read of x.
+template <int XF, int IDN = 0>
 __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, int64_t C,
                                                            ColAffine af, uint8_t* __restrict__ q, int64_t ldq,
-                                                           uint8_t* __restrict__ qt, int64_t ldqt, int64_t pnks) {
+                                                           uint8_t* __restrict__ qt, int64_t ldqt, int64_t pnks,
+                                                           float* __restrict__ sout = nullptr) {
   __shared__ uint32_t img[AP_T * AP_LD];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t k0 = (int64_t)blockIdx.x * AP_T, m0 = (int64_t)blockIdx.y * AP_T;
   const int64_t cb = k0 + 4 * lane;
-  const float4 mv = *reinterpret_cast<const float4*>(af.mean + cb);
-  const float4 iv = *reinterpret_cast<const float4*>(af.invstd + cb);
-  const float4 gv = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb) : make_float4(1, 1, 1, 1);
-  const float4 bv = af.beta ? *reinterpret_cast<const float4*>(af.beta + cb) : make_float4(0, 0, 0, 0);
-  const float4 lv = af.mean_lo ? *reinterpret_cast<const float4*>(af.mean_lo + cb) : make_float4(0, 0, 0, 0);
-  const float mu[4] = {mv.x, mv.y, mv.z, mv.w}, is[4] = {iv.x, iv.y, iv.z, iv.w};
-  const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, be[4] = {bv.x, bv.y, bv.z, bv.w};
-  const float lo[4] = {lv.x, lv.y, lv.z, lv.w};
+  float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {1.f, 1.f, 1.f, 1.f}, ga[4] = {1.f, 1.f, 1.f, 1.f};
+  float be[4] = {0.f, 0.f, 0.f, 0.f}, lo[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (!IDN) {
+    const float4 mv = *reinterpret_cast<const float4*>(af.mean + cb);
+    const float4 iv = *reinterpret_cast<const float4*>(af.invstd + cb);
+    const float4 gv = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb) : make_float4(1, 1, 1, 1);
+    const float4 bv = af.beta ? *reinterpret_cast<const float4*>(af.beta + cb) : make_float4(0, 0, 0, 0);
+    const float4 lv = af.mean_lo ? *reinterpret_cast<const float4*>(af.mean_lo + cb) : make_float4(0, 0, 0, 0);
+    mu[0] = mv.x, mu[1] = mv.y, mu[2] = mv.z, mu[3] = mv.w;
+    is[0] = iv.x, is[1] = iv.y, is[2] = iv.z, is[3] = iv.w;
+    ga[0] = gv.x, ga[1] = gv.y, ga[2] = gv.z, ga[3] = gv.w;
+    be[0] = bv.x, be[1] = bv.y, be[2] = bv.z, be[3] = bv.w;
+    lo[0] = lv.x, lo[1] = lv.y, lo[2] = lv.z, lo[3] = lv.w;
+  }
   const float4 xb = xin_bias4<XF>(xin, cb);
   uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
 #pragma unroll 4
@@ -273,9 +283,15 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
     if (m < M) {
       const float4 f = xin_load4<XF>(xin, m * C + cb, xb);
       const float v[4] = {f.x, f.y, f.z, f.w};
+      int sg[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) code |= fp4_code(tsign(fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]))) << (4 * j);
+      for (int j = 0; j < 4; ++j) {
+        sg[j] = IDN ? tsign(v[j]) : tsign(fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]));
+        code |= fp4_code(sg[j]) << (4 * j);
+      }
       *reinterpret_cast<uint16_t*>(q + m * ldq + k0 / 2 + 2 * lane) = (uint16_t)code;
+      if (IDN && sout != nullptr)
+        *reinterpret_cast<float4*>(sout + m * C + cb) = make_float4((float)sg[0], (float)sg[1], (float)sg[2], (float)sg[3]);
     }
     const int slot = (lane >> 1) ^ (((r >> 6) & 3) << 3);
     img16[(r * AP_LD + slot) * 2 + (lane & 1)] = (uint16_t)code;
@@ -877,6 +893,18 @@ BNN_API int bnn_sign_pack_i8(const float* x, int64_t M, int64_t K, int64_t ldx, 
   return check_launch("bnn_sign_pack_i8");
 }
 
+BNN_API int bnn_sign_f32(const float* x, float* y, int64_t n, void* stream);
+
+// Whether bnn_sign_pack_fp4 takes the 256 x 256-tile kernel (bn_apply_pack_fp4_k<0, 1>): both outputs
+// as FP4 (rows + transpose or panel transpose), whole 256-column tiles, dense 16-B aligned rows, and a
+// grid of >= 1024 tiles (below that the 64 x 64 tiles fill the chip better).
+static bool sp_wide_ok(const float* x, int64_t M, int64_t K, int64_t ldx, const uint8_t* q4, int64_t ldq4,
+                       const int8_t* qt, int64_t ldqt, int32_t qt_fmt) {
+  return q4 && qt && (qt_fmt == 1 || qt_fmt == 2) && K % AP_T == 0 && ldx == K && 2 * ldq4 == K && aligned16(x) &&
+         (K / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024 && (M + AP_T - 1) / AP_T <= 65535 &&
+         2 * ldqt >= (M + AP_T - 1) / AP_T * AP_T;
+}
+
 BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t* q4, int64_t ldq4,
                               int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
   if (!x || M < 0 || K < 0 || ldx < K || (!q4 && !qt)) {
@@ -896,6 +924,12 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
   }
   if (M == 0 && !qt) return 0;
   const int vec = aligned16(x) && (ldx % 4 == 0);
+  if (sp_wide_ok(x, M, K, ldx, q4, ldq4, qt, ldqt, qt_fmt)) {   // the 256 x 256-tile form, same codes
+    hipLaunchKernelGGL((bn_apply_pack_fp4_k<0, 1>), dim3((unsigned)(K / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+                       dim3(256), 0, S(stream), XIn{x, nullptr}, M, K, ColAffine{}, q4, ldq4,
+                       reinterpret_cast<uint8_t*>(qt), ldqt, qt_fmt == 2 ? ldqt / 32 : (int64_t)0, nullptr);
+    return check_launch("bnn_sign_pack_fp4");
+  }
   const int64_t gx = q4 ? (2 * ldq4) / TILE : (K + TILE - 1) / TILE;
   const int64_t gy = qt ? qt_tiles(ldqt, qt_fmt) : (M + TILE - 1) / TILE;
   if (gx == 0 || gy == 0) return 0;
@@ -907,6 +941,25 @@ BNN_API int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx,
                      ldx, reinterpret_cast<int8_t*>(q4), ldq4, qt, ldqt, vec, ColAffine{}, 1, (int64_t)0, AdamArgs{},
                      qt_fmt);
   return check_launch("bnn_sign_pack_fp4");
+}
+
+// bnn_sign_pack_fp4 + the fp32 sign write-back sout[m][k] = sign(x[m][k]) (row pitch K; may be x) from
+// one read of x when the 256 x 256-tile form applies; otherwise the two passes.
+BNN_API int bnn_sign_pack_fp4_out(const float* x, int64_t M, int64_t K, uint8_t* q4, int64_t ldq4, int8_t* qt,
+                                  int64_t ldqt, int32_t qt_fmt, float* sout, void* stream) {
+  if (!sout) {
+    set_error("bnn_sign_pack_fp4_out: sout required");
+    return kErrInval;
+  }
+  if (sp_wide_ok(x, M, K, K, q4, ldq4, qt, ldqt, qt_fmt) && aligned16(sout)) {
+    hipLaunchKernelGGL((bn_apply_pack_fp4_k<0, 1>), dim3((unsigned)(K / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
+                       dim3(256), 0, S(stream), XIn{x, nullptr}, M, K, ColAffine{}, q4, ldq4,
+                       reinterpret_cast<uint8_t*>(qt), ldqt, qt_fmt == 2 ? ldqt / 32 : (int64_t)0, sout);
+    return check_launch("bnn_sign_pack_fp4_out");
+  }
+  const int rc = bnn_sign_pack_fp4(x, M, K, K, q4, ldq4, qt, ldqt, qt_fmt, stream);
+  if (rc != 0) return rc;
+  return bnn_sign_f32(x, sout, M * K, stream);
 }
 
 // tuning hook (bnn_adam_pack_set_tile256): 1 (default) = the 256 x 256-tile kernel for grids of at

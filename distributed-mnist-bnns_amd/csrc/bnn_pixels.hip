@@ -83,10 +83,51 @@ __global__ __launch_bounds__(256) void row_sums_k(const int8_t* __restrict__ q, 
   if (lane == 0) out[n] = s;
 }
 
+// ToTensor's image of a byte (x = fl(u / 255), torchvision's img.float().div(255)) back to the byte:
+// u = rint(255 x) when 0 <= u <= 255 and fl(u / 255) == x bit for bit, else bad |= 1 (one vector
+// atomic per wave that saw a mismatch).  4 elements per thread (16-B loads), grid-stride.
+__global__ __launch_bounds__(256) void unit_to_pixels_k(const float* __restrict__ x, int64_t n, uint8_t* __restrict__ u,
+                                                        int* __restrict__ bad) {
+  bool miss = false;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float r = rintf(e[j] * 255.f);
+      const bool ok = r >= 0.f && r <= 255.f && (r / 255.f) == e[j];
+      miss |= !ok;
+      w |= (uint32_t)(ok ? (int)r : 0) << (8 * j);
+    }
+    reinterpret_cast<uint32_t*>(u)[i] = w;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float r = rintf(x[i] * 255.f);
+    const bool ok = r >= 0.f && r <= 255.f && (r / 255.f) == x[i];
+    miss |= !ok;
+    u[i] = (uint8_t)(ok ? (int)r : 0);
+  }
+  if (__any(miss) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
 }  // namespace
 }  // namespace bnn
 
 using namespace bnn;
+
+BNN_API int bnn_unit_to_pixels(const float* x, int64_t n, uint8_t* u, int32_t* bad, void* stream) {
+  if (!x || !u || !bad || n < 0 || !aligned16(x) || (reinterpret_cast<uintptr_t>(u) & 3) != 0) {
+    set_error("bnn_unit_to_pixels: bad arguments (n=%lld; x 16-B, u 4-B aligned)", (long long)n);
+    return kErrInval;
+  }
+  if (n == 0) return 0;
+  const int64_t blocks = std::min<int64_t>((n / 4 + 255) / 256 + 1, 8192);
+  hipLaunchKernelGGL(unit_to_pixels_k, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     x, n, u, reinterpret_cast<int*>(bad));
+  return check_launch("bnn_unit_to_pixels");
+}
 
 BNN_API int bnn_pixels_pack(const uint8_t* x, int64_t M, int64_t K, int64_t ldx, int8_t* q, int64_t ldq,
                             int8_t* qt, int64_t ldqt, void* stream) {

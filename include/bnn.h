@@ -61,6 +61,12 @@ int bnn_sign_pack_fp4(const float* x, int64_t M, int64_t K, int64_t ldx, uint8_t
  * y may alias x). */
 int bnn_sign_f32(const float* x, float* y, int64_t n, bnn_stream_t stream);
 
+/* bnn_sign_pack_fp4 (ldx = K; q4 and qt both, qt_fmt 1 rows / 2 panels) that also writes the fp32
+ * sign sout[m][k] = sign(x[m][k]) -- the BinarizeLinear input write-back of :76 -- from the same read
+ * of x (256 x 256 tiles: K % 256 == 0, >= 1024 tiles; else the two passes).  sout may alias x. */
+int bnn_sign_pack_fp4_out(const float* x, int64_t M, int64_t K, uint8_t* q4, int64_t ldq4, int8_t* qt,
+                          int64_t ldqt, int32_t qt_fmt, float* sout, bnn_stream_t stream);
+
 /* Bit-planes for the XNOR-popcount path: word w of row m holds k = 32w..32w+31 (bit k%32);
  * sbits = 1 where x<0, nzbits = 1 where x!=0.  ldw >= ceil(K/32) words, padding words zeroed. */
 int bnn_sign_pack_bits(const float* x, int64_t M, int64_t K, int64_t ldx, uint32_t* sbits,
@@ -165,6 +171,12 @@ int bnn_gemm_i8_affine_bnstats_s20(const int8_t* A, int64_t lda, const int8_t* B
                                    uint8_t* Shi, int64_t ldc, int64_t M, int64_t N, int64_t K, double* stat,
                                    int64_t stat_rows, const float* b_scale, const float* bias, bnn_stream_t stream);
 
+/* The fp32 images ToTensor makes (x = fl(u / 255), mnist-dist2.py:96-99) back to their bytes: u[i] =
+ * rint(255 x[i]); *bad |= 1 (device int, zero it first) if any x[i] is not exactly fl(u / 255) for a
+ * byte u.  Lets the drop-in's 784-input BinarizeLinear, handed fp32 images, run its u8-pixel GEMMs
+ * (one exact int8 pass instead of three digit planes).  x 16-B aligned, u 4-B aligned.
+ * replaces: nothing in the reference (transforms.ToTensor's inverse, for the pixel operands). */
+int bnn_unit_to_pixels(const float* x, int64_t n, uint8_t* u, int32_t* bad, bnn_stream_t stream);
 /* ---------------------------------------------------------------- u8 pixels (first layer)
  * Replaces the fp32 pixel tensor the reference's loader builds (ToTensor = u8/255, optionally
  * Normalize; mnist-dist2.py:96-99, mnist-distributed-BNNS2.py:82) as the operand of fc1
@@ -269,6 +281,7 @@ int bnn_gemm_fp6_bnstats(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
                          float* part, bnn_stream_t stream);
 const char* bnn_gemm_fp6_kernel(int64_t M, int64_t N);
 const char* bnn_gemm_fp6_kernel_k(int64_t M, int64_t N, int64_t K);   /* + " split-K S" */
+const char* bnn_gemm_fp6_kernel_kr(int64_t M, int64_t N, int64_t K, int32_t res);   /* with / without the residual plane */
 int bnn_gemm_fp6_set_variant(int32_t variant);   /* tuning hook (-1 = default) */
 /* 1: on grids of >= 2 rounds of 128 x 512 tiles with no bias, M % 128 == 0, N % 512 == 0 and B in
  * panels (the backward GEMMs), the default tile runs persistent -- one workgroup per CU, the waves
@@ -279,9 +292,11 @@ int bnn_gemm_fp6_set_persistent(int32_t on);
 /* Half-tile form of the backward GEMMs: mode 1 runs the dX launches (residual plane) on 64 x 512
  * tiles, two 4-wave workgroups per CU, the second resident of each CU held back stagger_us in the
  * first round so one workgroup's fp32 epilogue drains while the other's MFMAs run; mode 2 also the
- * dW launches; 0 = the 128 x 512 tile (default).  Same fragments and accumulation order per output
- * element: bit-identical C.  mode < 0 queries. */
+ * dW launches; 0 = the 128 x 512 tile.  Default 1 (dX + res 8.83 -> 8.31 ms; dW slower on half
+ * tiles, profiles/r06_b_fp6_half.log).  Same fragments and accumulation order per output element:
+ * bit-identical C.  mode < 0 queries. */
 int bnn_gemm_fp6_set_half(int32_t mode, double stagger_us);
+int bnn_gemm_fp6_set_half_group(int32_t group);   /* tuning hook: raster group rows of the half-tile form (0 = default) */
 
 /* XNOR/AND-popcount VALU GEMM on bit-planes (same contract as the (1,1) form):
  * C[m][n] = sum_w popc(nzA&nzB) - 2*popc(nzA&nzB&(sA^sB)) + bias[n]; kw = words per row

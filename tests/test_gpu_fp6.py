@@ -24,7 +24,12 @@ def F():
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     from bnn_amd import functional
-    return functional
+    # the row operands here carry the residual plane at every size (the networks add it from
+    # functional.FP6_RES_MIN_ROWS rows on); restored after the module
+    prev = functional.FP6_RES_MIN_ROWS
+    functional.FP6_RES_MIN_ROWS = 0
+    yield functional
+    functional.FP6_RES_MIN_ROWS = prev
 
 
 def host(t):
@@ -281,3 +286,42 @@ def test_fp6_persistent_gemm_bit_identical(F, M, N, K, res):
         op_head.res = None
     val, _, _ = decode(op_head, 2048, residual=res)
     assert rel_err(host(C1)[:2048], val[:, :K] @ w.astype(np.float64).T) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (16384, 4096, 1088), (8256, 4096, 512)])
+@pytest.mark.parametrize("res", [True, False])
+def test_fp6_half_tile_gemm_bit_identical(F, M, N, K, res):
+    """The half-tile form (64 x 512 tiles, two 4-wave workgroups per CU, the default for the
+    residual-plane dX launches; bnn_gemm_fp6_set_half) against the 128 x 512 tile, with and without
+    a first-round stagger: C bit-identical with and without the residual plane, on grids of >= 2
+    rounds, an odd number of 64-row tile rows (8256 = 129 x 64) and an odd number of k-steps (17);
+    within 2e-6 of the float64 product of the decoded operand."""
+    from bnn_amd import _lib as L
+    rng = np.random.default_rng(M + N + K + res + 7)
+    x = (rng.standard_normal((M, K)) * np.exp(rng.uniform(-3, 3, (M, 1)))).astype(np.float32)
+    w = rng.integers(-1, 2, (N, K)).astype(np.float32)
+    w4, _ = F.sign_pack_fp4(torch.as_tensor(w).cuda())
+    P = F.fp4_panels(w4, N, K)
+    op = F.quant6_rows(torch.as_tensor(x).cuda())
+    if not res:
+        op.res = None
+    prev = L.lib().bnn_gemm_fp6_set_half(-1, 0.0)
+    ks = P.numel() // (((N + 511) // 512) * 512 * 32)
+    outs = {}
+    try:
+        for mode, st in ((0, 0.0), (2, 0.0), (2, 60.0)):
+            L.call("bnn_gemm_fp6_set_half", mode, st)
+            name = L.lib().bnn_gemm_fp6_kernel_kr(M, N, op.Kp, int(res)).decode()
+            assert ("<1, 4, 2, 4, 2>" in name) == (mode > 0), (mode, name)
+            outs[(mode, st)] = F.gemm_fp6(op, None, N, panels=P, panel_ks=ks)
+        torch.cuda.synchronize()
+    finally:
+        L.call("bnn_gemm_fp6_set_half", prev, 0.0)
+    C0 = outs[(0, 0.0)]
+    for k, C in outs.items():
+        assert torch.equal(C, C0), k
+    op_head = F.quant6_rows(torch.as_tensor(x[:2048]).cuda())
+    if not res:
+        op_head.res = None
+    val, _, _ = decode(op_head, 2048, residual=res)
+    assert rel_err(host(C0)[:2048], val[:, :K] @ w.astype(np.float64).T) < 2e-6

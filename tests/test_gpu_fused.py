@@ -143,6 +143,41 @@ def test_sign_pack_panel_transpose(F, M, K):
     assert np.array_equal(got[live], ref[live])
 
 
+@pytest.mark.parametrize("M,K,qt_fmt", [(65536, 4096, "fp4"), (65536, 4096, "fp4p"), (16700, 4096, "fp4p"),
+                                         (300, 700, "fp4p")])
+def test_sign_pack_wide_tiles_and_writeback(F, M, K, qt_fmt):
+    """bnn_sign_pack_fp4 on 256 x 256 tiles (taken for dense rows, K % 256 == 0 and >= 1024 tiles)
+    writes the same FP4 rows and transpose (row-major or panel layout) as the 64 x 64-tile kernel
+    (forced here by a row pitch != K), exact zeros, -0.0 and NaN included; and the drop-in's
+    write-back entry (bnn_sign_pack_fp4_out: sign(x) as fp32 + both operands from one read) equals
+    sign() + the plain pack (small shapes: its two-pass fallback)."""
+    from bnn_amd import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    big = torch.randn(M, K + 256, device="cuda", generator=g)
+    big[:, 5] = 0.0
+    big[7, :40] = -0.0
+    big[11, 3] = float("nan")
+    x = big[:, :K].contiguous()
+    q_w, qt_w = F.sign_pack_fp4(x, want_qt=True, qt_fmt=qt_fmt)
+    q_t = torch.empty_like(q_w)
+    qt_t = torch.zeros_like(qt_w) if qt_fmt == "fp4p" else torch.empty_like(qt_w)
+    L.call("bnn_sign_pack_fp4", L.ptr(big), M, K, K + 256, L.ptr(q_t), q_t.shape[1], L.ptr(qt_t), qt_t.shape[1],
+           {"fp4": 1, "fp4p": 2}[qt_fmt], L.stream())
+    assert torch.equal(q_w, q_t)
+    if qt_fmt == "fp4p":
+        live = torch.arange(qt_w.shape[0], device="cuda") < K          # panel rows past K: padding
+        qt_w = qt_w.view((K + 511) // 512, -1, 512, 32)
+        qt_t = qt_t.view(qt_w.shape)
+        live = live.view((K + 511) // 512, 1, 512, 1).expand(qt_w.shape)
+        assert torch.equal(qt_w[live], qt_t[live])
+    else:
+        assert torch.equal(qt_w, qt_t)
+    if qt_fmt == "fp4p":
+        s, q4, qt4 = F.sign_pack_fp4_writeback(x, want_qt=True)
+        assert torch.equal(s, F.sign(x)) and torch.equal(q4, q_t)
+        assert torch.equal(qt4.view(qt_w.shape)[live], qt_t[live])
+
+
 def _apply_pack_case(F, M, C, fmt, with_qt):
     from bnn_amd import _lib as L
     rng = np.random.default_rng(M * 7 + C + fmt)

@@ -145,6 +145,52 @@ def test_fc1_pixels_matches_fp32_path(F, t10k):
     assert rel_err(y8, yf) <= 2e-6
 
 
+def test_dropin_fc1_recognises_totensor_images(F, t10k):
+    """The drop-in BinarizeLinear(784, N) handed fp32 ToTensor images (x = fl(u / 255), as
+    mnist-dist2.py's loader makes them, on the host or on the GPU) runs the u8-pixel GEMMs: output
+    and weight / bias gradients bit-identical to binary_linear_pixels on the bytes, within 2e-6 of
+    the fp32-digit path; dead pixel columns get exactly zero weight gradient.  Inputs that are not
+    such images (one element off by an ulp, a Normalize'd image, an input that needs its own
+    gradient) keep the fp32 path."""
+    from models.binarized_modules import BinarizeLinear
+    rng = np.random.default_rng(11)
+    u = t10k[:300]
+    torch.manual_seed(3)
+    lin = BinarizeLinear(784, 256).cuda()
+    w0 = lin.weight.detach().clone()
+    for where in ("host", "gpu"):
+        xt = torch.as_tensor(O.to_tensor(u)).cuda() if where == "host" else \
+            torch.as_tensor(u).cuda().float().div(255.0)
+        n0 = F.UNIT_PIXELS
+        lin.weight.grad = lin.bias.grad = None
+        y = lin(xt)
+        assert F.UNIT_PIXELS == n0 + 1, where
+        g = torch.as_tensor(rng.standard_normal((300, 256)).astype(np.float32)).cuda()
+        y.backward(g)
+        w8 = w0.clone().requires_grad_(True)
+        b8 = lin.bias.detach().clone().requires_grad_(True)
+        y8 = F.binary_linear_pixels(torch.as_tensor(u).cuda(), w8, b8)
+        y8.backward(g)
+        assert torch.equal(y, y8) and torch.equal(lin.weight.grad, w8.grad) and torch.equal(lin.bias.grad, b8.grad)
+        yf = F.binary_linear(xt, w0, lin.bias.detach(), binarize_input=False)
+        assert rel_err(host(y), host(yf)) <= 2e-6
+        dead = ~u.any(0)
+        assert not host(lin.weight.grad)[:, dead].any()
+        lin.weight.data = w0.clone()
+        del lin.weight.org
+    for name, xt in (("ulp", torch.as_tensor(O.to_tensor(u)).cuda()),
+                     ("normalize", (torch.as_tensor(O.to_tensor(u)).cuda() - 0.1307) / 0.3081)):
+        if name == "ulp":
+            xt.view(-1)[12345] = torch.nextafter(xt.view(-1)[12345], torch.tensor(2.0, device="cuda"))
+        n0 = F.UNIT_PIXELS
+        lin(xt)
+        assert F.UNIT_PIXELS == n0, name
+    xg = torch.as_tensor(O.to_tensor(u)).cuda().requires_grad_(True)
+    n0 = F.UNIT_PIXELS
+    lin(xg).sum().backward()
+    assert F.UNIT_PIXELS == n0 and xg.grad is not None
+
+
 def test_fc1_pixels_empty_batch(F):
     w = torch.randn(16, 784, device="cuda", requires_grad=True)
     b = torch.randn(16, device="cuda", requires_grad=True)

@@ -4,7 +4,7 @@ tiles, two workgroups per CU, bnn_gemm_fp6_set_half) at several first-round stag
 the residual plane (as the wide step's dX launches), dW the four planes.  Every form's C is checked
 bit-identical to the default's.
 
-    python tools/fp6_half_ab.py "0:0 1:0 1:65 1:130" [rounds] [reps]     (mode:stagger_us; dW uses mode 2)
+    python tools/fp6_half_ab.py "0:0 1:0 1:65 1:130" [rounds] [reps]     (mode:stagger_us[:group]; dW uses mode 2)
 """
 import os
 import statistics
@@ -18,7 +18,7 @@ from bnn_amd import functional as BF  # noqa: E402
 
 
 def main():
-    cfgs = [(int(a), float(b)) for a, b in (c.split(":") for c in sys.argv[1].split())]
+    cfgs = [(int(t[0]), float(t[1]), int(t[2]) if len(t) > 2 else 0) for t in (c.split(":") for c in sys.argv[1].split())]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     torch.manual_seed(0)
@@ -37,8 +37,9 @@ def main():
         times = {c: [] for c in cfgs}
 
         def run(c):
-            mode, st = c
+            mode, st, grp = c
             L.call("bnn_gemm_fp6_set_half", (mode if res or mode == 0 else 2), st)
+            L.call("bnn_gemm_fp6_set_half_group", grp)
             BF.gemm_fp6(op, None, N, out=C, panels=panels, panel_ks=K // 64)
 
         for c in cfgs:
@@ -60,9 +61,10 @@ def main():
                 times[c].append(s.elapsed_time(e) / reps)
         for c in cfgs:
             med, mn = statistics.median(times[c]), min(times[c])
-            print(f"{tag:7s} mode {c[0]} stagger {c[1]:6.1f} us: median {med:7.3f} ms  min {mn:7.3f}  "
+            print(f"{tag:7s} mode {c[0]} stagger {c[1]:6.1f} us group {c[2]}: median {med:7.3f} ms  min {mn:7.3f}  "
                   f"{ops / med / 1e9:7.1f} TOPS alg", flush=True)
-        L.call("bnn_gemm_fp6_set_half", 0, 0.0)
+        L.call("bnn_gemm_fp6_set_half", 1, 0.0)
+        L.call("bnn_gemm_fp6_set_half_group", 0)
         del op, w4, panels, C, ref
         torch.cuda.empty_cache()
     BF.FP6_RES = True
