@@ -1553,12 +1553,9 @@ __global__ __launch_bounds__(BN2_T) void bn2d_bwd_stats_rows_k(X2 x, const float
     const int64_t xo = plane * HW + (int64_t)(2 * ph) * W, yo = plane * pp + (int64_t)ph * PW;
     float2 top[PW], bot[PW];
     float g[PW];
+    x2_rows<XF, PW>(x, xo, xb, top, bot);
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
-      bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
-      g[q] = dy[yo + q];
-    }
+    for (int q = 0; q < PW; ++q) g[q] = dy[yo + q];
     float fa = 0.f, fb = 0.f;
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
@@ -1600,11 +1597,7 @@ __global__ __launch_bounds__(256) void bn2d_apply_rows_k(X2 x, int64_t N, int64_
   const float xb = x2_bias<XF>(x, c);
   const int64_t xo = plane * ((int64_t)H * W) + (int64_t)(2 * ph) * W;
   float2 top[PW], bot[PW];
-#pragma unroll
-  for (int q = 0; q < PW; ++q) {
-    top[q] = x2_ld2<XF, true>(x, xo + 2 * q, xb);
-    bot[q] = x2_ld2<XF, true>(x, xo + W + 2 * q, xb);
-  }
+  x2_rows<XF, PW>(x, xo, xb, top, bot);
   float* yr = y + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
 #pragma unroll
   for (int q = 0; q < PW; ++q) yr[q] = bn2_window(top[q], bot[q], k, hardtanh).out;
@@ -1633,12 +1626,9 @@ __global__ __launch_bounds__(256) void bn2d_bwd_apply_rows_k(X2 x, const float* 
   const float* dr = dy + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
   float2 top[PW], bot[PW];
   float gp[PW];
+  x2_rows<XF, PW>(x, xo, xb, top, bot);
 #pragma unroll
-  for (int q = 0; q < PW; ++q) {
-    top[q] = x2_ld2<XF>(x, xo + 2 * q, xb);
-    bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, xb);
-    gp[q] = dr[q];
-  }
+  for (int q = 0; q < PW; ++q) gp[q] = dr[q];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
     const Win w = bn2_window(top[q], bot[q], k, hardtanh);
@@ -2312,7 +2302,7 @@ static int bn2d_fwd_train_impl(X2 x, int xf, int64_t N, int64_t C, int64_t H, in
                                int32_t pool, void* work, void* stream) {
   if (!bn2_args_ok(reinterpret_cast<const float*>(x.p), N, C, H, W, pool) || !save_mean || !save_invstd || !work ||
       !y || (running_mean == nullptr) != (running_var == nullptr) || xf < 0 || xf > 2 || (xf == 0 && x.bias) ||
-      (x.bias && !aligned16(x.bias))) {
+      (x.bias && !aligned16(x.bias)) || (xf != 0 && N * C * H * W * xf >= (1LL << 31))) {
     set_error("bnn_bn2d_fwd_train: bad arguments (N=%lld C=%lld H=%lld W=%lld pool=%d; H*W must be a multiple "
               "of 4, pool 0 or 2 with even H, W)", (long long)N, (long long)C, (long long)H, (long long)W, pool);
     return kErrInval;
@@ -2390,7 +2380,7 @@ static int bn2d_bwd_impl(X2 x, int xf, const float* dy, int64_t N, int64_t C, in
                          void* stream, bool batch_stats, float* k0_out = nullptr, float* k1_out = nullptr) {
   if (!bn2_args_ok(reinterpret_cast<const float*>(x.p), N, C, H, W, pool) || !dy || !save_mean || !save_invstd ||
       !work || (dx && !aligned16(dx)) || (!pool && !aligned16(dy)) || xf < 0 || xf > 2 || (xf == 0 && x.bias) ||
-      (x.bias && !aligned16(x.bias))) {
+      (x.bias && !aligned16(x.bias)) || (xf != 0 && N * C * H * W * xf >= (1LL << 31))) {
     set_error("bnn_bn2d_bwd: bad arguments");
     return kErrInval;
   }

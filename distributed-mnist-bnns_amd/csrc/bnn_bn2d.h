@@ -58,50 +58,56 @@ __device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
   return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
 }
 
-// Every read of the compact (int8 / int16) conv outputs goes around the reading CU's vector L1
-// (BN2_LOADS 1: nt loads, which the compiler still merges into 16-B instructions).  With plain
-// loads the BatchNorm2d forward passes returned different statistics from run to run -- never in
-// one process alone, in about one step in ten while other processes used the same GPU (the
-// two-rank data-parallel tests run that way) -- although the conv sums in memory were identical
-// every time; host synchronisations before and between the passes and a 512 MB L2 eviction left it
-// so, loads that bypass L1 (agent-scope sc1, round 5) removed it (0 of 156 steps, plain 11 of 156;
-// tools/race_trace.py, profiles/r05_race_*.log).  sc1 and nt loads are served by L2 and skip L1
-// alone (MI355X_MICROARCH.md, visibility table), so the stale bytes came from the consumer CU's L1:
-// the fix belongs to every consumer of freshly written compact data, the forward and backward
-// BatchNorm2d passes and conv1's fused filter gradient alike.  BN2_LOADS 0 / 2
-// build the plain / sc1-atomic forms (A/B only).
+// Every read of the compact (int8 / int16) conv outputs is an agent-scope (sc1) load, which the
+// reading CU's vector L1 never serves.  With plain loads the BatchNorm2d forward passes returned
+// different statistics from run to run -- never in one process alone, in about one step in ten
+// while other processes used the same GPU (the two-rank data-parallel tests run that way) --
+// although the conv sums in memory were identical every time; host synchronisations before and
+// between the passes and a 512 MB L2 eviction left it so, sc1 loads removed it (0 of 156 steps,
+// plain 11 of 156; tools/race_trace.py, profiles/r05_race_*.log), and nt loads -- which still hit a
+// line L1 holds -- did not (round 6: the two-rank BinCNN test failed with them,
+// profiles/r06_c_gpu_tests_a.log).  The stale bytes come from the consumer CU's L1, so every consumer
+// of freshly written compact data bypasses it: the forward and backward BatchNorm2d passes and
+// conv1's fused filter gradient.  The loads are buffer loads (aux = sc1) of up to
+// 16 B, so the rows kernels keep their 16-B instructions (round 5's 4- / 8-B atomic loads cost
+// ~0.05 ms per BinCNN step).  BN2_LOADS: 1 sc1 buffer loads (default), 0 plain, 2 agent-scope
+// atomic loads (round 5), 3 nt loads -- A/B only.  Compact buffers are < 2 GB (host checks).
 #ifndef BN2_LOADS
 #define BN2_LOADS 1
 #endif
-template <bool COH>
-__device__ __forceinline__ uint2 x2_raw8(const void* p) {
-  if constexpr (COH && BN2_LOADS == 2) {
-    const uint64_t v =
-        __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-  } else if constexpr (COH && BN2_LOADS == 1) {
-    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
-    return make_uint2(v.x, v.y);
-  }
-  return *reinterpret_cast<const uint2*>(p);
+constexpr int BN2_SC1 = 16;   // buffer-instruction aux bits: sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x2_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
-template <bool COH>
-__device__ __forceinline__ uint32_t x2_raw4(const void* p) {
-  if constexpr (COH && BN2_LOADS == 2)
-    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else if constexpr (COH && BN2_LOADS == 1)
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-  return *reinterpret_cast<const uint32_t*>(p);
-}
-template <bool COH, typename T>
-__device__ __forceinline__ T x2_raw_small(const T* p) {   // 1 or 2 bytes
-  if constexpr (COH && BN2_LOADS == 2)
-    return (T)__hip_atomic_load(reinterpret_cast<const typename std::make_unsigned<T>::type*>(p), __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-  else if constexpr (COH && BN2_LOADS == 1)
+
+// n-byte load (n = 2, 4, 8 or 16) at byte offset off of a compact buffer, through the L1 policy above
+template <int NB, bool COH>
+__device__ __forceinline__ auto x2_raw(const void* base, int64_t off) {
+  using T = typename std::conditional<NB == 16, v4u, typename std::conditional<NB == 8, v2u,
+            typename std::conditional<NB == 4, uint32_t, uint16_t>::type>::type>::type;
+  const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+  if constexpr (COH && BN2_LOADS == 1) {
+    const __amdgpu_buffer_rsrc_t r = x2_rsrc(base);
+    if constexpr (NB == 16) return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, BN2_SC1);
+    else if constexpr (NB == 8) return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, BN2_SC1);
+    else if constexpr (NB == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, BN2_SC1);
+    else return __builtin_amdgcn_raw_buffer_load_b16(r, (int)off, 0, BN2_SC1);
+  } else if constexpr (COH && BN2_LOADS == 2 && NB <= 8) {
+    using U = typename std::conditional<NB == 8, uint64_t,
+              typename std::conditional<NB == 4, uint32_t, uint16_t>::type>::type;
+    const U v = __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (NB == 8) return v2u{(uint32_t)v, (uint32_t)(v >> 32)};
+    else return (T)v;
+  } else if constexpr (COH && BN2_LOADS == 3) {
     return __builtin_nontemporal_load(p);
-  return *p;
+  } else {
+    return *p;
+  }
 }
+
+__device__ __forceinline__ float lo16f(uint32_t u) { return (float)(int16_t)(u & 0xFFFFu); }
+__device__ __forceinline__ float hi16f(uint32_t u) { return (float)(int16_t)(u >> 16); }
 
 // 4 consecutive elements of one channel plane from flat index idx (a multiple of 4)
 template <int XF, bool COH = true>
@@ -109,13 +115,12 @@ __device__ __forceinline__ float4 x2_ld4(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x.p) + idx);
   } else if constexpr (XF == 1) {
-    const uint32_t u = x2_raw4<COH>(reinterpret_cast<const int8_t*>(x.p) + idx);
+    const uint32_t u = x2_raw<4, COH>(x.p, idx);
     return make_float4((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b,
                        (float)(int8_t)((u >> 16) & 0xFF) + b, (float)(int8_t)(u >> 24) + b);
   } else {
-    const uint2 u = x2_raw8<COH>(reinterpret_cast<const int16_t*>(x.p) + idx);
-    return make_float4((float)(int16_t)(u.x & 0xFFFF) + b, (float)(int16_t)(u.x >> 16) + b,
-                       (float)(int16_t)(u.y & 0xFFFF) + b, (float)(int16_t)(u.y >> 16) + b);
+    const v2u u = x2_raw<8, COH>(x.p, 2 * idx);
+    return make_float4(lo16f(u.x) + b, hi16f(u.x) + b, lo16f(u.y) + b, hi16f(u.y) + b);
   }
 }
 
@@ -125,19 +130,60 @@ __device__ __forceinline__ float2 x2_ld2(const X2& x, int64_t idx, float b) {
   if constexpr (XF == 0) {
     return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x.p) + idx);
   } else if constexpr (XF == 1) {
-    const uint16_t u = (uint16_t)x2_raw_small<COH>(reinterpret_cast<const int16_t*>(reinterpret_cast<const int8_t*>(x.p) + idx));
-    return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)(u >> 8) + b);
+    const uint32_t u = (uint32_t)x2_raw<2, COH>(x.p, idx);
+    return make_float2((float)(int8_t)(u & 0xFF) + b, (float)(int8_t)((u >> 8) & 0xFF) + b);
   } else {
-    const uint32_t u = x2_raw4<COH>(reinterpret_cast<const int16_t*>(x.p) + idx);
-    return make_float2((float)(int16_t)(u & 0xFFFF) + b, (float)(int16_t)(u >> 16) + b);
+    const uint32_t u = x2_raw<4, COH>(x.p, 2 * idx);
+    return make_float2(lo16f(u) + b, hi16f(u) + b);
   }
 }
 
 template <int XF, bool COH = true>
 __device__ __forceinline__ float x2_ld1(const X2& x, int64_t idx, float b) {
-  if constexpr (XF == 0) return reinterpret_cast<const float*>(x.p)[idx];
-  else if constexpr (XF == 1) return (float)x2_raw_small<COH>(reinterpret_cast<const int8_t*>(x.p) + idx) + b;
-  else return (float)x2_raw_small<COH>(reinterpret_cast<const int16_t*>(x.p) + idx) + b;
+  if constexpr (XF == 0) {
+    return reinterpret_cast<const float*>(x.p)[idx];
+  } else if constexpr (XF == 1) {
+    // the byte's 2-byte-aligned pair, then its half
+    const uint32_t u = (uint32_t)x2_raw<2, COH>(x.p, idx & ~(int64_t)1);
+    return (float)(int8_t)((idx & 1) ? (u >> 8) : (u & 0xFF)) + b;
+  } else {
+    return (float)(int16_t)x2_raw<2, COH>(x.p, 2 * idx) + b;
+  }
+}
+
+// The two rows (2 ph, 2 ph + 1) of a 2x2-pooled plane as 2 PW element pairs each, from row offset xo
+// (elements).  int16: the rows are one contiguous run of 8 PW bytes -- 16-B aligned for even PW, 8-B
+// for odd (H W 2 = 8 PH PW bytes per plane, 8 ph PW per row pair) -- loaded in 16- / 8-B pieces.
+template <int XF, int PW>
+__device__ __forceinline__ void x2_rows(const X2& x, int64_t xo, float b, float2 (&top)[PW], float2 (&bot)[PW]) {
+  if constexpr (XF == 2) {
+    uint32_t w[2 * PW];
+    if constexpr (PW % 2 == 0) {
+#pragma unroll
+      for (int i = 0; i < PW / 2; ++i) {
+        const v4u v = x2_raw<16, true>(x.p, 2 * xo + 16 * i);
+        w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        const v2u v = x2_raw<8, true>(x.p, 2 * xo + 8 * i);
+        w[2 * i] = v.x, w[2 * i + 1] = v.y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      top[q] = make_float2(lo16f(w[q]) + b, hi16f(w[q]) + b);
+      bot[q] = make_float2(lo16f(w[PW + q]) + b, hi16f(w[PW + q]) + b);
+    }
+  } else {
+    constexpr int W = 2 * PW;
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      top[q] = x2_ld2<XF>(x, xo + 2 * q, b);
+      bot[q] = x2_ld2<XF>(x, xo + W + 2 * q, b);
+    }
+  }
 }
 
 // The backward of one 2x2 window (bn2d_bwd_apply_k): dz of its 4 elements (torch scan order) from

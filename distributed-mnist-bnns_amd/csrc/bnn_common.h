@@ -27,6 +27,7 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // GEMM epilogue output stores, non-temporal (the nt bit: streamed, not kept in the caches): the big
 // GEMMs' outputs (1-2 GB per launch) are far beyond the 256 MB MALL, and the streamed stores drain

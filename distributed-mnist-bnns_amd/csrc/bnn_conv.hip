@@ -2307,7 +2307,8 @@ BNN_API int bnn_conv2d_bwd_filter_bn(const void* zq, const float* zbias, int32_t
   if (!zq || !dyp || !mean || !invstd || !sg || !sgx || !x || !dw || !work || (zfmt != 1 && zfmt != 2) ||
       !bnn_conv2d_bwd_filter_bn_ok(N, C, H, W, Co, KH, KW, stride, pad, dil, groups) ||
       !make_shape(N, C, H, W, Co, KH, KW, stride, pad, dil, groups, &s) || !c1_filt_geom(s, &cf, &clds) ||
-      (reinterpret_cast<uintptr_t>(dyp) & 7) != 0 || (reinterpret_cast<uintptr_t>(zq) & 7) != 0) {
+      (reinterpret_cast<uintptr_t>(dyp) & 7) != 0 || (reinterpret_cast<uintptr_t>(zq) & 7) != 0 ||
+      N * Co * s.OH * s.OW * zfmt >= (1LL << 31)) {   // the compact sums are read by 32-bit buffer offsets
     set_error("bnn_conv2d_bwd_filter_bn: bad arguments");
     return kErrInval;
   }

@@ -83,9 +83,11 @@ __global__ __launch_bounds__(256) void row_sums_k(const int8_t* __restrict__ q, 
   if (lane == 0) out[n] = s;
 }
 
-// ToTensor's image of a byte (x = fl(u / 255), torchvision's img.float().div(255)) back to the byte:
-// u = rint(255 x) when 0 <= u <= 255 and fl(u / 255) == x bit for bit, else bad |= 1 (one vector
-// atomic per wave that saw a mismatch).  4 elements per thread (16-B loads), grid-stride.
+// ToTensor's image of a byte back to the byte: u = rint(255 x) when 0 <= u <= 255 and x is, bit for
+// bit, fl(u / 255) (torchvision's img.float().div(255) on the host: a correctly rounded division) or
+// fl(u * fl(1 / 255)) (the same division by a scalar on the GPU, which torch runs as a multiply by
+// the reciprocal); else bad |= 1 (one vector atomic per wave that saw a mismatch).  4 elements per
+// thread (16-B loads), grid-stride.
 __global__ __launch_bounds__(256) void unit_to_pixels_k(const float* __restrict__ x, int64_t n, uint8_t* __restrict__ u,
                                                         int* __restrict__ bad) {
   bool miss = false;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void unit_to_pixels_k(const float* __restrict_
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float r = rintf(e[j] * 255.f);
-      const bool ok = r >= 0.f && r <= 255.f && (r / 255.f) == e[j];
+      const bool ok = r >= 0.f && r <= 255.f && ((r / 255.f) == e[j] || r * (1.f / 255.f) == e[j]);
       miss |= !ok;
       w |= (uint32_t)(ok ? (int)r : 0) << (8 * j);
     }
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void unit_to_pixels_k(const float* __restrict_
   }
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float r = rintf(x[i] * 255.f);
-    const bool ok = r >= 0.f && r <= 255.f && (r / 255.f) == x[i];
+    const bool ok = r >= 0.f && r <= 255.f && ((r / 255.f) == x[i] || r * (1.f / 255.f) == x[i]);
     miss |= !ok;
     u[i] = (uint8_t)(ok ? (int)r : 0);
   }

@@ -22,12 +22,17 @@ def F():
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
     from bnn_amd import functional
-    return functional
+    # the quantised row operands carry the residual plane at every size here (the networks add it
+    # from functional.FP6_RES_MIN_ROWS rows on), so the fused passes' residual output is compared too
+    prev = functional.FP6_RES_MIN_ROWS
+    functional.FP6_RES_MIN_ROWS = 0
+    yield functional
+    functional.FP6_RES_MIN_ROWS = prev
 
 
 def eq(a, b):
     torch.cuda.synchronize()
-    return torch.equal(a, b)
+    return (a is None and b is None) or (a is not None and b is not None and torch.equal(a, b))
 
 
 def _inputs(F, M, C, seed):

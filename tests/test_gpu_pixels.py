@@ -147,7 +147,8 @@ def test_fc1_pixels_matches_fp32_path(F, t10k):
 
 def test_dropin_fc1_recognises_totensor_images(F, t10k):
     """The drop-in BinarizeLinear(784, N) handed fp32 ToTensor images (x = fl(u / 255), as
-    mnist-dist2.py's loader makes them, on the host or on the GPU) runs the u8-pixel GEMMs: output
+    mnist-dist2.py's loader makes them on the host, or fl(u * fl(1 / 255)), torch's division by a
+    scalar on the GPU) runs the u8-pixel GEMMs: output
     and weight / bias gradients bit-identical to binary_linear_pixels on the bytes, within 2e-6 of
     the fp32-digit path; dead pixel columns get exactly zero weight gradient.  Inputs that are not
     such images (one element off by an ulp, a Normalize'd image, an input that needs its own
@@ -180,8 +181,9 @@ def test_dropin_fc1_recognises_totensor_images(F, t10k):
         del lin.weight.org
     for name, xt in (("ulp", torch.as_tensor(O.to_tensor(u)).cuda()),
                      ("normalize", (torch.as_tensor(O.to_tensor(u)).cuda() - 0.1307) / 0.3081)):
-        if name == "ulp":
-            xt.view(-1)[12345] = torch.nextafter(xt.view(-1)[12345], torch.tensor(2.0, device="cuda"))
+        if name == "ulp":     # 2 ulps: the host and GPU roundings of u / 255 differ by at most one
+            two = torch.tensor(2.0, device="cuda")
+            xt.view(-1)[12345] = torch.nextafter(torch.nextafter(xt.view(-1)[12345], two), two)
         n0 = F.UNIT_PIXELS
         lin(xt)
         assert F.UNIT_PIXELS == n0, name
