@@ -1230,6 +1230,10 @@ _CONV_C1F = [os.environ.get("BNN_CONV_C1F")]
 # default (off)
 if os.environ.get("BNN_FP6_PERS") is not None:
     L.call("bnn_gemm_fp6_set_persistent", int(os.environ["BNN_FP6_PERS"] != "0"))
+# BNN_FP6_HALF=0 / 1 / 2: the FP6 GEMM's half-tile form off / on the residual-plane (dX) launches (the
+# library's default) / on every launch (A/B timing; bnn_gemm_fp6_set_half)
+if os.environ.get("BNN_FP6_HALF") is not None:
+    L.call("bnn_gemm_fp6_set_half", int(os.environ["BNN_FP6_HALF"]), 0.0)
 # BNN_PIX_TILE=1 / 2: the u8-pixel statistics GEMM's tile, 128 x 128 / 256 x 256 (A/B timing)
 if os.environ.get("BNN_PIX_TILE") is not None:
     L.call("bnn_gemm_i8_bnstats_set_tile", int(os.environ["BNN_PIX_TILE"]))
