@@ -836,22 +836,36 @@ def pixels_to_float(u, normalize=None):
 
 
 UNIT_PIXELS = 0          # fp32 ToTensor images recognised as bytes (tests check the path ran)
+CAPTURE_GUARDS = []      # mismatch flags of the recognitions captured into a graph (graph.GraphedStep)
 
 
-def unit_to_pixels(x):
+def unit_to_pixels(x, guard=None):
     """fp32 images [.., K] that are exactly ToTensor's fl(u / 255) -> their bytes u (uint8, same
-    shape), else None.  One pass (bnn_unit_to_pixels) and one host read of its mismatch flag; None
-    during graph capture (the flag cannot be read there)."""
+    shape), else None.  One pass (bnn_unit_to_pixels) and one host read of its mismatch flag.
+
+    During graph capture the flag cannot be read: without a guard the call returns None (the
+    caller keeps its fp32 path); with one (an int32 [1] zero tensor, owned by the caller, which
+    passes it only when its eager calls recognised the images) the pass is captured with the guard
+    as its sticky mismatch flag, the bytes are returned, and the guard joins CAPTURE_GUARDS, which
+    GraphedStep reads before each replay -- a replay over inputs that are not ToTensor images makes
+    the next call raise."""
     global UNIT_PIXELS
     _check(x)
-    if x.numel() == 0 or (x.is_cuda and torch.cuda.is_current_stream_capturing()):
+    capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+    if x.numel() == 0 or (capturing and guard is None):
         return None
     x = x if x.is_contiguous() else x.contiguous()
     u = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    bad = torch.zeros((1,), dtype=torch.int32, device=x.device)
+    if capturing:
+        _check(guard, dtype=torch.int32)
+        bad = guard
+    else:
+        bad = torch.zeros((1,), dtype=torch.int32, device=x.device)
     with _timed("unit_to_pixels_k", 0, 5 * x.numel()):
         L.call("bnn_unit_to_pixels", L.ptr(x), x.numel(), L.ptr(u), L.ptr(bad), L.stream())
-    if int(bad.item()) != 0:
+    if capturing:
+        CAPTURE_GUARDS.append(guard)
+    elif int(bad.item()) != 0:
         return None
     UNIT_PIXELS += 1
     return u

@@ -17,7 +17,13 @@ whole step -- forward, loss, backward, the fused latent update -- once and repla
   (tests/test_gpu_rccl.py::test_rccl_exchange_captured_in_graph: replays equal eager steps bit for
   bit on a one-rank RCCL group).  Every rank captures and replays the same step.
 """
+import time
+
 import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from . import functional as BF
 
 
 class GraphedStep:
@@ -38,9 +44,18 @@ class GraphedStep:
         # the captured Adam reads its bias corrections from device tables built for the current lr
         if hasattr(optimizer, "build_schedules"):
             optimizer.build_schedules()
+        # let RCCL's watchdog retire the warm-up's collectives (it polls every 100 ms), and capture in
+        # thread-local mode so that its event queries from another thread cannot invalidate the capture
+        torch.cuda.synchronize()
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+            time.sleep(0.25)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        BF.CAPTURE_GUARDS.clear()
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = step_fn()
+        # sticky mismatch flags of the fp32-image recognitions the step captured (nn.BinarizeLinear)
+        self.guards = list(BF.CAPTURE_GUARDS)
+        BF.CAPTURE_GUARDS.clear()
         # the capture ran the host side of one step without executing it on the device
         self._shadow(-1)
 
@@ -52,8 +67,22 @@ class GraphedStep:
                 if st and "step" in st:
                     st["step"] += n
 
+    def check(self):
+        """Raise if a replay so far saw fp32 inputs that are not ToTensor images at a layer whose
+        capture took the u8-pixel path (one host read per guard; __call__ runs it first)."""
+        for g in self.guards:
+            if int(g.item()) != 0:
+                raise L.BnnError("GraphedStep: a replay fed fp32 inputs that are not ToTensor images "
+                                  "(fl(u / 255)) to a BinarizeLinear captured on its u8-pixel path; that "
+                                  "replay's step is wrong -- set detect_pixels = False on the layer (or "
+                                  "feed uint8 pixels) and capture again")
+
     def __call__(self, n=1):
-        """Replay the captured step n times; returns the step function's (static) output."""
+        """Replay the captured step n times; returns the step function's (static) output.  A step
+        with captured pixel recognitions is checked before the replays (GraphedStep.check) --
+        that waits for the previous replay; call check() after the last one."""
+        if self.guards:
+            self.check()
         limit = self.opt.schedule_limit() if hasattr(self.opt, "schedule_limit") else None
         if limit is not None and self.ds.steps + int(n) > limit:
             # the *_sched kernels index the table by the device counter without a bound

@@ -136,7 +136,16 @@ class BinarizeLinear(nn.Linear):
             # fp32 images straight from ToTensor (mnist-dist2.py:96-99): exactly fl(u / 255) for bytes
             # u, so fc1 runs on the bytes -- the same F.linear value within fp32 rounding (the u8
             # path's integer sums are exact), one int8 pass instead of three digit planes each way
-            u = BF.unit_to_pixels(input)
+            # under graph capture the recognition is replayed only if this layer's eager calls made
+            # it (the warm-up of graph.GraphedStep does), guarded by a device flag the replays check
+            if torch.cuda.is_current_stream_capturing():
+                guard = self.__dict__.get("_pixel_guard") if self.__dict__.get("_pixel_mode") else None
+                u = BF.unit_to_pixels(input, guard=guard) if guard is not None else None
+            else:
+                u = BF.unit_to_pixels(input)
+                self._pixel_mode = u is not None
+                if u is not None and self.__dict__.get("_pixel_guard") is None:
+                    self._pixel_guard = torch.zeros((1,), dtype=torch.int32, device=input.device)
             if u is not None:
                 if self.org_protocol:
                     _apply_org_protocol(self.weight)

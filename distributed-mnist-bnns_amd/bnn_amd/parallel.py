@@ -36,6 +36,7 @@ MI355X design:
   profiled on one GPU (an AVG over one rank leaves every gradient bit-identical).
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -54,6 +55,9 @@ def init_rccl(device, rank, world_size, init_method=None):
     last 24 collectives, 1,599.5 us, 0.00 % overlapped by compute kernels); a high-priority stream
     is given a queue of its own (profiles/r03_exchange_rccl_overlap_hiprio.txt: 5,886.1 us, 85.37 %
     overlapped -- one-rank collectives, so the durations are not xGMI traffic)."""
+    # graph.GraphedStep captures collectives: keep RCCL work events out of torch's recycling cache,
+    # so the watchdog thread never queries an event a capture has re-recorded
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
     kw = {"init_method": init_method} if init_method else {}
     dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, pg_options=opts, **kw)

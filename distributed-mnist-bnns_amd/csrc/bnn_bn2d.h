@@ -58,22 +58,21 @@ __device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
   return (XF != 0 && x.bias != nullptr) ? x.bias[c] : 0.f;
 }
 
-// Every read of the compact (int8 / int16) conv outputs is an agent-scope (sc1) load, which the
-// reading CU's vector L1 never serves.  With plain loads the BatchNorm2d forward passes returned
-// different statistics from run to run -- never in one process alone, in about one step in ten
-// while other processes used the same GPU (the two-rank data-parallel tests run that way) --
-// although the conv sums in memory were identical every time; host synchronisations before and
-// between the passes and a 512 MB L2 eviction left it so, sc1 loads removed it (0 of 156 steps,
-// plain 11 of 156; tools/race_trace.py, profiles/r05_race_*.log), and nt loads -- which still hit a
-// line L1 holds -- did not (round 6: the two-rank BinCNN test failed with them,
-// profiles/r06_c_gpu_tests_a.log).  The stale bytes come from the consumer CU's L1, so every consumer
-// of freshly written compact data bypasses it: the forward and backward BatchNorm2d passes and
-// conv1's fused filter gradient.  The loads are buffer loads (aux = sc1) of up to
-// 16 B, so the rows kernels keep their 16-B instructions (round 5's 4- / 8-B atomic loads cost
-// ~0.05 ms per BinCNN step).  BN2_LOADS: 1 sc1 buffer loads (default), 0 plain, 2 agent-scope
-// atomic loads (round 5), 3 nt loads -- A/B only.  Compact buffers are < 2 GB (host checks).
+// Every read of the compact (int8 / int16) conv outputs is an agent-scope relaxed atomic load
+// (global_load ... sc1, 2 to 8 B; 16-B reads are two 8-B loads).  With plain loads the BatchNorm2d
+// forward statistics differed from run to run -- never in one process alone, in about one step in
+// ten while other processes used the same GPU (the two-rank data-parallel tests run that way) --
+// although the conv sums in memory were identical every time (tools/race_trace.py: plain 11 of 156
+// steps, profiles/r05_race_*.log).  The atomic form: 0 of 156 (round 5) and 0 of 120 steps (round 6,
+// profiles/r06_f_race_trace_atomic.log).  Two other forms failed in round 6: nt loads (the two-rank
+// BinCNN test, profiles/r06_c_gpu_tests_a.log) and buffer loads carrying the SAME sc1 bit as the
+// atomic loads (6 of 120 steps, profiles/r06_e_race_trace_sc1buf.log) -- so the L1 bypass the sc1
+// bit encodes is not by itself what removes the difference, and the mechanism is not identified
+// (DESIGN.md §8 lists the evidence).  The consumers: the forward and backward BatchNorm2d passes and
+// conv1's fused filter gradient.  BN2_LOADS: 2 atomic (default), 0 plain, 1 sc1 buffer loads, 3 nt
+// loads -- A/B only.  Compact buffers are < 2 GB (host checks).
 #ifndef BN2_LOADS
-#define BN2_LOADS 1
+#define BN2_LOADS 2
 #endif
 constexpr int BN2_SC1 = 16;   // buffer-instruction aux bits: sc1
 
@@ -99,6 +98,11 @@ __device__ __forceinline__ auto x2_raw(const void* base, int64_t off) {
     const U v = __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (NB == 8) return v2u{(uint32_t)v, (uint32_t)(v >> 32)};
     else return (T)v;
+  } else if constexpr (COH && BN2_LOADS == 2) {   // 16 B: two 8-B atomic loads
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
   } else if constexpr (COH && BN2_LOADS == 3) {
     return __builtin_nontemporal_load(p);
   } else {

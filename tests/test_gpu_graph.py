@@ -215,3 +215,53 @@ def test_graph_replay_past_schedule_raises(F):
             g(2)
     finally:
         ds.deactivate()
+
+
+def test_graph_captures_totensor_recognition_with_guard(F):
+    """fp32 ToTensor images (mnist-dist2.py:96-99, the GPU's fl(u * fl(1 / 255))) at fc1: the
+    warm-up recognises them, the capture replays the recognition (nn.BinarizeLinear's guard), so
+    the replays equal the eager device-step steps bit for bit -- the graph does not fall back to the
+    fp32-digit GEMMs the eager steps skipped.  A replay over inputs that are not ToTensor images then
+    makes the next call (and check()) raise."""
+    from bnn_amd.graph import GraphedStep
+    from bnn_amd.nets import binary_params
+    from bnn_amd.optim import LatentAdam
+    u, y = _batch(256)
+    x = u.float() / 255.0
+    runs = []
+    for graphed in (False, True):
+        m = _model(5)
+        torch.manual_seed(99)
+        ds = F.DeviceStep().activate()
+        try:
+            opt = LatentAdam(m.parameters(), lr=0.01, clamp_params=binary_params(m), device_step=ds)
+            xs = x.clone()
+            step = _step_fn(m, opt, xs, y)
+            losses = []
+            if graphed:
+                n0 = F.UNIT_PIXELS
+                g = GraphedStep(step, opt, ds, warmup=2)
+                assert F.UNIT_PIXELS == n0 + 3 and len(g.guards) == 1      # 2 warm-up + the capture
+                for _ in range(3):
+                    losses.append(float(g().item()))
+                g.check()
+                runs.append((_state(m, opt), losses))
+                xs.mul_(1.0001)                                           # no longer fl(u / 255)
+                g()
+                with pytest.raises(RuntimeError, match="not ToTensor images"):
+                    g()
+                with pytest.raises(RuntimeError, match="not ToTensor images"):
+                    g.check()
+            else:
+                for i in range(5):
+                    loss = step()
+                    if i >= 2:
+                        losses.append(float(loss.item()))
+                runs.append((_state(m, opt), losses))
+            torch.cuda.synchronize()
+        finally:
+            ds.deactivate()
+    (a, la), (b, lb) = runs
+    assert la == lb
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
