@@ -132,7 +132,38 @@ __global__ __launch_bounds__(CE_T1) void ce_fwd1_k(const float* __restrict__ p, 
   const int t = threadIdx.x;
   double l = 0.0;
   int n = 0;
-  for (int64_t i = t; i < M; i += CE_T1) row_loss<C>(p, y, i, ignore, lse, l, n);
+  // U rows per trip, all their loads issued before any is used (the same row order as one at a time)
+  constexpr int U = C <= 16 ? 4 : 1;
+  for (int64_t i0 = t; i0 < M; i0 += U * CE_T1) {
+    float v[U][C];
+    int64_t yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = min(i0 + (int64_t)u * CE_T1, M - 1);   // clamped: unconditional loads
+#pragma unroll
+      for (int j = 0; j < C; ++j) v[u][j] = p[i * C + j];
+      yv[u] = y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * CE_T1;
+      if (i >= M) break;
+      float mx = v[u][0];
+#pragma unroll
+      for (int j = 1; j < C; ++j) mx = fmaxf(mx, v[u][j]);
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < C; ++j) sm += expf(v[u][j] - mx);
+      const float ls = mx + logf(sm);
+      lse[i] = ls;
+      if (yv[u] == ignore) continue;
+      float py = __builtin_nanf("");
+#pragma unroll
+      for (int j = 0; j < C; ++j) py = (j == yv[u]) ? v[u][j] : py;
+      l += (double)(ls - py);
+      n += 1;
+    }
+  }
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     l += __shfl_xor(l, o, 64);
@@ -158,21 +189,19 @@ __global__ __launch_bounds__(CE_T1) void ce_fwd1_k(const float* __restrict__ p, 
   }
 }
 
+// one thread per element (row-major, coalesced loads and stores; a row's 10 elements over 10 lanes)
 template <int C>
 __global__ __launch_bounds__(CE_T) void ce_bwd_k(const float* __restrict__ p, const int64_t* __restrict__ y,
                                                 const float* __restrict__ lse, const float* __restrict__ cnt,
                                                 const float* __restrict__ go, int64_t M, int64_t ignore,
                                                 float* __restrict__ dp) {
-  const int64_t i = (int64_t)blockIdx.x * CE_T + threadIdx.x;
-  if (i >= M) return;
+  const int64_t e = (int64_t)blockIdx.x * CE_T + threadIdx.x;
+  if (e >= M * C) return;
+  const int64_t i = e / C;
+  const int j = (int)(e - i * C);
   const float g = go[0] / cnt[0];
-  const float ls = lse[i];
   const int64_t yi = y[i];
-  const float* pr = p + i * C;
-  float* dr = dp + i * C;
-  const bool ign = yi == ignore;
-#pragma unroll
-  for (int j = 0; j < C; ++j) dr[j] = ign ? 0.f : g * (expf(pr[j] - ls) - (j == yi ? 1.f : 0.f));
+  dp[e] = yi == ignore ? 0.f : g * (expf(p[e] - lse[i]) - (j == yi ? 1.f : 0.f));
 }
 
 }  // namespace
@@ -233,7 +262,7 @@ BNN_API int bnn_cross_entropy_bwd(const float* p, const int64_t* y, int64_t M, i
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* lse = reinterpret_cast<const float*>(work);
   const float* cnt = reinterpret_cast<const float*>(reinterpret_cast<const char*>(work) + ce_lse_bytes(M));
-  BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_bwd_k<CV>), dim3((unsigned)((M + CE_T - 1) / CE_T)), dim3(CE_T), 0, s,
+  BNN_CE_SWITCH((int)C, hipLaunchKernelGGL((ce_bwd_k<CV>), dim3((unsigned)((M * CV + CE_T - 1) / CE_T)), dim3(CE_T), 0, s,
                                             p, y, lse, cnt, go, M, ignore_index, dp));
   return check_launch("bnn_cross_entropy_bwd");
 }

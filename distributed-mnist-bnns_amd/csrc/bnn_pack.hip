@@ -56,37 +56,37 @@ struct ColAffine {
   int vec;             // all four 16-B aligned -> float4 parameter loads
 };
 
-// One 16-element run of a latent-weight row updated in place by Adam + clamp (ADAM mode of
+// One 4-element run of a latent-weight row updated in place by Adam + clamp (ADAM mode of
 // sign_pack_tile_k: the fused latent update of mnist-dist2.py:131-137 that also writes the next
-// forward's ternary operands).  p, g, m, v share the row-major [M][K] layout (ldx = K).
-__device__ __forceinline__ void adam16(float* __restrict__ prow, int64_t off, int64_t k, int64_t K, bool vec,
-                                       const AdamArgs& a0, float (&v)[16]) {
-  const AdamArgs a = adam_resolve(a0);
-  float g[16], mm[16], vv[16];
-  load16(prow, k, K, vec, v);
-  load16(a.g + off, k, K, vec, g);
-  load16(a.m + off, k, K, vec, mm);
-  load16(a.v + off, k, K, vec, vv);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) v[j] = adam_elem(v[j], g[j], mm[j], vv[j], a);
-  if (vec && k + 16 <= K) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<float4*>(prow + k + 4 * i) = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-      *reinterpret_cast<float4*>(a.m + off + k + 4 * i) =
-          make_float4(mm[4 * i], mm[4 * i + 1], mm[4 * i + 2], mm[4 * i + 3]);
-      *reinterpret_cast<float4*>(a.v + off + k + 4 * i) =
-          make_float4(vv[4 * i], vv[4 * i + 1], vv[4 * i + 2], vv[4 * i + 3]);
-    }
+// forward's ternary operands).  p, g, m, v share the row-major [M][K] layout; off = the row's
+// offset, columns k..k+3; sg = the new signs (0 beyond K).
+__device__ __forceinline__ void adam4(float* __restrict__ prow, int64_t off, int64_t k, int64_t K, bool vec,
+                                      const AdamArgs& a, int (&sg)[4]) {
+  if (vec && k + 4 <= K) {
+    const float4 pv = *reinterpret_cast<const float4*>(prow + k);
+    const float4 gv = *reinterpret_cast<const float4*>(a.g + off + k);
+    float4 mv = *reinterpret_cast<const float4*>(a.m + off + k);
+    float4 vv = *reinterpret_cast<const float4*>(a.v + off + k);
+    float4 np;
+    np.x = adam_elem(pv.x, gv.x, mv.x, vv.x, a);
+    np.y = adam_elem(pv.y, gv.y, mv.y, vv.y, a);
+    np.z = adam_elem(pv.z, gv.z, mv.z, vv.z, a);
+    np.w = adam_elem(pv.w, gv.w, mv.w, vv.w, a);
+    *reinterpret_cast<float4*>(prow + k) = np;
+    *reinterpret_cast<float4*>(a.m + off + k) = mv;
+    *reinterpret_cast<float4*>(a.v + off + k) = vv;
+    sg[0] = tsign(np.x), sg[1] = tsign(np.y), sg[2] = tsign(np.z), sg[3] = tsign(np.w);
   } else {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < 4; ++j) {
+      sg[j] = 0;
       if (k + j < K) {
-        prow[k + j] = v[j];
-        a.m[off + k + j] = mm[j];
-        a.v[off + k + j] = vv[j];
-      } else {
-        v[j] = 0.f;
+        float mm = a.m[off + k + j], vv = a.v[off + k + j];
+        const float np = adam_elem(prow[k + j], a.g[off + k + j], mm, vv, a);
+        prow[k + j] = np;
+        a.m[off + k + j] = mm;
+        a.v[off + k + j] = vv;
+        sg[j] = tsign(np);
       }
     }
   }
@@ -94,7 +94,7 @@ __device__ __forceinline__ void adam16(float* __restrict__ prow, int64_t off, in
 
 // One 64x64 tile of x -> ternary rows (q: FMT 0 = int8 per element, FMT 1 = FP4 e2m1 nibbles,
 // element k in byte k/2, low nibble for even k) and/or the transposed int8 tile (qt).
-// ADAM = 1: x is a latent weight updated in place first (adam16), and its new sign is packed.
+// ADAM = 1: x is a latent weight updated in place first (adam4), and its new sign is packed.
 template <int FMT, int AFF = 0, int ADAM = 0>
 __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
                                                         int64_t K, int64_t ldx, int8_t* __restrict__ q,
@@ -146,24 +146,43 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
   if (it > 0) __syncthreads();                // the previous tile's transposed reads are done
   const int64_t m0 = ty * TILE;
   const int64_t m = m0 + r;
-  float v[16];
-  if (ADAM && m < M) {
-    adam16(const_cast<float*>(x) + m * ldx, m * ldx, k0 + c, K, vec, ad, v);
-  } else if (m < M) {
-    load16(x + m * ldx, k0 + c, K, vec, v);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = 0.f;
-  }
-  if (AFF) {
-    const int64_t cb = k0 + c;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      v[j] = (m < M && cb + j < K) ? fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]) : 0.f;
-  }
   int s[16];
+  if constexpr (ADAM) {
+    // the update as whole 256-B row runs (16 lanes x float4 per row, 16 rows per pass: every wave
+    // load instruction covers 4 full rows; lane = 16 consecutive floats moved 64-B pieces), the new
+    // signs through the LDS tile into the row-run layout the packing below uses
+    const AdamArgs a = adam_resolve(ad);
+    const int ar = t >> 4, ac = (t & 15) * 4;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) s[j] = tsign(v[j]);
+    for (int pr = 0; pr < TILE / 16; ++pr) {
+      const int rr = ar + 16 * pr;
+      const int64_t mr = m0 + rr;
+      int sg[4] = {0, 0, 0, 0};
+      if (mr < M) adam4(const_cast<float*>(x) + mr * ldx, mr * ldx, k0 + ac, K, vec, a, sg);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[rr][ac + j] = sg[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[j] = tile[r][c + j];
+    if (qt != nullptr) __syncthreads();   // read before the transpose below rewrites the tile
+  } else {
+    float v[16];
+    if (m < M) {
+      load16(x + m * ldx, k0 + c, K, vec, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = 0.f;
+    }
+    if (AFF) {
+      const int64_t cb = k0 + c;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        v[j] = (m < M && cb + j < K) ? fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[j] = tsign(v[j]);
+  }
   if (FMT == 0 && q != nullptr && m < M && k0 + c < ldq) {
     v4i w;
     w.x = pack4(s[0], s[1], s[2], s[3]);
