@@ -114,6 +114,8 @@ def parse():
                     help="time the unchanged-script path instead: the reference Net through the drop-in "
                          "models.binarized_modules (.org protocol, torch BatchNorm / Hardtanh / CrossEntropyLoss, "
                          "torch.optim.Adam + the .org copy loop of mnist-dist2.py:131-137) on fp32 images")
+    ap.add_argument("--dropin-bn", action="store_true",
+                    help="with --dropin: bn1..bn3 as bnn_amd.nn.BatchNorm1d (torch's module on libbnn's passes)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path's secondary timing")
     ap.add_argument("--fp32-input", action="store_true",
                     help="feed fp32 images (u/255) instead of the u8 pixels the MLPs' fc1 consumes")
@@ -135,13 +137,16 @@ def build(cfg, backend):
     return model
 
 
-def build_dropin(cfg):
+def build_dropin(cfg, dropin_bn=False):
     """The reference's own call pattern on the drop-in module (mnist-dist2.py:46-76 Net built from
     models.binarized_modules' BinarizeLinear / BinarizeConv2d with torch's BatchNorm, Hardtanh,
-    Dropout, LogSoftmax): ``org_protocol`` and ``mutate_input`` left at the reference's behaviour."""
+    Dropout, LogSoftmax): ``org_protocol`` and ``mutate_input`` left at the reference's behaviour.
+    dropin_bn: bn1..bn3 swapped for bnn_amd.nn.BatchNorm1d as well (MLPs)."""
     from bnn_amd import nets
     name = CONFIGS[cfg][0]
-    return nets.BinCNN() if name == "cnn" else nets.MODELS[name]()
+    if name == "cnn":
+        return nets.BinCNN()
+    return nets.MODELS[name](dropin_bn=True) if dropin_bn else nets.MODELS[name]()
 
 
 def dropin_step_fn(model, x, y, lr):
@@ -160,11 +165,11 @@ def dropin_step_fn(model, x, y, lr):
     return step
 
 
-def time_dropin(cfg, batch, dev, lr, steps, warmup):
+def time_dropin(cfg, batch, dev, lr, steps, warmup, dropin_bn=False):
     """(ms per step, samples/s) of the drop-in path on this GPU: the same batch shape as fp32 images."""
     from bnn_amd.data import synthetic_mnist
     torch.manual_seed(0)
-    model = build_dropin(cfg).to(dev).train()
+    model = build_dropin(cfg, dropin_bn).to(dev).train()
     x, y = synthetic_mnist(batch, seed=1234, device=dev, as_u8=False)
     step = dropin_step_fn(model, x, y, lr)
     for _ in range(warmup):
@@ -177,8 +182,9 @@ def time_dropin(cfg, batch, dev, lr, steps, warmup):
     dt = (time.perf_counter() - t0) / steps
     out = {"ms_per_step": round(dt * 1e3, 3), "value": round(batch / dt, 2), "unit": "samples/s", "steps": steps,
            "warmup": warmup, "loss_last_step": round(float(loss.item()), 5),
-           "path": "models.binarized_modules drop-in (.org protocol, torch BatchNorm/Hardtanh/CrossEntropyLoss, "
-                   "torch.optim.Adam + .org copy loop), fp32 images"}
+           "path": ("models.binarized_modules drop-in (.org protocol, "
+                    + ("bnn_amd.nn.BatchNorm1d, torch " if dropin_bn else "torch BatchNorm/")
+                    + "Hardtanh/CrossEntropyLoss, torch.optim.Adam + .org copy loop), fp32 images")}
     del model, x, y, step
     torch.cuda.empty_cache()
     return out
@@ -347,7 +353,9 @@ def main():
 
     batch = args.batch or CONFIGS[args.config][1]
     torch.manual_seed(0)
-    model = (build_dropin(args.config) if args.dropin else build(args.config, args.backend)).to(dev).train()
+    if args.dropin_bn and not args.dropin:
+        raise SystemExit("--dropin-bn goes with --dropin")
+    model = (build_dropin(args.config, args.dropin_bn) if args.dropin else build(args.config, args.backend)).to(dev).train()
     # --exchange at N = 1: a one-rank RCCL group issuing every collective of an N-GPU step
     exchange = (GradExchange(model, bucket_mb=args.bucket_mb, force_collectives=args.exchange)
                 if use_exchange else None)
@@ -462,7 +470,7 @@ def main():
                  + ", random-init weights"),
         "config": {"workload": CONFIGS[args.config][2] + (" -- drop-in path (the unchanged reference loop)"
                                                            if args.dropin else ""),
-                   "model": args.config + ("-dropin" if args.dropin else ""), "global_batch": batch * world,
+                   "model": args.config + ("-dropin" + ("-bn" if args.dropin_bn else "") if args.dropin else ""), "global_batch": batch * world,
                    "per_gpu_batch": batch, "seq_len": 1, "parallelism": f"dp{world}",
                    "backend": args.backend, "exchange": bool(use_exchange), "hip_graph": bool(args.graph),
                    "loss_last_step": round(final_loss, 5)},
@@ -502,6 +510,12 @@ def main():
             result["dropin"] = time_dropin(args.config, batch, dev, args.lr, steps=5, warmup=2)
         except RuntimeError as e:        # e.g. out of memory: report, never fail the bench line
             result["dropin"] = {"error": repr(e)[:200]}
+        if CONFIGS[args.config][0] != "cnn":
+            # the same with bn1..bn3 swapped for bnn_amd.nn.BatchNorm1d
+            try:
+                result["dropin_bn"] = time_dropin(args.config, batch, dev, args.lr, steps=5, warmup=2, dropin_bn=True)
+            except RuntimeError as e:
+                result["dropin_bn"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and not args.no_gpu_torch and args.config in CPU_WIDTHS:
         try:
             gb = min(batch, 16384) if args.config == "wide" else batch

@@ -1657,9 +1657,11 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
     (mnist-dist2.py:52-74).  Running stats are updated in place in training mode."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh):
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh, handoff=True):
         _check(x, weight, bias, running_mean, running_var)
-        ctx.q6 = _q6_wanted(x, x.shape[-1], training)
+        # handoff = False: dx is always a dense tensor (nn.BatchNorm1d's drop-in, whose input may
+        # feed other ops the FP6 digit hand-off would not see)
+        ctx.q6 = handoff and _q6_wanted(x, x.shape[-1], training)
         x = _c2d(x)
         M, C = x.shape
         y = torch.empty_like(x)
@@ -1698,7 +1700,7 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
             with _timed("bn_bwd", 0, 16 * M * C):
                 _bn_bwd_call(ctx.training, x, dy, M, C, w, b, mean, invstd, mlo, ctx.hardtanh, dx, dw, db, ws)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 class DropoutBatchNormHardtanhFunction(torch.autograd.Function):
@@ -1940,13 +1942,13 @@ def _bn_module_args(bn):
     return rm, rv, bn_training, factor
 
 
-def batch_norm_hardtanh(x, bn, hardtanh=True):
+def batch_norm_hardtanh(x, bn, hardtanh=True, handoff=True):
     """Apply an ``nn.BatchNorm1d`` module (its parameters, buffers, momentum / eps /
     track_running_stats semantics as in torch's ``_BatchNorm.forward``) followed by Hardtanh,
-    through libbnn."""
+    through libbnn.  handoff = False: never hand FP6 digits of dx to the producing linear."""
     rm, rv, bn_training, factor = _bn_module_args(bn)
     return BatchNormHardtanhFunction.apply(x, bn.weight, bn.bias, rm, rv, bn_training, factor, bn.eps,
-                                           hardtanh)
+                                           hardtanh, bool(handoff))
 
 
 # ----------------------------------------------------------------------------- BatchNorm2d (+ Hardtanh + MaxPool2d)

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import functional as BF
-from .nn import BinarizeConv2d, BinarizeLinear
+from .nn import BatchNorm1d, BinarizeConv2d, BinarizeLinear
 
 
 def _configure(module, org_protocol, mutate_input, backend=None):
@@ -33,21 +33,25 @@ class MLP(nn.Module):
     """mnist-dist2.py:46-76 with explicit widths."""
 
     def __init__(self, h1, h2, h3, p_drop=0.3, org_protocol=True, mutate_input=True, backend=None,
-                 fused_bn=False, normalize=None):
+                 fused_bn=False, normalize=None, dropin_bn=False):
         super().__init__()
+        # dropin_bn: bn1..bn3 are bnn_amd.nn.BatchNorm1d (torch's module on libbnn's passes), the
+        # drop-in a user of the reference swaps for nn.BatchNorm1d; the modules and state_dict keep
+        # their names and shapes either way
+        BN = BatchNorm1d if dropin_bn else nn.BatchNorm1d
         # fused_bn: bn_i -> htanh_i run as one libbnn BatchNorm+Hardtanh pass (same parameters,
         # buffers and math; replaces torch's BatchNorm1d kernels, DESIGN.md)
         self.fused_bn = fused_bn
         self.fused_head = True     # with fused_bn: drop -> bn3 -> htanh3 -> fc4 as one libbnn op
         self.fc1 = BinarizeLinear(784, h1)
         self.htanh1 = nn.Hardtanh()
-        self.bn1 = nn.BatchNorm1d(h1)
+        self.bn1 = BN(h1)
         self.fc2 = BinarizeLinear(h1, h2)
         self.htanh2 = nn.Hardtanh()
-        self.bn2 = nn.BatchNorm1d(h2)
+        self.bn2 = BN(h2)
         self.fc3 = BinarizeLinear(h2, h3)
         self.htanh3 = nn.Hardtanh()
-        self.bn3 = nn.BatchNorm1d(h3)
+        self.bn3 = BN(h3)
         self.fc4 = nn.Linear(h3, 10)
         self.logsoftmax = nn.LogSoftmax(dim=1)
         self.drop = nn.Dropout(p_drop)

@@ -33,7 +33,7 @@ import torch.nn as nn
 
 from . import functional as BF
 
-__all__ = ["Binarize", "HingeLoss", "SqrtHingeLossFunction", "Quantize", "BinarizeLinear",
+__all__ = ["Binarize", "HingeLoss", "SqrtHingeLossFunction", "Quantize", "BinarizeLinear", "BatchNorm1d",
            "BinarizeConv2d", "CrossEntropyLoss"]
 
 
@@ -169,6 +169,31 @@ class BinarizeLinear(nn.Linear):
                 self.bias.org = self.bias.data.clone()          # :82
         return BF.binary_linear(input, self.weight, self.bias, binarize, self.backend,
                                 cache=not self.org_protocol, xpack=xpack)
+
+
+class BatchNorm1d(nn.BatchNorm1d):
+    """torch.nn.BatchNorm1d on libbnn's BatchNorm passes, for the reference Nets' bn1..bn3
+    (mnist-dist2.py:52-57: nn.BatchNorm1d(3072 * r) etc. between BinarizeLinear and Hardtanh).
+    Same constructor, parameters, buffers and state_dict as torch's; torch's _BatchNorm.forward
+    semantics (batch statistics with the biased variance in training, the unbiased one into the
+    running variance, momentum or the cumulative average for momentum=None, num_batches_tracked,
+    track_running_stats=False, affine=False, eval mode) through functional.batch_norm_hardtanh
+    with the Hardtanh off.  The statistics are fixed-order double sums (deterministic).  Inputs:
+    [M, C] fp32 on the GPU; anything else raises (no silent torch fallback).
+
+    Not in the reference's models/binarized_modules.py: a user of the drop-in swaps
+    nn.BatchNorm1d for it to take torch's channels_last BatchNorm kernels (121 of the 182 ms of the
+    wide drop-in step) off the path."""
+
+    def forward(self, input):
+        if input.dim() != 2 or not input.is_cuda or input.dtype != torch.float32:
+            raise TypeError(f"bnn_amd.nn.BatchNorm1d: needs a [M, C] float32 CUDA input (got {tuple(input.shape)} "
+                            f"{input.dtype} on {input.device}); use torch.nn.BatchNorm1d for other inputs")
+        if input.shape[1] != self.num_features:
+            raise ValueError(f"bnn_amd.nn.BatchNorm1d: expected {self.num_features} features, got {input.shape[1]}")
+        if self.training and input.shape[0] <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")   # torch's message
+        return BF.batch_norm_hardtanh(input, self, hardtanh=False, handoff=False)
 
 
 class BinarizeConv2d(nn.Conv2d):

@@ -82,3 +82,14 @@ def test_conv_bf3_plans_are_bank_conflict_free(L):
     assert cyc == 400
     # shapes neither kernel takes report -1
     assert L.bnn_conv_bf3_plan(4, 8, 9, 9, 8, 3, 3, 2, 1, 1, 1, out) == 0 and out[0] == -1 and out[4] == -1
+
+
+def test_bn_dropin_rejects_cpu_and_non_2d_inputs():
+    """bnn_amd.nn.BatchNorm1d raises for what it does not run on the GPU (no silent torch fallback)."""
+    import pytest
+    import torch
+    from bnn_amd.nn import BatchNorm1d
+    bn = BatchNorm1d(8)
+    assert isinstance(bn, torch.nn.BatchNorm1d) and set(bn.state_dict()) == set(torch.nn.BatchNorm1d(8).state_dict())
+    with pytest.raises(TypeError, match="float32 CUDA"):
+        bn(torch.randn(4, 8))
