@@ -1546,24 +1546,51 @@ __global__ __launch_bounds__(BN2_T) void bn2d_bwd_stats_rows_k(X2 x, const float
   const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
   double a = 0.0, b = 0.0;
   const int64_t pairs = (n1 - n0) * PH;
-  for (int64_t i = threadIdx.x; i < pairs; i += BN2_T) {
+  // XF = 2: each trip's 256 row pairs staged through LDS by address-ordered loads (Rows16)
+  __shared__ uint2 lds[XF == 2 ? 256 * Rows16<PW>::LD : 1];
+  const float inv_ph = 1.f / (float)PH;
+  for (int64_t i0 = 0; i0 < pairs; i0 += BN2_T) {   // uniform trips: every thread reaches the barriers
+    const int64_t i = i0 + threadIdx.x;
     const int64_t q0 = i / PH;
     const int ph = (int)(i - q0 * PH);
     const int64_t plane = (n0 + q0) * C + c;
     const int64_t xo = plane * HW + (int64_t)(2 * ph) * W, yo = plane * pp + (int64_t)ph * PW;
     float2 top[PW], bot[PW];
+    if constexpr (XF == 2) {
+      if (i0 > 0) __syncthreads();                     // the previous trip's LDS reads are done
+      const int np = (int)((pairs - i0) < BN2_T ? (pairs - i0) : BN2_T);
+      rows16_stage<PW>(x, np, [&](int pr) {
+        // pair qq of the chunk -> (image qq / PH, pooled row); 32-bit quotient by a float
+        // reciprocal, corrected (pairs < 2^22: off by at most one)
+        const int qq = (int)i0 + pr;
+        int qq0 = (int)((float)qq * inv_ph);
+        qq0 += (qq0 + 1) * PH <= qq;
+        qq0 -= qq0 * PH > qq;
+        return 2 * (((n0 + qq0) * C + c) * HW + (int64_t)(qq - qq0 * PH) * (2 * W));
+      }, lds);
+      __syncthreads();
+      if (i >= pairs) continue;
+      rows16_unpack<PW>(lds, (int)threadIdx.x, xb, top, bot);
+    } else {
+      if (i >= pairs) continue;
+      x2_rows<XF, PW>(x, xo, xb, top, bot);
+    }
     float g[PW];
-    x2_rows<XF, PW>(x, xo, xb, top, bot);
 #pragma unroll
     for (int q = 0; q < PW; ++q) g[q] = dy[yo + q];
     float fa = 0.f, fb = 0.f;
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
       const Win w = bn2_window(top[q], bot[q], k, hardtanh);
-      const float yv = w.y[w.arg];
+      float yv = w.y[0], xa = w.xh[0];   // w.y[w.arg], w.xh[w.arg] as selects (no indexed private array)
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        yv = w.arg == j ? w.y[j] : yv;
+        xa = w.arg == j ? w.xh[j] : xa;
+      }
       const float gg = (!hardtanh || (yv > -1.f && yv < 1.f)) ? g[q] : 0.f;
       fa += gg;
-      fb = fmaf(gg, w.xh[w.arg], fb);
+      fb = fmaf(gg, xa, fb);
     }
     a += (double)fa;
     b += (double)fb;
@@ -1589,6 +1616,16 @@ __global__ __launch_bounds__(256) void bn2d_apply_rows_k(X2 x, int64_t N, int64_
   constexpr int W = 2 * PW;
   const int PH = H / 2;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float2 top[PW], bot[PW];
+  // XF = 2: the workgroup's 256 row pairs are one contiguous 4 W * 256-byte run, staged through LDS
+  // by address-ordered loads (Rows16) before any thread leaves
+  __shared__ uint2 lds[XF == 2 ? 256 * Rows16<PW>::LD : 1];
+  if constexpr (XF == 2) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x, total = N * C * PH;
+    const int np = (int)((total - i0) < 256 ? (total - i0) : 256);
+    rows16_stage<PW>(x, np, [&](int pr) { return (i0 + pr) * (int64_t)(4 * W); }, lds);
+    __syncthreads();
+  }
   if (i >= N * C * PH) return;
   const int64_t plane = i / PH;
   const int ph = (int)(i - plane * PH);
@@ -1596,8 +1633,10 @@ __global__ __launch_bounds__(256) void bn2d_apply_rows_k(X2 x, int64_t N, int64_
   const Bn2Chan k = bn2_chan(c, mean, invstd, gamma, beta);
   const float xb = x2_bias<XF>(x, c);
   const int64_t xo = plane * ((int64_t)H * W) + (int64_t)(2 * ph) * W;
-  float2 top[PW], bot[PW];
-  x2_rows<XF, PW>(x, xo, xb, top, bot);
+  if constexpr (XF == 2)
+    rows16_unpack<PW>(lds, (int)threadIdx.x, xb, top, bot);
+  else
+    x2_rows<XF, PW>(x, xo, xb, top, bot);
   float* yr = y + plane * ((int64_t)PH * PW) + (int64_t)ph * PW;
 #pragma unroll
   for (int q = 0; q < PW; ++q) yr[q] = bn2_window(top[q], bot[q], k, hardtanh).out;

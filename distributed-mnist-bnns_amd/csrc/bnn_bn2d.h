@@ -190,6 +190,50 @@ __device__ __forceinline__ void x2_rows(const X2& x, int64_t xo, float b, float2
   }
 }
 
+// int16 row pairs of a pooled plane staged through LDS for a workgroup of 256 threads (one pair per
+// thread): the lanes load the pairs' 8-B words in address order -- a wave instruction reads 512
+// contiguous bytes wherever the pairs are contiguous -- instead of each lane loading its own 4 W-byte
+// pair (64 lanes x 16 B spread over 7 KB per instruction: the L1-bypassing atomic loads above cannot
+// merge those in L1, every instruction became 64 line requests).  Words per pair: 2 rows x 2 PW
+// int16 = PW; LDS stride PW words, padded to odd (2-way bank conflicts at most).
+template <int PW>
+struct Rows16 {
+  static constexpr int NW = PW;
+  static constexpr int LD = (PW % 2) ? PW : PW + 1;
+};
+
+// stage np (<= 256) pairs; base(pr) = byte offset of pair pr from x.p
+template <int PW, typename Base>
+__device__ __forceinline__ void rows16_stage(const X2& x, int np, Base base, uint2* lds) {
+  constexpr int NW = Rows16<PW>::NW, LD = Rows16<PW>::LD;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int w = (int)threadIdx.x + 256 * k;
+    const int pr = w / NW, kw = w - pr * NW;
+    if (pr < np) {
+      const v2u v = x2_raw<8, true>(x.p, base(pr) + 8 * kw);
+      lds[pr * LD + kw] = make_uint2(v.x, v.y);
+    }
+  }
+}
+
+// pair t's two rows as PW element pairs each (same values as x2_rows<2, PW>)
+template <int PW>
+__device__ __forceinline__ void rows16_unpack(const uint2* lds, int t, float b, float2 (&top)[PW], float2 (&bot)[PW]) {
+  constexpr int LD = Rows16<PW>::LD;
+  uint32_t w[2 * PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const uint2 v = lds[t * LD + i];
+    w[2 * i] = v.x, w[2 * i + 1] = v.y;
+  }
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    top[q] = make_float2(lo16f(w[q]) + b, hi16f(w[q]) + b);
+    bot[q] = make_float2(lo16f(w[PW + q]) + b, hi16f(w[PW + q]) + b);
+  }
+}
+
 // The backward of one 2x2 window (bn2d_bwd_apply_k): dz of its 4 elements (torch scan order) from
 // the pooled gradient gp routed to the argmax and masked by the Hardtanh, m0 = sum g / n,
 // m1 = sum g xhat / n and sc = gamma * invstd.
