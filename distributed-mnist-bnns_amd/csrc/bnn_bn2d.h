@@ -69,7 +69,8 @@ __device__ __forceinline__ float x2_bias(const X2& x, int64_t c) {
 // atomic loads (6 of 120 steps, profiles/r06_e_race_trace_sc1buf.log) -- so the L1 bypass the sc1
 // bit encodes is not by itself what removes the difference, and the mechanism is not identified
 // (DESIGN.md §8 lists the evidence).  The consumers: the forward and backward BatchNorm2d passes and
-// conv1's fused filter gradient.  BN2_LOADS: 2 atomic (default), 0 plain, 1 sc1 buffer loads, 3 nt
+// conv1's fused filter gradient; the rows kernels stage their row pairs through LDS (Rows16 below)
+// so that these loads stay address-ordered across the lanes.  BN2_LOADS: 2 atomic (default), 0 plain, 1 sc1 buffer loads, 3 nt
 // loads -- A/B only.  Compact buffers are < 2 GB (host checks).
 #ifndef BN2_LOADS
 #define BN2_LOADS 2
