@@ -212,7 +212,10 @@ __global__ __launch_bounds__(256, RED_OCC) void bn_reduce_k(XIn xin, const float
 // split and fold order (deterministic).  The forward merge takes two independent passes instead of
 // a serial Chan chain (two dependent double divisions per chunk): the batch sum first (its
 // fixed-order double sum gives the mean), then M2 = sum_r [M2_r + n_r (S_r / n_r - mean)^2].
-constexpr int FF_COLS = 16, FF_GROUPS = 16, FF_B = 8;
+#ifndef BN_FF_B
+#define BN_FF_B 8   // partials per batched load round (A/B hook; any value keeps the summation order)
+#endif
+constexpr int FF_COLS = 16, FF_GROUPS = 16, FF_B = BN_FF_B;
 
 inline dim3 ffin_grid(int64_t C) { return dim3((unsigned)((C + FF_COLS - 1) / FF_COLS)); }
 

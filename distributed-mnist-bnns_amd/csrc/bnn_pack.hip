@@ -246,6 +246,13 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
 // transposed in registers by three block-swap stages) -> 8 transposed rows x 16 B.
 // LDS reads are conflict-free: bank = 32 (mg & 1) + 33 b + (kb ^ ((mg >> 1) << 3)) mod 64.
 constexpr int AP_T = 256, AP_LD = 33;
+// phase-1 row unroll of the 256 x 256-tile passes (rows in flight per wave); A/B hooks
+#ifndef APK_UNROLL
+#define APK_UNROLL 4
+#endif
+#ifndef ADAMPK_UNROLL
+#define ADAMPK_UNROLL 4
+#endif
 
 __device__ __forceinline__ void nib_swap(uint32_t& a, uint32_t& b, int s, uint32_t mask) {
   const uint32_t t = ((a >> s) ^ b) & mask;
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
   }
   const float4 xb = xin_bias4<XF>(xin, cb);
   uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
-#pragma unroll 4
+#pragma unroll APK_UNROLL
   for (int i = 0; i < AP_T / 4; ++i) {
     const int r = wave + 4 * i;
     const int64_t m = m0 + r;
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(256) void adam_pack_fp4_k(float* __restrict__ p, Ad
   const int64_t k0 = (int64_t)blockIdx.x * AP_T, m0 = (int64_t)blockIdx.y * AP_T;
   const int64_t cb = k0 + 4 * lane;
   uint16_t* img16 = reinterpret_cast<uint16_t*>(img);
-#pragma unroll 4
+#pragma unroll ADAMPK_UNROLL
   for (int i = 0; i < AP_T / 4; ++i) {
     const int r = wave + 4 * i;
     const int64_t off = (m0 + r) * K + cb;            // N % 256 == 0: every row is in range
