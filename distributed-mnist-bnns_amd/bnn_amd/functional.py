@@ -810,6 +810,10 @@ class BinaryLinearFunction(torch.autograd.Function):
 def binary_linear(x, weight, bias=None, binarize_input=True, backend="fp4", cache=False, xpack=None):
     """Functional BinarizeLinear core: 2-D or N-D input (leading dims flattened).  ``cache``: the
     weight is a latent weight whose packed operands are cached on it (packed_weight)."""
+    if x.dim() == 2:
+        # no reshape view: the output tensor itself carries the FP6 hand-off request (_Q6_WANT) to
+        # the BatchNorm that consumes it, and its gradient comes back to this Function unchanged
+        return BinaryLinearFunction.apply(x, weight, bias, binarize_input, backend, cache, xpack)
     lead = x.shape[:-1]
     y = BinaryLinearFunction.apply(x.reshape(-1, x.shape[-1]), weight, bias, binarize_input, backend, cache, xpack)
     return y.reshape(*lead, weight.shape[0])
@@ -1659,8 +1663,8 @@ class BatchNormHardtanhFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, hardtanh, handoff=True):
         _check(x, weight, bias, running_mean, running_var)
-        # handoff = False: dx is always a dense tensor (nn.BatchNorm1d's drop-in, whose input may
-        # feed other ops the FP6 digit hand-off would not see)
+        # handoff = False: no FP6 digits of dx for the producing linear (dx is a dense tensor either
+        # way here: x is fp32, never a compact placeholder)
         ctx.q6 = handoff and _q6_wanted(x, x.shape[-1], training)
         x = _c2d(x)
         M, C = x.shape

@@ -193,7 +193,10 @@ class BatchNorm1d(nn.BatchNorm1d):
             raise ValueError(f"bnn_amd.nn.BatchNorm1d: expected {self.num_features} features, got {input.shape[1]}")
         if self.training and input.shape[0] <= 1:
             raise ValueError("Expected more than 1 value per channel when training")   # torch's message
-        return BF.batch_norm_hardtanh(input, self, hardtanh=False, handoff=False)
+        # the FP6 digit hand-off stays on: dx is written in full as well and the digits are keyed to
+        # that tensor, so a producing BinarizeLinear takes them only when it receives exactly this
+        # gradient (a gradient summed with another consumer's is quantised afresh)
+        return BF.batch_norm_hardtanh(input, self, hardtanh=False)
 
 
 class BinarizeConv2d(nn.Conv2d):

@@ -87,6 +87,8 @@ def test_bn_dropin_net_step_matches_torch_bn(NN):
     assert isinstance(b.bn1, NN.BatchNorm1d) and not isinstance(a.bn1, NN.BatchNorm1d)
     opts = [torch.optim.Adam(m.parameters(), lr=0.01) for m in (a, b)]
     crit = torch.nn.CrossEntropyLoss()
+    from bnn_amd import functional as BF
+    h0 = BF.Q6_HANDOFFS
     for step in range(3):
         losses = []
         for m, opt in zip((a, b), opts):
@@ -111,3 +113,28 @@ def test_bn_dropin_net_step_matches_torch_bn(NN):
             for k in sa:
                 if k.startswith("bn") and ("running" in k or "num_batches" in k):
                     assert torch.allclose(sb[k].float(), sa[k].float(), atol=1e-5, rtol=1e-4), k
+    # bn2's gradient reached fc2 with its FP6 digits (no second quantising pass over it)
+    assert BF.Q6_HANDOFFS > h0
+
+
+def test_bn_dropin_handoff_with_a_second_consumer(NN):
+    """fc's output feeding the drop-in BatchNorm AND another op: autograd sums the two gradients, so
+    fc's backward receives a tensor without the BatchNorm's digits and quantises the sum itself --
+    the gradients equal those with torch's BatchNorm1d in the same graph."""
+    from models.binarized_modules import BinarizeLinear
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(512, 256, generator=g, device="cuda")
+    grads = []
+    for bn_cls in (torch.nn.BatchNorm1d, NN.BatchNorm1d):
+        torch.manual_seed(2)
+        fc = BinarizeLinear(256, 128).cuda()
+        fc.org_protocol = False
+        bn = bn_cls(128).cuda()
+        y = fc(x.clone())
+        loss = (bn(y) * torch.linspace(-1, 1, 128, device="cuda")).sum() + 0.5 * (y * y).mean()
+        loss.backward()
+        grads.append((fc.weight.grad.clone(), fc.bias.grad.clone()))
+    (wa, ba), (wb, bb) = grads
+    assert float((wb - wa).abs().max()) <= 1e-4 * float(wa.abs().max()), float((wb - wa).abs().max())
+    assert float((bb - ba).abs().max()) <= 1e-4 * float(ba.abs().max()) + 1e-6
+
