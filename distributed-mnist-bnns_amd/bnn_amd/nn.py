@@ -144,8 +144,13 @@ class BinarizeLinear(nn.Linear):
             else:
                 u = BF.unit_to_pixels(input)
                 self._pixel_mode = u is not None
-                if u is not None and self.__dict__.get("_pixel_guard") is None:
-                    self._pixel_guard = torch.zeros((1,), dtype=torch.int32, device=input.device)
+                if u is not None:
+                    # a fresh (zero) guard for the next capture; an eager warm-up precedes every one
+                    g = self.__dict__.get("_pixel_guard")
+                    if g is None or g.device != input.device:
+                        self._pixel_guard = torch.zeros((1,), dtype=torch.int32, device=input.device)
+                    else:
+                        g.zero_()
             if u is not None:
                 if self.org_protocol:
                     _apply_org_protocol(self.weight)
