@@ -1100,27 +1100,62 @@ __global__ __launch_bounds__(B3_T) void conv_bwd_data_bf3_k(const float* __restr
     for (int a = 0; a < NT; ++a)
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[a][m] = mf4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < g.Kp; k0 += 32) {
-      const int k = k0 + 8 * chunk;
-      const int tq = fdivi(k, inv_cop), co0 = k - tq * g.Cop;
-      const int tap = min(tq, g.taps - 1);                 // padded k: zero weights
-      const int kh = fdivi(tap, inv_kw), kw = tap - kh * g.KW;
-      const int hoff = (g.KH - 1 - kh) * g.OWp + (g.KW - 1 - kw);
-      bf8 av[NT];
+    if (g.Cop == 32 && g.Kp == 32 * g.taps) {
+      // one k-step = one tap (32 channels): the tap, its (kh, kw) and the halo offset are uniform
+      // (scalar registers), each lane's fragment addresses a fixed base plus that offset -- the
+      // general loop below spends ~20 VALU per k-step on per-lane index arithmetic.  Same MFMAs in
+      // the same order (bit-identical).
+      const int abase = (lane & 15) * g.ws + 8 * chunk;
+      int bbase[MT];
 #pragma unroll
-      for (int a = 0; a < NT; ++a)
-        av[a] = *reinterpret_cast<const bf8*>(wsb + (a * 16 + (lane & 15)) * g.ws + k);
+      for (int m = 0; m < MT; ++m) bbase[m] = hb[m] * g.ps + 8 * chunk;
+      int kh = 0, kw = 0;
+      for (int tap = 0; tap < g.taps; ++tap) {
+        const int hoff = ((g.KH - 1 - kh) * g.OWp + (g.KW - 1 - kw)) * g.ps;
+        bf8 av[NT];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        bf8 bv[MT];
+        for (int a = 0; a < NT; ++a)
+          av[a] = *reinterpret_cast<const bf8*>(wsb + a * 16 * g.ws + abase + 32 * tap);
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-          bv[m] = *reinterpret_cast<const bf8*>(img + j * plane + (hb[m] + hoff) * g.ps + co0);
+        for (int j = 0; j < 3; ++j) {
+          bf8 bv[MT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+          for (int m = 0; m < MT; ++m)
+            bv[m] = *reinterpret_cast<const bf8*>(img + j * plane + bbase[m] + hoff);
 #pragma unroll
-          for (int a = 0; a < NT; ++a)
-            acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[m], acc[a][m], 0, 0, 0);
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int a = 0; a < NT; ++a)
+              acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[m], acc[a][m], 0, 0, 0);
+        }
+        if (++kw == g.KW) {
+          kw = 0;
+          ++kh;
+        }
+      }
+    } else {
+      for (int k0 = 0; k0 < g.Kp; k0 += 32) {
+        const int k = k0 + 8 * chunk;
+        const int tq = fdivi(k, inv_cop), co0 = k - tq * g.Cop;
+        const int tap = min(tq, g.taps - 1);                 // padded k: zero weights
+        const int kh = fdivi(tap, inv_kw), kw = tap - kh * g.KW;
+        const int hoff = (g.KH - 1 - kh) * g.OWp + (g.KW - 1 - kw);
+        bf8 av[NT];
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+          av[a] = *reinterpret_cast<const bf8*>(wsb + (a * 16 + (lane & 15)) * g.ws + k);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          bf8 bv[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            bv[m] = *reinterpret_cast<const bf8*>(img + j * plane + (hb[m] + hoff) * g.ps + co0);
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int a = 0; a < NT; ++a)
+              acc[a][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[m], acc[a][m], 0, 0, 0);
+        }
       }
     }
     float* xn = dx + n * (int64_t)g.C * HW;
