@@ -9,6 +9,8 @@ Hardtanh, Dropout, LogSoftmax around it), trained by the reference's loop verbat
 * ``frozen`` -- mnist-dist3.py:38-67 (Net 784-192-192-192-10), :78-84 (Adam, DDP), :113-119 (the
   loop without the ``.org`` protocol: Adam updates the binarised copy that the next forward
   overwrites, so the binary weights stay frozen at their initial signs), batch 64 per rank.
+* ``org-bn`` -- ``org`` with the Net's bn1..bn3 swapped for ``bnn_amd.nn.BatchNorm1d`` on the
+  drop-in side (the oracle keeps torch's): the same bars.
 
 Inside DDP's forward the drop-in layers reassign ``weight.data = sign(weight.org)``
 (binarized_modules.py:77-79) and mutate their input (:76), and DDP's all-reduce fires inside
@@ -56,9 +58,10 @@ TOL = 1e-5
 FC_BIAS = ("fc1.bias", "fc2.bias", "fc3.bias")
 BINARY_W = ("fc1.weight", "fc2.weight", "fc3.weight")
 CASES = {
-    # kind: (widths, batch per rank, org protocol)
-    "org": ((3072, 1536, 768), 100, True),        # mnist-dist2.py
-    "frozen": ((192, 192, 192), 64, False),       # mnist-dist3.py
+    # kind: (widths, batch per rank, org protocol, drop-in BatchNorm1d on our side)
+    "org": ((3072, 1536, 768), 100, True, False),        # mnist-dist2.py
+    "frozen": ((192, 192, 192), 64, False, False),       # mnist-dist3.py
+    "org-bn": ((3072, 1536, 768), 100, True, True),      # mnist-dist2.py + bnn_amd.nn.BatchNorm1d
 }
 STEPS = 3
 LR = 0.01
@@ -72,8 +75,8 @@ def _free_port():
     return port
 
 
-def _make_net(linear, widths):
-    """mnist-dist2.py:46-76 / mnist-dist3.py:38-67 with the Linear class injected."""
+def _make_net(linear, widths, bn=nn.BatchNorm1d):
+    """mnist-dist2.py:46-76 / mnist-dist3.py:38-67 with the Linear (and BatchNorm1d) class injected."""
     h1, h2, h3 = widths
 
     class Net(nn.Module):
@@ -81,13 +84,13 @@ def _make_net(linear, widths):
             super().__init__()
             self.fc1 = linear(784, h1)
             self.htanh1 = nn.Hardtanh()
-            self.bn1 = nn.BatchNorm1d(h1)
+            self.bn1 = bn(h1)
             self.fc2 = linear(h1, h2)
             self.htanh2 = nn.Hardtanh()
-            self.bn2 = nn.BatchNorm1d(h2)
+            self.bn2 = bn(h2)
             self.fc3 = linear(h2, h3)
             self.htanh3 = nn.Hardtanh()
-            self.bn3 = nn.BatchNorm1d(h3)
+            self.bn3 = bn(h3)
             self.fc4 = nn.Linear(h3, 10)
             self.logsoftmax = nn.LogSoftmax(dim=1)
             self.drop = nn.Dropout(0.3)
@@ -162,15 +165,16 @@ def _worker(rank, world, port, q, kind):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from models.binarized_modules import BinarizeLinear
         from oracle.bnn_torch import RefLinear
-        widths, batch, org = CASES[kind]
+        widths, batch, org, dropin_bn = CASES[kind]
+        from bnn_amd.nn import BatchNorm1d
 
-        def build(linear):
+        def build(linear, bn=nn.BatchNorm1d):
             torch.manual_seed(100 + rank)          # per-rank init, as mnist-dist2.py: DDP broadcasts rank 0's
-            m = _make_net(linear, widths).cuda().train()
+            m = _make_net(linear, widths, bn).cuda().train()
             opt = torch.optim.Adam(m.parameters(), lr=LR)                       # mnist-dist2.py:89
             return nn.parallel.DistributedDataParallel(m, device_ids=[0]), opt  # :93
 
-        ours, opt_o = build(BinarizeLinear)
+        ours, opt_o = build(BinarizeLinear, BatchNorm1d if dropin_bn else nn.BatchNorm1d)
         ref, opt_r = build(RefLinear)
         # z1 anchoring: the oracle's fc1 output takes the drop-in's value (its gradient still flows
         # through the oracle's own fc1).  fc1's input is continuous, z1 carries each implementation's
@@ -247,7 +251,7 @@ def _worker(rank, world, port, q, kind):
         q.put((rank, "ERR " + traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["org", "frozen"])
+@pytest.mark.parametrize("kind", ["org", "frozen", "org-bn"])
 def test_ddp_around_dropin_modules_matches_reference_semantics(kind):
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
