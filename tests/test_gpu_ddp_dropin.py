@@ -10,7 +10,8 @@ Hardtanh, Dropout, LogSoftmax around it), trained by the reference's loop verbat
   loop without the ``.org`` protocol: Adam updates the binarised copy that the next forward
   overwrites, so the binary weights stay frozen at their initial signs), batch 64 per rank.
 * ``org-bn`` -- ``org`` with the Net's bn1..bn3 swapped for ``bnn_amd.nn.BatchNorm1d`` on the
-  drop-in side (the oracle keeps torch's): the same bars.
+  drop-in side (the oracle keeps torch's): the BatchNorm outputs within 1e-5 of torch's, then
+  anchored like z1 (ties on the batch mean, see the worker), and the same bars.
 
 Inside DDP's forward the drop-in layers reassign ``weight.data = sign(weight.org)``
 (binarized_modules.py:77-79) and mutate their input (:76), and DDP's all-reduce fires inside
@@ -183,6 +184,22 @@ def _worker(rank, world, port, q, kind):
         z1 = {}
         ours.module.fc1.register_forward_hook(lambda m, i, o: z1.__setitem__("v", o.detach()))
         ref.module.fc1.register_forward_hook(lambda m, i, o: z1["v"] + (o - o.detach()))   # exactly z1
+        bn_out, bn_err = {}, []
+        if dropin_bn:
+            # the BatchNorm outputs anchored the same way: both sides' outputs are compared (<= 1e-5
+            # norm-wise), then the oracle continues from ours.  libbnn's batch mean carries a lo part
+            # (x - mean = (x - hi) - lo) where torch's is one fp32 value, so an element on the batch
+            # mean (z1 takes discrete values: pixel sums / 255) can come out as +-tiny on one side and
+            # exactly 0 on the other, and the next layer's sign() turns that into a different ternary
+            # input.  Each side's own BatchNorm backward still runs.
+            for name in ("bn1", "bn2", "bn3"):
+                getattr(ours.module, name).register_forward_hook(
+                    lambda m, i, o, name=name: bn_out.__setitem__(name, o.detach()))
+
+                def take(m, i, o, name=name):
+                    bn_err.append(_rel(bn_out[name], o.detach()))
+                    return bn_out[name] + (o - o.detach())
+                getattr(ref.module, name).register_forward_hook(take)
         crit = nn.CrossEntropyLoss()
         g = torch.Generator(device="cuda").manual_seed(1234 + rank)
         report = []
@@ -197,6 +214,9 @@ def _worker(rank, world, port, q, kind):
             lo, out_o, g_o, pre_o = _reference_step(ours, opt_o, crit, data.clone(), target, org)
             torch.manual_seed(1000 + 10 * step + rank)
             lr_, out_r, g_r, _ = _reference_step(ref, opt_r, crit, data.clone(), target, org)
+            if dropin_bn:
+                assert max(bn_err) <= TOL, (kind, step, "BatchNorm outputs", max(bn_err))
+                bn_err.clear()
             dl = abs(float(lo) - float(lr_))
             assert dl <= TOL * max(1.0, abs(float(lr_))), (kind, step, "loss", float(lo), float(lr_))
             assert _rel(out_o, out_r) <= TOL, (kind, step, "log-probs", _rel(out_o, out_r))
