@@ -340,6 +340,9 @@ __global__ __launch_bounds__(256) void bn_apply_pack_fp4_k(XIn xin, int64_t M, i
   // pnks > 0: the transpose in the FP4 panel layout of the FP6 GEMM's B operand (bnn_fp4_panelize:
   // [C/512][pnks][512][32 B]) -- row n's 16 B at batch m0 + 32 mg are half mg & 1 of k-step
   // (m0 + 32 mg) / 64; a wave's 8 rows per store are 32-B pieces of 8 lines the c loop completes
+#if defined(APK_DIAG_NOQT)   // timing-only build: no transpose stores (wrong results)
+  if (out[0][0] == 0x12345678u)
+#endif
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int64_t n = k0 + 8 * kb + c;
