@@ -51,6 +51,7 @@ SIGNATURES = {
     "bnn_linear_nsmall_workspace": (I64, [I64, I64, I64]),
     "bnn_linear_nsmall_fwd": (I32, [P, I64, I64, P, P, I64, P, P]),
     "bnn_linear_nsmall_bwd": (I32, [P, P, P, I64, I64, I64, P, P, P, P, I64, P]),
+    "bnn_col_sums_narrow": (I32, [P, I64, I64, I64, P, P]),
     "bnn_cross_entropy_ok": (I32, [I64]),
     "bnn_cross_entropy_workspace": (I64, [I64]),
     "bnn_cross_entropy_fwd": (I32, [P, P, I64, I64, I64, P, P, I64, P]),

@@ -839,6 +839,7 @@ def pixels_to_float(u, normalize=None):
     return x
 
 
+COL_SUMS = os.environ.get("BNN_COLSUM", "1") != "0"   # the head's db4 on bnn_col_sums_narrow (0: torch's sum)
 UNIT_PIXELS = 0          # fp32 ToTensor images recognised as bytes (tests check the path ran)
 CAPTURE_GUARDS = []      # mismatch flags of the recognitions captured into a graph (graph.GraphedStep)
 
@@ -1857,7 +1858,13 @@ class DropoutBNHardtanhLinearFunction(torch.autograd.Function):
                        L.ptr(ws), L.stream())
         if ctx.q6 or ctx.z16:
             setattr(dx, _Q6_ATTR, (_q6_key(dx), rows, cols, cs))
-        db4 = dy4.sum(0) if ctx.has_b4 and ctx.needs_input_grad[10] else None
+        db4 = None
+        if ctx.has_b4 and ctx.needs_input_grad[10]:
+            if COL_SUMS and M <= 32768 and dy4.is_contiguous():   # one libbnn launch (fixed order)
+                db4 = torch.empty((HEAD_NOUT,), dtype=torch.float32, device=dev)
+                L.call("bnn_col_sums_narrow", L.ptr(dy4), M, HEAD_NOUT, HEAD_NOUT, L.ptr(db4), L.stream())
+            else:
+                db4 = dy4.sum(0)
         return (dx, dgw if ctx.needs_input_grad[1] else None, dgb if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, dw4 if ctx.needs_input_grad[9] else None, db4)
 

@@ -649,6 +649,10 @@ int bnn_linear_nsmall_fwd(const float* x, int64_t M, int64_t K, const float* w, 
                           float* y, bnn_stream_t stream);
 int bnn_linear_nsmall_bwd(const float* x, const float* w, const float* dy, int64_t M, int64_t K, int64_t N,
                           float* dx, float* dw, float* db, void* work, int64_t work_bytes, bnn_stream_t stream);
+/* out[n] = sum over rows of y[m][n] (row-major, leading dimension ld) for a narrow matrix: N <= 16,
+ * 0 < M <= 32768 -- the fused head's bias gradient db4 = dY4.sum(0) (mnist-dist2.py:76, fc4's
+ * bias).  One workgroup, double sums in a fixed order (deterministic). */
+int bnn_col_sums_narrow(const float* y, int64_t M, int64_t N, int64_t ld, float* out, void* stream);
 
 /* The training step's loss (replaces criterion = nn.CrossEntropyLoss() on the nets' LogSoftmax
  * output, mnist-dist2.py:118-137): p [M][C] fp32 rows (C in {2, 10, 16, 32, 64}: the MNIST heads),

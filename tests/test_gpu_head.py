@@ -112,3 +112,21 @@ def test_wide_step_with_fused_head_equals_unfused(F):
             assert np.linalg.norm(a - b) <= 1e-5 * ref, k
         else:
             assert rel_err(a, b) <= 2e-5, (k, rel_err(a, b))
+
+
+@pytest.mark.parametrize("M,N,ld", [(4096, 10, 10), (1, 10, 10), (65, 3, 16), (32768, 16, 16)])
+def test_col_sums_narrow_matches_torch(M, N, ld):
+    """bnn_col_sums_narrow (the fused head's bias gradient db4 = dY4.sum(0)): the column sums of a
+    narrow matrix against float64, within fp32 rounding of the result; repeat calls bit-identical."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    from bnn_amd import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    y = torch.randn(M, ld, generator=g, device="cuda")
+    out = torch.empty(N, device="cuda")
+    L.call("bnn_col_sums_narrow", L.ptr(y), M, N, ld, L.ptr(out), L.stream())
+    ref = y[:, :N].double().sum(0)
+    assert float((out.double() - ref).abs().max()) <= 1e-6 * max(1.0, float(ref.abs().max()))
+    out2 = torch.empty_like(out)
+    L.call("bnn_col_sums_narrow", L.ptr(y), M, N, ld, L.ptr(out2), L.stream())
+    assert torch.equal(out, out2)
