@@ -2212,6 +2212,17 @@ BNN_API int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t 
                           nout, b4, y4, stream);
 }
 
+// Row chunks of the fused head's backward statistics pass: the BatchNorm chunks, but never fewer
+// than 16 rows.  A narrow head (config 3: 768 columns at 4,096 rows) would otherwise get 4-row chunks
+// (bn_chunk_rows fills the chip with threads) -- 1,024 chunk partials of dgamma / dbeta and of
+// dW4's 10 x C products (31 MB) to write and fold -- and the keep-bit plane, whose words are 8 rows,
+// would be re-hashed instead of read.  Fixed per shape (deterministic).
+inline int64_t head_chunk_rows(int64_t M, int64_t C) { return std::max<int64_t>(bn_chunk_rows(M, C), 16); }
+inline int64_t head_chunks(int64_t M, int64_t C) {
+  const int64_t rows = head_chunk_rows(M, C);
+  return std::max<int64_t>(1, (M + rows - 1) / rows);
+}
+
 static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float* w4, int32_t nout, int64_t M,
                                int64_t C, const float* gamma, const float* beta, const float* save_mean,
                                const float* save_invstd, const float* save_mean_lo, float p, uint64_t seed,
@@ -2231,8 +2242,9 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
   Drop dp = make_drop(p, seed);
   dp.bits = dp.on ? keep_bits : nullptr;   // the apply pass reads the forward's keep bits in any shape
   Drop dpr = dp;                           // the statistics pass where its 8-row batches are whole words
-  if (!keep_bits_fused(M, C)) dpr.bits = nullptr;
-  const int64_t R = bn_chunks(M, C);
+  const int64_t hrows = head_chunk_rows(M, C);
+  if (!(RED_RB == 8 && hrows % 8 == 0)) dpr.bits = nullptr;
+  const int64_t R = head_chunks(M, C);
   double* p0 = reinterpret_cast<double*>(work);
   double* p1 = p0 + R * C;
   float* k0 = reinterpret_cast<float*>(p1 + R * C);
@@ -2241,14 +2253,14 @@ static int bn_head_bwd_q6_impl(XIn xin, bool z16, const float* dy4, const float*
   if (g_head_red_cols == 2) {
     auto kr = z16 ? (dpr.bits ? bn_head_reduce2_k<HEAD_NOUT, true, true> : bn_head_reduce2_k<HEAD_NOUT, true, false>)
                   : (dpr.bits ? bn_head_reduce2_k<HEAD_NOUT, false, true> : bn_head_reduce2_k<HEAD_NOUT, false, false>);
-    const dim3 g2((unsigned)(((C / 2) * bn_chunks(M, C) + 255) / 256));
+    const dim3 g2((unsigned)(((C / 2) * R + 255) / 256));
     hipLaunchKernelGGL(kr, g2, dim3(256), 0, s, xin, dy4, w4, M, C, save_mean, save_mean_lo, save_invstd, gamma,
-                       beta, p0, p1, pw, bn_chunk_rows(M, C), dpr);
+                       beta, p0, p1, pw, hrows, dpr);
   } else {
     auto kr = z16 ? (dpr.bits ? bn_head_reduce_k<HEAD_NOUT, true, true> : bn_head_reduce_k<HEAD_NOUT, true, false>)
                   : (dpr.bits ? bn_head_reduce_k<HEAD_NOUT, false, true> : bn_head_reduce_k<HEAD_NOUT, false, false>);
-    hipLaunchKernelGGL(kr, reduce_grid(M, C), dim3(256), 0, s, xin, dy4, w4, M, C, save_mean, save_mean_lo,
-                       save_invstd, gamma, beta, p0, p1, pw, bn_chunk_rows(M, C), dpr);
+    hipLaunchKernelGGL(kr, dim3((unsigned)(((C / 4) * R + 255) / 256)), dim3(256), 0, s, xin, dy4, w4, M, C, save_mean,
+                       save_mean_lo, save_invstd, gamma, beta, p0, p1, pw, hrows, dpr);
   }
   hipLaunchKernelGGL(bn_bwd_final_k, ffin_grid(C), dim3(256), 0, s, p0, p1, C, R, dgamma, dbeta, k0, k1);
   hipLaunchKernelGGL(head_dw_final_k, dim3((unsigned)((nout * C + HD_FF_COLS - 1) / HD_FF_COLS)),
