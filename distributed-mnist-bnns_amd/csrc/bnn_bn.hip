@@ -31,9 +31,12 @@ constexpr int BN_ROWS = 256;  // most rows per partial-statistics chunk
 // Rows per chunk of the column reductions: 256, halved while the reduction (one thread per 4
 // columns and chunk) would have fewer than 2^17 threads -- a [4096, 3072] batch gets 16-row
 // chunks (196 K threads) instead of 48 workgroups, a [65536, 8192] one keeps 256.
+#ifndef BN_FILL_LOG2
+#define BN_FILL_LOG2 17
+#endif
 inline int64_t bn_chunk_rows(int64_t M, int64_t C) {
   int64_t rows = BN_ROWS;
-  while (rows > 1 && (C / 4) * ((M + rows - 1) / rows) < (1 << 17)) rows >>= 1;
+  while (rows > 1 && (C / 4) * ((M + rows - 1) / rows) < (1 << BN_FILL_LOG2)) rows >>= 1;
   return rows;
 }
 inline int64_t bn_chunks(int64_t M, int64_t C) {
