@@ -32,7 +32,7 @@ constexpr int BN_ROWS = 256;  // most rows per partial-statistics chunk
 // columns and chunk) would have fewer than 2^17 threads -- a [4096, 3072] batch gets 16-row
 // chunks (196 K threads) instead of 48 workgroups, a [65536, 8192] one keeps 256.
 #ifndef BN_FILL_LOG2
-#define BN_FILL_LOG2 17
+#define BN_FILL_LOG2 16
 #endif
 inline int64_t bn_chunk_rows(int64_t M, int64_t C) {
   int64_t rows = BN_ROWS;
