@@ -1338,11 +1338,14 @@ static int device_cus() {
   return cus;
 }
 
+#ifndef FP6_SPLIT_CAP
+#define FP6_SPLIT_CAP 1024
+#endif
 static Fp6Plan plan6(int64_t M, int64_t N, int64_t K) {
   if (g_variant6 >= 0) return Fp6Plan{find6(g_variant6), 1};
   const Variant6* v = find6(7);
   const int64_t tiles = ((M + v->bm - 1) / v->bm) * ((N + v->bn - 1) / v->bn), ncu = device_cus();
-  const int64_t s = std::min<int64_t>(ncu / std::max<int64_t>(tiles, 1), (K / 64) / 4);
+  const int64_t s = std::min<int64_t>(std::min<int64_t>(ncu / std::max<int64_t>(tiles, 1), (K / 64) / 4), FP6_SPLIT_CAP);
   return Fp6Plan{v, (int)std::max<int64_t>(1, s)};
 }
 
