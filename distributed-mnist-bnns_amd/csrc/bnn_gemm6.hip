@@ -1339,7 +1339,7 @@ static int device_cus() {
 }
 
 #ifndef FP6_SPLIT_CAP
-#define FP6_SPLIT_CAP 1024
+#define FP6_SPLIT_CAP 8
 #endif
 static Fp6Plan plan6(int64_t M, int64_t N, int64_t K) {
   if (g_variant6 >= 0) return Fp6Plan{find6(g_variant6), 1};
