@@ -1365,9 +1365,16 @@ static int gemm_fp6_impl(const uint8_t* alo, const uint8_t* ahi, const uint8_t* 
 // Whether a launch takes the half-tile form (bnn_gemm_fp6_set_half): mode 1 the residual-plane (dX)
 // launches, mode 2 every launch; no bias, whole K per tile, 64 x 512-tiled shapes of >= 2 rounds of
 // two workgroups per CU.
+// FP6_HALF_SMALL: also an unsplit grid of under one round of 128 x 512 tiles (config 3's dX), where the
+// half tiles double the workgroups that share the chip.
+#ifndef FP6_HALF_SMALL
+#define FP6_HALF_SMALL 0
+#endif
 static bool fp6_half_applies(int64_t M, int64_t N, int ksplit, bool has_bias, bool res) {
-  return g_fp6_half > 0 && (res || g_fp6_half > 1) && !has_bias && ksplit <= 1 && g_variant6 < 0 && M % 64 == 0 &&
-         N % 512 == 0 && (M / 64) * (N / 512) >= 4 * device_cus();
+  if (g_fp6_half <= 0 || has_bias || ksplit > 1 || g_variant6 >= 0 || M % 64 != 0 || N % 512 != 0) return false;
+  const int64_t tiles = (M / 64) * (N / 512);
+  if (res || g_fp6_half > 1) return tiles >= 4 * device_cus();
+  return FP6_HALF_SMALL && tiles < 2 * device_cus();
 }
 
 static bool fp6_pers_applies(int64_t M, int64_t N, int ksplit, bool has_bias, bool panel) {
