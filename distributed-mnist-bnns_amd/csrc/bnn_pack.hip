@@ -1165,6 +1165,10 @@ BNN_API int bnn_quant_cols_t(const float* x, int64_t M, int64_t N, int64_t ldx, 
   return bnn_quant_cols_t_dsum(x, M, N, ldx, digits_t, ldqt, plane, scale, colsum, nullptr, work, stream);
 }
 
+// the 256 x 256 form from this many tiles up (below it, the 64 x 64 tiles fill the chip better)
+#ifndef AP_FAST_MIN_TILES
+#define AP_FAST_MIN_TILES 1024
+#endif
 BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float* mean, const float* invstd,
                               const float* mean_lo, const float* gamma, const float* beta, int32_t fmt, void* q,
                               int64_t ldq, int8_t* qt, int64_t ldqt, int32_t qt_fmt, void* stream) {
@@ -1189,7 +1193,7 @@ BNN_API int bnn_bn_apply_pack(const float* x, int64_t M, int64_t C, const float*
                      aligned16(mean) && aligned16(invstd) && (!gamma || aligned16(gamma)) &&
                          (!beta || aligned16(beta)) && (!mean_lo || aligned16(mean_lo))};
   const bool fast = fmt == 1 && q && qt && (qt_fmt == 1 || qt_fmt == 2) && C % AP_T == 0 && af.vec && vec &&
-                    (C / AP_T) * ((M + AP_T - 1) / AP_T) >= 1024;
+                    (C / AP_T) * ((M + AP_T - 1) / AP_T) >= AP_FAST_MIN_TILES;
   if (fast) {
     hipLaunchKernelGGL((bn_apply_pack_fp4_k<0>), dim3((unsigned)(C / AP_T), (unsigned)((M + AP_T - 1) / AP_T)),
                        dim3(256), 0, S(stream), XIn{x, nullptr}, M, C, af, reinterpret_cast<uint8_t*>(q), ldq,
