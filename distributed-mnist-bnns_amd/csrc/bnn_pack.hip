@@ -95,6 +95,10 @@ __device__ __forceinline__ void adam4(float* __restrict__ prow, int64_t off, int
 // One 64x64 tile of x -> ternary rows (q: FMT 0 = int8 per element, FMT 1 = FP4 e2m1 nibbles,
 // element k in byte k/2, low nibble for even k) and/or the transposed int8 tile (qt).
 // ADAM = 1: x is a latent weight updated in place first (adam4), and its new sign is packed.
+// PK_COAL 1: the non-Adam modes load whole 256-B row runs too (below); 0: 16 columns per lane
+#ifndef PK_COAL
+#define PK_COAL 1
+#endif
 template <int FMT, int AFF = 0, int ADAM = 0>
 __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict__ x, int64_t M,
                                                         int64_t K, int64_t ldx, int8_t* __restrict__ q,
@@ -110,13 +114,21 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
   __shared__ int tile[TILE][TILE + 1];
   const int64_t k0 = (int64_t)blockIdx.x * TILE;
   const int t = threadIdx.x, r = t >> 2, c = (t & 3) * 16;
+#if PK_COAL
+  // the row-run form: lane = 4 consecutive columns of a 256-B row run, parameters for those 4
+  float mu[4], lo[4], is[4], ga[4], be[4];
+  constexpr int NP = 4;
+  const int64_t cb = k0 + (t & 15) * 4;
+#else
   float mu[16], lo[16], is[16], ga[16], be[16];
+  constexpr int NP = 16;
+  const int64_t cb = k0 + c;
+#endif
   if (AFF) {
-    // per-column parameters for columns k0+c .. +15: float4 loads when the run is in range
-    const int64_t cb = k0 + c;
-    if (af.vec && cb + 16 <= K) {
+    // per-column parameters for columns cb .. cb + NP - 1: float4 loads when the run is in range
+    if (af.vec && cb + NP <= K) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NP / 4; ++i) {
         const float4 a = *reinterpret_cast<const float4*>(af.mean + cb + 4 * i);
         const float4 b = *reinterpret_cast<const float4*>(af.invstd + cb + 4 * i);
         const float4 g = af.gamma ? *reinterpret_cast<const float4*>(af.gamma + cb + 4 * i) : make_float4(1, 1, 1, 1);
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < NP; ++j) {
         const bool in = cb + j < K;
         mu[j] = in ? af.mean[cb + j] : 0.f;
         lo[j] = (in && af.mean_lo) ? af.mean_lo[cb + j] : 0.f;
@@ -167,6 +179,38 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
     for (int j = 0; j < 16; ++j) s[j] = tile[r][c + j];
     if (qt != nullptr) __syncthreads();   // read before the transpose below rewrites the tile
   } else {
+#if PK_COAL
+    // as the ADAM mode: every wave load instruction covers 4 whole 256-B row runs (lane = 4
+    // consecutive columns), the signs go through the LDS tile into the 16-column layout below.
+    // The same per-element arithmetic as the 16-column form (bit-identical).
+    const int ar = t >> 4, ac = (t & 15) * 4;
+#pragma unroll
+    for (int pr = 0; pr < TILE / 16; ++pr) {
+      const int rr = ar + 16 * pr;
+      const int64_t mr = m0 + rr;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (mr < M) {
+        const float* row = x + mr * ldx;
+        if (vec && cb + 4 <= K) {
+          const float4 f = *reinterpret_cast<const float4*>(row + cb);
+          v[0] = f.x, v[1] = f.y, v[2] = f.z, v[3] = f.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (cb + j < K) ? row[cb + j] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float y = v[j];
+        if (AFF) y = (mr < M && cb + j < K) ? fmaf(((y - mu[j]) - lo[j]) * is[j], ga[j], be[j]) : 0.f;
+        tile[rr][ac + j] = tsign(y);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s[j] = tile[r][c + j];
+    if (qt != nullptr) __syncthreads();   // read before the transpose below rewrites the tile
+#else
     float v[16];
     if (m < M) {
       load16(x + m * ldx, k0 + c, K, vec, v);
@@ -175,13 +219,13 @@ __global__ __launch_bounds__(256) void sign_pack_tile_k(const float* __restrict_
       for (int j = 0; j < 16; ++j) v[j] = 0.f;
     }
     if (AFF) {
-      const int64_t cb = k0 + c;
 #pragma unroll
       for (int j = 0; j < 16; ++j)
         v[j] = (m < M && cb + j < K) ? fmaf(((v[j] - mu[j]) - lo[j]) * is[j], ga[j], be[j]) : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) s[j] = tsign(v[j]);
+#endif
   }
   if (FMT == 0 && q != nullptr && m < M && k0 + c < ldq) {
     v4i w;
