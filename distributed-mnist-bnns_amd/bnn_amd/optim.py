@@ -20,9 +20,18 @@ With ``device_step`` (a ``functional.DeviceStep``) the step is graph-capturable:
 corrections come from a device table indexed by the device step counter (bit-identical to the
 per-launch values), and the counter is advanced on the device after the last update.
 """
+import os
+
 import torch
 
 from . import functional as BF
+
+# Side streams for the binarized weights' Adam + pack launches (bnn_adam_clamp_pack): the k-th such
+# launch of a step runs on stream k mod (1 + ADAM_STREAMS), 0 = the caller's, each forked from the
+# caller's stream just before its launch and joined back after the last.  The small layers' launches
+# are latency-bound and overlap (in eager steps and as parallel branches of a captured graph); every
+# launch touches only its own tensors, so the results are bit-identical.  0 = all on one stream.
+ADAM_STREAMS = int(os.environ.get("BNN_ADAM_STREAMS", "2"))
 
 
 def org_protocol_step(model, optimizer):
@@ -50,6 +59,14 @@ class LatentAdam(torch.optim.Optimizer):
         self.grad_scale = grad_scale
         self.device_step = device_step
         self._sched = {}              # group index -> (device table, (lr, betas) it was built for)
+        self._sides = {}              # device -> side streams (ADAM_STREAMS)
+
+    def _side_streams(self, device):
+        ss = self._sides.get(device)
+        if ss is None:
+            ss = [torch.cuda.Stream(device=device) for _ in range(ADAM_STREAMS)]
+            self._sides[device] = ss
+        return ss
 
     def _schedule(self, gi, group, step, device, build):
         """Device table for this group covering the device counter's steps: entry c holds the bias
@@ -100,6 +117,8 @@ class LatentAdam(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         ds = self.device_step
         capturing = ds is not None and torch.cuda.is_current_stream_capturing()
+        npack = 0
+        joined = {}                   # id(side stream) -> stream to join back into the caller's
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             sched = None
@@ -133,11 +152,30 @@ class LatentAdam(torch.optim.Optimizer):
                 kw = dict(sched=sched, ctr=ds.ctr) if sched is not None else {}
                 # a binarized layer's weight also gets its next-forward ternary operands rewritten in
                 # the same pass (bnn_adam_clamp_pack); anything else: plain fused Adam + clamp
-                if not BF.adam_clamp_pack_(p, *args, **kw):
+                side = None
+                if ADAM_STREAMS > 0 and p.is_cuda and p.dim() == 2 and getattr(p, "_bnn_pack", None) is not None:
+                    j = npack % (ADAM_STREAMS + 1)
+                    npack += 1
+                    if j > 0:
+                        side = self._side_streams(p.device)[j - 1]
+                if side is None:
+                    done = BF.adam_clamp_pack_(p, *args, **kw)
+                else:
+                    main = torch.cuda.current_stream(p.device)
+                    side.wait_stream(main)       # the gradient, the state and the counter are ready
+                    with torch.cuda.stream(side):
+                        done = BF.adam_clamp_pack_(p, *args, **kw)
+                    if done:
+                        joined[id(side)] = (side, main)
+                        if g is not p.grad:
+                            g.record_stream(side)
+                if not done:
                     small.append((p, g, st["exp_avg"], st["exp_avg_sq"], st["step"], id(p) in self._clamp))
             if small:
                 BF.adam_clamp_multi_(small, group["lr"], b1, b2, group["eps"], self.grad_scale,
                                      sched=sched, ctr=ds.ctr if sched is not None else None)
+        for side, main in joined.values():
+            main.wait_stream(side)
         if ds is not None:
             ds.advance()
         return loss
