@@ -28,10 +28,11 @@ from . import functional as BF
 
 # Side streams for the binarized weights' Adam + pack launches (bnn_adam_clamp_pack): the k-th such
 # launch of a step runs on stream k mod (1 + ADAM_STREAMS), 0 = the caller's, each forked from the
-# caller's stream just before its launch and joined back after the last.  The small layers' launches
-# are latency-bound and overlap (in eager steps and as parallel branches of a captured graph); every
-# launch touches only its own tensors, so the results are bit-identical.  0 = all on one stream.
-ADAM_STREAMS = int(os.environ.get("BNN_ADAM_STREAMS", "2"))
+# caller's stream just before its launch and joined back after the last.  Every launch touches only
+# its own tensors, so the results are bit-identical.  Measured, off by default (0 = one stream): at
+# 2 the captured graphs' parallel branches made config 3's step 0.76-0.81 ms against 0.69 and the
+# 192-wide net's 0.42 against 0.25; the wide step did not move (profiles/r06_af_adam_streams_ab.txt).
+ADAM_STREAMS = int(os.environ.get("BNN_ADAM_STREAMS", "0"))
 
 
 def org_protocol_step(model, optimizer):
