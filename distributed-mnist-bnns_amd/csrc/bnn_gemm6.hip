@@ -1135,9 +1135,6 @@ __global__ __launch_bounds__(512, 2) void gemm_fp6_pers_k(Gemm6Params p) {
   }
 }
 
-#ifndef SPLITK_SUM_BATCH
-#define SPLITK_SUM_BATCH 1
-#endif
 // C = bias + sum over splits of the partials, in split order (deterministic); float4 per thread
 __global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restrict__ part, int S, int64_t M, int64_t N,
                                                           const float* __restrict__ bias, float* __restrict__ C,
@@ -1146,18 +1143,6 @@ __global__ __launch_bounds__(256) void gemm6_splitk_sum_k(const float* __restric
   if (i >= M * N) return;
   const int64_t m = i / N, n = i - m * N;       // N % 4 == 0 (host check): 4 elements of one row
   float4 a = *reinterpret_cast<const float4*>(part + i);
-#if SPLITK_SUM_BATCH
-  // up to 8 splits: every partial's load issued before the first add, the adds in split order
-  if (S <= 8) {
-    float4 b[7];
-#pragma unroll
-    for (int sp = 1; sp < 8; ++sp)
-      if (sp < S) b[sp - 1] = *reinterpret_cast<const float4*>(part + sp * M * N + i);
-#pragma unroll
-    for (int sp = 1; sp < 8; ++sp)
-      if (sp < S) a.x += b[sp - 1].x, a.y += b[sp - 1].y, a.z += b[sp - 1].z, a.w += b[sp - 1].w;
-  } else
-#endif
   for (int sp = 1; sp < S; ++sp) {
     const float4 b = *reinterpret_cast<const float4*>(part + sp * M * N + i);
     a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
