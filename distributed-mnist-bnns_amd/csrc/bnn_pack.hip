@@ -813,14 +813,22 @@ constexpr int QC_RT = 8;
 #define DZQ_OCC 3   // waves per SIMD (<= 168 VGPRs): the pass waits on memory, so occupancy is its lever
 #endif
 
-__host__ __device__ inline int64_t qc_strips(int64_t M) { return (M + TILE * QC_RT - 1) / (TILE * QC_RT); }
+__host__ __device__ inline int64_t qc_strips(int64_t M, int rt = QC_RT) { return (M + TILE * rt - 1) / (TILE * rt); }
+// Row tiles per workgroup by shape: QC_RT_SMALL on grids of under 1,024 workgroups at QC_RT (config 3's
+// 4096 x 3072 dz: 384 workgroups of 8 sequential tiles), where the chip would sit mostly idle.
+#ifndef QC_RT_SMALL
+#define QC_RT_SMALL 2
+#endif
+inline int qc_rt(int64_t M, int64_t C) {
+  return ((C + TILE - 1) / TILE) * qc_strips(M, QC_RT) < 1024 ? QC_RT_SMALL : QC_RT;
+}
 
 template <int XF>
 __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, const float* __restrict__ dy,
                                                             int64_t M, int64_t N, BnCols bc,
                                                             const float* __restrict__ scale, int8_t* __restrict__ dt,
                                                             int64_t ldqt, int64_t plane, int64_t* __restrict__ dsum,
-                                                            double* __restrict__ part = nullptr) {
+                                                            double* __restrict__ part = nullptr, int rt = QC_RT) {
   constexpr int TM = 2 * TILE;                                       // rows per store tile
   __shared__ __attribute__((aligned(16))) int tile[TM * TILE];       // swizzled (qct_at<TILE, true, 32>)
   double csum[4] = {0.0, 0.0, 0.0, 0.0};
@@ -858,10 +866,10 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
       }
     }
   };
-  const int64_t mb = (int64_t)by * QC_RT * TILE;
+  const int64_t mb = (int64_t)by * rt * TILE;
   long long dacc = 0;   // this thread's column (n0 + t/4) digit sum over the strip
   load(mb);
-  for (int it = 0; it < QC_RT; ++it) {
+  for (int it = 0; it < rt; ++it) {
     const int64_t m0 = mb + (int64_t)it * TILE;
     if (m0 >= ldqt) break;                      // uniform per workgroup
     if (it > 0 && (it & 1) == 0) __syncthreads();   // the previous store tile's reads are done
@@ -883,7 +891,7 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
       *reinterpret_cast<int4*>(tile + row * TILE + ((cg ^ (((row >> 5) & 3) << 2)) << 2)) =
           make_int4(packed[0], packed[1], packed[2], packed[3]);
     }
-    const bool last = it + 1 == QC_RT || m0 + TILE >= ldqt;
+    const bool last = it + 1 == rt || m0 + TILE >= ldqt;
     if (!last) load(m0 + TILE);
     if ((it & 1) == 1 || last) {
       if ((it & 1) == 0) {   // an odd tile count: the second half of the store tile is zeros
@@ -899,7 +907,7 @@ __global__ __launch_bounds__(256, DZQ_OCC) void bn_dz_quant_cols_t_k(XIn xin, co
   }
   if (dsum != nullptr && (t & 3) == 0 && n0 + (t >> 2) < N && dacc != 0)
     atomicAdd(reinterpret_cast<unsigned long long*>(dsum + n0 + (t >> 2)), (unsigned long long)dacc);
-  if (part != nullptr && by < qc_strips(M)) {
+  if (part != nullptr && by < qc_strips(M, rt)) {
     // fixed-order fold of the 16 row groups' sums (the tile is free: every qct_store read is done)
     __syncthreads();
     double* ps = reinterpret_cast<double*>(tile);   // [16][64] doubles = 8 KiB <= 32 KiB
@@ -1318,7 +1326,7 @@ static int64_t i8c_pmx_bytes(int64_t M, int64_t C) {
 }
 
 BNN_API int64_t bnn_bn_bwd_i8cols_workspace(int64_t M, int64_t C) {
-  return round_up(bn_workspace_bytes(M, C), 256) + i8c_pmx_bytes(M, C) + qc_strips(M) * C * (int64_t)sizeof(double);
+  return round_up(bn_workspace_bytes(M, C), 256) + i8c_pmx_bytes(M, C) + qc_strips(M, qc_rt(M, C)) * C * (int64_t)sizeof(double);
 }
 
 static int bn_bwd_i8cols_impl(XIn xin, int xf, const float* dy, int64_t M, int64_t C, const float* gamma,
@@ -1353,15 +1361,16 @@ static int bn_bwd_i8cols_impl(XIn xin, int xf, const float* dy, int64_t M, int64
     if (rc) return rc;
   }
   const BnCols bc{save_mean, save_mean_lo, save_invstd, gamma, beta, k0, k1, 1.f / (float)M, hardtanh};
-  const dim3 qg((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + QC_RT - 1) / QC_RT));
+  const int rt = qc_rt(M, C);
+  const dim3 qg((unsigned)((C + TILE - 1) / TILE), (unsigned)((ldqt / TILE + rt - 1) / rt));
   if (xf == 2)
     hipLaunchKernelGGL(bn_dz_quant_cols_t_k<2>, qg, dim3(256), 0, s, xin, dy, M, C, bc, scale, digits_t, ldqt, plane,
-                       dsum, colsum ? part : nullptr);
+                       dsum, colsum ? part : nullptr, rt);
   else
     hipLaunchKernelGGL(bn_dz_quant_cols_t_k<0>, qg, dim3(256), 0, s, xin, dy, M, C, bc, scale, digits_t, ldqt, plane,
-                       dsum, colsum ? part : nullptr);
+                       dsum, colsum ? part : nullptr, rt);
   if (colsum)
-    hipLaunchKernelGGL(bn_dz_colsum_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, qc_strips(M), C, colsum);
+    hipLaunchKernelGGL(bn_dz_colsum_k, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, qc_strips(M, rt), C, colsum);
   return check_launch("bnn_bn_bwd_i8cols");
 }
 
