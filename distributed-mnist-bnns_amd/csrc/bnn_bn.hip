@@ -2220,7 +2220,10 @@ BNN_API int bnn_bn_head_fwd_i16(const int16_t* x16, const float* xbias, int64_t 
 // (bn_chunk_rows fills the chip with threads) -- 1,024 chunk partials of dgamma / dbeta and of
 // dW4's 10 x C products (31 MB) to write and fold -- and the keep-bit plane, whose words are 8 rows,
 // would be re-hashed instead of read.  Fixed per shape (deterministic).
-inline int64_t head_chunk_rows(int64_t M, int64_t C) { return std::max<int64_t>(bn_chunk_rows(M, C), 16); }
+#ifndef HEAD_MIN_ROWS
+#define HEAD_MIN_ROWS 16
+#endif
+inline int64_t head_chunk_rows(int64_t M, int64_t C) { return std::max<int64_t>(bn_chunk_rows(M, C), HEAD_MIN_ROWS); }
 inline int64_t head_chunks(int64_t M, int64_t C) {
   const int64_t rows = head_chunk_rows(M, C);
   return std::max<int64_t>(1, (M + rows - 1) / rows);
